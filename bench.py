@@ -1,0 +1,243 @@
+"""ViT-CNN training throughput on MI355X (BASELINE.json metric): patches/s, 9x9 HSI(144)+LiDAR, batch 64/GPU.
+
+One step = forward + weighted CE + backward (+ RCCL gradient all-reduce when N > 1) + fused AdamW
+over one resident synthetic batch (hsi U[0,1) [64,144,9,9], lidar U[0,1) [64,1,9,9], labels in
+[1,15]; random-init weights of the reference architecture).  N = 1 captures the whole step in a
+hipGraph; N > 1 captures forward+backward and runs the all-reduce and AdamW eagerly.
+
+  python bench.py [--gpus N --steps K --warmup W]            (torch.distributed.run for N > 1)
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with `roofline` for the dominant
+kernel (HIP-event timed inside this process) and `cpu_baseline` (the CPU oracle, rank 0, N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "vit-cnn_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+GFLOP_PER_PATCH = 0.5235      # SURVEY.md section 8d (de-duplicated algebra, fwd+bwd)
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--kernel-reps", type=int, default=50)
+    return ap.parse_args()
+
+
+def synthetic(batch, seed, device):
+    g = torch.Generator().manual_seed(seed)
+    hsi = torch.rand(batch, 144, 9, 9, generator=g)
+    lidar = torch.rand(batch, 1, 9, 9, generator=g)
+    target = torch.randint(1, 16, (batch,), generator=g)
+    return hsi.to(device), lidar.to(device), target.to(device)
+
+
+def time_kernel(fn, reps, stream):
+    """Average device time of fn() (one kernel launch sequence) with HIP events on `stream`."""
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(reps):
+        fn()
+    e.record(stream)
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e-3
+
+
+def dominant_kernel_roofline(model, batch, reps):
+    """Re-launch the step's dominant kernel on its live workspace buffers and time it with events.
+
+    Dominant kernel (profiles/): the fp32 MFMA GEMM of hsi1.local_feature (im2col'ed 3x3 conv,
+    M = B*49, N = 256, K = 9*144) — roofline bound: MFMA (fp32 peak).  Algorithmic work per
+    launch = 2*M*N*K flop."""
+    from vitcnn_amd._lib import lib
+    from vitcnn_amd.model import _Program
+    dev = model.flat_params.device
+    prog = _Program(model, dev, batch, True, "grad")
+    L = lib()
+    M, N, K = batch * 49, 256, 9 * 144
+    col = prog.ws.f("hsi1.local_feature.col", M * K)
+    out = prog.ws.f("hsi1.local_feature.out", M * N)
+    W, b = prog.P["hsi1.local_feature.conv.weight"], prog.P["hsi1.local_feature.conv.bias"]
+    stream = torch.cuda.current_stream(dev)
+
+    def fn():
+        L.vc_gemm(0, 1, M, N, K, 1.0, col, K, 0, W, K, 0, 0.0, out, N, 0, 1, b, None, 0, 0, 1, prog.scr_p,
+                  prog.scr_n, stream.cuda_stream)
+
+    t = time_kernel(fn, reps, stream)
+    flops = 2.0 * M * N * K
+    achieved = flops / t / 1e12
+    return {"kernel": "gemm_f32_mfma<false,true> (hsi1.local_feature conv3x3, M=%d N=%d K=%d)" % (M, N, K),
+            "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+            "avg_launch_us": round(t * 1e6, 2), "flop_per_launch": flops}
+
+
+def cpu_baseline(steps):
+    """The CPU oracle (reference op order, naive sequential scan) timed on this host: one warm-up
+    step, then `steps` timed B=64 training steps (forward, CE, backward, AdamW, loss.item())."""
+    from oracle import vitcnn_oracle as O
+    from vitcnn_amd import Multimodality_Mamba
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
+    state = O.make_state(m.state_dict())
+    opt = O.make_adamw(state)
+    hsi, lidar, target = synthetic(64, 1234, "cpu")
+    w = O.ce_class_weights(16)
+    O.train_step(state, hsi, lidar, target, w, opt)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        O.train_step(state, hsi, lidar, target, w, opt)
+    dt = time.perf_counter() - t0
+    return {"value": round(64 * steps / dt, 3), "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} timed B=64 training steps (after 1 warm-up) of oracle/vitcnn_oracle.py, fp32, "
+                      f"torch CPU with {threads} threads; {dt / steps:.2f} s/step"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba
+    torch.manual_seed(0)
+    model = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16, "multi_clock_gate").to(dev).train()
+    if world > 1:
+        dist.broadcast(model.flat_params.data, 0)
+    opt = AdamW(model.parameters(), lr=8e-4)
+    opt.grad_scale = 1.0 / world
+    w = torch.ones(16)
+    w[0] = 0.0
+    crit = CrossEntropyLoss(weight=w.to(dev))
+    hsi, lidar, target = synthetic(args.batch, 1000 + rank, dev)
+    holder = {}
+
+    def fwd_bwd():
+        logits = model(hsi, lidar)
+        loss = crit(logits, target)
+        loss.backward()
+        holder["loss"] = loss
+
+    def allreduce():
+        if world > 1:
+            dist.all_reduce(model.flat_params.grad, op=dist.ReduceOp.SUM)
+
+    def eager_step():
+        opt.zero_grad(set_to_none=True)
+        fwd_bwd()
+        allreduce()
+        opt.step()
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(max(3, args.warmup)):
+            eager_step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+
+    use_graph = not args.no_graph
+    graph = None
+    if use_graph:
+        opt.zero_grad(set_to_none=True)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fwd_bwd()
+            if world == 1:
+                opt.step()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+            if world > 1:
+                allreduce()
+                opt.step()
+        else:
+            eager_step()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    loss_val = float(holder["loss"].item())
+    t = torch.tensor([elapsed], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # reference-loop variant: loss.item() host sync every step (model_utils.py:936)
+    t1 = time.perf_counter()
+    nsync = min(args.steps, 50)
+    for _ in range(nsync):
+        step()
+        holder["loss"].item()
+    torch.cuda.synchronize(dev)
+    ms_sync = (time.perf_counter() - t1) / nsync * 1e3
+
+    roof = dominant_kernel_roofline(model, args.batch, args.kernel_reps)
+    patches = world * args.batch * args.steps
+    value = patches / elapsed
+    out = {
+        "metric": "training patches/sec, 9×9 HSI(144)+LiDAR patch, batch 64, 1/2/4/8 GPU",
+        "value": round(value, 1), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (U[0,1) HSI/LiDAR patches, random-init weights, resident in HBM)",
+        "config": {"workload": "ViT-CNN (Multimodality_Mamba) train step, Houston2013 shape 144+1 bands, 9x9, "
+                               "16 classes", "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                   "parallelism": f"dp{world}", "hipgraph": use_graph},
+        "ms_per_step_with_loss_item": round(ms_sync, 4),
+        "final_loss": round(loss_val, 6),
+        "model_flops_util": {"gflop_per_patch": GFLOP_PER_PATCH,
+                             "achieved_tflops": round(value / world * GFLOP_PER_PATCH * 1e-3, 3),
+                             "peak_tflops_fp32_mfma": PEAK_FP32_MFMA_TFLOPS,
+                             "frac": round(value / world * GFLOP_PER_PATCH * 1e-3 / PEAK_FP32_MFMA_TFLOPS, 5)},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,186 @@
+/*
+ * vitcnn.h — C ABI of the MI355X (gfx950) ViT-CNN training hot path.
+ *
+ * libvitcnn_hip.so exports one entry point per fused device op of the reference's
+ * "ViT-CNN (ours)" model (Multimodality_Mamba, /root/reference/model/Multimodality_Mamba/
+ * Mutimodality_Mamba7.py:1141-1181) and of its training iteration (model_utils.py:918-936).
+ * The reference has no native layer of its own: each entry
+ * point below replaces a PyTorch op sequence of the reference, cited per function, and is
+ * what the reference's plugin (get_model -> nn.Module.forward / loss.backward /
+ * optimizer.step) binds through the Python mirror in vit-cnn_amd/vitcnn_amd (ctypes).
+ *
+ * Conventions (all functions):
+ *   - plain device pointers (fp32 unless stated; int32 index tables), sizes and leading
+ *     dimensions in elements; activations are channels-last [rows, C] row-major;
+ *   - the caller owns every buffer, including the fp32 workspace `ws` (ws_floats elements)
+ *     that reductions use for fixed-order partial sums; nothing is allocated, nothing
+ *     synchronises, so every call is capturable into a hipGraph;
+ *   - work is enqueued on `stream`; return 0 on success, a hipError_t code on a launch
+ *     failure, 1 (hipErrorInvalidValue) on an invalid shape — the Python mirror raises
+ *     RuntimeError, like the reference's shape errors;
+ *   - `beta_*` arguments select overwrite (0) or accumulate (1) for outputs that several
+ *     backward branches feed.
+ */
+#ifndef VITCNN_H
+#define VITCNN_H
+
+#include <stddef.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+#define VC_API extern "C" __attribute__((visibility("default")))
+#else
+#define VC_API __attribute__((visibility("default")))
+#endif
+
+/* ---------------------------------------------------------------- dense contractions
+ * C[b] = alpha * op(A[b]) op(B[b]) + beta*C[b] (+ bias[n]) (+ addend[(m % add_mod)*add_ld + n]) (ReLU if flags&1)
+ * op(A)(m,k) = transA ? A[k*lda+m] : A[m*lda+k];  op(B)(k,n) = transB ? B[n*ldb+k] : B[k*ldb+n].
+ * fp32 in / fp32 accumulate on v_mfma_f32_16x16x4_f32; split-K (fixed-order) when the output
+ * grid is small and ws is given.  Replaces nn.Conv2d 1x1 / 3x3-after-im2col / nn.Linear /
+ * torch.matmul forward and backward (Mutimodality_Mamba7.py:258, :1040, :1068, :1071, :101-134,
+ * :147, :152, :1098, :1124, :1160; transformers modeling_mamba.py:372, :433, :438, :481). */
+VC_API int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
+                   const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                   float beta, float* C, long ldc, long strideC, int batch,
+                   const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                   float* ws, long ws_floats, hipStream_t stream);
+
+/* out[c] = beta*out[c] + sum_r X[r*ldx + c]  (bias gradients; fixed-order two-stage) */
+VC_API int vc_colsum(int R, int C, const float* X, long ldx, float* out, float beta,
+                     float* ws, long ws_floats, hipStream_t stream);
+
+/* ---------------------------------------------------------------- normalisation
+ * LayerNorm over the last dim (nn.LayerNorm eps=1e-6 via build_norm_layer,
+ * mmpretrain/models/utils/norm.py:119-123; used at Mutimodality_Mamba7.py:656, :985,
+ * :1083, :1085).  Saves per-row mean / rstd for the backward. */
+VC_API int vc_layernorm_fwd(int R, int C, const float* x, long ldx, const float* w, const float* b, float eps,
+                            float* y, long ldy, float* mean, float* rstd, hipStream_t stream);
+VC_API int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
+                            const float* mean, const float* rstd, float* dx, long lddx, float beta_dx,
+                            float* dw, float* db, float beta_w, float* ws, long ws_floats, hipStream_t stream);
+
+/* BatchNorm2d over channels-last rows (torch train/eval semantics, eps, momentum):
+ * ms_conv_bn_relu.bn (Mutimodality_Mamba7.py:1039), FusionLayer BN (:1103, :1129),
+ * NonLocal W[1] (:113).  train=1: batch stats (biased var) -> save_mean/save_invstd and the
+ * running stats (unbiased var) are updated in place; train=0: save_* from running stats. */
+VC_API int vc_bn_stats(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                       float* save_mean, float* save_invstd, float* run_mean, float* run_var,
+                       float* ws, long ws_floats, hipStream_t stream);
+VC_API int vc_bn_apply(long M, int C, const float* x, long ldx, const float* mean, const float* invstd,
+                       const float* w, const float* b, int relu, float* y, long ldy, hipStream_t stream);
+VC_API int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
+                     const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
+                     float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w,
+                     float* ws, long ws_floats, hipStream_t stream);
+
+/* ---------------------------------------------------------------- layout / spatial
+ * NCHW input patches (the reference's batch layout, datasets.py:571-572) -> channels-last. */
+VC_API int vc_nchw_to_nhwc(int B, int C, int HW, const float* x, float* y, hipStream_t stream);
+
+/* 3x3 valid im2col of a channels-last [B,H,W,C] map with the preceding BatchNorm's affine
+ * (bn_* may be null) fused in: col[(b,oh,ow), c*9+kh*3+kw] — ms_conv_bn_relu
+ * (Mutimodality_Mamba7.py:1035-1048), column order matching the [Co, Ci, 3, 3] weight. */
+VC_API int vc_im2col3x3(int B, int H, int W, int C, const float* x, const float* bn_mean, const float* bn_invstd,
+                        const float* bn_w, const float* bn_b, float* col, hipStream_t stream);
+/* gradient of vc_im2col3x3 w.r.t. its (post-BN) input, gather form: dx [B,H,W,C] overwritten */
+VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx, hipStream_t stream);
+
+/* nn.MaxPool2d(2) of the NonLocal phi/g branches (Mutimodality_Mamba7.py:94, :136-138):
+ * x channels-last [B,H,W,C] with row stride ldx -> y [B,H/2,W/2,C] + winning tap (uint8). */
+VC_API int vc_maxpool2_fwd(int B, int H, int W, int C, const float* x, long ldx, float* y, unsigned char* arg,
+                           hipStream_t stream);
+VC_API int vc_maxpool2_bwd(int B, int H, int W, int C, const float* dy, const unsigned char* arg, float* dx,
+                           long lddx, hipStream_t stream);
+
+/* ---------------------------------------------------------------- Mamba mixer (10 scan orders)
+ * hsiMamba '81_2+8' / '49_2+8' (Mutimodality_Mamba7.py:608-701, :787-867) over transformers
+ * MambaMixer (modeling_mamba.py:359-481).  order/inv_order: int32 [ndir, L] token order per
+ * direction and its inverse; xz = in_proj(LN(tokens)) computed ONCE per token [B*L, 2D];
+ * per-direction sequences are gathered through `order`, never materialised.
+ * u [ndir*B*L, D] = SiLU(causal dwconv1d_k4(x-part) + bias). */
+VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order, const float* xz,
+                                const float* conv_w, const float* conv_b, float* u, hipStream_t stream);
+/* selective scan (fp32 state, N = 16) + D skip + SiLU(z) gate; dt = softplus(dt_w @ xdbl[:, :R] + dt_b)
+ * computed in-kernel; xdbl = x_proj(u) [ndir*B*L, R+32]; y [ndir*B*L, D]  (modeling_mamba.py:175-283) */
+VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
+                             const float* xz, const int* order, const float* dt_w, const float* dt_b,
+                             const float* A_log, const float* Dskip, float* y, hipStream_t stream);
+/* ysum[b,l,:] = sum_k softmax(gate_logits)_k y[k, b, inv_k(l), :]  (un-permute + gate, :694-701) */
+VC_API int vc_mamba_combine_fwd(int B, int L, int D, int ndir, const int* inv_order, const float* gate_logits,
+                                const float* y, float* ysum, hipStream_t stream);
+/* backward of scan + combine: du, ddt_lin (pre-softplus), dz per sequence position; the B/C
+ * columns of dxdbl (ld R+32); dA_log [D,16], dDskip [D], dgate_logits [ndir] (all overwritten) */
+VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
+                             const float* xz, const int* order, const float* dt_w, const float* dt_b,
+                             const float* A_log, const float* Dskip, const float* gate_logits,
+                             const float* dysum, float* du, float* ddt_lin, float* dz, float* dxdbl,
+                             float* dA_log, float* dDskip, float* dgate_logits, float* ws, long ws_floats,
+                             hipStream_t stream);
+/* backward of gather + conv1d + SiLU: du is turned into dpre in place; dxz [B*L, 2D] overwritten
+ * (both halves, summed over the directions); conv weight [D,1,4] / bias [D] grads overwritten */
+VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order, const int* inv_order,
+                                const float* xz, const float* conv_w, const float* conv_b, float* du,
+                                const float* dz, float* dxz, float* dconv_w, float* dconv_b, float* ws,
+                                long ws_floats, hipStream_t stream);
+
+/* ---------------------------------------------------------------- TokenLearner
+ * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64).  params: S x 5 floats
+ * [conv.0.weight(2), conv.0.bias, conv.1.weight, conv.1.bias]; bn_buffers: S x 2
+ * [running_mean, running_var]; stats: S x 2 [mean, invstd] saved for the backward;
+ * a: [B, S, HW] spatial weights.  The pooled tokens Z = a x / HW are a vc_gemm. */
+VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg,
+                             hipStream_t stream);
+VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
+                          float* bn_buffers, float eps, float momentum, float* stats, float* a, hipStream_t stream);
+VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
+                          const float* stats, const float* da, float* df, float* dparams, hipStream_t stream);
+/* dx[i,:] += d(avg)/C, dx[i, argmax] += d(max), summed over the S tokens (accumulates) */
+VC_API int vc_tl_pixel_bwd(long M, int C, int S, const float* df, const float* params, const int* amx, float* dx,
+                           long lddx, hipStream_t stream);
+
+/* ---------------------------------------------------------------- non-local cross attention
+ * NONLocalBlock2D core (Mutimodality_Mamba7.py:143-152): softmax(theta phi^T) g, no scaling.
+ * theta [B*S, Ci]; pooled [B*P, 2Ci] = maxpooled phi | g; att [B,S,P] saved; o [B*S, Ci]. */
+VC_API int vc_nonlocal_attn_fwd(int B, int S, int P, int Ci, const float* theta, const float* pooled, float* att,
+                                float* o, hipStream_t stream);
+VC_API int vc_nonlocal_attn_bwd(int B, int S, int P, int Ci, const float* theta, const float* pooled,
+                                const float* att, const float* dout, float* dtheta, float* dpooled,
+                                hipStream_t stream);
+
+/* ---------------------------------------------------------------- fusion glue, head, loss, optimiser */
+/* torch.concat((x1, x2), 1) with ChannelExchange (even channels swapped) when exchange=1
+ * (fusionBlock, Mutimodality_Mamba7.py:1133-1136; exchange semantics inferred) */
+VC_API int vc_cat2_fwd(long M, int C1, int C2, const float* x1, long ld1, const float* x2, long ld2, int exchange,
+                       float* out, hipStream_t stream);
+VC_API int vc_cat2_bwd(long M, int C1, int C2, const float* dout, int exchange, float* dx1, long ld1, float beta1,
+                       float* dx2, long ld2, float beta2, hipStream_t stream);
+/* GLfusionBlock (:1112-1115 with NonLocal's W_y + z, :155-156): out [M, 2C] =
+ * [ (BN(w_pre) + fc) + fl | fl + fc ] */
+VC_API int vc_glf_combine_fwd(long M, int C, const float* w_pre, const float* bn_mean, const float* bn_invstd,
+                              const float* bn_w, const float* bn_b, const float* fc, const float* fl, float* out,
+                              hipStream_t stream);
+/* out = beta*out + a (+ b) over [M, C] strided rows */
+VC_API int vc_add2_2d(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
+                      float beta, hipStream_t stream);
+/* avgpool(f1) + avgpool(f2) -> feat [B,C]; logits = feat W^T + bias (Mutimodality_Mamba7.py:1174-1178) */
+VC_API int vc_head_fwd(int B, int S1, int S2, int C, int ncls, const float* f1, const float* f2, const float* W,
+                       const float* bias, float* feat, float* logits, hipStream_t stream);
+VC_API int vc_head_bwd(int B, int S1, int S2, int C, int ncls, const float* dlogits, const float* W,
+                       const float* feat, float* df1, float* df2, float* dW, float* db, hipStream_t stream);
+/* nn.CrossEntropyLoss(weight) mean (model_utils.py:311): target int64, weight may be null */
+VC_API int vc_ce_fwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
+                     long long ignore_index, float* loss, hipStream_t stream);
+VC_API int vc_ce_bwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
+                     long long ignore_index, const float* grad_out, float* dlogits, hipStream_t stream);
+/* torch.optim.AdamW step (model_utils.py:309-310) over a flat buffer; hyper = device
+ * [lr, beta1, beta2, eps, weight_decay, grad_scale]; *step (device float) is incremented first */
+VC_API int vc_adamw(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                    const float* hyper, float* step, hipStream_t stream);
+/* ptr[idx[i]] += val  (BatchNorm num_batches_tracked counters) */
+VC_API int vc_index_add_i64(int n, const int* idx, long long* ptr, long long val, hipStream_t stream);
+/* dx = dy * (y > 0)  (nn.ReLU backward from the saved output) */
+VC_API int vc_relu_bwd(long n, const float* dy, const float* y, float* dx, hipStream_t stream);
+VC_API int vc_fill(long n, float* ptr, float value, hipStream_t stream);
+
+#endif /* VITCNN_H */

@@ -1,0 +1,350 @@
+// Fusion glue, classifier head, weighted cross-entropy, fused AdamW and small utilities.
+//
+//   vc_cat2_*            torch.concat((x1, x2), 1) of fusionBlock with the (inferred)
+//                        ChannelExchange folded into the copy (Mutimodality_Mamba7.py:1133-1136)
+//   vc_glf_combine_*     GLfusionBlock: localf = (BN(W o) + z) + x2, globalf = x2 + x1,
+//                        cat(localf, globalf) (:154-156, :1112-1115)
+//   vc_head_*            AdaptiveAvgPool2d(1) of both fusion maps, add, Linear(128 -> ncls) (:1174-1178)
+//   vc_ce_*              nn.CrossEntropyLoss(weight) mean reduction (model_utils.py:311, :922)
+//   vc_adamw             torch.optim.AdamW step over the flat parameter buffer (model_utils.py:309-310)
+#include "common.h"
+
+namespace {
+
+__global__ void cat2_fwd(long M, int C1, int C2, const float* __restrict__ x1, long ld1, const float* __restrict__ x2,
+                         long ld2, int exchange, float* __restrict__ out) {
+  const int Ct = C1 + C2;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * Ct) return;
+  const long m = idx / Ct;
+  const int c = idx % Ct;
+  float v;
+  if (c < C1) v = (exchange && (c & 1) == 0) ? x2[m * ld2 + c] : x1[m * ld1 + c];
+  else {
+    const int c2 = c - C1;
+    v = (exchange && (c2 & 1) == 0) ? x1[m * ld1 + c2] : x2[m * ld2 + c2];
+  }
+  out[idx] = v;
+}
+
+__global__ void cat2_bwd(long M, int C1, int C2, const float* __restrict__ dout, int exchange, float* __restrict__ dx1,
+                         long ld1, float beta1, float* __restrict__ dx2, long ld2, float beta2) {
+  const int Cm = C1 > C2 ? C1 : C2;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * Cm) return;
+  const long m = idx / Cm;
+  const int c = idx % Cm;
+  const float* dr = dout + m * (C1 + C2);
+  const bool sw = exchange && (c & 1) == 0;
+  if (dx1 && c < C1) {
+    const float g = sw ? dr[C1 + c] : dr[c];
+    float* p = dx1 + m * ld1 + c;
+    *p = (beta1 != 0.f ? beta1 * *p : 0.f) + g;
+  }
+  if (dx2 && c < C2) {
+    const float g = sw ? dr[c] : dr[C1 + c];
+    float* p = dx2 + m * ld2 + c;
+    *p = (beta2 != 0.f ? beta2 * *p : 0.f) + g;
+  }
+}
+
+__global__ void glf_combine_fwd(long M, int C, const float* __restrict__ wpre, const float* __restrict__ mean,
+                                const float* __restrict__ invstd, const float* __restrict__ gam,
+                                const float* __restrict__ bet, const float* __restrict__ fc,
+                                const float* __restrict__ fl, float* __restrict__ out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * C) return;
+  const long m = idx / C;
+  const int c = idx % C;
+  const float wy = (wpre[idx] - mean[c]) * invstd[c] * gam[c] + bet[c];
+  const float z = fc[idx], x2 = fl[idx];
+  out[m * 2 * C + c] = (wy + z) + x2;
+  out[m * 2 * C + C + c] = x2 + z;
+}
+
+__global__ void add2_2d(long M, int C, const float* __restrict__ a, long lda, const float* __restrict__ b, long ldb,
+                        float* __restrict__ out, long ldo, float beta) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * C) return;
+  const long m = idx / C;
+  const int c = idx % C;
+  float v = a[m * lda + c];
+  if (b) v += b[m * ldb + c];
+  float* p = out + m * ldo + c;
+  *p = (beta != 0.f ? beta * *p : 0.f) + v;
+}
+
+// feat[b,c] = mean_p f1[b,p,c] + mean_q f2[b,q,c];  logits = feat W^T + bias   (block per b)
+__global__ __launch_bounds__(256) void head_fwd(int S1, int S2, int C, int ncls, const float* __restrict__ f1,
+                                                const float* __restrict__ f2, const float* __restrict__ W,
+                                                const float* __restrict__ bias, float* __restrict__ feat,
+                                                float* __restrict__ logits) {
+  extern __shared__ float fs[];
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int p = 0; p < S1; ++p) s1 += f1[((long)b * S1 + p) * C + c];
+    for (int q = 0; q < S2; ++q) s2 += f2[((long)b * S2 + q) * C + c];
+    const float v = s1 / (float)S1 + s2 / (float)S2;
+    fs[c] = v;
+    feat[(long)b * C + c] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = wave; k < ncls; k += 4) {
+    float acc = 0.f;
+    for (int c = lane; c < C; c += 64) acc += fs[c] * W[(long)k * C + c];
+    acc = wave_sum(acc);
+    if (lane == 0) logits[(long)b * ncls + k] = acc + bias[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void head_bwd_x(int S1, int S2, int C, int ncls, const float* __restrict__ dlog,
+                                                  const float* __restrict__ W, float* __restrict__ df1,
+                                                  float* __restrict__ df2) {
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float g = 0.f;
+    for (int k = 0; k < ncls; ++k) g += dlog[(long)b * ncls + k] * W[(long)k * C + c];
+    const float g1 = g / (float)S1, g2 = g / (float)S2;
+    for (int p = 0; p < S1; ++p) df1[((long)b * S1 + p) * C + c] = g1;
+    for (int q = 0; q < S2; ++q) df2[((long)b * S2 + q) * C + c] = g2;
+  }
+}
+
+__global__ void head_bwd_w(int B, int C, int ncls, const float* __restrict__ dlog, const float* __restrict__ feat,
+                           float* __restrict__ dW, float* __restrict__ db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncls * (C + 1)) return;
+  const int k = i / (C + 1), c = i % (C + 1);
+  float acc = 0.f;
+  if (c < C) {
+    for (int b = 0; b < B; ++b) acc += dlog[(long)b * ncls + k] * feat[(long)b * C + c];
+    dW[(long)k * C + c] = acc;
+  } else {
+    for (int b = 0; b < B; ++b) acc += dlog[(long)b * ncls + k];
+    db[k] = acc;
+  }
+}
+
+// loss = sum_b w[y_b] * (lse_b - logit[b, y_b]) / sum_b w[y_b]   (targets == ignore_index contribute 0)
+__global__ __launch_bounds__(256) void ce_fwd(int B, int ncls, const float* __restrict__ logits,
+                                              const long long* __restrict__ target, const float* __restrict__ w,
+                                              long long ignore_index, float* __restrict__ loss) {
+  __shared__ float r1[4], r2[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float num = 0.f, den = 0.f;
+  for (int b = wave; b < B; b += 4) {
+    const float* lr = logits + (long)b * ncls;
+    float mx = -INFINITY;
+    for (int k = lane; k < ncls; k += 64) mx = fmaxf(mx, lr[k]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int k = lane; k < ncls; k += 64) se += __expf(lr[k] - mx);
+    se = wave_sum(se);
+    const long long y = target[b];
+    if (lane == 0 && y != ignore_index) {
+      const float wy = w ? w[y] : 1.f;
+      num += wy * (logf(se) + mx - lr[y]);
+      den += wy;
+    }
+  }
+  num = wave_sum(num);
+  den = wave_sum(den);
+  if (lane == 0) {
+    r1[wave] = num;
+    r2[wave] = den;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = (r1[0] + r1[1] + r1[2] + r1[3]) / (r2[0] + r2[1] + r2[2] + r2[3]);
+}
+
+__global__ __launch_bounds__(256) void ce_bwd(int B, int ncls, const float* __restrict__ logits,
+                                              const long long* __restrict__ target, const float* __restrict__ w,
+                                              long long ignore_index, const float* __restrict__ gout,
+                                              float* __restrict__ dlogits) {
+  __shared__ float r2[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float den = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const long long y = target[b];
+    if (y != ignore_index) den += w ? w[y] : 1.f;
+  }
+  den = wave_sum(den);
+  if (lane == 0) r2[wave] = den;
+  __syncthreads();
+  den = r2[0] + r2[1] + r2[2] + r2[3];
+  const float g = (gout ? gout[0] : 1.f) / den;
+  for (int b = wave; b < B; b += 4) {
+    const float* lr = logits + (long)b * ncls;
+    float mx = -INFINITY;
+    for (int k = lane; k < ncls; k += 64) mx = fmaxf(mx, lr[k]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int k = lane; k < ncls; k += 64) se += __expf(lr[k] - mx);
+    se = wave_sum(se);
+    const long long y = target[b];
+    const float wy = (y == ignore_index) ? 0.f : (w ? w[y] : 1.f);
+    for (int k = lane; k < ncls; k += 64) {
+      const float p = __expf(lr[k] - mx) / se;
+      dlogits[(long)b * ncls + k] = g * wy * (p - (k == y ? 1.f : 0.f));
+    }
+  }
+}
+
+__global__ void step_inc(float* step) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) step[0] += 1.f;
+}
+
+// hyper = [lr, beta1, beta2, eps, weight_decay, grad_scale]; torch.optim.AdamW (amsgrad=False);
+// grad_scale folds the 1/world_size of a data-parallel gradient SUM into the update
+__global__ void adamw(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                      float* __restrict__ v, const float* __restrict__ hyper, const float* __restrict__ step) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const float t = step[0];
+  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+  const float gi = g[i] * hyper[5];
+  float pi = p[i] * (1.f - lr * wd);
+  const float mi = m[i] + (gi - m[i]) * (1.f - b1);
+  const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / sqrtf(bc2) + eps;
+  p[i] = pi - (lr / bc1) * (mi / denom);
+}
+
+__global__ void index_add_i64(int n, const int* __restrict__ idx, long long* __restrict__ ptr, long long val) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ptr[idx[i]] += val;
+}
+
+__global__ void relu_bwd(long n, const float* __restrict__ dy, const float* __restrict__ y, float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dx[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+
+__global__ void fill_f32(long n, float* __restrict__ p, float v) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+}  // namespace
+
+VC_API int vc_cat2_fwd(long M, int C1, int C2, const float* x1, long ld1, const float* x2, long ld2, int exchange,
+                       float* out, hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && C1 > 0 && C2 > 0 && (!exchange || C1 == C2));
+  if (M == 0) return VC_OK;
+  hipLaunchKernelGGL(cat2_fwd, dim3(vc_cdiv(M * (C1 + C2), 256)), dim3(256), 0, stream, M, C1, C2, x1, ld1, x2, ld2,
+                     exchange, out);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_cat2_bwd(long M, int C1, int C2, const float* dout, int exchange, float* dx1, long ld1, float beta1,
+                       float* dx2, long ld2, float beta2, hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && C1 > 0 && C2 > 0 && (!exchange || C1 == C2));
+  if (M == 0) return VC_OK;
+  const int Cm = C1 > C2 ? C1 : C2;
+  hipLaunchKernelGGL(cat2_bwd, dim3(vc_cdiv(M * Cm, 256)), dim3(256), 0, stream, M, C1, C2, dout, exchange, dx1, ld1,
+                     beta1, dx2, ld2, beta2);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_glf_combine_fwd(long M, int C, const float* w_pre, const float* bn_mean, const float* bn_invstd,
+                              const float* bn_w, const float* bn_b, const float* fc, const float* fl, float* out,
+                              hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && C > 0);
+  if (M == 0) return VC_OK;
+  hipLaunchKernelGGL(glf_combine_fwd, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, M, C, w_pre, bn_mean,
+                     bn_invstd, bn_w, bn_b, fc, fl, out);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// out = beta*out + a (+ b)
+VC_API int vc_add2_2d(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
+                      float beta, hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && C > 0);
+  if (M == 0) return VC_OK;
+  hipLaunchKernelGGL(add2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, M, C, a, lda, b, ldb, out, ldo, beta);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_head_fwd(int B, int S1, int S2, int C, int ncls, const float* f1, const float* f2, const float* W,
+                       const float* bias, float* feat, float* logits, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && S1 > 0 && S2 > 0 && C > 0 && ncls > 0);
+  hipLaunchKernelGGL(head_fwd, dim3(B), dim3(256), sizeof(float) * C, stream, S1, S2, C, ncls, f1, f2, W, bias, feat,
+                     logits);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_head_bwd(int B, int S1, int S2, int C, int ncls, const float* dlogits, const float* W, const float* feat,
+                       float* df1, float* df2, float* dW, float* db, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && S1 > 0 && S2 > 0 && C > 0 && ncls > 0);
+  hipLaunchKernelGGL(head_bwd_x, dim3(B), dim3(256), 0, stream, S1, S2, C, ncls, dlogits, W, df1, df2);
+  VC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(head_bwd_w, dim3(vc_cdiv(ncls * (C + 1), 256)), dim3(256), 0, stream, B, C, ncls, dlogits, feat,
+                     dW, db);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_ce_fwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
+                     long long ignore_index, float* loss, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && ncls > 0);
+  hipLaunchKernelGGL(ce_fwd, dim3(1), dim3(256), 0, stream, B, ncls, logits, target, weight, ignore_index, loss);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_ce_bwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
+                     long long ignore_index, const float* grad_out, float* dlogits, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && ncls > 0);
+  hipLaunchKernelGGL(ce_bwd, dim3(1), dim3(256), 0, stream, B, ncls, logits, target, weight, ignore_index, grad_out,
+                     dlogits);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// step += 1 on device, then one fused AdamW update over n elements (graph-replay safe: the
+// step count and hyper-parameters live in device memory)
+VC_API int vc_adamw(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, const float* hyper,
+                    float* step, hipStream_t stream) {
+  VC_REQUIRE(n >= 0);
+  hipLaunchKernelGGL(step_inc, dim3(1), dim3(64), 0, stream, step);
+  VC_CHECK_LAUNCH();
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(adamw, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, params, grads, exp_avg, exp_avg_sq, hyper,
+                     step);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_index_add_i64(int n, const int* idx, long long* ptr, long long val, hipStream_t stream) {
+  VC_REQUIRE(n >= 0);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(index_add_i64, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, idx, ptr, val);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_relu_bwd(long n, const float* dy, const float* y, float* dx, hipStream_t stream) {
+  VC_REQUIRE(n >= 0);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(relu_bwd, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, dy, y, dx);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_fill(long n, float* ptr, float value, hipStream_t stream) {
+  VC_REQUIRE(n >= 0);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(fill_f32, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, ptr, value);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}

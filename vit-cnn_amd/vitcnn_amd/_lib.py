@@ -1,0 +1,96 @@
+"""ctypes binding of libvitcnn_hip.so (the C ABI in include/vitcnn.h).
+
+The argument types of every entry point are read from the header itself, so the Python
+side can never drift from the C declarations.  There is no fallback: if the library is
+missing or a symbol is absent, importing the product path raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VITCNN_LIB", os.path.join(_PKG, "libvitcnn_hip.so"))
+_HEADER_CANDIDATES = [
+    os.path.join(_PKG, "..", "..", "include", "vitcnn.h"),
+    os.path.join(_PKG, "vitcnn.h"),
+]
+
+_TYPE_MAP = {
+    "long long": ctypes.c_longlong,
+    "int": ctypes.c_int,
+    "long": ctypes.c_long,
+    "float": ctypes.c_float,
+    "size_t": ctypes.c_size_t,
+    "hipStream_t": ctypes.c_void_p,
+}
+
+
+def header_path() -> str:
+    for p in _HEADER_CANDIDATES:
+        if os.path.exists(p):
+            return os.path.abspath(p)
+    raise RuntimeError("vitcnn.h not found next to the package (include/vitcnn.h)")
+
+
+def parse_header(path: str | None = None):
+    """{name: [ctypes arg types]} for every `VC_API int vc_*(...)` declaration."""
+    text = open(path or header_path()).read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"VC_API\s+int\s+(vc_\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+        name, args = m.group(1), m.group(2)
+        types = []
+        for a in args.split(","):
+            a = " ".join(a.split())
+            if not a or a == "void":
+                continue
+            if "*" in a:
+                types.append(ctypes.c_void_p)
+                continue
+            base = a.rsplit(" ", 1)[0].replace("const ", "").strip()
+            if base not in _TYPE_MAP:
+                raise RuntimeError(f"vitcnn.h: unsupported argument type '{a}' in {name}")
+            types.append(_TYPE_MAP[base])
+        out[name] = types
+    return out
+
+
+class _Lib:
+    def __init__(self):
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"HIP extension not built: {LIB_PATH} is missing (run `make -C vit-cnn_amd/csrc` "
+                "or __graft_entry__.build()); there is no CPU fallback")
+        self.handle = ctypes.CDLL(LIB_PATH)
+        self.sigs = parse_header()
+        self.raw = {}
+        for name, types in self.sigs.items():
+            fn = getattr(self.handle, name)  # AttributeError -> symbol missing: fail loudly
+            fn.argtypes = types
+            fn.restype = ctypes.c_int
+            self.raw[name] = fn
+            setattr(self, name, self._checked(name, fn))
+
+    @staticmethod
+    def _checked(name, fn):
+        def call(*args):
+            rc = fn(*args)
+            if rc != 0:
+                raise RuntimeError(f"{name} failed with code {rc} "
+                                   f"({'invalid shape/argument' if rc == 1 else 'HIP launch error'})")
+            return rc
+
+        call.__name__ = name
+        return call
+
+
+_LIB = None
+
+
+def lib() -> _Lib:
+    global _LIB
+    if _LIB is None:
+        _LIB = _Lib()
+    return _LIB

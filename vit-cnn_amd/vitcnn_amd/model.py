@@ -1,0 +1,665 @@
+"""ViT-CNN ("Multimodality_Mamba") on MI355X: flat parameter storage + HIP forward/backward programs.
+
+Drop-in for the reference module `Multimodality_Mamba`
+(`/root/reference/model/Multimodality_Mamba/Mutimodality_Mamba7.py:1141-1181`):
+same constructor signature, same state_dict (1704 keys, `layers.py`), same
+`forward(hsi[B,C1,P,P], lidar[B,C2,P,P]) -> logits[B,ncls]` contract, train/eval BatchNorm
+semantics, `.to(device)`, `parameters()`, `load_state_dict()`.
+
+MI355X-first design:
+  * all parameters live in ONE flat fp32 buffer (nn.Parameters are views of it), BN running
+    stats in one flat fp32 buffer, `num_batches_tracked` in one int64 buffer.  Gradients come
+    back as one flat tensor (`model.flat_params.grad`), so AdamW is one kernel and the data-
+    parallel all-reduce is one RCCL call;
+  * activations are channels-last `[rows, C]` in a per-batch-size workspace whose addresses
+    never change, so a whole training step can be captured into a hipGraph;
+  * every op runs in a hand-written gfx950 kernel of libvitcnn_hip.so (C ABI, include/vitcnn.h);
+    there is no CPU path: a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import math
+import weakref
+from typing import Dict
+
+import torch
+import torch.nn as nn
+
+from ._lib import lib
+from .layers import ConvBnReluParams, FusionParams, GlobalLocalParams
+from .scan_orders import scan_orders
+
+F32 = 4
+LN_EPS = 1e-6
+BN_EPS = 1e-5
+BN_MOM = 0.1
+NDIR = 10
+
+UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
+                   "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
+
+
+class _Workspace:
+    """Named, persistent device buffers for one (device, batch, mode) — stable addresses."""
+
+    def __init__(self, device):
+        self.device = device
+        self.t: Dict[str, torch.Tensor] = {}
+        self.generation = 0
+
+    def get(self, name, numel, dtype=torch.float32):
+        t = self.t.get(name)
+        if t is None or t.numel() != numel or t.dtype != dtype:
+            t = torch.empty(max(int(numel), 1), dtype=dtype, device=self.device)
+            self.t[name] = t
+        return t
+
+    def f(self, name, numel):
+        return self.get(name, numel).data_ptr()
+
+    def tensor(self, name):
+        return self.t[name]
+
+
+class Multimodality_Mamba(nn.Module):
+    """ViT-CNN (ours).  Signature of Mutimodality_Mamba7.py:1142; like the reference, `patch_size`,
+    `stride`, `dim_embedding` and `path_type` are accepted and ignored.  `img_size` is the patch
+    side P (the reference hard-codes 9; other P follow the documented generalisation of
+    SURVEY.md section 8 row A-MUUFL)."""
+
+    def __init__(self, img_size=9, patch_size=1, stride=1, in_channels1=144, in_channels2=1, dim_embedding=32,
+                 num_class=16, path_type="multi_clock_gate"):
+        super().__init__()
+        P = int(img_size)
+        if P < 7:
+            raise ValueError("ViT-CNN needs patches of at least 7x7 (two valid 3x3 stages + 2x2 pooling)")
+        self.patch, self.c1, self.c2, self.ncls = P, int(in_channels1), int(in_channels2), int(num_class)
+        self.embedding_dim = dim_embedding
+        plane_hsi = [self.c1, 256, self.c1]
+        plane_lidar = [self.c2, 16, 32]
+        self.hsi1 = GlobalLocalParams(P, plane_hsi[0], plane_hsi[1], 144)
+        self.hsi2 = GlobalLocalParams(P - 2, plane_hsi[1], plane_hsi[2], 256)
+        self.lidar1 = ConvBnReluParams(plane_lidar[0], plane_lidar[1])
+        self.lidar2 = ConvBnReluParams(plane_lidar[1], plane_lidar[2])
+        self.fusion1 = FusionParams(plane_hsi[1], plane_lidar[1], 128)
+        self.fusion2 = FusionParams(plane_hsi[2], plane_lidar[2], 128)
+        self.avg = nn.AdaptiveAvgPool2d(1)
+        self.classifier = nn.Linear(128, self.ncls)
+        self._build_flat()
+        self._ws: Dict[tuple, _Workspace] = {}
+        self._dev_cache: Dict[str, object] = {}
+
+    # ------------------------------------------------------------------ flat storage
+    def _build_flat(self):
+        named = list(nn.Module.named_parameters(self))
+        active = [(n, p) for n, p in named if not n.startswith(UNUSED_PREFIXES)]
+        unused = [(n, p) for n, p in named if n.startswith(UNUSED_PREFIXES)]
+        self._poff: Dict[str, int] = {}
+        off = 0
+        for n, p in active + unused:
+            self._poff[n] = off
+            off += p.numel()
+        self._n_active = sum(p.numel() for _, p in active)
+        self._n_params = off
+        device = named[0][1].device
+        flat = torch.empty(off, dtype=torch.float32, device=device)
+        for n, p in named:
+            flat[self._poff[n]:self._poff[n] + p.numel()].copy_(p.detach().reshape(-1))
+        self._pnames = [n for n, _ in active + unused]
+        self._pmods = {}
+        for mn, m in nn.Module.named_modules(self):
+            for pn in m._parameters:
+                self._pmods[(mn + "." if mn else "") + pn] = (m, pn)
+        # float buffers (BN running stats) and int64 counters
+        self._boff, self._ioff = {}, {}
+        fb, ib = [], []
+        self._bmods = {}
+        for mn, m in nn.Module.named_modules(self):
+            for bn, b in m._buffers.items():
+                if b is None:
+                    continue
+                full = (mn + "." if mn else "") + bn
+                self._bmods[full] = (m, bn)
+                (fb if b.is_floating_point() else ib).append((full, b))
+        o = 0
+        for n, b in fb:
+            self._boff[n] = o
+            o += b.numel()
+        bflat = torch.empty(max(o, 1), dtype=torch.float32, device=device)
+        for n, b in fb:
+            bflat[self._boff[n]:self._boff[n] + b.numel()].copy_(b.reshape(-1))
+        o = 0
+        for n, b in ib:
+            self._ioff[n] = o
+            o += b.numel()
+        iflat = torch.zeros(max(o, 1), dtype=torch.int64, device=device)
+        for n, b in ib:
+            iflat[self._ioff[n]:self._ioff[n] + b.numel()].copy_(b.reshape(-1))
+        self._bshape = {n: tuple(b.shape) for n, b in fb + ib}
+        # counters that a training forward increments: every BN the forward actually runs
+        self._tracked = [self._ioff[n] for n, _ in ib if not n.startswith(UNUSED_PREFIXES)]
+        self._rebind(flat, bflat, iflat)
+        me = weakref.ref(self)
+        for _, p in named:
+            p._vc_owner = me
+
+    def _rebind(self, flat, bflat, iflat):
+        object.__setattr__(self, "_flat_store", flat.detach().requires_grad_(True))
+        object.__setattr__(self, "_bflat", bflat)
+        object.__setattr__(self, "_iflat", iflat)
+        base = self._flat_store.detach()
+        for n in self._pnames:
+            m, pn = self._pmods[n]
+            p = m._parameters[pn]
+            o = self._poff[n]
+            p.data = base[o:o + p.numel()].view(p.shape)
+        for n, (m, bn) in self._bmods.items():
+            shape = self._bshape[n]
+            numel = int(math.prod(shape)) if shape else 1
+            if n in self._boff:
+                o = self._boff[n]
+                m._buffers[bn] = bflat[o:o + numel].view(shape)
+            else:
+                o = self._ioff[n]
+                m._buffers[bn] = iflat[o:o + numel].view(shape)
+        self._ptr_cache = None
+        self._ws = {}
+        self._dev_cache = {}
+
+    def _flat_intact(self):
+        base = self._flat_store.data_ptr()
+        for n in (self._pnames[0], self._pnames[-1]):
+            m, pn = self._pmods[n]
+            if m._parameters[pn].data_ptr() != base + F32 * self._poff[n]:
+                return False
+        return True
+
+    def _ensure_flat(self):
+        if not self._flat_intact():  # e.g. parameters replaced by user code: re-flatten current values
+            dev = self._flat_store.device
+            flat = torch.empty(self._n_params, dtype=torch.float32, device=dev)
+            for n in self._pnames:
+                m, pn = self._pmods[n]
+                o = self._poff[n]
+                flat[o:o + m._parameters[pn].numel()].copy_(m._parameters[pn].detach().reshape(-1))
+            self._rebind(flat, self._bflat, self._iflat)
+
+    def _apply(self, fn, recurse=True):
+        flat = fn(self._flat_store.detach())
+        if flat.dtype != torch.float32:
+            raise RuntimeError("ViT-CNN MI355X path computes in fp32 master weights; dtype casts are not supported")
+        self._rebind(flat, fn(self._bflat), fn(self._iflat))
+        return self
+
+    @property
+    def flat_params(self) -> torch.Tensor:
+        """The single fp32 parameter tensor; after backward its .grad holds every gradient."""
+        return self._flat_store
+
+    @property
+    def n_active_params(self) -> int:
+        """Leading elements of flat_params that receive gradients (the rest are the unused
+        hsiMamba.tokenlearner / ln3 parameters the reference never calls)."""
+        return self._n_active
+
+    def zero_grad(self, set_to_none: bool = True):
+        super().zero_grad(set_to_none=set_to_none)
+        if set_to_none:
+            self._flat_store.grad = None
+        elif self._flat_store.grad is not None:
+            self._flat_store.grad.zero_()
+
+    # ------------------------------------------------------------------ device caches
+    def _ptrs(self):
+        base = self._flat_store.data_ptr()
+        if self._ptr_cache is None or self._ptr_cache[0] != base:
+            bb, ib = self._bflat.data_ptr(), self._iflat.data_ptr()
+            p = {n: base + F32 * o for n, o in self._poff.items()}
+            b = {n: bb + F32 * o for n, o in self._boff.items()}
+            self._ptr_cache = (base, p, b, ib)
+        return self._ptr_cache
+
+    def _device_tables(self, device):
+        key = str(device)
+        t = self._dev_cache.get(key)
+        if t is None:
+            t = {}
+            for H in (self.patch, self.patch - 2):
+                orders = scan_orders(H)
+                inv = [[0] * len(o) for o in orders]
+                for k, o in enumerate(orders):
+                    for pos, tok in enumerate(o):
+                        inv[k][tok] = pos
+                t[("order", H)] = torch.tensor(orders, dtype=torch.int32, device=device).contiguous()
+                t[("inv", H)] = torch.tensor(inv, dtype=torch.int32, device=device).contiguous()
+            t["tracked"] = torch.tensor(self._tracked, dtype=torch.int32, device=device)
+            self._dev_cache[key] = t
+        return t
+
+    def _workspace(self, device, B, mode):
+        key = (str(device), int(B), mode)
+        ws = self._ws.get(key)
+        if ws is None:
+            ws = _Workspace(device)
+            self._ws[key] = ws
+        return ws
+
+    def _scratch(self, device, B):
+        need = self._scratch_floats(B)
+        key = "scratch"
+        t = self._dev_cache.get(str(device), {}).get(key)
+        if t is None or t.numel() < need:
+            t = torch.empty(need, dtype=torch.float32, device=device)
+            self._device_tables(device)[key] = t
+        return t
+
+    def _scratch_floats(self, B):
+        need = 1 << 22
+        for blk in (self.hsi1, self.hsi2):
+            L = blk.img * blk.img
+            D = blk.embed // 2
+            nseq = NDIR * B
+            nchunk = -(-D // 16)
+            need = max(need, nchunk * nseq * L * 32 + nseq * D * 16 + nseq * D + nseq * nchunk + (1 << 20))
+        return int(need)
+
+    # ------------------------------------------------------------------ nn.Module API
+    def forward(self, hsi: torch.Tensor, lidar: torch.Tensor) -> torch.Tensor:
+        if hsi.device.type != "cuda":
+            raise RuntimeError("ViT-CNN MI355X path: inputs must be on a ROCm (cuda) device; no CPU fallback")
+        if hsi.dim() != 4 or hsi.shape[1] != self.c1 or hsi.shape[2] != self.patch or hsi.shape[3] != self.patch:
+            raise RuntimeError(f"expected hsi [B, {self.c1}, {self.patch}, {self.patch}], got {list(hsi.shape)}")
+        if lidar.dim() != 4 or lidar.shape[0] != hsi.shape[0] or lidar.shape[1] != self.c2 or \
+                lidar.shape[2] != self.patch or lidar.shape[3] != self.patch:
+            raise RuntimeError(f"expected lidar [B, {self.c2}, {self.patch}, {self.patch}], got {list(lidar.shape)}")
+        self._ensure_flat()
+        if self._flat_store.device != hsi.device:
+            raise RuntimeError("model and inputs are on different devices")
+        hsi = hsi.detach().to(torch.float32).contiguous()
+        lidar = lidar.detach().to(torch.float32).contiguous()
+        needs_grad = torch.is_grad_enabled() and self._flat_store.requires_grad
+        return _VitCnnFunction.apply(self, hsi, lidar, self._flat_store, needs_grad)
+
+
+class _VitCnnFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, hsi, lidar, flat, needs_grad):
+        prog = _Program(model, hsi.device, hsi.shape[0], model.training, "grad" if needs_grad else "nograd")
+        logits = prog.forward(hsi, lidar)
+        ctx.prog = prog
+        ctx.gen = prog.ws.generation
+        ctx.model = model
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        prog = ctx.prog
+        if prog.ws.generation != ctx.gen:
+            raise RuntimeError("ViT-CNN MI355X path: another training forward of the same batch size overwrote "
+                               "the saved activations before this backward; call backward before the next forward")
+        grad = prog.backward(dlogits.detach().to(torch.float32).contiguous())
+        return None, None, None, grad, None
+
+
+class _Program:
+    """The forward / backward launch sequence of one training step (channels-last activations)."""
+
+    def __init__(self, model: Multimodality_Mamba, device, B, train, mode):
+        self.m = model
+        self.L = lib()
+        self.B = int(B)
+        self.train = 1 if train else 0
+        self.ws = model._workspace(device, B, ("train" if train else "eval", mode))
+        self.tab = model._device_tables(device)
+        self.scr = model._scratch(device, B)
+        self.scr_p, self.scr_n = self.scr.data_ptr(), self.scr.numel()
+        _, self.P, self.BUF, self.I64 = model._ptrs()
+        self.s = torch.cuda.current_stream(device).cuda_stream
+        self.device = device
+
+    # ---------------------------------------------------------------- gemm wrappers
+    def mm_nt(self, M, N, K, A, lda, W, ldw, C, ldc, bias=0, alpha=1.0, beta=0.0, add=0, add_ld=0, add_mod=0,
+              relu=0):
+        """C[M,N] = alpha * A[M,K] W[N,K]^T + beta*C + bias + addend"""
+        self.L.vc_gemm(0, 1, M, N, K, alpha, A, lda, 0, W, ldw, 0, beta, C, ldc, 0, 1, bias or None, add or None,
+                       add_ld, add_mod, relu, self.scr_p, self.scr_n, self.s)
+
+    def mm_nn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0):
+        """C[M,N] = alpha * A[M,K] B[K,N] + beta*C"""
+        self.L.vc_gemm(0, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
+                       self.scr_p, self.scr_n, self.s)
+
+    def mm_tn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0):
+        """C[M,N] = alpha * A^T B, A stored [K, M] (weight gradients: M,N small, K = rows)"""
+        self.L.vc_gemm(1, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
+                       self.scr_p, self.scr_n, self.s)
+
+    def colsum(self, R, C, X, ldx, out, beta=0.0):
+        self.L.vc_colsum(R, C, X, ldx, out, beta, self.scr_p, self.scr_n, self.s)
+
+    # ---------------------------------------------------------------- building blocks (forward)
+    def bn_stats(self, pfx, X, ldx, M, C, tag):
+        ws = self.ws
+        mean, inv = ws.f(tag + ".bm", C), ws.f(tag + ".bi", C)
+        self.L.vc_bn_stats(self.train, M, C, X, ldx, BN_EPS, BN_MOM, mean, inv, self.BUF[pfx + ".running_mean"],
+                           self.BUF[pfx + ".running_var"], self.scr_p, self.scr_n, self.s)
+        return mean, inv
+
+    def layernorm(self, pfx, X, R, C, tag):
+        ws = self.ws
+        Y, mu, rs = ws.f(tag, R * C), ws.f(tag + ".m", R), ws.f(tag + ".r", R)
+        self.L.vc_layernorm_fwd(R, C, X, C, self.P[pfx + ".weight"], self.P[pfx + ".bias"], LN_EPS, Y, C, mu, rs,
+                                self.s)
+        return Y
+
+    def conv_bn_relu3(self, pfx, X, H, Cin, Cout):
+        """ms_conv_bn_relu: BN(X) -> conv3x3 valid (+bias) -> ReLU."""
+        B, S = self.B, (H - 2) * (H - 2)
+        mean, inv = self.bn_stats(pfx + ".bn", X, Cin, B * H * H, Cin, pfx + ".bn")
+        col = self.ws.f(pfx + ".col", B * S * 9 * Cin)
+        self.L.vc_im2col3x3(B, H, H, Cin, X, mean, inv, self.P[pfx + ".bn.weight"], self.P[pfx + ".bn.bias"], col,
+                            self.s)
+        out = self.ws.f(pfx + ".out", B * S * Cout)
+        self.mm_nt(B * S, Cout, 9 * Cin, col, 9 * Cin, self.P[pfx + ".conv.weight"], 9 * Cin, out, Cout,
+                   bias=self.P[pfx + ".conv.bias"], relu=1)
+        return out
+
+    def conv1x1_bn_relu(self, seq, X, M, Cin, Cout):
+        """Sequential(Conv2d 1x1, BatchNorm2d, ReLU) (FusionLayer of GLfusionBlock / fusionBlock)."""
+        pre = self.ws.f(seq + ".pre", M * Cout)
+        self.mm_nt(M, Cout, Cin, X, Cin, self.P[seq + ".0.weight"], Cin, pre, Cout, bias=self.P[seq + ".0.bias"])
+        mean, inv = self.bn_stats(seq + ".1", pre, Cout, M, Cout, seq + ".1")
+        out = self.ws.f(seq + ".out", M * Cout)
+        self.L.vc_bn_apply(M, Cout, pre, Cout, mean, inv, self.P[seq + ".1.weight"], self.P[seq + ".1.bias"], 1, out,
+                           Cout, self.s)
+        return out
+
+    def fusion(self, pfx, X1, C1, X2, C2, M, Cout):
+        cat = self.ws.f(pfx + ".cat", M * (C1 + C2))
+        self.L.vc_cat2_fwd(M, C1, C2, X1, C1, X2, C2, 1 if C1 == C2 else 0, cat, self.s)
+        return self.conv1x1_bn_relu(pfx + ".FusionLayer", cat, M, C1 + C2, Cout)
+
+    def token_learner(self, pfx, X, L_, C, S):
+        B, ws = self.B, self.ws
+        rows = B * L_
+        mx, amx, avg = ws.f(pfx + ".mx", rows), ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), ws.f(pfx + ".avg",
+                                                                                                           rows)
+        self.L.vc_tl_pixel_stats(rows, C, X, C, mx, amx, avg, self.s)
+        st, a = ws.f(pfx + ".st", 2 * S), ws.f(pfx + ".a", B * S * L_)
+        self.L.vc_tl_attn_fwd(self.train, B, L_, S, mx, avg, self.P[pfx + ".tokenizers.0.conv.0.weight"],
+                              self.BUF[pfx + ".tokenizers.0.conv.1.running_mean"], BN_EPS, BN_MOM, st, a, self.s)
+        Z = ws.f(pfx + ".Z", B * S * C)
+        self.L.vc_gemm(0, 0, S, C, L_, 1.0 / L_, a, L_, S * L_, X, C, L_ * C, 0.0, Z, C, S * C, B, None, None, 0, 0, 0,
+                       self.scr_p, self.scr_n, self.s)
+        return Z
+
+    def block(self, blk, pfx, X, H):
+        B, ws, P = self.B, self.ws, self.P
+        Cin, Cout, E = blk.cin, blk.cout, blk.embed
+        D, R = E // 2, math.ceil(E / 16)
+        XW = R + 32
+        L_, Hs = H * H, H - 2
+        S, Ci, Pk = Hs * Hs, Cout // 2, (Hs // 2) * (Hs // 2)
+        rows = B * L_
+        gv, mx = pfx + ".global_view", pfx + ".global_view.layers.0"
+        order, inv = self.tab[("order", H)].data_ptr(), self.tab[("inv", H)].data_ptr()
+        # --- hsiMamba global view (Mutimodality_Mamba7.py:419-701, :983-1017)
+        T = ws.f(pfx + ".T", rows * E)
+        self.mm_nt(rows, E, Cin, X, Cin, P[gv + ".patch_embed.projection.weight"], Cin, T, E,
+                   add=P[gv + ".pos_embed"], add_ld=E, add_mod=L_)
+        Xn = self.layernorm(gv + ".pre_norm", T, rows, E, pfx + ".Xn")
+        XZ = ws.f(pfx + ".XZ", rows * 2 * D)
+        self.mm_nt(rows, 2 * D, E, Xn, E, P[mx + ".in_proj.weight"], E, XZ, 2 * D)
+        U = ws.f(pfx + ".U", NDIR * rows * D)
+        self.L.vc_mamba_dirconv_fwd(B, L_, D, NDIR, order, XZ, P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"], U,
+                                    self.s)
+        XD = ws.f(pfx + ".XD", NDIR * rows * XW)
+        self.mm_nt(NDIR * rows, XW, D, U, D, P[mx + ".x_proj.weight"], D, XD, XW)
+        Y = ws.f(pfx + ".Y", NDIR * rows * D)
+        self.L.vc_mamba_scan_fwd(B, L_, D, R, NDIR, U, XD, XZ, order, P[mx + ".dt_proj.weight"],
+                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], Y, self.s)
+        YS = ws.f(pfx + ".YS", rows * D)
+        self.L.vc_mamba_combine_fwd(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, YS, self.s)
+        T2 = ws.f(pfx + ".T2", rows * E)
+        self.mm_nt(rows, E, D, YS, D, P[mx + ".out_proj.weight"], D, T2, E, add=T, add_ld=E, add_mod=rows)
+        G = self.layernorm(gv + ".ln1", T2, rows, E, pfx + ".G")
+        # --- global feature: change_dim -> TokenLearner -> ln3
+        CD = ws.f(pfx + ".CD", rows * Cout)
+        self.mm_nt(rows, Cout, E, G, E, P[pfx + ".change_dim.weight"], E, CD, Cout, bias=P[pfx + ".change_dim.bias"])
+        Zg = self.token_learner(pfx + ".global_feature", CD, L_, Cout, S)
+        Fg = self.layernorm(pfx + ".ln3", Zg, B * S, Cout, pfx + ".Fg")
+        # --- local feature: BN -> conv3x3 -> ReLU
+        Fl = self.conv_bn_relu3(pfx + ".local_feature", X, H, Cin, Cout)
+        # --- channel feature: conv1x1 -> TokenLearner -> ln4
+        CF = ws.f(pfx + ".CF", rows * Cout)
+        self.mm_nt(rows, Cout, Cin, X, Cin, P[pfx + ".channel_feature.weight"], Cin, CF, Cout,
+                   bias=P[pfx + ".channel_feature.bias"])
+        Zc = self.token_learner(pfx + ".channel_token", CF, L_, Cout, S)
+        Fc = self.layernorm(pfx + ".ln4", Zc, B * S, Cout, pfx + ".Fc")
+        # --- GLfusionBlock(x1 = channel, x2 = local): non-local cross attention (:140-159, :1107-1117)
+        nl = pfx + ".FusionLayer.cross_attention"
+        M = B * S
+        TH = ws.f(pfx + ".TH", M * Ci)
+        self.mm_nt(M, Ci, Cout, Fl, Cout, P[nl + ".theta.weight"], Cout, TH, Ci, bias=P[nl + ".theta.bias"])
+        PG = ws.f(pfx + ".PG", M * 2 * Ci)
+        self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, PG, 2 * Ci, bias=P[nl + ".phi.0.bias"])
+        self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".g.0.weight"], Cout, PG + F32 * Ci, 2 * Ci, bias=P[nl + ".g.0.bias"])
+        PP = ws.f(pfx + ".PP", B * Pk * 2 * Ci)
+        PA = ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr()
+        self.L.vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, PG, 2 * Ci, PP, PA, self.s)
+        ATT, O = ws.f(pfx + ".ATT", M * Pk), ws.f(pfx + ".O", M * Ci)
+        self.L.vc_nonlocal_attn_fwd(B, S, Pk, Ci, TH, PP, ATT, O, self.s)
+        WP = ws.f(pfx + ".WP", M * Cout)
+        self.mm_nt(M, Cout, Ci, O, Ci, P[nl + ".W.0.weight"], Ci, WP, Cout, bias=P[nl + ".W.0.bias"])
+        wm, wi = self.bn_stats(nl + ".W.1", WP, Cout, M, Cout, pfx + ".W1")
+        CAT1 = ws.f(pfx + ".CAT1", M * 2 * Cout)
+        self.L.vc_glf_combine_fwd(M, Cout, WP, wm, wi, P[nl + ".W.1.weight"], P[nl + ".W.1.bias"], Fc, Fl, CAT1,
+                                  self.s)
+        FM = self.conv1x1_bn_relu(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout)
+        # --- fusionBlock(global, fused) with ChannelExchange
+        return self.fusion(pfx + ".fusion", Fg, Cout, FM, Cout, M, Cout)
+
+    def forward(self, hsi, lidar):
+        m, B, ws = self.m, self.B, self.ws
+        ws.generation += 1
+        Pp = m.patch
+        X0 = ws.f("x0", B * Pp * Pp * m.c1)
+        self.L.vc_nchw_to_nhwc(B, m.c1, Pp * Pp, hsi.data_ptr(), X0, self.s)
+        if m.c2 == 1:
+            ws.t["lidar_in"] = lidar  # keep alive for the backward
+            LX = lidar.data_ptr()
+        else:
+            LX = ws.f("lx0", B * Pp * Pp * m.c2)
+            self.L.vc_nchw_to_nhwc(B, m.c2, Pp * Pp, lidar.data_ptr(), LX, self.s)
+        ws.t["hsi_in"] = hsi
+        self.X0, self.LX = X0, LX
+        H1 = self.block(m.hsi1, "hsi1", X0, Pp)
+        H2 = self.block(m.hsi2, "hsi2", H1, Pp - 2)
+        L1 = self.conv_bn_relu3("lidar1", LX, Pp, m.c2, 16)
+        L2 = self.conv_bn_relu3("lidar2", L1, Pp - 2, 16, 32)
+        S1, S2 = (Pp - 2) ** 2, (Pp - 4) ** 2
+        F1 = self.fusion("fusion1", H1, m.hsi1.cout, L1, 16, B * S1, 128)
+        F2 = self.fusion("fusion2", H2, m.hsi2.cout, L2, 32, B * S2, 128)
+        logits = torch.empty(B, m.ncls, dtype=torch.float32, device=self.device)
+        feat = ws.f("feat", B * 128)
+        self.L.vc_head_fwd(B, S1, S2, 128, m.ncls, F1, F2, self.P["classifier.weight"], self.P["classifier.bias"],
+                           feat, logits.data_ptr(), self.s)
+        if self.train:
+            tr = self.tab["tracked"]
+            self.L.vc_index_add_i64(tr.numel(), tr.data_ptr(), self.I64, 1, self.s)
+        self.H1, self.H2, self.L1, self.L2, self.F1, self.F2, self.feat = H1, H2, L1, L2, F1, F2, feat
+        return logits
+
+    # ---------------------------------------------------------------- backward
+    def bn_bwd(self, pfx, tag, dY, lddy, X, ldx, relu_out, M, C, dX, lddx, beta_dx):
+        ws = self.ws
+        self.L.vc_bn_bwd(self.train, M, C, dY, lddy, X, ldx, relu_out or None, C, ws.f(tag + ".bm", C),
+                         ws.f(tag + ".bi", C), self.P[pfx + ".weight"], dX or None, lddx, beta_dx,
+                         self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n, self.s)
+
+    def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx):
+        ws = self.ws
+        self.L.vc_layernorm_bwd(R, C, dY, C, X, C, self.P[pfx + ".weight"], ws.f(tag + ".m", R), ws.f(tag + ".r", R),
+                                dX, C, beta_dx, self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p,
+                                self.scr_n, self.s)
+
+    def linear_bwd(self, wname, bname, dY, M, N, K, X, ldx, dX, beta_dx, lddy=None):
+        """Y[M,N] = X[M,K] W[N,K]^T + b:  dW = dY^T X, db = colsum(dY), dX (+)= dY W."""
+        lddy = lddy or N
+        self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K)
+        if bname:
+            self.colsum(M, N, dY, lddy, self.G[bname])
+        if dX:
+            self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
+
+    def conv1x1_bn_relu_bwd(self, seq, X, M, Cin, Cout, dOut, dX, beta_dx):
+        ws = self.ws
+        pre, out = ws.f(seq + ".pre", M * Cout), ws.f(seq + ".out", M * Cout)
+        dpre = ws.f(seq + ".dpre", M * Cout)
+        self.bn_bwd(seq + ".1", seq + ".1", dOut, Cout, pre, Cout, out, M, Cout, dpre, Cout, 0.0)
+        self.linear_bwd(seq + ".0.weight", seq + ".0.bias", dpre, M, Cout, Cin, X, Cin, dX, beta_dx)
+
+    def fusion_bwd(self, pfx, X1, C1, X2, C2, M, Cout, dOut, dX1, beta1, dX2, beta2):
+        ws = self.ws
+        cat = ws.f(pfx + ".cat", M * (C1 + C2))
+        dcat = ws.f(pfx + ".dcat", M * (C1 + C2))
+        self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer", cat, M, C1 + C2, Cout, dOut, dcat, 0.0)
+        self.L.vc_cat2_bwd(M, C1, C2, dcat, 1 if C1 == C2 else 0, dX1 or None, C1, beta1, dX2 or None, C2, beta2,
+                           self.s)
+
+    def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx):
+        B, ws = self.B, self.ws
+        S = (H - 2) * (H - 2)
+        out, col = ws.f(pfx + ".out", B * S * Cout), ws.f(pfx + ".col", B * S * 9 * Cin)
+        dpre = ws.f(pfx + ".dpre", B * S * Cout)
+        self.L.vc_relu_bwd(B * S * Cout, dOut, out, dpre, self.s)
+        dcol = ws.f(pfx + ".dcol", B * S * 9 * Cin)
+        self.linear_bwd(pfx + ".conv.weight", pfx + ".conv.bias", dpre, B * S, Cout, 9 * Cin, col, 9 * Cin, dcol, 0.0)
+        dxbn = ws.f(pfx + ".dxbn", B * H * H * Cin)
+        self.L.vc_col2im3x3(B, H, H, Cin, dcol, dxbn, self.s)
+        self.bn_bwd(pfx + ".bn", pfx + ".bn", dxbn, Cin, X, Cin, 0, B * H * H, Cin, dX, Cin, beta_dx)
+
+    def token_learner_bwd(self, pfx, X, L_, C, S, dZ, dX):
+        """dX (overwritten) = gradient of the TokenLearner input."""
+        B, ws = self.B, self.ws
+        rows = B * L_
+        a, st = ws.f(pfx + ".a", B * S * L_), ws.f(pfx + ".st", 2 * S)
+        da = ws.f(pfx + ".da", B * S * L_)
+        self.L.vc_gemm(0, 1, S, L_, C, 1.0 / L_, dZ, C, S * C, X, C, L_ * C, 0.0, da, L_, S * L_, B, None, None, 0, 0,
+                       0, self.scr_p, self.scr_n, self.s)
+        self.L.vc_gemm(1, 0, L_, C, S, 1.0 / L_, a, L_, S * L_, dZ, C, S * C, 0.0, dX, C, L_ * C, B, None, None, 0, 0,
+                       0, self.scr_p, self.scr_n, self.s)
+        df = ws.f(pfx + ".df", S * rows)
+        par = self.P[pfx + ".tokenizers.0.conv.0.weight"]
+        self.L.vc_tl_attn_bwd(self.train, B, L_, S, ws.f(pfx + ".mx", rows), ws.f(pfx + ".avg", rows), par, st, da, df,
+                              self.G[pfx + ".tokenizers.0.conv.0.weight"], self.s)
+        self.L.vc_tl_pixel_bwd(rows, C, S, df, par, ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), dX, C, self.s)
+
+    def block_bwd(self, blk, pfx, X, H, dOut, dX):
+        """dX (accumulated, beta=1) = gradient w.r.t. the block input, or None to skip input grads."""
+        B, ws, P, G = self.B, self.ws, self.P, self.G
+        Cin, Cout, E = blk.cin, blk.cout, blk.embed
+        D, R = E // 2, math.ceil(E / 16)
+        XW = R + 32
+        L_, Hs = H * H, H - 2
+        S, Ci, Pk = Hs * Hs, Cout // 2, (Hs // 2) * (Hs // 2)
+        rows, M = B * L_, B * S
+        gv, mx = pfx + ".global_view", pfx + ".global_view.layers.0"
+        nl = pfx + ".FusionLayer.cross_attention"
+        order, inv = self.tab[("order", H)].data_ptr(), self.tab[("inv", H)].data_ptr()
+        f = ws.f
+        Fg, Fl, Fc = f(pfx + ".Fg", M * Cout), f(pfx + ".local_feature.out", M * Cout), f(pfx + ".Fc", M * Cout)
+        FMo = f(pfx + ".FusionLayer.FusionLayer.out", M * Cout)
+        # fusionBlock(Fg, FM)
+        dFg, dFM = f(pfx + ".dFg", M * Cout), f(pfx + ".dFM", M * Cout)
+        self.fusion_bwd(pfx + ".fusion", Fg, Cout, FMo, Cout, M, Cout, dOut, dFg, 0.0, dFM, 0.0)
+        # GLfusionBlock FusionLayer
+        CAT1, dCAT1 = f(pfx + ".CAT1", M * 2 * Cout), f(pfx + ".dCAT1", M * 2 * Cout)
+        self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout, dFM, dCAT1, 0.0)
+        dFc, dFl = f(pfx + ".dFc", M * Cout), f(pfx + ".dFl", M * Cout)
+        self.L.vc_add2_2d(M, Cout, dCAT1, 2 * Cout, dCAT1 + F32 * Cout, 2 * Cout, dFc, Cout, 0.0, self.s)
+        self.L.vc_add2_2d(M, Cout, dFc, Cout, 0, 0, dFl, Cout, 0.0, self.s)
+        # localf = BN(W o) + Fc + Fl  ->  non-local branch
+        WP, dWP = f(pfx + ".WP", M * Cout), f(pfx + ".dWP", M * Cout)
+        self.bn_bwd(nl + ".W.1", pfx + ".W1", dCAT1, 2 * Cout, WP, Cout, 0, M, Cout, dWP, Cout, 0.0)
+        O, dO = f(pfx + ".O", M * Ci), f(pfx + ".dO", M * Ci)
+        self.linear_bwd(nl + ".W.0.weight", nl + ".W.0.bias", dWP, M, Cout, Ci, O, Ci, dO, 0.0)
+        TH, PP, ATT = f(pfx + ".TH", M * Ci), f(pfx + ".PP", B * Pk * 2 * Ci), f(pfx + ".ATT", M * Pk)
+        dTH, dPP = f(pfx + ".dTH", M * Ci), f(pfx + ".dPP", B * Pk * 2 * Ci)
+        self.L.vc_nonlocal_attn_bwd(B, S, Pk, Ci, TH, PP, ATT, dO, dTH, dPP, self.s)
+        dPG = f(pfx + ".dPG", M * 2 * Ci)
+        self.L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dPP, ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr(),
+                               dPG, 2 * Ci, self.s)
+        self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, Ci, Cout, Fc, Cout, dFc, 1.0, lddy=2 * Ci)
+        self.linear_bwd(nl + ".g.0.weight", nl + ".g.0.bias", dPG + F32 * Ci, M, Ci, Cout, Fc, Cout, dFc, 1.0,
+                        lddy=2 * Ci)
+        self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
+        # local feature
+        self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0)
+        # channel feature: ln4 -> TokenLearner -> conv1x1
+        Zc, dZc = f(pfx + ".channel_token.Z", M * Cout), f(pfx + ".dZc", M * Cout)
+        self.ln_bwd(pfx + ".ln4", pfx + ".Fc", dFc, Zc, M, Cout, dZc, 0.0)
+        CF, dCF = f(pfx + ".CF", rows * Cout), f(pfx + ".dCF", rows * Cout)
+        self.token_learner_bwd(pfx + ".channel_token", CF, L_, Cout, S, dZc, dCF)
+        self.linear_bwd(pfx + ".channel_feature.weight", pfx + ".channel_feature.bias", dCF, rows, Cout, Cin, X, Cin,
+                        dX or 0, 1.0)
+        # global feature: ln3 -> TokenLearner -> change_dim
+        Zg, dZg = f(pfx + ".global_feature.Z", M * Cout), f(pfx + ".dZg", M * Cout)
+        self.ln_bwd(pfx + ".ln3", pfx + ".Fg", dFg, Zg, M, Cout, dZg, 0.0)
+        CD, dCD = f(pfx + ".CD", rows * Cout), f(pfx + ".dCD", rows * Cout)
+        self.token_learner_bwd(pfx + ".global_feature", CD, L_, Cout, S, dZg, dCD)
+        Gm, dG = f(pfx + ".G", rows * E), f(pfx + ".dG", rows * E)
+        self.linear_bwd(pfx + ".change_dim.weight", pfx + ".change_dim.bias", dCD, rows, Cout, E, Gm, E, dG, 0.0)
+        # hsiMamba: ln1 -> out_proj -> scan/combine -> x_proj/dt_proj -> conv -> in_proj -> pre_norm -> patch_embed
+        T2, dT = f(pfx + ".T2", rows * E), f(pfx + ".dT", rows * E)
+        self.ln_bwd(gv + ".ln1", pfx + ".G", dG, T2, rows, E, dT, 0.0)
+        YS, dYS = f(pfx + ".YS", rows * D), f(pfx + ".dYS", rows * D)
+        self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0)
+        U, XD, XZ = f(pfx + ".U", NDIR * rows * D), f(pfx + ".XD", NDIR * rows * XW), f(pfx + ".XZ", rows * 2 * D)
+        dU, dDTL, dZ = f(pfx + ".dU", NDIR * rows * D), f(pfx + ".dDTL", NDIR * rows * D), f(pfx + ".dZ",
+                                                                                                NDIR * rows * D)
+        dXD = f(pfx + ".dXD", NDIR * rows * XW)
+        self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, XZ, order, P[mx + ".dt_proj.weight"],
+                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], dYS, dU,
+                                 dDTL, dZ, dXD, G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"], self.scr_p,
+                                 self.scr_n, self.s)
+        nr = NDIR * rows
+        # dt_proj: dt_lin = xdbl[:, :R] W_dt^T + b_dt
+        self.mm_nn(nr, R, D, dDTL, D, P[mx + ".dt_proj.weight"], R, dXD, XW)
+        self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R)
+        self.colsum(nr, D, dDTL, D, G[mx + ".dt_proj.bias"])
+        # x_proj: xdbl = u W_x^T
+        self.linear_bwd(mx + ".x_proj.weight", None, dXD, nr, XW, D, U, D, dU, 1.0)
+        dXZ = f(pfx + ".dXZ", rows * 2 * D)
+        self.L.vc_mamba_dirconv_bwd(B, L_, D, NDIR, order, inv, XZ, P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"],
+                                    dU, dZ, dXZ, G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"], self.scr_p,
+                                    self.scr_n, self.s)
+        Xn, dXn = f(pfx + ".Xn", rows * E), f(pfx + ".dXn", rows * E)
+        self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0)
+        T = f(pfx + ".T", rows * E)
+        self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dT, 1.0)   # dT = residual + LN grad
+        self.colsum(B, L_ * E, dT, L_ * E, G[gv + ".pos_embed"])
+        self.linear_bwd(gv + ".patch_embed.projection.weight", None, dT, rows, E, Cin, X, Cin, dX or 0, 1.0)
+
+    def backward(self, dlogits):
+        m, B, ws = self.m, self.B, self.ws
+        grad = torch.empty(m._n_params, dtype=torch.float32, device=self.device)
+        if m._n_params > m._n_active:  # parameters the reference forward never uses get no gradient
+            self.L.vc_fill(m._n_params - m._n_active, grad.data_ptr() + F32 * m._n_active, 0.0, self.s)
+        gb = grad.data_ptr()
+        self.G = {n: gb + F32 * o for n, o in m._poff.items()}
+        Pp = m.patch
+        S1, S2 = (Pp - 2) ** 2, (Pp - 4) ** 2
+        C1o, C2o = m.hsi1.cout, m.hsi2.cout
+        dF1, dF2 = ws.f("dF1", B * S1 * 128), ws.f("dF2", B * S2 * 128)
+        self.L.vc_head_bwd(B, S1, S2, 128, m.ncls, dlogits.data_ptr(), self.P["classifier.weight"], self.feat, dF1,
+                           dF2, self.G["classifier.weight"], self.G["classifier.bias"], self.s)
+        dH1, dH2 = ws.f("dH1", B * S1 * C1o), ws.f("dH2", B * S2 * C2o)
+        dL1, dL2 = ws.f("dL1", B * S1 * 16), ws.f("dL2", B * S2 * 32)
+        self.fusion_bwd("fusion1", self.H1, C1o, self.L1, 16, B * S1, 128, dF1, dH1, 0.0, dL1, 0.0)
+        self.fusion_bwd("fusion2", self.H2, C2o, self.L2, 32, B * S2, 128, dF2, dH2, 0.0, dL2, 0.0)
+        self.conv_bn_relu3_bwd("lidar2", self.L1, Pp - 2, 16, 32, dL2, dL1, 1.0)
+        self.conv_bn_relu3_bwd("lidar1", self.LX, Pp, m.c2, 16, dL1, 0, 0.0)
+        self.block_bwd(m.hsi2, "hsi2", self.H1, Pp - 2, dH2, dH1)
+        self.block_bwd(m.hsi1, "hsi1", self.X0, Pp, dH1, None)
+        return grad
