@@ -81,7 +81,7 @@ def dominant_kernel_roofline(model, batch, reps):
     stream = torch.cuda.current_stream(dev)
 
     def fn():
-        L.vc_gemm(0, 1, M, N, K, 1.0, col, K, 0, W, K, 0, 0.0, out, N, 0, 1, b, None, 0, 0, 1, prog.scr_p,
+        L.vc_gemm(0, 1, M, N, K, 1.0, col, K, 0, W, K, 0, 0.0, out, N, 0, 1, b, None, 0, 0, 1, None, prog.scr_p,
                   prog.scr_n, stream.cuda_stream)
 
     t = time_kernel(fn, reps, stream)

@@ -37,14 +37,17 @@
  * C[b] = alpha * op(A[b]) op(B[b]) + beta*C[b] (+ bias[n]) (+ addend[(m % add_mod)*add_ld + n]) (ReLU if flags&1)
  * op(A)(m,k) = transA ? A[k*lda+m] : A[m*lda+k];  op(B)(k,n) = transB ? B[n*ldb+k] : B[k*ldb+n].
  * fp32 in / fp32 accumulate on v_mfma_f32_16x16x4_f32; split-K (fixed-order) when the output
- * grid is small and ws is given.  Replaces nn.Conv2d 1x1 / 3x3-after-im2col / nn.Linear /
- * torch.matmul forward and backward (Mutimodality_Mamba7.py:258, :1040, :1068, :1071, :101-134,
- * :147, :152, :1098, :1124, :1160; transformers modeling_mamba.py:372, :433, :438, :481). */
+ * grid is small and ws is given.  bias_grad (batch 1 only, may be null) additionally receives
+ * alpha * sum_k op(A)(m,k) (+ beta * bias_grad[m]) through an implicit ones column of op(B): the
+ * bias gradient of a layer rides along its weight-gradient GEMM.  Replaces nn.Conv2d 1x1 /
+ * 3x3-after-im2col / nn.Linear / torch.matmul forward and backward (Mutimodality_Mamba7.py:258,
+ * :1040, :1068, :1071, :101-134, :147, :152, :1098, :1124, :1160; transformers
+ * modeling_mamba.py:372, :433, :438, :481). */
 VC_API int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
                    const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
                    float beta, float* C, long ldc, long strideC, int batch,
                    const float* bias, const float* addend, long add_ld, int add_mod, int flags,
-                   float* ws, long ws_floats, hipStream_t stream);
+                   float* bias_grad, float* ws, long ws_floats, hipStream_t stream);
 
 /* out[c] = beta*out[c] + sum_r X[r*ldx + c]  (bias gradients; fixed-order two-stage) */
 VC_API int vc_colsum(int R, int C, const float* X, long ldx, float* out, float beta,
@@ -127,14 +130,15 @@ VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order,
 /* ---------------------------------------------------------------- TokenLearner
  * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64).  params: S x 5 floats
  * [conv.0.weight(2), conv.0.bias, conv.1.weight, conv.1.bias]; bn_buffers: S x 2
- * [running_mean, running_var]; stats: S x 2 [mean, invstd] saved for the backward;
+ * [running_mean, running_var]; stats: S x 2 fp64 [mean, invstd] saved for the backward (the
+ * per-token statistics and gradient sums accumulate in fp64, as torch's CPU BatchNorm does);
  * a: [B, S, HW] spatial weights.  The pooled tokens Z = a x / HW are a vc_gemm. */
 VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg,
                              hipStream_t stream);
 VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          float* bn_buffers, float eps, float momentum, float* stats, float* a, hipStream_t stream);
+                          float* bn_buffers, float eps, float momentum, double* stats, float* a, hipStream_t stream);
 VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          const float* stats, const float* da, float* df, float* dparams, hipStream_t stream);
+                          const double* stats, const float* da, float* df, float* dparams, hipStream_t stream);
 /* dx[i,:] += d(avg)/C, dx[i, argmax] += d(max), summed over the S tokens (accumulates) */
 VC_API int vc_tl_pixel_bwd(long M, int C, int S, const float* df, const float* params, const int* amx, float* dx,
                            long lddx, hipStream_t stream);

@@ -40,7 +40,7 @@ def rnd(*shape, seed=0, scale=1.0):
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("M,N,K", [(5184, 144, 144), (37, 41, 9), (1, 16, 128), (130, 70, 1296)])
+@pytest.mark.parametrize("M,N,K", [(5184, 144, 144), (37, 41, 9), (1, 16, 128), (130, 70, 1296), (68, 132, 100), (260, 36, 44)])
 def test_gemm_layouts(L, ws, ta, tb, M, N, K):
     A = rnd(K, M, seed=1) if ta else rnd(M, K, seed=1)
     B = rnd(N, K, seed=2) if tb else rnd(K, N, seed=2)
@@ -51,7 +51,7 @@ def test_gemm_layouts(L, ws, ta, tb, M, N, K):
     lda = M if ta else K
     ldb = K if tb else N
     L.vc_gemm(ta, tb, M, N, K, 1.0, P(Ad), lda, 0, P(Bd), ldb, 0, 0.0, P(C), N, 0, 1, P(bd), None, 0, 0, 0,
-              P(ws), ws.numel(), S())
+              None, P(ws), ws.numel(), S())
     torch.cuda.synchronize()
     assert rel_err(C.cpu().numpy(), ref.numpy()) < 1e-5
 
@@ -64,10 +64,27 @@ def test_gemm_splitk_weight_grad(L, ws, M, N, K):
     ref = dY.t() @ X * 0.5 + C0
     C = C0.to(DEV)
     dYd, Xd = dY.to(DEV), X.to(DEV)  # keep device copies alive until the kernel has run
+    bg0 = rnd(M, seed=7)
+    bg = bg0.to(DEV)
     L.vc_gemm(1, 0, M, N, K, 0.5, P(dYd), M, 0, P(Xd), N, 0, 1.0, P(C), N, 0, 1, None, None, 0, 0, 0,
-              P(ws), ws.numel(), S())
+              P(bg), P(ws), ws.numel(), S())
     torch.cuda.synchronize()
     assert rel_err(C.cpu().numpy(), ref.numpy()) < 1e-5
+    # fused bias gradient: column sums of op(A) through the implicit ones column of op(B)
+    assert rel_err(bg.cpu().numpy(), (dY.sum(0) * 0.5 + bg0).numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(72, 9, 51840), (16, 9, 64), (256, 1296, 200)])
+def test_gemm_bias_grad_overwrite(L, ws, M, N, K):
+    dY, X = rnd(K, M, seed=14), rnd(K, N, seed=15)
+    dYd, Xd = dY.to(DEV), X.to(DEV)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    bg = torch.full((M,), float("nan"), device=DEV)
+    L.vc_gemm(1, 0, M, N, K, 1.0, P(dYd), M, 0, P(Xd), N, 0, 0.0, P(C), N, 0, 1, None, None, 0, 0, 0,
+              P(bg), P(ws), ws.numel(), S())
+    torch.cuda.synchronize()
+    assert rel_err(C.cpu().numpy(), (dY.t() @ X).numpy()) < 1e-5
+    assert rel_err(bg.cpu().numpy(), dY.sum(0).numpy()) < 1e-5
 
 
 def test_gemm_batched_relu_addend(L, ws):
@@ -78,7 +95,7 @@ def test_gemm_batched_relu_addend(L, ws):
     C = torch.empty(Bt, M, N, device=DEV)
     Ad, Xd = A.to(DEV), X.to(DEV)
     L.vc_gemm(0, 0, M, N, K, 1.0 / 81, P(Ad), K, M * K, P(Xd), N, K * N, 0.0, P(C), N, M * N, Bt,
-              None, None, 0, 0, 1, P(ws), ws.numel(), S())
+              None, None, 0, 0, 1, None, P(ws), ws.numel(), S())
     torch.cuda.synchronize()
     assert rel_err(C.cpu().numpy(), ref.numpy()) < 1e-5
     # addend with row modulo (positional embedding broadcast over the batch)
@@ -87,7 +104,7 @@ def test_gemm_batched_relu_addend(L, ws):
     C2 = torch.empty(4 * M, N, device=DEV)
     A2d, Wd, addd = A2.to(DEV), W.to(DEV), add.to(DEV)
     L.vc_gemm(0, 1, 4 * M, N, K, 1.0, P(A2d), K, 0, P(Wd), K, 0, 0.0, P(C2), N, 0, 1, None,
-              P(addd), N, M, 0, P(ws), ws.numel(), S())
+              P(addd), N, M, 0, None, P(ws), ws.numel(), S())
     torch.cuda.synchronize()
     assert rel_err(C2.cpu().numpy(), ref2.numpy()) < 1e-5
 

@@ -11,12 +11,15 @@
 
 namespace {
 
-constexpr int MAXP = 32;
+constexpr int MAXP = 16;  // 2x2-pooled 9x9 grid (the largest patch the build supports: 11x11 inputs)
 constexpr int MAXCI = 256;
 
-__global__ __launch_bounds__(256) void nl_fwd(int S, int P, int Ci, const float* __restrict__ theta,
+// PT = number of pooled keys (compile-time so the per-row score array stays in registers)
+template <int PT>
+__global__ __launch_bounds__(256) void nl_fwd(int S, int Ci, const float* __restrict__ theta,
                                               const float* __restrict__ pooled, float* __restrict__ att,
                                               float* __restrict__ o) {
+  constexpr int P = PT;
   extern __shared__ float kv[];  // [P][2*Ci]
   const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* src = pooled + (long)b * P * 2 * Ci;
@@ -24,8 +27,9 @@ __global__ __launch_bounds__(256) void nl_fwd(int S, int P, int Ci, const float*
   __syncthreads();
   for (int s = wave; s < S; s += 4) {
     const float* q = theta + ((long)b * S + s) * Ci;
-    float sc[MAXP];
+    float sc[PT];
     float mx = -INFINITY;
+#pragma unroll
     for (int j = 0; j < P; ++j) {
       float acc = 0.f;
       for (int c = lane; c < Ci; c += 64) acc += q[c] * kv[j * 2 * Ci + c];
@@ -33,14 +37,17 @@ __global__ __launch_bounds__(256) void nl_fwd(int S, int P, int Ci, const float*
       mx = fmaxf(mx, sc[j]);
     }
     float den = 0.f;
+#pragma unroll
     for (int j = 0; j < P; ++j) {
       sc[j] = __expf(sc[j] - mx);
       den += sc[j];
     }
     const float inv = 1.f / den;
+#pragma unroll
     for (int j = 0; j < P; ++j) sc[j] *= inv;
     if (lane < P) {
       float v = 0.f;
+#pragma unroll
       for (int j = 0; j < P; ++j)
         if (j == lane) v = sc[j];
       att[((long)b * S + s) * P + lane] = v;
@@ -48,16 +55,19 @@ __global__ __launch_bounds__(256) void nl_fwd(int S, int P, int Ci, const float*
     float* orow = o + ((long)b * S + s) * Ci;
     for (int c = lane; c < Ci; c += 64) {
       float acc = 0.f;
+#pragma unroll
       for (int j = 0; j < P; ++j) acc += sc[j] * kv[j * 2 * Ci + Ci + c];
       orow[c] = acc;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void nl_bwd(int S, int P, int Ci, const float* __restrict__ theta,
+template <int PT>
+__global__ __launch_bounds__(256) void nl_bwd(int S, int Ci, const float* __restrict__ theta,
                                               const float* __restrict__ pooled, const float* __restrict__ att,
                                               const float* __restrict__ dout, float* __restrict__ dtheta,
                                               float* __restrict__ dpooled) {
+  constexpr int P = PT;
   extern __shared__ float sm[];
   float* kv = sm;                   // [P][2Ci]
   float* ds = kv + P * 2 * Ci;      // [S][P] dscore
@@ -69,17 +79,20 @@ __global__ __launch_bounds__(256) void nl_bwd(int S, int P, int Ci, const float*
   __syncthreads();
   for (int s = wave; s < S; s += 4) {
     const float* dr = dout + ((long)b * S + s) * Ci;
-    float da[MAXP];
+    float da[PT];
     float dot = 0.f;
+#pragma unroll
     for (int j = 0; j < P; ++j) {
       float acc = 0.f;
       for (int c = lane; c < Ci; c += 64) acc += dr[c] * kv[j * 2 * Ci + Ci + c];
       da[j] = wave_sum(acc);
       dot += at[s * P + j] * da[j];
     }
+#pragma unroll
     for (int j = 0; j < P; ++j) da[j] = at[s * P + j] * (da[j] - dot);
     if (lane < P) {
       float v = 0.f;
+#pragma unroll
       for (int j = 0; j < P; ++j)
         if (j == lane) v = da[j];
       ds[s * P + lane] = v;
@@ -87,6 +100,7 @@ __global__ __launch_bounds__(256) void nl_bwd(int S, int P, int Ci, const float*
     float* dq = dtheta + ((long)b * S + s) * Ci;
     for (int c = lane; c < Ci; c += 64) {
       float acc = 0.f;
+#pragma unroll
       for (int j = 0; j < P; ++j) acc += da[j] * kv[j * 2 * Ci + c];
       dq[c] = acc;
     }
@@ -111,7 +125,14 @@ VC_API int vc_nonlocal_attn_fwd(int B, int S, int P, int Ci, const float* theta,
                                 float* o, hipStream_t stream) {
   VC_REQUIRE(B > 0 && S > 0 && P > 0 && P <= MAXP && Ci > 0 && Ci <= MAXCI);
   const size_t sm = sizeof(float) * (size_t)P * 2 * Ci;
-  hipLaunchKernelGGL(nl_fwd, dim3(B), dim3(256), sm, stream, S, P, Ci, theta, pooled, att, o);
+#define VC_NL_FWD(PT_) hipLaunchKernelGGL((nl_fwd<PT_>), dim3(B), dim3(256), sm, stream, S, Ci, theta, pooled, att, o)
+  switch (P) {  // pooled key counts of 5x5 / 7x7 / 9x9 query grids, then generic buckets
+    case 4: VC_NL_FWD(4); break;
+    case 9: VC_NL_FWD(9); break;
+    case 16: VC_NL_FWD(16); break;
+    default: return VC_EINVAL;
+  }
+#undef VC_NL_FWD
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -121,7 +142,15 @@ VC_API int vc_nonlocal_attn_bwd(int B, int S, int P, int Ci, const float* theta,
   VC_REQUIRE(B > 0 && S > 0 && P > 0 && P <= MAXP && Ci > 0 && Ci <= MAXCI);
   const size_t sm = sizeof(float) * ((size_t)P * 2 * Ci + 2 * (size_t)S * P);
   VC_REQUIRE(sm <= 160 * 1024);
-  hipLaunchKernelGGL(nl_bwd, dim3(B), dim3(256), sm, stream, S, P, Ci, theta, pooled, att, dout, dtheta, dpooled);
+#define VC_NL_BWD(PT_) \
+  hipLaunchKernelGGL((nl_bwd<PT_>), dim3(B), dim3(256), sm, stream, S, Ci, theta, pooled, att, dout, dtheta, dpooled)
+  switch (P) {
+    case 4: VC_NL_BWD(4); break;
+    case 9: VC_NL_BWD(9); break;
+    case 16: VC_NL_BWD(16); break;
+    default: return VC_EINVAL;
+  }
+#undef VC_NL_BWD
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

@@ -48,6 +48,22 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v;
 }
 
+// DPP (data-parallel primitives) lane moves within 16-lane rows: VALU ops, no LDS crossbar.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// sum over each aligned 16-lane row, result in every lane of the row:
+// quad_perm[1,0,3,2] -> quad_perm[2,3,0,1] -> row_half_mirror -> row_mirror
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  return v;
+}
+
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
@@ -65,12 +81,65 @@ __device__ __forceinline__ float block256_sum(float v, float* sh) {
   return r;
 }
 
+// out[c] = beta*out[c] + sum_{p<P} part[p*stride + off + c]
+// block = 16 columns x 16 partial lanes: coalesced 64-B row segments, 16 independent load streams
+// per column, fixed-order LDS combine (deterministic).
+static __global__ __launch_bounds__(256) void sum_rows_kernel(int P, int C, const float* __restrict__ part, long stride,
+                                                              long off, float* __restrict__ out, float beta) {
+  __shared__ float sh[16][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float s = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += 16) s += part[(long)p * stride + off + c];
+  }
+  sh[pl][cl] = s;
+  __syncthreads();
+  if (pl == 0 && c < C) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v += sh[i][cl];
+    out[c] = (beta != 0.f ? beta * out[c] : 0.f) + v;
+  }
+}
+
+static inline int launch_sum_rows(int P, int C, const float* part, long stride, long off, float* out, float beta,
+                                  hipStream_t stream) {
+  if (C <= 0) return 0;
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, P, C, part, stride, off, out, beta);
+  return (int)hipGetLastError();
+}
+
+// double-precision variant (BatchNorm statistics and gradient sums accumulate in fp64 like
+// torch's CPU kernels, acc_type<float> = double)
+static __global__ __launch_bounds__(256) void sum_rows_d_kernel(int P, int C, const double* __restrict__ part,
+                                                                long stride, long off, double* __restrict__ out) {
+  __shared__ double sh[16][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += 16) s += part[(long)p * stride + off + c];
+  }
+  sh[pl][cl] = s;
+  __syncthreads();
+  if (pl == 0 && c < C) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v += sh[i][cl];
+    out[c] = v;
+  }
+}
+
 // Chan's parallel combination of (count, mean, M2) triples.
-__device__ __forceinline__ void welford_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
-  float nn = n + nb;
-  if (nn <= 0.f) return;
-  float d = meanb - mean;
-  float fb = nb / nn;
+template <typename T>
+__device__ __forceinline__ void welford_merge(T& n, T& mean, T& m2, T nb, T meanb, T m2b) {
+  T nn = n + nb;
+  if (nn <= T(0)) return;
+  T d = meanb - mean;
+  T fb = nb / nn;
   mean = mean + d * fb;
   m2 = m2 + m2b + d * d * n * fb;
   n = nn;

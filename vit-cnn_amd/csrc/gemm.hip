@@ -13,7 +13,7 @@
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 16;
+constexpr int BM = 64, BN = 64;
 constexpr int LDS_STRIDE = 81;  // 64 + 17: conflict-free fragment reads, <=2-way stores
 
 enum { F_RELU = 1 };
@@ -36,61 +36,123 @@ __device__ __forceinline__ float epilogue(const Epi& e, float acc, const float* 
   return v;
 }
 
+struct GemmArgs {
+  int M, N, K, Ne, k_chunk, nsplit;   // Ne = N + 1 when the implicit ones column (bias gradient) is on
+  const float* A;
+  long lda, sA;
+  const float* B;
+  long ldb, sB;
+  float* C;
+  long ldc, sC;
+  float* bias_grad;                   // [M]: column N of the product (sum over K of A)
+  float* part;                        // split-K partial slabs [batch*nsplit][M][Ne]
+  Epi epi;
+};
+
 // A element (m,k): TA ? A[k*lda + m] : A[m*lda + k];  B element (k,n): TB ? B[n*ldb + k] : B[k*ldb + n]
-template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_f32_mfma(int M, int N, int K, int k_chunk, int nsplit,
-                                                     const float* __restrict__ A, long lda, long sA,
-                                                     const float* __restrict__ B, long ldb, long sB,
-                                                     float* __restrict__ C, long ldc, long sC, Epi epi,
-                                                     float* __restrict__ part) {
+// 64x64 output tile per 256-thread block (4 waves of 32x32 = 2x2 v_mfma_f32_16x16x4_f32), BK = 16
+// K steps staged through LDS (k-major, 81-float rows) with a one-tile register prefetch; small
+// LDS footprint (10 KB) keeps up to 8 blocks per CU resident to hide global-load latency.
+// VA / VB: the operand is 16-B aligned with a leading dimension divisible by 4, so every thread
+// fetches its 4 tile elements with one float4 (edges fall back to guarded scalar loads).
+constexpr int BK = 16;
+
+template <bool TA, bool TB, bool VA, bool VB>
+__global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
   __shared__ float As[BK * LDS_STRIDE];
   __shared__ float Bs[BK * LDS_STRIDE];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int zb = blockIdx.z / nsplit, zs = blockIdx.z % nsplit;
-  const int kbeg = zs * k_chunk;
-  const int kend = min(K, kbeg + k_chunk);
-  A += (long)zb * sA;
-  B += (long)zb * sB;
+  const int zb = blockIdx.z / g.nsplit, zs = blockIdx.z % g.nsplit;
+  const int kbeg = zs * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const float* A = g.A + (long)zb * g.sA;
+  const float* Bp = g.B + (long)zb * g.sB;
+  const bool ones = g.Ne > g.N;
 
   float ra[4], rb[4];
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int m, k;
+  // element i of this thread's share of the A tile: (m, k) in tile coordinates
+  auto a_idx = [&](int i, int& m, int& k) {
+    if (VA) {
+      if (TA) { k = tid >> 4; m = (tid & 15) * 4 + i; }
+      else    { m = tid >> 2; k = (tid & 3) * 4 + i; }
+    } else {
       if (TA) { m = tid & 63; k = (tid >> 6) + 4 * i; }
       else    { k = tid & 15; m = (tid >> 4) + 16 * i; }
-      int gm = m0 + m, gk = k0 + k;
-      float v = 0.f;
-      if (gm < M && gk < kend) v = TA ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk];
-      ra[i] = v;
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int n, k;
+  };
+  auto b_idx = [&](int i, int& n, int& k) {
+    if (VB) {
+      if (TB) { n = tid >> 2; k = (tid & 3) * 4 + i; }
+      else    { k = tid >> 4; n = (tid & 15) * 4 + i; }
+    } else {
       if (TB) { k = tid & 15; n = (tid >> 4) + 16 * i; }
       else    { n = tid & 63; k = (tid >> 6) + 4 * i; }
-      int gn = n0 + n, gk = k0 + k;
-      float v = 0.f;
-      if (gn < N && gk < kend) v = TB ? B[(long)gn * ldb + gk] : B[(long)gk * ldb + gn];
-      rb[i] = v;
+    }
+  };
+  auto a_at = [&](int gm, int gk) -> float {
+    return (gm < g.M && gk < kend) ? (TA ? A[(long)gk * g.lda + gm] : A[(long)gm * g.lda + gk]) : 0.f;
+  };
+  auto b_at = [&](int gn, int gk) -> float {
+    if (gk >= kend) return 0.f;
+    if (gn < g.N) return TB ? Bp[(long)gn * g.ldb + gk] : Bp[(long)gk * g.ldb + gn];
+    return (ones && gn == g.N) ? 1.f : 0.f;
+  };
+  auto load = [&](int k0) {
+    if (VA) {
+      int m, k;
+      a_idx(0, m, k);
+      const int gm = m0 + m, gk = k0 + k;
+      const bool full = TA ? (gk < kend && gm + 3 < g.M) : (gm < g.M && gk + 3 < kend);
+      if (full) {
+        const float4 v = *reinterpret_cast<const float4*>(TA ? A + (long)gk * g.lda + gm : A + (long)gm * g.lda + gk);
+        ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[i] = TA ? a_at(gm + i, gk) : a_at(gm, gk + i);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int m, k;
+        a_idx(i, m, k);
+        ra[i] = a_at(m0 + m, k0 + k);
+      }
+    }
+    if (VB) {
+      int n, k;
+      b_idx(0, n, k);
+      const int gn = n0 + n, gk = k0 + k;
+      const bool full = TB ? (gn < g.N && gk + 3 < kend) : (gk < kend && gn + 3 < g.N);
+      if (full) {
+        const float4 v = *reinterpret_cast<const float4*>(TB ? Bp + (long)gn * g.ldb + gk : Bp + (long)gk * g.ldb + gn);
+        rb[0] = v.x; rb[1] = v.y; rb[2] = v.z; rb[3] = v.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rb[i] = TB ? b_at(gn, gk + i) : b_at(gn + i, gk);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int n, k;
+        b_idx(i, n, k);
+        rb[i] = b_at(n0 + n, k0 + k);
+      }
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int m, k;
-      if (TA) { m = tid & 63; k = (tid >> 6) + 4 * i; }
-      else    { k = tid & 15; m = (tid >> 4) + 16 * i; }
+      a_idx(i, m, k);
       As[k * LDS_STRIDE + m] = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int n, k;
-      if (TB) { k = tid & 15; n = (tid >> 4) + 16 * i; }
-      else    { n = tid & 63; k = (tid >> 6) + 4 * i; }
+      b_idx(i, n, k);
       Bs[k * LDS_STRIDE + n] = rb[i];
     }
   };
@@ -111,10 +173,10 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int M, int N, int K, int k_
 #pragma unroll
       for (int ks = 0; ks < BK / 4; ++ks) {
         const int kk = ks * 4 + fk;
-        float a0 = As[kk * LDS_STRIDE + wm * 32 + fr];
-        float a1 = As[kk * LDS_STRIDE + wm * 32 + 16 + fr];
-        float b0 = Bs[kk * LDS_STRIDE + wn * 32 + fr];
-        float b1 = Bs[kk * LDS_STRIDE + wn * 32 + 16 + fr];
+        const float a0 = As[kk * LDS_STRIDE + wm * 32 + fr];
+        const float a1 = As[kk * LDS_STRIDE + wm * 32 + 16 + fr];
+        const float b0 = Bs[kk * LDS_STRIDE + wn * 32 + fr];
+        const float b1 = Bs[kk * LDS_STRIDE + wn * 32 + 16 + fr];
         acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
         acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
         acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
@@ -133,29 +195,36 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(int M, int N, int K, int k_
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * 32 + mi * 16 + fk * 4 + r;
         const int n = n0 + wn * 32 + ni * 16 + fr;
-        if (m < M && n < N) {
-          if (nsplit > 1) {
-            part[((long)blockIdx.z * M + m) * N + n] = acc[mi][ni][r];
+        if (m < g.M && n < g.Ne) {
+          if (g.nsplit > 1) {
+            g.part[((long)blockIdx.z * g.M + m) * g.Ne + n] = acc[mi][ni][r];
+          } else if (n < g.N) {
+            float* cp = g.C + (long)zb * g.sC + (long)m * g.ldc + n;
+            *cp = epilogue(g.epi, acc[mi][ni][r], cp, m, n);
           } else {
-            float* cp = C + (long)zb * sC + (long)m * ldc + n;
-            *cp = epilogue(epi, acc[mi][ni][r], cp, m, n);
+            float* bp = g.bias_grad + m;
+            *bp = g.epi.alpha * acc[mi][ni][r] + (g.epi.beta != 0.f ? g.epi.beta * *bp : 0.f);
           }
         }
       }
 }
 
-__global__ void splitk_reduce(int M, int N, int nsplit, int batch, const float* __restrict__ part,
-                              float* __restrict__ C, long ldc, long sC, Epi epi) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)batch * M * N;
+__global__ void splitk_reduce(GemmArgs g, int batch) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)batch * g.M * g.Ne;
   if (idx >= total) return;
-  int n = idx % N;
-  int m = (idx / N) % M;
-  int b = idx / ((long)M * N);
+  const int n = idx % g.Ne;
+  const int m = (idx / g.Ne) % g.M;
+  const int b = idx / ((long)g.M * g.Ne);
   float s = 0.f;
-  for (int z = 0; z < nsplit; ++z) s += part[(((long)b * nsplit + z) * M + m) * N + n];
-  float* cp = C + (long)b * sC + (long)m * ldc + n;
-  *cp = epilogue(epi, s, cp, m, n);
+  for (int z = 0; z < g.nsplit; ++z) s += g.part[(((long)b * g.nsplit + z) * g.M + m) * g.Ne + n];
+  if (n < g.N) {
+    float* cp = g.C + (long)b * g.sC + (long)m * g.ldc + n;
+    *cp = epilogue(g.epi, s, cp, m, n);
+  } else {
+    float* bp = g.bias_grad + m;
+    *bp = g.epi.alpha * s + (g.epi.beta != 0.f ? g.epi.beta * *bp : 0.f);
+  }
 }
 
 // stage 1 of a column sum: block (cx, ry) sums rows [ry*rows_per, ...) of 64 columns
@@ -174,34 +243,30 @@ __global__ __launch_bounds__(256) void colsum_partial(int R, int Cn, const float
   if (rl == 0 && c < Cn) part[(long)blockIdx.y * Cn + c] = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
 }
 
-__global__ void colsum_final(int P, int Cn, const float* __restrict__ part, float* __restrict__ out, float beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Cn) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(long)p * Cn + c];
-  out[c] = (beta != 0.f ? beta * out[c] : 0.f) + s;
-}
-
 }  // namespace
 
-// C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b] (+ bias[n]) (+ addend[(m % add_mod), n]) (relu)
+// C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b] (+ bias[n]) (+ addend[(m % add_mod), n]) (relu);
+// bias_grad (optional): bias_grad[m] = alpha * sum_k op(A)(m,k) + beta * bias_grad[m]
 VC_EXPORT int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
                       const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
                       float beta, float* C, long ldc, long strideC, int batch,
                       const float* bias, const float* addend, long add_ld, int add_mod, int flags,
-                      float* ws, long ws_floats, hipStream_t stream) {
+                      float* bias_grad, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1);
+  VC_REQUIRE(!bias_grad || batch == 1);
   if (M == 0 || N == 0) return VC_OK;
   Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, flags};
-  const int tn = vc_cdiv(N, BN), tm = vc_cdiv(M, BM);
-  long tiles = (long)tn * tm * batch;
-  // split K when the output grid cannot fill the 256 CUs (weight gradients: M,N small, K = rows)
+  const int Ne = N + (bias_grad ? 1 : 0);
+  const int tn = vc_cdiv(Ne, BN), tm = vc_cdiv(M, BM);
+  const long tiles = (long)tn * tm * batch;
+  // split K only when the output grid is far from filling the 256 CUs and each slice keeps
+  // >= 256 of K (weight gradients: M, N small, K = rows)
   int nsplit = 1;
-  if (ws && tiles < 256 && K >= 4 * BK) {
-    long want = (512 + tiles - 1) / tiles;
-    long maxk = K / (2 * BK);
+  if (ws && tiles < 128 && K >= 512) {
+    const long want = (256 + tiles - 1) / tiles;
+    const long maxk = K / 256;
     nsplit = (int)std::min<long>(std::min<long>(want, maxk), 64);
-    while (nsplit > 1 && (long)nsplit * batch * M * N > ws_floats) --nsplit;
+    while (nsplit > 1 && (long)nsplit * batch * M * Ne > ws_floats) --nsplit;
     if (nsplit < 1) nsplit = 1;
   }
   int k_chunk = K;
@@ -209,10 +274,17 @@ VC_EXPORT int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
     k_chunk = vc_cdiv(vc_cdiv(K, nsplit), BK) * BK;
     nsplit = vc_cdiv(K, k_chunk);
   }
+  GemmArgs g{M, N, K, Ne, k_chunk, nsplit, A, lda, strideA, B, ldb, strideB, C, ldc, strideC, bias_grad, ws, epi};
   dim3 grid(tn, tm, batch * nsplit), block(256);
-#define VC_LAUNCH_GEMM(TA_, TB_)                                                                          \
-  hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_>), grid, block, 0, stream, M, N, K, k_chunk, nsplit, A, lda, \
-                     strideA, B, ldb, strideB, C, ldc, strideC, epi, ws)
+  const bool va = ((uintptr_t)A % 16 == 0) && (lda % 4 == 0) && (batch == 1 || strideA % 4 == 0);
+  const bool vb = ((uintptr_t)B % 16 == 0) && (ldb % 4 == 0) && (batch == 1 || strideB % 4 == 0);
+#define VC_LAUNCH_GEMM(TA_, TB_)                                                                           \
+  do {                                                                                                     \
+    if (va && vb) hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, true, true>), grid, block, 0, stream, g);    \
+    else if (va) hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, true, false>), grid, block, 0, stream, g);    \
+    else if (vb) hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, false, true>), grid, block, 0, stream, g);    \
+    else hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, false, false>), grid, block, 0, stream, g);           \
+  } while (0)
   if (transA && transB) VC_LAUNCH_GEMM(true, true);
   else if (transA) VC_LAUNCH_GEMM(true, false);
   else if (transB) VC_LAUNCH_GEMM(false, true);
@@ -220,9 +292,8 @@ VC_EXPORT int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
 #undef VC_LAUNCH_GEMM
   VC_CHECK_LAUNCH();
   if (nsplit > 1) {
-    long total = (long)batch * M * N;
-    hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, M, N, nsplit, batch, ws, C,
-                       ldc, strideC, epi);
+    const long total = (long)batch * M * Ne;
+    hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, g, batch);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;
@@ -233,16 +304,20 @@ VC_EXPORT int vc_colsum(int R, int Cn, const float* X, long ldx, float* out, flo
                         hipStream_t stream) {
   VC_REQUIRE(R >= 0 && Cn >= 0);
   if (Cn == 0) return VC_OK;
-  int rows_per = 256;
+  // ~64-128 rows per partial block, at most 512 partials, then a 16x16 parallel final sum
+  int rows_per = std::max(64, vc_cdiv(R, 512));
   int P = std::max(1, vc_cdiv(R, rows_per));
   while ((long)P * Cn > ws_floats && rows_per < (1 << 30)) {
     rows_per *= 2;
     P = std::max(1, vc_cdiv(R, rows_per));
   }
   VC_REQUIRE((long)P * Cn <= ws_floats);
+  if (P == 1) {  // small R: a single pass writes the result directly
+    hipLaunchKernelGGL(colsum_partial, dim3(vc_cdiv(Cn, 64), 1), dim3(256), 0, stream, R, Cn, X, ldx, rows_per, ws);
+    VC_CHECK_LAUNCH();
+    return launch_sum_rows(1, Cn, ws, Cn, 0, out, beta, stream);
+  }
   hipLaunchKernelGGL(colsum_partial, dim3(vc_cdiv(Cn, 64), P), dim3(256), 0, stream, R, Cn, X, ldx, rows_per, ws);
   VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_final, dim3(vc_cdiv(Cn, 256)), dim3(256), 0, stream, P, Cn, ws, out, beta);
-  VC_CHECK_LAUNCH();
-  return VC_OK;
+  return launch_sum_rows(P, Cn, ws, Cn, 0, out, beta, stream);
 }

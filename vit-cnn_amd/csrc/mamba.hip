@@ -58,53 +58,87 @@ struct ScanArgs {
   const float* dskip;  // [D]
 };
 
-__device__ __forceinline__ float dt_lin(const float* row, const float* wrow, int R, float bias) {
-  float a = bias;
-  for (int r = 0; r < R; ++r) a += wrow[r] * row[r];
-  return a;
-}
-
-__global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ y) {
-  extern __shared__ float smem[];
-  const int XW = a.R + 2 * NST;
-  float* xs = smem;                    // [L][XW]
-  float* ws = xs + a.L * XW;           // [16][R]
-  const int s = blockIdx.x, k = s / a.B, b = s % a.B;
-  const int tid = threadIdx.x, dl = tid >> 4, n = tid & 15;
-  const int d = blockIdx.y * DPB + dl;
-  const bool valid = d < a.D;
-  const float* xsrc = a.xdbl + (long)s * a.L * XW;
-  for (int i = tid; i < a.L * XW; i += 256) xs[i] = xsrc[i];
-  for (int i = tid; i < DPB * a.R; i += 256) {
-    const int dd = blockIdx.y * DPB + i / a.R;
-    ws[i] = dd < a.D ? a.wdt[(long)dd * a.R + i % a.R] : 0.f;
-  }
-  __syncthreads();
-  const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
-  const float bdt = valid ? a.bdt[d] : 0.f;
-  const float Dd = valid ? a.dskip[d] : 0.f;
-  const float* wrow = ws + dl * a.R;
-  float h = 0.f;
-  for (int t = 0; t < a.L; ++t) {
-    const float* row = xs + t * XW;
-    const float dt = softplus_f(dt_lin(row, wrow, a.R, bdt));
-    const float ut = valid ? a.u[((long)s * a.L + t) * a.D + d] : 0.f;
-    const float dA = __expf(dt * A);
-    h = dA * h + dt * row[a.R + n] * ut;
-    const float ys = group16_sum(h * row[a.R + NST + n]);
-    if (n == 0 && valid) {
-      const float zt = a.xz[((long)b * a.L + a.order[k * a.L + t]) * (2L * a.D) + a.D + d];
-      y[((long)s * a.L + t) * a.D + d] = (ys + Dd * ut) * silu_f(zt);
-    }
-  }
-}
-
 __device__ __forceinline__ float gate_softmax(const float* logits, int ndir, int k) {
   float mx = logits[0];
   for (int i = 1; i < ndir; ++i) mx = fmaxf(mx, logits[i]);
   float den = 0.f;
   for (int i = 0; i < ndir; ++i) den += __expf(logits[i] - mx);
   return __expf(logits[k] - mx) / den;
+}
+
+// Stage one sequence (seq s = k*B + b, channels d0..d0+15) into LDS:
+//   xs [L][XW] x_proj output rows (dt-rank | B | C), us [L][16] u, zs [L][16] z gathered through
+//   the direction order, dr [L][16] (bwd only) d(ysum) gathered through the order,
+//   dts [L][16] dt = softplus(W_dt xs[:R] + b_dt) and dsp [L][16] softplus' (bwd only).
+// Everything the sequential loop touches afterwards is LDS or registers.
+template <bool BWD>
+__device__ __forceinline__ void scan_stage(const ScanArgs& a, int s, int d0, float* xs, float* wsm, float* dts,
+                                           float* dsp, float* us, float* zs, float* dr, const float* dysum) {
+  const int XW = a.R + 2 * NST;
+  const int k = s / a.B, b = s % a.B;
+  const int tid = threadIdx.x;
+  const float* xsrc = a.xdbl + (long)s * a.L * XW;
+  for (int i = tid; i < a.L * XW; i += 256) xs[i] = xsrc[i];
+  for (int i = tid; i < DPB * a.R; i += 256) {
+    const int dd = d0 + i / a.R;
+    wsm[i] = dd < a.D ? a.wdt[(long)dd * a.R + i % a.R] : 0.f;
+  }
+  for (int i = tid; i < a.L * DPB; i += 256) {
+    const int t = i / DPB, d = d0 + i % DPB;
+    float uv = 0.f, zv = 0.f, gv = 0.f;
+    if (d < a.D) {
+      const long tok = (long)b * a.L + a.order[k * a.L + t];
+      uv = a.u[((long)s * a.L + t) * a.D + d];
+      zv = a.xz[tok * (2L * a.D) + a.D + d];
+      if (BWD) gv = dysum[tok * a.D + d];
+    }
+    us[i] = uv;
+    zs[i] = BWD ? zv : silu_f(zv);
+    if (BWD) dr[i] = gv;
+  }
+  __syncthreads();
+  for (int i = tid; i < a.L * DPB; i += 256) {
+    const int t = i / DPB, dl = i % DPB, d = d0 + dl;
+    float dtl = d < a.D ? a.bdt[d] : 0.f;
+    const float* row = xs + t * XW;
+    const float* w = wsm + dl * a.R;
+    for (int r = 0; r < a.R; ++r) dtl += w[r] * row[r];
+    dts[i] = softplus_f(dtl);
+    if (BWD) dsp[i] = dtl > 20.f ? 1.f : sigmoid_f(dtl);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ y) {
+  extern __shared__ float smem[];
+  const int XW = a.R + 2 * NST;
+  float* xs = smem;                    // [L][XW]
+  float* wsm = xs + a.L * XW;          // [16][R]
+  float* dts = wsm + DPB * a.R;        // [L][16]
+  float* us = dts + a.L * DPB;         // [L][16]
+  float* zs = us + a.L * DPB;          // [L][16] silu(z)
+  float* yb = zs + a.L * DPB;          // [L][16]
+  const int s = blockIdx.x, d0 = blockIdx.y * DPB;
+  const int tid = threadIdx.x, dl = tid >> 4, n = tid & 15;
+  const int d = d0 + dl;
+  const bool valid = d < a.D;
+  scan_stage<false>(a, s, d0, xs, wsm, dts, nullptr, us, zs, nullptr, nullptr);
+  const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
+  const float Dd = valid ? a.dskip[d] : 0.f;
+  float h = 0.f;
+  for (int t = 0; t < a.L; ++t) {
+    const float* row = xs + t * XW;
+    const float dt = dts[t * DPB + dl];
+    const float ut = us[t * DPB + dl];
+    h = __expf(dt * A) * h + dt * row[a.R + n] * ut;
+    const float ys = row16_sum(h * row[a.R + NST + n]);
+    if (n == 0) yb[t * DPB + dl] = (ys + Dd * ut) * zs[t * DPB + dl];
+  }
+  __syncthreads();
+  for (int i = tid; i < a.L * DPB; i += 256) {
+    const int t = i / DPB, dd = d0 + i % DPB;
+    if (dd < a.D) y[((long)s * a.L + t) * a.D + dd] = yb[i];
+  }
 }
 
 struct ScanBwdOut {
@@ -122,41 +156,36 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
   extern __shared__ float smem[];
   const int XW = a.R + 2 * NST;
   const int nck = (a.L + CK - 1) / CK;
-  float* xs = smem;                          // [L][XW]
-  float* ws = xs + a.L * XW;                 // [16][R]
-  float* ck = ws + DPB * a.R;                // [nck][256]
-  float* bc = ck + nck * 256;                // [4][L][32]
-  float* red = bc + 4 * a.L * 32;            // [4]
-  const int s = blockIdx.x, k = s / a.B, b = s % a.B;
+  float* xs = smem;                       // [L][XW]
+  float* wsm = xs + a.L * XW;             // [16][R]
+  float* dts = wsm + DPB * a.R;           // [L][16]
+  float* dsp = dts + a.L * DPB;           // [L][16]
+  float* us = dsp + a.L * DPB;            // [L][16]
+  float* zs = us + a.L * DPB;             // [L][16]
+  float* dr = zs + a.L * DPB;             // [L][16]
+  float* ck = dr + a.L * DPB;             // [nck][256]
+  float* bc = ck + nck * 256;             // [4][CK][32]
+  float* red = bc + 4 * CK * 32;          // [4]
+  const int s = blockIdx.x, k = s / a.B, d0 = blockIdx.y * DPB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, dl = tid >> 4, n = tid & 15;
-  const int d = blockIdx.y * DPB + dl;
+  const int d = d0 + dl;
   const bool valid = d < a.D;
-  const float* xsrc = a.xdbl + (long)s * a.L * XW;
-  for (int i = tid; i < a.L * XW; i += 256) xs[i] = xsrc[i];
-  for (int i = tid; i < DPB * a.R; i += 256) {
-    const int dd = blockIdx.y * DPB + i / a.R;
-    ws[i] = dd < a.D ? a.wdt[(long)dd * a.R + i % a.R] : 0.f;
-  }
-  __syncthreads();
+  scan_stage<true>(a, s, d0, xs, wsm, dts, dsp, us, zs, dr, dysum);
   const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
-  const float bdt = valid ? a.bdt[d] : 0.f;
   const float Dd = valid ? a.dskip[d] : 0.f;
   const float g = gate_softmax(gate_logits, ndir, k);
-  const float* wrow = ws + dl * a.R;
-  const long ld2 = 2L * a.D;
 
   // phase 1: forward recurrence, checkpoint the state entering every CK-step chunk
   float h = 0.f;
   for (int t = 0; t < a.L; ++t) {
     if (t % CK == 0) ck[(t / CK) * 256 + tid] = h;
-    const float* row = xs + t * XW;
-    const float dt = softplus_f(dt_lin(row, wrow, a.R, bdt));
-    const float ut = valid ? a.u[((long)s * a.L + t) * a.D + d] : 0.f;
-    h = __expf(dt * A) * h + dt * row[a.R + n] * ut;
+    const float dt = dts[t * DPB + dl];
+    h = __expf(dt * A) * h + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
   }
 
-  // phase 2: reverse sweep chunk by chunk
+  // phase 2: reverse sweep, one checkpoint chunk at a time
   float dh_carry = 0.f, dA_acc = 0.f, dD_acc = 0.f, dg_acc = 0.f;
+  float* dst = o.dbc_part + ((long)blockIdx.y * gridDim.x + s) * a.L * 2 * NST;
   for (int c = nck - 1; c >= 0; --c) {
     const int t0 = c * CK;
     const float hin = ck[c * 256 + tid];
@@ -166,10 +195,8 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
     for (int i = 0; i < CK; ++i) {
       const int t = t0 + i;
       if (t < a.L) {
-        const float* row = xs + t * XW;
-        const float dt = softplus_f(dt_lin(row, wrow, a.R, bdt));
-        const float ut = valid ? a.u[((long)s * a.L + t) * a.D + d] : 0.f;
-        hh = __expf(dt * A) * hh + dt * row[a.R + n] * ut;
+        const float dt = dts[t * DPB + dl];
+        hh = __expf(dt * A) * hh + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
       }
       hreg[i] = hh;
     }
@@ -177,30 +204,23 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
     for (int i = CK - 1; i >= 0; --i) {
       const int t = t0 + i;
       if (t >= a.L) continue;
-      const float* row = xs + t * XW;
-      const float dtl = dt_lin(row, wrow, a.R, bdt);
-      const float dt = softplus_f(dtl);
+      const int ti = t * DPB + dl;
+      const float dt = dts[ti];
       const float dA = __expf(dt * A);
-      const float Bn = row[a.R + n], Cn = row[a.R + NST + n];
+      const float Bn = xs[t * XW + a.R + n], Cn = xs[t * XW + a.R + NST + n];
       const float ht = hreg[i];
       const float hp = i > 0 ? hreg[i > 0 ? i - 1 : 0] : hin;
-      float ut = 0.f, zt = 0.f, draw = 0.f;
-      if (valid) {
-        const long tokrow = (long)b * a.L + a.order[k * a.L + t];
-        ut = a.u[((long)s * a.L + t) * a.D + d];
-        zt = a.xz[tokrow * ld2 + a.D + d];
-        draw = dysum[tokrow * a.D + d];
-      }
+      const float ut = us[ti], zt = zs[ti], draw = dr[ti];
       const float dout = g * draw;
-      const float ypre = group16_sum(ht * Cn) + Dd * ut;
+      const float ypre = row16_sum(ht * Cn) + Dd * ut;
       const float sg = sigmoid_f(zt);
       const float sz = zt * sg;
       const float dy = dout * sz;
       const float dh = dh_carry + Cn * dy;
       const float ddA = dh * hp;
       dA_acc += ddA * dA * dt * A;
-      const float ddt = group16_sum(ddA * dA * A + dh * Bn * ut);
-      const float dus = group16_sum(dh * dt * Bn);
+      const float ddt = row16_sum(ddA * dA * A + dh * Bn * ut);
+      const float dus = row16_sum(dh * dt * Bn);
       dh_carry = dh * dA;
       float vb = dh * dt * ut, vc = dy * ht;
       vb += __shfl_xor(vb, 16, 64);
@@ -208,26 +228,26 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
       vc += __shfl_xor(vc, 16, 64);
       vc += __shfl_xor(vc, 32, 64);
       if (lane < 16) {
-        bc[(wave * a.L + t) * 32 + lane] = vb;
-        bc[(wave * a.L + t) * 32 + 16 + lane] = vc;
+        bc[(wave * CK + i) * 32 + lane] = vb;
+        bc[(wave * CK + i) * 32 + 16 + lane] = vc;
       }
       if (n == 0 && valid) {
         const long o_idx = ((long)s * a.L + t) * a.D + d;
         o.du[o_idx] = dus + dy * Dd;
-        o.ddtl[o_idx] = ddt * (dtl > 20.f ? 1.f : sigmoid_f(dtl));
+        o.ddtl[o_idx] = ddt * dsp[ti];
         o.dz[o_idx] = dout * ypre * sg * (1.f + zt * (1.f - sg));
         dD_acc += dy * ut;
         dg_acc += draw * ypre * sz;
       }
     }
-  }
-  __syncthreads();
-  // phase 3: per-block partials
-  float* dst = o.dbc_part + ((long)blockIdx.y * gridDim.x + s) * a.L * 2 * NST;
-  for (int i = tid; i < a.L * 32; i += 256) {
-    const int t = i / 32, j = i % 32;
-    dst[i] = bc[(0 * a.L + t) * 32 + j] + bc[(1 * a.L + t) * 32 + j] + bc[(2 * a.L + t) * 32 + j] +
-             bc[(3 * a.L + t) * 32 + j];
+    __syncthreads();
+    for (int j = tid; j < CK * 32; j += 256) {
+      const int i = j >> 5, col = j & 31, t = t0 + i;
+      if (t < a.L)
+        dst[(long)t * 32 + col] = bc[(0 * CK + i) * 32 + col] + bc[(1 * CK + i) * 32 + col] +
+                                  bc[(2 * CK + i) * 32 + col] + bc[(3 * CK + i) * 32 + col];
+    }
+    __syncthreads();
   }
   if (valid) {
     o.da_part[(long)s * a.D * NST + d * NST + n] = dA_acc;
@@ -238,6 +258,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
   __syncthreads();
   if (tid == 0) o.dg_part[(long)s * gridDim.y + blockIdx.y] = red[0] + red[1] + red[2] + red[3];
 }
+
 
 __global__ void combine_fwd(int B, int L, int D, int ndir, const int* __restrict__ inv, const float* __restrict__ logits,
                             const float* __restrict__ y, float* __restrict__ out) {
@@ -260,23 +281,27 @@ __global__ void combine_fwd(int B, int L, int D, int ndir, const int* __restrict
 }
 
 // dlogit_j = g_j (dg_j - sum_k g_k dg_k),  dg_k = sum over the k-th direction's partials
-__global__ void gate_grad(int ndir, int per_dir, const float* __restrict__ logits, const float* __restrict__ part,
-                          float* __restrict__ dlogits) {
+__global__ __launch_bounds__(256) void gate_grad(int ndir, int per_dir, const float* __restrict__ logits,
+                                                 const float* __restrict__ part, float* __restrict__ dlogits) {
   __shared__ float dg[64], gg[64];
-  const int tid = threadIdx.x;
-  if (tid < ndir) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int kk = wave; kk < ndir; kk += 4) {
     float s = 0.f;
-    for (int i = 0; i < per_dir; ++i) s += part[(long)tid * per_dir + i];
-    dg[tid] = s;
-    gg[tid] = gate_softmax(logits, ndir, tid);
+    for (int i = lane; i < per_dir; i += 64) s += part[(long)kk * per_dir + i];
+    s = wave_sum(s);
+    if (lane == 0) {
+      dg[kk] = s;
+      gg[kk] = gate_softmax(logits, ndir, kk);
+    }
   }
   __syncthreads();
-  if (tid < ndir) {
+  if (threadIdx.x < ndir) {
     float dot = 0.f;
     for (int i = 0; i < ndir; ++i) dot += gg[i] * dg[i];
-    dlogits[tid] = gg[tid] * (dg[tid] - dot);
+    dlogits[threadIdx.x] = gg[threadIdx.x] * (dg[threadIdx.x] - dot);
   }
 }
+
 
 __global__ void sum_bc_chunks(long rows, int nchunk, int XW, int R, const float* __restrict__ part,
                               float* __restrict__ dxdbl) {
@@ -343,17 +368,19 @@ __global__ void dirconv_bwd_gather(int B, int L, int D, int ndir, const int* __r
   dxz[idx] = acc;
 }
 
-// partial sums for conv1d weight/bias grads: part[p][d][0..3] = sum dpre*x_{t-3+j}, [4] = sum dpre
+// partial sums for conv1d weight/bias grads over a chunk of (seq, t) rows:
+// part[p][d*4 + j] = sum dpre * x_{t-3+j},  part[p][4D + d] = sum dpre
+// block = 16 channels x 16 row lanes (64-B row segments, 16 independent streams per channel)
 __global__ __launch_bounds__(256) void dirconv_bwd_wgrad(int B, int L, int D, const int* __restrict__ order,
                                                          const float* __restrict__ xz, const float* __restrict__ dpre,
                                                          long rows, int rows_per, float* __restrict__ part) {
-  __shared__ float sh[5][4][64];
-  const int dlc = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int d = blockIdx.x * 64 + dlc;
+  __shared__ float sh[5][16][17];
+  const int dlc = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int d = blockIdx.x * 16 + dlc;
   const long r0 = (long)blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if (d < D) {
-    for (long r = r0 + rl; r < r1; r += 4) {
+    for (long r = r0 + rl; r < r1; r += 16) {
       const int t = r % L;
       const int s = r / L;
       const int k = s / B, b = s % B;
@@ -369,22 +396,15 @@ __global__ __launch_bounds__(256) void dirconv_bwd_wgrad(int B, int L, int D, co
 #pragma unroll
   for (int j = 0; j < 5; ++j) sh[j][rl][dlc] = acc[j];
   __syncthreads();
-  if (rl == 0 && d < D) {
+  if (threadIdx.x < 80) {
+    const int j = threadIdx.x / 16, dd = threadIdx.x % 16, dg = blockIdx.x * 16 + dd;
+    if (dg < D) {
+      float v = 0.f;
 #pragma unroll
-    for (int j = 0; j < 5; ++j)
-      part[((long)blockIdx.y * D + d) * 5 + j] = sh[j][0][dlc] + sh[j][1][dlc] + sh[j][2][dlc] + sh[j][3][dlc];
+      for (int i = 0; i < 16; ++i) v += sh[j][i][dd];
+      part[(long)blockIdx.y * 5 * D + (j < 4 ? dg * 4 + j : 4 * D + dg)] = v;
+    }
   }
-}
-
-__global__ void dirconv_wgrad_final(int P, int D, const float* __restrict__ part, float* __restrict__ dw,
-                                    float* __restrict__ db) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= D * 5) return;
-  const int d = i / 5, j = i % 5;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[((long)p * D + d) * 5 + j];
-  if (j < 4) dw[d * 4 + j] = s;
-  else db[d] = s;
 }
 
 }  // namespace
@@ -400,10 +420,12 @@ VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order,
   return VC_OK;
 }
 
-static size_t scan_fwd_smem(int L, int R) { return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R); }
+static size_t scan_fwd_smem(int L, int R) {
+  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 4 * (size_t)L * DPB);
+}
 static size_t scan_bwd_smem(int L, int R) {
   const int nck = (L + CK - 1) / CK;
-  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + nck * 256 + 4 * L * 32 + 4);
+  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 5 * (size_t)L * DPB + nck * 256 + 4 * CK * 32 + 4);
 }
 
 VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl, const float* xz,
@@ -464,7 +486,7 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   rc = vc_colsum(nseq, D, p_d, (long)D, dDskip, 0.f, p_rest, rest, stream);
   if (rc) return rc;
   // dg partials are laid out [k][b][chunk]: per direction B*nchunk contiguous values
-  hipLaunchKernelGGL(gate_grad, dim3(1), dim3(64), 0, stream, ndir, B * nchunk, gate_logits, p_g, dgate_logits);
+  hipLaunchKernelGGL(gate_grad, dim3(1), dim3(256), 0, stream, ndir, B * nchunk, gate_logits, p_g, dgate_logits);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -484,14 +506,15 @@ VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order,
   hipLaunchKernelGGL(dirconv_bwd_gather, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, B, L, D, ndir, inv_order,
                      conv_w, du, dz, dxz);
   VC_CHECK_LAUNCH();
-  int rows_per = 256;
+  int rows_per = std::max<long>(64, (rows + 255) / 256);
   while ((long)vc_cdiv(rows, rows_per) * D * 5 > ws_floats) rows_per *= 2;
   const int P = vc_cdiv(rows, rows_per);
-  hipLaunchKernelGGL(dirconv_bwd_wgrad, dim3(vc_cdiv(D, 64), P), dim3(256), 0, stream, B, L, D, order, xz, du, rows,
+  hipLaunchKernelGGL(dirconv_bwd_wgrad, dim3(vc_cdiv(D, 16), P), dim3(256), 0, stream, B, L, D, order, xz, du, rows,
                      rows_per, ws);
   VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(dirconv_wgrad_final, dim3(vc_cdiv(D * 5, 256)), dim3(256), 0, stream, P, D, ws, dconv_w,
-                     dconv_b);
-  VC_CHECK_LAUNCH();
+  int rc = launch_sum_rows(P, 4 * D, ws, 5L * D, 0L, dconv_w, 0.f, stream);
+  if (rc) return rc;
+  rc = launch_sum_rows(P, D, ws, 5L * D, 4L * D, dconv_b, 0.f, stream);
+  if (rc) return rc;
   return VC_OK;
 }

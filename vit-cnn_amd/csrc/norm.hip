@@ -112,30 +112,20 @@ __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, 
   }
 }
 
-// out[c] = beta*out[c] + sum_p part[p*stride + off + c]
-__global__ void reduce_parts(int P, int C, const float* __restrict__ part, long stride, long off,
-                             float* __restrict__ out, float beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(long)p * stride + off + c];
-  out[c] = (beta != 0.f ? beta * out[c] : 0.f) + s;
-}
-
 // ---------------------------------------------------------------- BatchNorm (channels-last)
 __global__ __launch_bounds__(256) void bn_stats_partial(int M, int C, const float* __restrict__ x, long ldx,
-                                                        int rows_per, float* __restrict__ part) {
-  __shared__ float sh[3][4][64];
+                                                        int rows_per, double* __restrict__ part) {
+  __shared__ double sh[3][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per;
   const long r1 = min((long)M, r0 + rows_per);
-  float n = 0.f, mean = 0.f, m2 = 0.f;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
   if (c < C) {
     for (long r = r0 + rl; r < r1; r += 4) {
-      float v = x[r * ldx + c];
-      n += 1.f;
-      float d = v - mean;
+      const double v = x[r * ldx + c];
+      n += 1.0;
+      const double d = v - mean;
       mean += d / n;
       m2 += d * (v - mean);
     }
@@ -146,30 +136,41 @@ __global__ __launch_bounds__(256) void bn_stats_partial(int M, int C, const floa
   __syncthreads();
   if (rl == 0 && c < C) {
     for (int k = 1; k < 4; ++k) welford_merge(n, mean, m2, sh[0][k][cl], sh[1][k][cl], sh[2][k][cl]);
-    float* p = part + ((long)blockIdx.y * C + c) * 3;
+    double* p = part + (long)blockIdx.y * 3 * C + c;
     p[0] = n;
-    p[1] = mean;
-    p[2] = m2;
+    p[C] = mean;
+    p[2 * C] = m2;
   }
 }
 
-__global__ void bn_stats_final(int P, int C, long M, const float* __restrict__ part, float eps, float momentum,
-                               float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                               float* __restrict__ run_mean, float* __restrict__ run_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int p = 0; p < P; ++p) {
-    const float* q = part + ((long)p * C + c) * 3;
-    welford_merge(n, mean, m2, q[0], q[1], q[2]);
-  }
-  const float var = m2 / (float)M;
-  save_mean[c] = mean;
-  save_invstd[c] = rsqrtf(var + eps);
+// block = 16 channels x 16 partial lanes; each lane Chan-merges its partials, then a fixed-order
+// 16-way merge in LDS
+__global__ __launch_bounds__(256) void bn_stats_final(int P, int C, long M, const double* __restrict__ part, float eps,
+                                                      float momentum, float* __restrict__ save_mean,
+                                                      float* __restrict__ save_invstd, float* __restrict__ run_mean,
+                                                      float* __restrict__ run_var) {
+  __shared__ double sh[3][16][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  if (c < C)
+    for (int p = pl; p < P; p += 16) {
+      const double* q = part + (long)p * 3 * C + c;
+      welford_merge(n, mean, m2, q[0], q[C], q[2 * C]);
+    }
+  sh[0][pl][cl] = n;
+  sh[1][pl][cl] = mean;
+  sh[2][pl][cl] = m2;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  for (int k = 1; k < 16; ++k) welford_merge(n, mean, m2, sh[0][k][cl], sh[1][k][cl], sh[2][k][cl]);
+  const double var = m2 / (double)M;
+  save_mean[c] = (float)mean;
+  save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (run_mean) {
-    const float unb = M > 1 ? m2 / (float)(M - 1) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+    const double unb = M > 1 ? m2 / (double)(M - 1) : var;
+    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
+    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
   }
 }
 
@@ -198,53 +199,53 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(int M, int C, const float*
                                                       const float* __restrict__ x, long ldx,
                                                       const float* __restrict__ relu_out, long ldo,
                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                      int rows_per, float* __restrict__ part) {
-  __shared__ float sh[2][4][64];
+                                                      int rows_per, double* __restrict__ part) {
+  __shared__ double sh[2][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per;
   const long r1 = min((long)M, r0 + rows_per);
-  float s1 = 0.f, s2 = 0.f;
+  double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const float mu = mean[c], is = invstd[c];
     for (long r = r0 + rl; r < r1; r += 4) {
       float d = dy[r * lddy + c];
       if (relu_out && !(relu_out[r * ldo + c] > 0.f)) d = 0.f;
       s1 += d;
-      s2 += d * (x[r * ldx + c] - mu) * is;
+      s2 += (double)d * ((x[r * ldx + c] - mu) * is);
     }
   }
   sh[0][rl][cl] = s1;
   sh[1][rl][cl] = s2;
   __syncthreads();
   if (rl == 0 && c < C) {
-    float* p = part + ((long)blockIdx.y * C + c) * 2;
+    double* p = part + (long)blockIdx.y * 2 * C + c;
     p[0] = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-    p[1] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+    p[C] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
   }
 }
 
-__global__ void bn_bwd_final(int P, int C, const float* __restrict__ part, float* __restrict__ sums,
-                             float* __restrict__ dw, float* __restrict__ db, float beta_w) {
+// dw/db from the reduced sums (sums[0:C] = sum dyv, sums[C:2C] = sum dyv*xhat)
+__global__ void bn_bwd_finish(int C, const double* __restrict__ sums, float* __restrict__ dw, float* __restrict__ db,
+                              float beta_w) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int p = 0; p < P; ++p) {
-    s1 += part[((long)p * C + c) * 2];
-    s2 += part[((long)p * C + c) * 2 + 1];
-  }
-  sums[c] = s1;
-  sums[C + c] = s2;
-  if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + s2;
-  if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + s1;
+  if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)sums[C + c];
+  if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)sums[c];
 }
 
 // train: dx = w*invstd*(dyv - s1/M - xhat*s2/M);  eval (sums == null): dx = w*invstd*dyv
 __global__ void bn_bwd_apply(long M, int C, const float* __restrict__ dy, long lddy, const float* __restrict__ x,
                              long ldx, const float* __restrict__ relu_out, long ldo, const float* __restrict__ mean,
                              const float* __restrict__ invstd, const float* __restrict__ w,
-                             const float* __restrict__ sums, float* __restrict__ dx, long lddx, float beta_dx) {
+                             const double* __restrict__ sums, float* __restrict__ dx, long lddx, float beta_dx,
+                             const double* __restrict__ red, float* __restrict__ dw, float* __restrict__ db,
+                             float beta_w) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < C) {
+    if (dw) dw[idx] = (beta_w != 0.f ? beta_w * dw[idx] : 0.f) + (float)red[C + idx];
+    if (db) db[idx] = (beta_w != 0.f ? beta_w * db[idx] : 0.f) + (float)red[idx];
+  }
   if (idx >= M * C) return;
   const long r = idx / C;
   const int c = idx % C;
@@ -253,8 +254,9 @@ __global__ void bn_bwd_apply(long M, int C, const float* __restrict__ dy, long l
   const float is = invstd[c];
   float v;
   if (sums) {
+    const float invM = 1.f / (float)M;
     const float xh = (x[r * ldx + c] - mean[c]) * is;
-    v = w[c] * is * (d - sums[c] / (float)M - xh * sums[C + c] / (float)M);
+    v = w[c] * is * (d - (float)sums[c] * invM - xh * ((float)sums[C + c] * invM));
   } else {
     v = w[c] * is * d;
   }
@@ -263,7 +265,7 @@ __global__ void bn_bwd_apply(long M, int C, const float* __restrict__ dy, long l
 }
 
 int bn_rows_per(long M, int C, long ws_floats, int per_row_floats) {
-  int rows_per = 64;
+  int rows_per = std::max<long>(32, (M + 255) / 256);
   while ((long)vc_cdiv(M, rows_per) * C * per_row_floats > ws_floats || vc_cdiv(M, rows_per) > 2048) rows_per *= 2;
   return rows_per;
 }
@@ -285,21 +287,19 @@ VC_EXPORT int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const f
                                float* db, float beta_w, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(C > 0 && C <= 64 * LN_MAXV && R >= 0);
   if (R == 0) return VC_OK;
-  int rows_per = 16;
+  int rows_per = std::max(16, vc_cdiv(R, 256));
   while ((long)vc_cdiv(R, rows_per) * 2 * C > ws_floats) rows_per *= 2;
   const int P = vc_cdiv(R, rows_per);
   hipLaunchKernelGGL(ln_bwd, dim3(P), dim3(256), 0, stream, R, C, rows_per, dy, lddy, x, ldx, w, mean, rstd, dx,
                      lddx, beta_dx, ws);
   VC_CHECK_LAUNCH();
   if (dw) {
-    hipLaunchKernelGGL(reduce_parts, dim3(vc_cdiv(C, 256)), dim3(256), 0, stream, P, C, ws, (long)2 * C, 0L, dw,
-                       beta_w);
-    VC_CHECK_LAUNCH();
+    int rc = launch_sum_rows(P, C, ws, (long)2 * C, 0L, dw, beta_w, stream);
+    if (rc) return rc;
   }
   if (db) {
-    hipLaunchKernelGGL(reduce_parts, dim3(vc_cdiv(C, 256)), dim3(256), 0, stream, P, C, ws, (long)2 * C, (long)C,
-                       db, beta_w);
-    VC_CHECK_LAUNCH();
+    int rc = launch_sum_rows(P, C, ws, (long)2 * C, (long)C, db, beta_w, stream);
+    if (rc) return rc;
   }
   return VC_OK;
 }
@@ -316,14 +316,17 @@ VC_EXPORT int vc_bn_stats(int train, long M, int C, const float* x, long ldx, fl
     VC_CHECK_LAUNCH();
     return VC_OK;
   }
-  VC_REQUIRE(M > 0);
-  const int rows_per = bn_rows_per(M, C, ws_floats, 3);
+  VC_REQUIRE(M > 0 && ((uintptr_t)ws & 7) == 0);
+  // partial (count, mean, M2) triples are fp64: the workspace holds ws_floats/2 doubles
+  double* wsd = reinterpret_cast<double*>(ws);
+  const long ws_doubles = ws_floats / 2;
+  const int rows_per = bn_rows_per(M, C, ws_doubles, 3);
   const int P = vc_cdiv(M, rows_per);
-  VC_REQUIRE((long)P * C * 3 <= ws_floats);
+  VC_REQUIRE((long)P * C * 3 <= ws_doubles);
   hipLaunchKernelGGL(bn_stats_partial, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, x, ldx, rows_per,
-                     ws);
+                     wsd);
   VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_final, dim3(vc_cdiv(C, 256)), dim3(256), 0, stream, P, C, M, ws, eps, momentum,
+  hipLaunchKernelGGL(bn_stats_final, dim3(vc_cdiv(C, 16)), dim3(256), 0, stream, P, C, M, wsd, eps, momentum,
                      save_mean, save_invstd, run_mean, run_var);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -345,19 +348,28 @@ VC_EXPORT int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, co
                         const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
                         float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w, float* ws,
                         long ws_floats, hipStream_t stream) {
-  VC_REQUIRE(C > 0 && M > 0);
-  const int rows_per = bn_rows_per(M, C, ws_floats - 2L * C, 2);
+  VC_REQUIRE(C > 0 && M > 0 && ((uintptr_t)ws & 7) == 0);
+  // per-row-block partial sums [P][2][C] and the final [2][C] sums are fp64
+  double* wsd = reinterpret_cast<double*>(ws);
+  const long ws_doubles = ws_floats / 2;
+  const int rows_per = bn_rows_per(M, C, ws_doubles - 2L * C, 2);
   const int P = vc_cdiv(M, rows_per);
-  VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_floats);
-  float* sums = ws + (long)P * C * 2;
+  VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_doubles);
+  double* sums = wsd + (long)P * C * 2;
   hipLaunchKernelGGL(bn_bwd_partial, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, dy, lddy, x, ldx,
-                     relu_out, ldo, mean, invstd, rows_per, ws);
+                     relu_out, ldo, mean, invstd, rows_per, wsd);
   VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_bwd_final, dim3(vc_cdiv(C, 256)), dim3(256), 0, stream, P, C, ws, sums, dw, db, beta_w);
+  // one pass over the [P][2C] partials gives both sums (sum dy, sum dy*xhat)
+  hipLaunchKernelGGL(sum_rows_d_kernel, dim3(vc_cdiv(2L * C, 16)), dim3(256), 0, stream, P, 2 * C, wsd, 2L * C, 0L,
+                     sums);
   VC_CHECK_LAUNCH();
   if (dx) {
-    hipLaunchKernelGGL(bn_bwd_apply, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, M, C, dy, lddy, x, ldx,
-                       relu_out, ldo, mean, invstd, w, train ? sums : (const float*)nullptr, dx, lddx, beta_dx);
+    hipLaunchKernelGGL(bn_bwd_apply, dim3(vc_cdiv(std::max<long>(M * C, C), 256)), dim3(256), 0, stream, M, C, dy,
+                       lddy, x, ldx, relu_out, ldo, mean, invstd, w, train ? sums : (const double*)nullptr, dx, lddx,
+                       beta_dx, sums, dw, db, beta_w);
+    VC_CHECK_LAUNCH();
+  } else {
+    hipLaunchKernelGGL(bn_bwd_finish, dim3(vc_cdiv(C, 256)), dim3(256), 0, stream, C, sums, dw, db, beta_w);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;

@@ -50,77 +50,85 @@ __global__ __launch_bounds__(256) void pixel_stats(long M, int C, const float* _
   }
 }
 
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  v = wave_sum(v);
+constexpr int TLT = 1024;  // threads per token block (16 waves): the token's B*HW elements are the long axis
+
+// Reductions over a token's B*HW elements accumulate in fp64, like torch's CPU BatchNorm
+// (acc_type<float> = double): these BN(1) inputs have a tiny spread around a large mean, so
+// fp32 sums lose ~3 digits in the statistics and in the backward's dgamma / dbeta / dx terms.
+__device__ __forceinline__ double block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) red[w] = v;
   __syncthreads();
-  const float r = red[0] + red[1] + red[2] + red[3];
+  double r = 0.0;
+#pragma unroll
+  for (int i = 0; i < TLT / 64; ++i) r += red[i];
   __syncthreads();
   return r;
 }
 
 // one block per token s; a[(b*S + s)*HW + p]
-__global__ __launch_bounds__(256) void attn_fwd(int train, int B, int HW, int S, const float* __restrict__ mx,
+__global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S, const float* __restrict__ mx,
                                                 const float* __restrict__ avg, const float* __restrict__ par,
                                                 float* __restrict__ buf, float eps, float momentum,
-                                                float* __restrict__ stats, float* __restrict__ a) {
-  __shared__ float red[4];
+                                                double* __restrict__ stats, float* __restrict__ a) {
+  __shared__ double red[TLT / 64];
   const int s = blockIdx.x;
   const float* p = par + (long)s * TPAR;
   const float w0 = p[0], w1 = p[1], bc = p[2], gam = p[3], bet = p[4];
   const long n = (long)B * HW;
-  float mean, invstd;
+  double mean, invstd;
   if (train) {
-    float acc = 0.f;
-    for (long i = threadIdx.x; i < n; i += 256) acc += w0 * mx[i] + w1 * avg[i] + bc;
-    mean = block_sum(acc, red) / (float)n;
-    float q = 0.f;
-    for (long i = threadIdx.x; i < n; i += 256) {
-      const float d = w0 * mx[i] + w1 * avg[i] + bc - mean;
+    double acc = 0.0;
+    for (long i = threadIdx.x; i < n; i += TLT) acc += (double)(w0 * mx[i] + w1 * avg[i] + bc);
+    mean = block_sum(acc, red) / (double)n;
+    double q = 0.0;
+    for (long i = threadIdx.x; i < n; i += TLT) {
+      const double d = (double)(w0 * mx[i] + w1 * avg[i] + bc) - mean;
       q += d * d;
     }
-    const float m2 = block_sum(q, red);
-    const float var = m2 / (float)n;
-    invstd = rsqrtf(var + eps);
+    const double m2 = block_sum(q, red);
+    const double var = m2 / (double)n;
+    invstd = 1.0 / sqrt(var + (double)eps);
     if (threadIdx.x == 0 && buf) {
       float* bb = buf + (long)s * TBUF;
-      const float unb = n > 1 ? m2 / (float)(n - 1) : var;
-      bb[0] = (1.f - momentum) * bb[0] + momentum * mean;
-      bb[1] = (1.f - momentum) * bb[1] + momentum * unb;
+      const double unb = n > 1 ? m2 / (double)(n - 1) : var;
+      bb[0] = (float)((1.0 - momentum) * bb[0] + momentum * mean);
+      bb[1] = (float)((1.0 - momentum) * bb[1] + momentum * unb);
     }
   } else {
     const float* bb = buf + (long)s * TBUF;
     mean = bb[0];
-    invstd = rsqrtf(bb[1] + eps);
+    invstd = 1.0 / sqrt((double)bb[1] + (double)eps);
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // saved as (mean, invstd) in fp64 for the backward
     stats[2 * s] = mean;
     stats[2 * s + 1] = invstd;
   }
-  for (long i = threadIdx.x; i < n; i += 256) {
+  for (long i = threadIdx.x; i < n; i += TLT) {
     const float f = w0 * mx[i] + w1 * avg[i] + bc;
-    const float bn = (f - mean) * invstd * gam + bet;
+    const float bn = (float)(((double)f - mean) * invstd) * gam + bet;
     const long b = i / HW, q = i % HW;
     a[((long)b * S + s) * HW + q] = sigmoid_f(fmaxf(bn, 0.f));
   }
 }
 
 // one block per token: da -> df[s][i] (grad of the 2->1 conv output) + the token's 5 param grads
-__global__ __launch_bounds__(256) void attn_bwd(int train, int B, int HW, int S, const float* __restrict__ mx,
+__global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S, const float* __restrict__ mx,
                                                 const float* __restrict__ avg, const float* __restrict__ par,
-                                                const float* __restrict__ stats, const float* __restrict__ da,
+                                                const double* __restrict__ stats, const float* __restrict__ da,
                                                 float* __restrict__ df, float* __restrict__ gpar) {
-  __shared__ float red[4];
+  __shared__ double red[TLT / 64];
   const int s = blockIdx.x;
   const float* p = par + (long)s * TPAR;
   const float w0 = p[0], w1 = p[1], bc = p[2], gam = p[3], bet = p[4];
-  const float mean = stats[2 * s], invstd = stats[2 * s + 1];
+  const double mean = stats[2 * s], invstd = stats[2 * s + 1];
   const long n = (long)B * HW;
-  float s1 = 0.f, s2 = 0.f;
-  for (long i = threadIdx.x; i < n; i += 256) {
-    const float xh = (w0 * mx[i] + w1 * avg[i] + bc - mean) * invstd;
-    const float bn = xh * gam + bet;
+  double s1 = 0.0, s2 = 0.0;
+  for (long i = threadIdx.x; i < n; i += TLT) {
+    const double xh = ((double)(w0 * mx[i] + w1 * avg[i] + bc) - mean) * invstd;
+    const float bn = (float)xh * gam + bet;
     const long b = i / HW, q = i % HW;
     float g1 = 0.f;
     if (bn > 0.f) {
@@ -132,18 +140,18 @@ __global__ __launch_bounds__(256) void attn_bwd(int train, int B, int HW, int S,
   }
   s1 = block_sum(s1, red);
   s2 = block_sum(s2, red);
-  float gw0 = 0.f, gw1 = 0.f, gb = 0.f;
-  for (long i = threadIdx.x; i < n; i += 256) {
-    const float xh = (w0 * mx[i] + w1 * avg[i] + bc - mean) * invstd;
-    const float bn = xh * gam + bet;
+  double gw0 = 0.0, gw1 = 0.0, gb = 0.0;
+  for (long i = threadIdx.x; i < n; i += TLT) {
+    const double xh = ((double)(w0 * mx[i] + w1 * avg[i] + bc) - mean) * invstd;
+    const float bn = (float)xh * gam + bet;
     const long b = i / HW, q = i % HW;
     float g1 = 0.f;
     if (bn > 0.f) {
       const float sg = sigmoid_f(bn);
       g1 = da[((long)b * S + s) * HW + q] * sg * (1.f - sg);
     }
-    const float d = train ? gam * invstd * (g1 - s1 / (float)n - xh * s2 / (float)n) : gam * invstd * g1;
-    df[(long)s * n + i] = d;
+    const double d = train ? gam * invstd * (g1 - s1 / (double)n - xh * s2 / (double)n) : gam * invstd * g1;
+    df[(long)s * n + i] = (float)d;
     gw0 += d * mx[i];
     gw1 += d * avg[i];
     gb += d;
@@ -153,11 +161,11 @@ __global__ __launch_bounds__(256) void attn_bwd(int train, int B, int HW, int S,
   gb = block_sum(gb, red);
   if (threadIdx.x == 0) {
     float* g = gpar + (long)s * TPAR;
-    g[0] = gw0;
-    g[1] = gw1;
-    g[2] = gb;
-    g[3] = s2;
-    g[4] = s1;
+    g[0] = (float)gw0;
+    g[1] = (float)gw1;
+    g[2] = (float)gb;
+    g[3] = (float)s2;
+    g[4] = (float)s1;
   }
 }
 
@@ -193,18 +201,18 @@ VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx,
 }
 
 VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          float* bn_buffers, float eps, float momentum, float* stats, float* a, hipStream_t stream) {
+                          float* bn_buffers, float eps, float momentum, double* stats, float* a, hipStream_t stream) {
   VC_REQUIRE(B > 0 && HW > 0 && S > 0);
-  hipLaunchKernelGGL(attn_fwd, dim3(S), dim3(256), 0, stream, train, B, HW, S, mx, avg, params, bn_buffers, eps,
+  hipLaunchKernelGGL(attn_fwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, S, mx, avg, params, bn_buffers, eps,
                      momentum, stats, a);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
 
 VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          const float* stats, const float* da, float* df, float* dparams, hipStream_t stream) {
+                          const double* stats, const float* da, float* df, float* dparams, hipStream_t stream) {
   VC_REQUIRE(B > 0 && HW > 0 && S > 0);
-  hipLaunchKernelGGL(attn_bwd, dim3(S), dim3(256), 0, stream, train, B, HW, S, mx, avg, params, stats, da, df,
+  hipLaunchKernelGGL(attn_bwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, S, mx, avg, params, stats, da, df,
                      dparams);
   VC_CHECK_LAUNCH();
   return VC_OK;

@@ -322,17 +322,18 @@ class _Program:
               relu=0):
         """C[M,N] = alpha * A[M,K] W[N,K]^T + beta*C + bias + addend"""
         self.L.vc_gemm(0, 1, M, N, K, alpha, A, lda, 0, W, ldw, 0, beta, C, ldc, 0, 1, bias or None, add or None,
-                       add_ld, add_mod, relu, self.scr_p, self.scr_n, self.s)
+                       add_ld, add_mod, relu, None, self.scr_p, self.scr_n, self.s)
 
     def mm_nn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0):
         """C[M,N] = alpha * A[M,K] B[K,N] + beta*C"""
         self.L.vc_gemm(0, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
-                       self.scr_p, self.scr_n, self.s)
+                       None, self.scr_p, self.scr_n, self.s)
 
-    def mm_tn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0):
-        """C[M,N] = alpha * A^T B, A stored [K, M] (weight gradients: M,N small, K = rows)"""
+    def mm_tn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0, bias_grad=0):
+        """C[M,N] = alpha * A^T B, A stored [K, M] (weight gradients: M,N small, K = rows);
+        bias_grad[M] (optional) = alpha * column sums of A, fused into the same GEMM"""
         self.L.vc_gemm(1, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
-                       self.scr_p, self.scr_n, self.s)
+                       bias_grad or None, self.scr_p, self.scr_n, self.s)
 
     def colsum(self, R, C, X, ldx, out, beta=0.0):
         self.L.vc_colsum(R, C, X, ldx, out, beta, self.scr_p, self.scr_n, self.s)
@@ -385,12 +386,13 @@ class _Program:
         mx, amx, avg = ws.f(pfx + ".mx", rows), ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), ws.f(pfx + ".avg",
                                                                                                            rows)
         self.L.vc_tl_pixel_stats(rows, C, X, C, mx, amx, avg, self.s)
-        st, a = ws.f(pfx + ".st", 2 * S), ws.f(pfx + ".a", B * S * L_)
+        st = ws.get(pfx + ".st", 2 * S, torch.float64).data_ptr()
+        a = ws.f(pfx + ".a", B * S * L_)
         self.L.vc_tl_attn_fwd(self.train, B, L_, S, mx, avg, self.P[pfx + ".tokenizers.0.conv.0.weight"],
                               self.BUF[pfx + ".tokenizers.0.conv.1.running_mean"], BN_EPS, BN_MOM, st, a, self.s)
         Z = ws.f(pfx + ".Z", B * S * C)
         self.L.vc_gemm(0, 0, S, C, L_, 1.0 / L_, a, L_, S * L_, X, C, L_ * C, 0.0, Z, C, S * C, B, None, None, 0, 0, 0,
-                       self.scr_p, self.scr_n, self.s)
+                       None, self.scr_p, self.scr_n, self.s)
         return Z
 
     def block(self, blk, pfx, X, H):
@@ -506,9 +508,7 @@ class _Program:
     def linear_bwd(self, wname, bname, dY, M, N, K, X, ldx, dX, beta_dx, lddy=None):
         """Y[M,N] = X[M,K] W[N,K]^T + b:  dW = dY^T X, db = colsum(dY), dX (+)= dY W."""
         lddy = lddy or N
-        self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K)
-        if bname:
-            self.colsum(M, N, dY, lddy, self.G[bname])
+        self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K, bias_grad=self.G[bname] if bname else 0)
         if dX:
             self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
 
@@ -543,12 +543,12 @@ class _Program:
         """dX (overwritten) = gradient of the TokenLearner input."""
         B, ws = self.B, self.ws
         rows = B * L_
-        a, st = ws.f(pfx + ".a", B * S * L_), ws.f(pfx + ".st", 2 * S)
+        a, st = ws.f(pfx + ".a", B * S * L_), ws.get(pfx + ".st", 2 * S, torch.float64).data_ptr()
         da = ws.f(pfx + ".da", B * S * L_)
         self.L.vc_gemm(0, 1, S, L_, C, 1.0 / L_, dZ, C, S * C, X, C, L_ * C, 0.0, da, L_, S * L_, B, None, None, 0, 0,
-                       0, self.scr_p, self.scr_n, self.s)
+                       0, None, self.scr_p, self.scr_n, self.s)
         self.L.vc_gemm(1, 0, L_, C, S, 1.0 / L_, a, L_, S * L_, dZ, C, S * C, 0.0, dX, C, L_ * C, B, None, None, 0, 0,
-                       0, self.scr_p, self.scr_n, self.s)
+                       0, None, self.scr_p, self.scr_n, self.s)
         df = ws.f(pfx + ".df", S * rows)
         par = self.P[pfx + ".tokenizers.0.conv.0.weight"]
         self.L.vc_tl_attn_bwd(self.train, B, L_, S, ws.f(pfx + ".mx", rows), ws.f(pfx + ".avg", rows), par, st, da, df,
@@ -626,8 +626,7 @@ class _Program:
         nr = NDIR * rows
         # dt_proj: dt_lin = xdbl[:, :R] W_dt^T + b_dt
         self.mm_nn(nr, R, D, dDTL, D, P[mx + ".dt_proj.weight"], R, dXD, XW)
-        self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R)
-        self.colsum(nr, D, dDTL, D, G[mx + ".dt_proj.bias"])
+        self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, bias_grad=G[mx + ".dt_proj.bias"])
         # x_proj: xdbl = u W_x^T
         self.linear_bwd(mx + ".x_proj.weight", None, dXD, nr, XW, D, U, D, dU, 1.0)
         dXZ = f(pfx + ".dXZ", rows * 2 * D)
