@@ -187,4 +187,24 @@ VC_API int vc_index_add_i64(int n, const int* idx, long long* ptr, long long val
 VC_API int vc_relu_bwd(long n, const float* dy, const float* y, float* dx, hipStream_t stream);
 VC_API int vc_fill(long n, float* ptr, float value, hipStream_t stream);
 
+/* ---------------------------------------------------------------- patch windows (callers of the step)
+ * The reference cuts patches on the host: MultiModalX.__getitem__ (datasets.py:550-593) for
+ * training batches and sliding_window/grouper + np.copy for whole-image inference
+ * (utils.py:357-415, :567-582; model_utils.py:1067-1132).  Here the image cube stays resident in
+ * HBM in its source layout, img[x][y][c] ([W][H][C], band-contiguous, fp32), and windows are
+ * gathered on the device straight into the model's [n][C][P][P] input layout.
+ *
+ * Window i's top-left corner: corners != NULL -> (corners[2i], corners[2i+1]);
+ * corners == NULL -> the (k0+i)-th window of sliding_window(step, (P,P)), row-major over
+ * (x outer, y inner) with the reference's clamping of the last window to W-P / H-P.
+ * xform (optional, training augmentation of datasets.py:511-526): bit0 = np.fliplr, bit1 = np.flipud
+ * (applied in that order), bits 2-3 = k of np.rot90(patch, k) (applied when no flip bit is set). */
+VC_API int vc_window_count(int W, int H, int P, int step, long* count);
+VC_API int vc_patch_gather(int W, int H, int C, int P, const float* cube, const int* corners, long k0, int step,
+                           int n, const unsigned char* xform, float* out, hipStream_t stream);
+/* probs[(x + P/2) * H + (y + P/2)][c] += (double)logits[i][c] for each window i (center_pixel
+ * mode of model_utils.py:1126-1128; windows are distinct, so no two i share a centre) */
+VC_API int vc_center_accumulate(int W, int H, int P, int ncls, const int* corners, long k0, int step, int n,
+                                const float* logits, double* probs, hipStream_t stream);
+
 #endif /* VITCNN_H */

@@ -1,0 +1,108 @@
+"""Data-parallel path on CPU processes (gloo, world size 2): the exchange step of SURVEY.md 8(e).
+
+Each rank computes the oracle gradient of its own shard (the per-rank B-patch step, BatchNorm
+local as in the MI355X path), writes it into the model's flat gradient layout and calls
+`parallel.allreduce_gradients`; the result must equal the mean of both shards' gradients computed
+in one process.  Parameter / buffer broadcasts are checked the same way.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import golden_batch, hash_state_dict
+
+B_SHARD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard_grad(model, sd, r):
+    """oracle gradient of shard r in the model's flat layout"""
+    from oracle import vitcnn_oracle as O
+    hsi, lidar, target = golden_batch("golden.b4", 4)
+    sl = slice(r * B_SHARD, (r + 1) * B_SHARD)
+    st = O.make_state(sd)
+    O.train_step(st, hsi[sl], lidar[sl], target[sl], O.ce_class_weights(16))
+    flat = torch.zeros(model.flat_params.numel())
+    for n, off in model._poff.items():
+        g = st[n].grad
+        if g is not None:
+            flat[off:off + g.numel()] = g.reshape(-1)
+    return flat
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from vitcnn_amd import Multimodality_Mamba, parallel
+    r, w, _ = parallel.init_from_env(backend="gloo")
+    assert (r, w) == (rank, world) and parallel.is_distributed()
+    sd = hash_state_dict()
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
+    m.load_state_dict(sd)
+    # replicas diverge, then broadcast_parameters makes them identical to rank 0
+    with torch.no_grad():
+        m.flat_params.add_(float(rank))
+        m.flat_buffers()[0].add_(float(rank))
+    parallel.broadcast_parameters(m)
+    parallel.broadcast_buffers(m)
+    ok_bcast = bool(torch.equal(m.flat_params.detach(), _load(sd).flat_params.detach()))
+    ok_buf = bool(torch.equal(m.flat_buffers()[0], _load(sd).flat_buffers()[0]))
+    m.flat_params.grad = _shard_grad(m, sd, rank)
+
+    class _Opt:
+        grad_scale = 1.0
+
+    opt = _Opt()
+    parallel.allreduce_gradients(m, opt)
+    g = m.flat_params.grad * opt.grad_scale
+    if rank == 0:
+        out.put((ok_bcast, ok_buf, g[: m.n_active_params].clone(), float(opt.grad_scale),
+                 float(m.flat_params.grad[m.n_active_params:].abs().sum())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _load(sd):
+    from vitcnn_amd import Multimodality_Mamba
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
+    m.load_state_dict(sd)
+    return m
+
+
+def test_allreduce_equals_mean_of_shard_gradients():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        ok_bcast, ok_buf, g, scale, tail = q.get(timeout=600)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert ok_bcast and ok_buf
+    assert scale == 0.5 and tail == 0.0
+    sd = hash_state_dict()
+    m = _load(sd)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(2)  # the workers' thread count: same CPU reduction order
+    try:
+        ref = (_shard_grad(m, sd, 0) + _shard_grad(m, sd, 1))[: m.n_active_params] / 2
+    finally:
+        torch.set_num_threads(nt)
+    err = float((g - ref).abs().max() / ref.abs().max())
+    assert err < 1e-6, err

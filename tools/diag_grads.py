@@ -9,7 +9,7 @@ for p in (REPO, os.path.join(REPO, "vit-cnn_amd"), os.path.join(REPO, "tests")):
 
 import torch  # noqa: E402
 
-from helpers import golden_batch, hash_state_dict  # noqa: E402
+from helpers import golden_batch, hash_state_dict, masked_oracle_step, relu_masks_from_workspace  # noqa: E402
 from oracle import vitcnn_oracle as O  # noqa: E402
 from vitcnn_amd import CrossEntropyLoss, Multimodality_Mamba  # noqa: E402
 
@@ -21,14 +21,15 @@ def main():
     w = O.ce_class_weights(16)
     st32 = O.make_state(sd)
     O.train_step(st32, hsi, lidar, target, w)
-    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
-    st64 = O.make_state(sd64)
-    O.train_step(st64, hsi.double(), lidar.double(), target, w.double())
     m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
     m.load_state_dict(sd)
     m = m.cuda().train()
     loss = CrossEntropyLoss(weight=w.cuda())(m(hsi.cuda(), lidar.cuda()), target.cuda())
     loss.backward()
+    torch.cuda.synchronize()
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    st64 = O.make_state(sd64)
+    masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(), relu_masks_from_workspace(m, B))
     flat = m.flat_params.grad.detach().cpu().double()
     named = dict(m.named_parameters())
     rows = []

@@ -202,6 +202,11 @@ class Multimodality_Mamba(nn.Module):
         hsiMamba.tokenlearner / ln3 parameters the reference never calls)."""
         return self._n_active
 
+    def flat_buffers(self):
+        """(fp32 running statistics, int64 num_batches_tracked) — every buffer of the model lives
+        in one of these two tensors (one broadcast each for data-parallel buffer sync)."""
+        return self._bflat, self._iflat
+
     def zero_grad(self, set_to_none: bool = True):
         super().zero_grad(set_to_none=set_to_none)
         if set_to_none:

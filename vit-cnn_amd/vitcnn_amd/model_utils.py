@@ -1,0 +1,205 @@
+"""Plugin surface of the reference (`model_utils.py`) for the ViT-CNN path, over the MI355X model.
+
+Same names, arguments, defaults and error behaviour as the reference functions this file
+replaces, so `main.py`-style drivers switch by changing one import:
+
+* `get_model(name, **kwargs) -> (model, optimizer, criterion, kwargs)`  — model_utils.py:47-511,
+  ViT-CNN branch :297-313, defaults :493-510, unknown name -> KeyError (:488-489).
+* `train(savename, run, bands, net, optimizer, criterion, data_loader, epoch, ...)` — :854-1045.
+* `save_model(savename, model, model_name, dataset_name, train_state, type, **kwargs)` — :1047-1064.
+* `test(run, net, img1, img2, hyperparams) -> probs[W, H, n_classes]` — :1067-1132.
+* `val(net, data_loader, device, supervision) -> accuracy` — :1135-1158.
+
+Only "Multimodality_Mamba" (the README's "ViT-CNN (ours)") is registered: the reference's other
+branches import modules that are absent from the reference tree and
+are out of scope for this path.
+
+Data parallelism: when a torch.distributed process group with more than
+one rank is initialised, `train` all-reduces the flat gradient after every backward (one RCCL
+call) and folds the 1/world average into the fused AdamW update; each rank iterates its own
+shard of the patches (see `parallel.shard_indices`).
+"""
+from __future__ import annotations
+
+import copy
+import datetime
+import os
+import re
+
+import numpy as np
+import torch
+
+from . import parallel
+from .losses import CrossEntropyLoss
+from .model import Multimodality_Mamba
+from .optim import AdamW
+from .window import SlidingWindowInference
+
+REGISTERED = ("Multimodality_Mamba",)
+
+
+def camel_to_snake(name: str) -> str:
+    """utils.py camel_to_snake: 'Multimodality_Mamba' -> 'multimodality__mamba'."""
+    s = re.sub("(.)([A-Z][a-z]+)", r"\1_\2", name)
+    return re.sub("([a-z0-9])([A-Z])", r"\1_\2", s).lower()
+
+
+def get_model(name, **kwargs):
+    """Instantiate the model, optimizer and criterion with the reference's defaults.
+
+    Required kwargs (as in the reference): n_classes, n_bands=(hsi_bands, lidar_bands),
+    ignored_labels, dataset.  `device` defaults to the first ROCm device (the MI355X path has no
+    CPU execution; the reference defaults to CPU).
+    """
+    if name not in REGISTERED:
+        raise KeyError("{} model is unknown.".format(name))
+    device = kwargs.setdefault("device", torch.device("cuda" if torch.cuda.is_available() else "cpu"))
+    n_classes = kwargs["n_classes"]
+    (n_bands, n_bands2) = kwargs["n_bands"]
+    weights = torch.ones(n_classes)
+    weights[torch.LongTensor(list(kwargs["ignored_labels"]))] = 0.0
+    weights = weights.to(device)
+    weights = kwargs.setdefault("weights", weights)
+    kwargs.setdefault("patch_size", 9)
+    patch_size = kwargs["patch_size"]
+    center_pixel = True
+    embed_dim = 64 // 2
+    kwargs.setdefault("applyPCA", False)
+    if kwargs["applyPCA"]:
+        n_bands = 30
+    path_type = "multi_clock_gate"
+    model = Multimodality_Mamba(img_size=patch_size, patch_size=1, stride=1, in_channels1=n_bands,
+                                in_channels2=n_bands2, dim_embedding=embed_dim, num_class=n_classes,
+                                path_type=path_type)
+    lr = kwargs.setdefault("lr", 8e-4)
+    model = model.to(device)
+    optimizer = AdamW(model.parameters(), lr=lr)
+    criterion = CrossEntropyLoss(weight=kwargs["weights"])
+    kwargs.setdefault("epoch", 200)
+    kwargs.setdefault("batch_size", 64)
+    kwargs.setdefault("scheduler", torch.optim.lr_scheduler.StepLR(optimizer, step_size=30, gamma=0.9))
+    kwargs.setdefault("supervision", "full")
+    kwargs.setdefault("flip_augmentation", False)
+    kwargs.setdefault("radiation_augmentation", False)
+    kwargs.setdefault("mixture_augmentation", False)
+    kwargs["center_pixel"] = center_pixel
+    return model, optimizer, criterion, kwargs
+
+
+def save_model(savename, model, model_name, dataset_name, train_state, type, **kwargs):
+    """Checkpoint scheme of model_utils.py:1047-1064: a plain state_dict (the reference's 1704 keys)
+    at ./checkpoints/<model>/<dataset>/<train_state>/<type>/<time><savename>_run{run}_epoch{epoch}_{metric:.2f}.pth.
+    Only rank 0 writes under data parallelism."""
+    if parallel.rank() != 0:
+        return None
+    model_dir = "./checkpoints/" + model_name + "/" + dataset_name + "/" + train_state + "/" + type + "/"
+    time_str = datetime.datetime.now().strftime("%Y_%m_%d_%H_%M_%S")
+    os.makedirs(model_dir, exist_ok=True)
+    if not isinstance(model, torch.nn.Module):
+        raise TypeError("save_model: only torch modules are checkpointed on this path")
+    filename = time_str + savename + "_run{run}_epoch{epoch}_{metric:.2f}".format(**kwargs)
+    path = model_dir + filename + ".pth"
+    torch.save({k: v.detach().cpu() for k, v in model.state_dict().items()}, path)
+    return path
+
+
+def train(savename, run, bands, net, optimizer, criterion, data_loader, epoch, scheduler=None, display_iter=100,
+          device=torch.device("cpu"), display=None, val_loader=None, supervision="full"):
+    """Training loop of model_utils.py:854-1045 (per-iteration loss.item(), scheduler per epoch,
+    best-state tracking, best/final checkpoints).  `display` (visdom) is optional here."""
+    if criterion is None:
+        raise Exception("Missing criterion. You must specify a loss function.")
+    if supervision != "full":
+        raise ValueError('supervision mode "{}" is unknown.'.format(supervision))
+    net.to(device)
+    save_epoch = 16 if epoch == 128 else (epoch // 20 if epoch > 20 else 1)
+    best_val_acc = 0.0
+    best_model_wts = None
+    losses = []
+    iter_ = 1
+    val_accuracies = []
+    for e in range(1, epoch + 1):
+        net.train()
+        avg_loss = 0.0
+        nb = 0
+        for batch_idx, (data, data2, target) in enumerate(data_loader):
+            data, data2, target = data.to(device), data2.to(device), target.to(device)
+            optimizer.zero_grad()
+            output = net(data, data2)
+            loss = criterion(output, target)
+            loss.backward()
+            parallel.allreduce_gradients(net, optimizer)
+            optimizer.step()
+            lv = loss.item()
+            avg_loss += lv
+            losses.append(lv)
+            nb += 1
+            if display_iter and iter_ % display_iter == 0 and parallel.rank() == 0:
+                mean_loss = float(np.mean(losses[max(0, len(losses) - 101):]))
+                print("Train (epoch {}/{}) [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
+                    e, epoch, batch_idx * len(data), len(data) * len(data_loader),
+                    100.0 * batch_idx / max(len(data_loader), 1), mean_loss), flush=True)
+                if display is not None and hasattr(display, "line"):
+                    display.line(X=np.arange(len(losses)), Y=np.asarray(losses), win="loss")
+            iter_ += 1
+        avg_loss /= max(nb, 1)
+        if val_loader is not None:
+            val_acc = val(net, val_loader, device=device, supervision=supervision)
+            val_accuracies.append(val_acc)
+            metric = -val_acc
+        else:
+            metric = avg_loss
+        if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+            scheduler.step(metric)
+        elif scheduler is not None:
+            scheduler.step()
+        if abs(metric) >= best_val_acc:
+            best_val_acc = abs(metric)
+            parallel.broadcast_buffers(net)
+            best_model_wts = copy.deepcopy(net.state_dict())
+            if e % save_epoch == 0:
+                save_model(savename, net, camel_to_snake(str(net.__class__.__name__)), data_loader.dataset.name,
+                           train_state="train", type="best_epoch", run=run, epoch=e, metric=abs(metric))
+        if e == epoch:
+            parallel.broadcast_buffers(net)
+            save_model(savename, net, camel_to_snake(str(net.__class__.__name__)), data_loader.dataset.name,
+                       train_state="train", type="final_epoch", run=run, epoch=e, metric=abs(metric))
+    return best_model_wts
+
+
+def val(net, data_loader, device="cpu", supervision="full"):
+    """model_utils.py:1135-1158: argmax accuracy over samples whose PREDICTION is not an ignored
+    label.  Like the reference, the network is not switched to eval mode (it runs in whatever
+    mode it is in — train mode when called from `train`).  The per-sample `.item()` loop becomes
+    an on-device comparison with one host sync per batch."""
+    ignored = sorted(set(getattr(data_loader.dataset, "ignored_labels", [])))
+    correct, total = 0, 0
+    for data, data2, target in data_loader:
+        with torch.no_grad():
+            data, data2, target = data.to(device), data2.to(device), target.to(device)
+            output = net(data, data2)
+            if isinstance(output, tuple):
+                output = output[0]
+            pred = output.argmax(dim=1).view(-1)
+            keep = torch.ones_like(pred, dtype=torch.bool)
+            for lab in ignored:
+                keep &= pred != lab
+            correct += int(((pred == target.view(-1)) & keep).sum())
+            total += int(keep.sum())
+    return correct / total
+
+
+def test(run, net, img1, img2, hyperparams):
+    """Whole-image inference of model_utils.py:1067-1132 (center-pixel mode): eval-mode forward over
+    every sliding window, probabilities accumulated at the window centres.  The image is uploaded
+    once; windows are gathered on the device (vc_window_gather) and the logits scattered into an
+    fp64 probability map on the device (vc_center_accumulate), so the Python generator + np.copy
+    per window of the reference disappears.  Returns a float64 numpy array [W, H, n_classes] like
+    the reference's `probs`."""
+    net.eval()
+    if hyperparams.get("applyPCA", False):
+        raise NotImplementedError("applyPCA is not on the ViT-CNN path")
+    runner = SlidingWindowInference(net, img1, img2, patch_size=hyperparams["patch_size"],
+                                    step=hyperparams.get("test_stride", 1), n_classes=hyperparams["n_classes"],
+                                    device=hyperparams["device"])
+    return runner.run(batch_size=hyperparams["batch_size"])
