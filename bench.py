@@ -125,7 +125,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba
+    from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba, fused_train_step
     torch.manual_seed(0)
     model = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16, "multi_clock_gate").to(dev).train()
     if world > 1:
@@ -139,10 +139,9 @@ def main():
     holder = {}
 
     def fwd_bwd():
-        logits = model(hsi, lidar)
-        loss = crit(logits, target)
-        loss.backward()
-        holder["loss"] = loss
+        # forward + weighted CE + backward issued from this thread (vitcnn_amd/step.py), so the
+        # step's side streams are captured with it
+        holder["loss"] = fused_train_step(model, crit, hsi, lidar, target)
 
     def allreduce():
         if world > 1:

@@ -178,7 +178,8 @@ VC_API int vc_ce_fwd(int B, int ncls, const float* logits, const long long* targ
 VC_API int vc_ce_bwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
                      long long ignore_index, const float* grad_out, float* dlogits, hipStream_t stream);
 /* torch.optim.AdamW step (model_utils.py:309-310) over a flat buffer; hyper = device
- * [lr, beta1, beta2, eps, weight_decay, grad_scale]; *step (device float) is incremented first */
+ * [lr, beta1, beta2, eps, weight_decay, grad_scale]; step = device float[3] state: step[0] = t is
+ * incremented first, step[1..2] receive the bias corrections (1 - beta1^t, sqrt(1 - beta2^t)) */
 VC_API int vc_adamw(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                     const float* hyper, float* step, hipStream_t stream);
 /* ptr[idx[i]] += val  (BatchNorm num_batches_tracked counters) */

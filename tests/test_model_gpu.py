@@ -222,3 +222,46 @@ def test_b64_against_reference_golden():
             assert gn == 0.0, n
         else:
             assert abs(gn - ref_n) <= 2e-3 * ref_n + atol, (n, gn, float(ref_n))
+
+
+def test_fused_step_and_graph_capture_match_autograd():
+    """fused_train_step (caller-thread, multi-stream) == crit(model(x)).backward() (autograd), bit for
+    bit, and a hipGraph capture of either replays to the same gradients."""
+    _need_gpu()
+    from vitcnn_amd import CrossEntropyLoss, fused_train_step
+    sd = hash_state_dict()
+    hsi, lidar, target = (t.to(DEV) for t in golden_batch("golden.b64", 64))
+    crit = CrossEntropyLoss(weight=O.ce_class_weights(16).to(DEV))
+    m = _product(sd).train()
+    loss_a = crit(m(hsi, lidar), target)
+    loss_a.backward()
+    g_auto = m.flat_params.grad.clone()
+    m2 = _product(sd).train()
+    loss_f = fused_train_step(m2, crit, hsi, lidar, target)
+    torch.cuda.synchronize()
+    assert float(loss_a) == float(loss_f)
+    assert torch.equal(m2.flat_params.grad, g_auto)
+    for use_fused in (True, False):
+        m3 = _product(sd).train()
+        holder = {}
+
+        def step():
+            if use_fused:
+                holder["l"] = fused_train_step(m3, crit, hsi, lidar, target)
+            else:
+                holder["l"] = crit(m3(hsi, lidar), target)
+                holder["l"].backward()
+
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        m3.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        m3.load_state_dict(sd)  # the warm-up step above updated the BN running statistics
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(m3.flat_params.grad, g_auto), use_fused

@@ -27,6 +27,36 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 static inline int vc_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Division by a launch-time constant without the integer-divide sequence: q = (mulhi(n, mul) + n) >> shr,
+// exact for 0 <= n < 2^31 and any divisor >= 1 (Granlund-Montgomery round-up multiplier).  Elementwise
+// kernels index with 32-bit ints (every tensor of the step has < 2^31 elements; checked on the host).
+struct FastDiv {
+  uint32_t div, mul, shr;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.div = d;
+  uint32_t p = 0;
+  while ((1ull << p) < d) ++p;
+  f.shr = p;
+  f.mul = (uint32_t)((((1ull << p) - d) << 32) / d + 1);
+  return f;
+}
+
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)((__umulhi((uint32_t)n, f.mul) + (uint32_t)n) >> f.shr);
+}
+
+// n = q * div + r
+__device__ __forceinline__ int fdivmod(int n, const FastDiv& f, int& r) {
+  const int q = fdiv(n, f);
+  r = n - q * (int)f.div;
+  return q;
+}
+
+#define VC_REQUIRE_I32(n) VC_REQUIRE((long)(n) < (1L << 31))
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

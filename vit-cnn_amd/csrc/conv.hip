@@ -29,24 +29,23 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc(int B, int C, int HW, const 
   }
 }
 
-__global__ void im2col3x3(int B, int H, int W, int C, const float* __restrict__ x, const float* __restrict__ mean,
+__global__ void im2col3x3(int total, FastDiv fC, FastDiv fOW, FastDiv fOH, int H, int W,
+                          const float* __restrict__ x, const float* __restrict__ mean,
                           const float* __restrict__ invstd, const float* __restrict__ w, const float* __restrict__ b,
                           float* __restrict__ col) {
-  const int OH = H - 2, OW = W - 2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * OH * OW * C;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int c = idx % C;
-  const long m = idx / C;
-  const int ow = m % OW;
-  const int oh = (m / OW) % OH;
-  const int bb = m / ((long)OW * OH);
+  const int C = fC.div;
+  int c, ow, oh;
+  const int m = fdivmod(idx, fC, c);
+  const int q = fdivmod(m, fOW, ow);
+  const int bb = fdivmod(q, fOH, oh);
   float sc = 1.f, sh = 0.f;
   if (mean) {
     sc = invstd[c] * w[c];
     sh = b[c] - mean[c] * sc;
   }
-  float* out = col + m * (9L * C) + 9L * c;
+  float* out = col + (long)m * (9 * C) + 9 * c;
   const float* xb = x + (((long)bb * H + oh) * W + ow) * C + c;
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh)
@@ -55,16 +54,16 @@ __global__ void im2col3x3(int B, int H, int W, int C, const float* __restrict__ 
 }
 
 // dx[b,ih,iw,c] = sum_{kh,kw} dcol[(b, ih-kh, iw-kw), c*9 + kh*3 + kw]
-__global__ void col2im3x3(int B, int H, int W, int C, const float* __restrict__ dcol, float* __restrict__ dx) {
-  const int OH = H - 2, OW = W - 2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * H * W * C;
+__global__ void col2im3x3(int total, FastDiv fC, FastDiv fW, FastDiv fH, const float* __restrict__ dcol,
+                          float* __restrict__ dx) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int c = idx % C;
-  const long p = idx / C;
-  const int iw = p % W;
-  const int ih = (p / W) % H;
-  const int bb = p / ((long)W * H);
+  const int C = fC.div, H = fH.div, W = fW.div;
+  const int OH = H - 2, OW = W - 2;
+  int c, iw, ih;
+  const int p = fdivmod(idx, fC, c);
+  const int q = fdivmod(p, fW, iw);
+  const int bb = fdivmod(q, fH, ih);
   float s = 0.f;
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
@@ -74,8 +73,8 @@ __global__ void col2im3x3(int B, int H, int W, int C, const float* __restrict__ 
     for (int kw = 0; kw < 3; ++kw) {
       const int ow = iw - kw;
       if (ow < 0 || ow >= OW) continue;
-      const long m = ((long)bb * OH + oh) * OW + ow;
-      s += dcol[m * (9L * C) + 9L * c + kh * 3 + kw];
+      const int m = (bb * OH + oh) * OW + ow;
+      s += dcol[(long)m * (9 * C) + 9 * c + kh * 3 + kw];
     }
   }
   dx[idx] = s;
@@ -83,17 +82,14 @@ __global__ void col2im3x3(int B, int H, int W, int C, const float* __restrict__ 
 
 // 2x2 / stride 2 floor max-pool over a channels-last [B, H, W, C] (row stride ldx);
 // arg = which of the 4 taps won (first max in (kh, kw) scan order, as torch).
-__global__ void maxpool2(int B, int H, int W, int C, const float* __restrict__ x, long ldx, float* __restrict__ y,
-                         unsigned char* __restrict__ arg) {
-  const int PH = H / 2, PW = W / 2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * PH * PW * C;
+__global__ void maxpool2(int total, FastDiv fC, FastDiv fPW, FastDiv fPH, int H, int W, const float* __restrict__ x,
+                         long ldx, float* __restrict__ y, unsigned char* __restrict__ arg) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int c = idx % C;
-  const long q = idx / C;
-  const int pw = q % PW;
-  const int ph = (q / PW) % PH;
-  const int bb = q / ((long)PW * PH);
+  int c, pw, ph;
+  const int q = fdivmod(idx, fC, c);
+  const int r = fdivmod(q, fPW, pw);
+  const int bb = fdivmod(r, fPH, ph);
   const float* xb = x + (((long)bb * H + 2 * ph) * W + 2 * pw) * ldx + c;
   float best = xb[0];
   int bi = 0;
@@ -109,24 +105,23 @@ __global__ void maxpool2(int B, int H, int W, int C, const float* __restrict__ x
   arg[idx] = (unsigned char)bi;
 }
 
-__global__ void maxpool2_bwd(int B, int H, int W, int C, const float* __restrict__ dy,
+__global__ void maxpool2_bwd(int total, FastDiv fC, FastDiv fW, FastDiv fH, const float* __restrict__ dy,
                              const unsigned char* __restrict__ arg, float* __restrict__ dx, long lddx) {
-  const int PH = H / 2, PW = W / 2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * H * W * C;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int c = idx % C;
-  const long p = idx / C;
-  const int iw = p % W;
-  const int ih = (p / W) % H;
-  const int bb = p / ((long)W * H);
+  const int C = fC.div, H = fH.div, W = fW.div;
+  const int PH = H / 2, PW = W / 2;
+  int c, iw, ih;
+  const int p = fdivmod(idx, fC, c);
+  const int q = fdivmod(p, fW, iw);
+  const int bb = fdivmod(q, fH, ih);
   const int ph = ih >> 1, pw = iw >> 1;
   float v = 0.f;
   if (ph < PH && pw < PW) {
-    const long q = (((long)bb * PH + ph) * PW + pw) * C + c;
+    const int q = ((bb * PH + ph) * PW + pw) * C + c;
     if (arg[q] == ((ih & 1) << 1 | (iw & 1))) v = dy[q];
   }
-  dx[p * lddx + c] = v;
+  dx[(long)p * lddx + c] = v;
 }
 
 }  // namespace
@@ -144,8 +139,9 @@ VC_API int vc_im2col3x3(int B, int H, int W, int C, const float* x, const float*
   VC_REQUIRE(B >= 0 && H >= 3 && W >= 3 && C > 0);
   long total = (long)B * (H - 2) * (W - 2) * C;
   if (total == 0) return VC_OK;
-  hipLaunchKernelGGL(im2col3x3, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, B, H, W, C, x, bn_mean, bn_invstd,
-                     bn_w, bn_b, col);
+  VC_REQUIRE_I32(total * 9);
+  hipLaunchKernelGGL(im2col3x3, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
+                     make_fastdiv(W - 2), make_fastdiv(H - 2), H, W, x, bn_mean, bn_invstd, bn_w, bn_b, col);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -154,7 +150,9 @@ VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx
   VC_REQUIRE(B >= 0 && H >= 3 && W >= 3 && C > 0);
   long total = (long)B * H * W * C;
   if (total == 0) return VC_OK;
-  hipLaunchKernelGGL(col2im3x3, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, B, H, W, C, dcol, dx);
+  VC_REQUIRE_I32(total * 9);
+  hipLaunchKernelGGL(col2im3x3, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
+                     make_fastdiv(W), make_fastdiv(H), dcol, dx);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -164,7 +162,9 @@ VC_API int vc_maxpool2_fwd(int B, int H, int W, int C, const float* x, long ldx,
   VC_REQUIRE(B >= 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C);
   long total = (long)B * (H / 2) * (W / 2) * C;
   if (total == 0) return VC_OK;
-  hipLaunchKernelGGL(maxpool2, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, B, H, W, C, x, ldx, y, arg);
+  VC_REQUIRE_I32((long)B * H * W * ldx);
+  hipLaunchKernelGGL(maxpool2, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
+                     make_fastdiv(W / 2), make_fastdiv(H / 2), H, W, x, ldx, y, arg);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -174,7 +174,9 @@ VC_API int vc_maxpool2_bwd(int B, int H, int W, int C, const float* dy, const un
   VC_REQUIRE(B >= 0 && H >= 2 && W >= 2 && C > 0 && lddx >= C);
   long total = (long)B * H * W * C;
   if (total == 0) return VC_OK;
-  hipLaunchKernelGGL(maxpool2_bwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, B, H, W, C, dy, arg, dx, lddx);
+  VC_REQUIRE_I32((long)B * H * W * lddx);
+  hipLaunchKernelGGL(maxpool2_bwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
+                     make_fastdiv(W), make_fastdiv(H), dy, arg, dx, lddx);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

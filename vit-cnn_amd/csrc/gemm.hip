@@ -209,15 +209,17 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
       }
 }
 
-__global__ void splitk_reduce(GemmArgs g, int batch) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)batch * g.M * g.Ne;
-  if (idx >= total) return;
-  const int n = idx % g.Ne;
-  const int m = (idx / g.Ne) % g.M;
-  const int b = idx / ((long)g.M * g.Ne);
+// grid (ceil(Ne/64), M, batch): one thread per output element, no index division; the
+// nsplit slab reads are independent (unrolled) and summed in fixed z order (deterministic)
+__global__ __launch_bounds__(64) void splitk_reduce(GemmArgs g) {
+  const int n = blockIdx.x * 64 + threadIdx.x;
+  if (n >= g.Ne) return;
+  const int m = blockIdx.y, b = blockIdx.z;
+  const long slab = (long)g.M * g.Ne;
+  const float* p = g.part + (long)b * g.nsplit * slab + (long)m * g.Ne + n;
   float s = 0.f;
-  for (int z = 0; z < g.nsplit; ++z) s += g.part[(((long)b * g.nsplit + z) * g.M + m) * g.Ne + n];
+#pragma unroll 8
+  for (int z = 0; z < g.nsplit; ++z) s += p[z * slab];
   if (n < g.N) {
     float* cp = g.C + (long)b * g.sC + (long)m * g.ldc + n;
     *cp = epilogue(g.epi, s, cp, m, n);
@@ -292,8 +294,7 @@ VC_EXPORT int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
 #undef VC_LAUNCH_GEMM
   VC_CHECK_LAUNCH();
   if (nsplit > 1) {
-    const long total = (long)batch * M * Ne;
-    hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, g, batch);
+    hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(Ne, 64), M, batch), dim3(64), 0, stream, g);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;

@@ -25,23 +25,24 @@ constexpr int NST = 16;     // ssm state size (config state_size=16, Mutimodalit
 constexpr int CK = 16;      // checkpoint interval of the backward recompute
 constexpr int DPB = 16;     // channels per block (4 waves x 4 channels)
 
-__global__ void dirconv_fwd(int B, int L, int D, int ndir, const int* __restrict__ order,
+// one thread per (k, b, t, d); index decomposition with launch-time FastDivs (no integer divide)
+__global__ void dirconv_fwd(int total, FastDiv fD, FastDiv fL, FastDiv fB, const int* __restrict__ order,
                             const float* __restrict__ xz, const float* __restrict__ cw, const float* __restrict__ cb,
                             float* __restrict__ u) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)ndir * B * L * D;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int d = idx % D;
-  const long st = idx / D;
-  const int t = st % L;
-  const int s = st / L;
-  const int k = s / B, b = s % B;
-  const long ld = 2L * D;
+  const int D = fD.div, L = fL.div;
+  int d, t, b;
+  const int st = fdivmod(idx, fD, d);
+  const int s = fdivmod(st, fL, t);
+  const int k = fdivmod(s, fB, b);
+  const int* ord = order + k * L;
+  const float* xb = xz + (long)b * L * (2 * D) + d;
   float pre = cb[d];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int tau = t - 3 + j;
-    if (tau >= 0) pre += cw[d * 4 + j] * xz[((long)b * L + order[k * L + tau]) * ld + d];
+    if (tau >= 0) pre += cw[d * 4 + j] * xb[ord[tau] * (2 * D)];
   }
   u[idx] = silu_f(pre);
 }
@@ -260,22 +261,23 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
 }
 
 
-__global__ void combine_fwd(int B, int L, int D, int ndir, const int* __restrict__ inv, const float* __restrict__ logits,
-                            const float* __restrict__ y, float* __restrict__ out) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * L * D;
+__global__ void combine_fwd(int total, FastDiv fD, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
+                            const float* __restrict__ logits, const float* __restrict__ y, float* __restrict__ out) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int d = idx % D;
-  const long bl = idx / D;
-  const int l = bl % L, b = bl / L;
+  const int D = fD.div, L = fL.div;
+  int d, l;
+  const int bl = fdivmod(idx, fD, d);
+  const int b = fdivmod(bl, fL, l);
   float mx = logits[0];
   for (int i = 1; i < ndir; ++i) mx = fmaxf(mx, logits[i]);
   float den = 0.f;
   for (int i = 0; i < ndir; ++i) den += __expf(logits[i] - mx);
+  const float rden = 1.f / den;
   float acc = 0.f;
   for (int kk = 0; kk < ndir; ++kk) {
-    const float gk = __expf(logits[kk] - mx) / den;
-    acc += gk * y[(((long)kk * B + b) * L + inv[kk * L + l]) * D + d];
+    const float gk = __expf(logits[kk] - mx) * rden;
+    acc += gk * y[((long)(kk * B + b) * L + inv[kk * L + l]) * D + d];
   }
   out[idx] = acc;
 }
@@ -303,49 +305,27 @@ __global__ __launch_bounds__(256) void gate_grad(int ndir, int per_dir, const fl
 }
 
 
-__global__ void sum_bc_chunks(long rows, int nchunk, int XW, int R, const float* __restrict__ part,
+__global__ void sum_bc_chunks(int rows, int nchunk, int XW, int R, const float* __restrict__ part,
                               float* __restrict__ dxdbl) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= rows * 2 * NST) return;
-  const long r = idx / (2 * NST);
-  const int j = idx % (2 * NST);
+  const int r = idx >> 5, j = idx & 31;  // 2 * NST == 32
   float s = 0.f;
-  for (int c = 0; c < nchunk; ++c) s += part[((long)c * rows + r) * 2 * NST + j];
-  dxdbl[r * XW + R + j] = s;
-}
-
-// dpre = du * SiLU'(pre), pre recomputed from xz (in place on du)
-__global__ void dirconv_bwd_pre(int B, int L, int D, const int* __restrict__ order, const float* __restrict__ xz,
-                                const float* __restrict__ cw, const float* __restrict__ cb, float* __restrict__ du,
-                                long total) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total) return;
-  const int d = idx % D;
-  const long st = idx / D;
-  const int t = st % L;
-  const int s = st / L;
-  const int k = s / B, b = s % B;
-  float pre = cb[d];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int tau = t - 3 + j;
-    if (tau >= 0) pre += cw[d * 4 + j] * xz[((long)b * L + order[k * L + tau]) * (2L * D) + d];
-  }
-  const float sg = sigmoid_f(pre);
-  du[idx] = du[idx] * sg * (1.f + pre * (1.f - sg));
+  for (int c = 0; c < nchunk; ++c) s += part[(long)c * rows * 2 * NST + idx];
+  dxdbl[(long)r * XW + R + j] = s;
 }
 
 // dxz[b,l,d]   = sum_k sum_j w[d,j] dpre[k,b,inv_k(l)+3-j,d]
 // dxz[b,l,D+d] = sum_k dz[k,b,inv_k(l),d]
-__global__ void dirconv_bwd_gather(int B, int L, int D, int ndir, const int* __restrict__ inv,
+__global__ void dirconv_bwd_gather(int total, FastDiv f2D, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
                                    const float* __restrict__ cw, const float* __restrict__ dpre,
                                    const float* __restrict__ dz, float* __restrict__ dxz) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * L * 2 * D;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int col = idx % (2 * D);
-  const long bl = idx / (2 * D);
-  const int l = bl % L, b = bl / L;
+  const int D = f2D.div >> 1, L = fL.div;
+  int col, l;
+  const int bl = fdivmod(idx, f2D, col);
+  const int b = fdivmod(bl, fL, l);
   float acc = 0.f;
   if (col < D) {
     const int d = col;
@@ -354,50 +334,67 @@ __global__ void dirconv_bwd_gather(int B, int L, int D, int ndir, const int* __r
     for (int j = 0; j < 4; ++j) w[j] = cw[d * 4 + j];
     for (int kk = 0; kk < ndir; ++kk) {
       const int tk = inv[kk * L + l];
-      const long base = ((long)kk * B + b) * L;
+      const float* base = dpre + (long)(kk * B + b) * L * D + d;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int t = tk + 3 - j;
-        if (t < L) acc += w[j] * dpre[(base + t) * D + d];
+        if (t < L) acc += w[j] * base[t * D];
       }
     }
   } else {
     const int d = col - D;
-    for (int kk = 0; kk < ndir; ++kk) acc += dz[(((long)kk * B + b) * L + inv[kk * L + l]) * D + d];
+    for (int kk = 0; kk < ndir; ++kk) acc += dz[((long)(kk * B + b) * L + inv[kk * L + l]) * D + d];
   }
   dxz[idx] = acc;
 }
 
-// partial sums for conv1d weight/bias grads over a chunk of (seq, t) rows:
-// part[p][d*4 + j] = sum dpre * x_{t-3+j},  part[p][4D + d] = sum dpre
+// Fused SiLU backward + conv1d weight/bias partial sums over a chunk of (seq, t) rows:
+//   dpre = du * SiLU'(pre) (pre recomputed from the 4 gathered taps, written in place over du),
+//   part[p][d*4 + j] = sum dpre * x_{t-3+j},  part[p][4D + d] = sum dpre
 // block = 16 channels x 16 row lanes (64-B row segments, 16 independent streams per channel)
-__global__ __launch_bounds__(256) void dirconv_bwd_wgrad(int B, int L, int D, const int* __restrict__ order,
-                                                         const float* __restrict__ xz, const float* __restrict__ dpre,
-                                                         long rows, int rows_per, float* __restrict__ part) {
+__global__ __launch_bounds__(256) void dirconv_bwd_wgrad(int D, FastDiv fL, FastDiv fB, const int* __restrict__ order,
+                                                         const float* __restrict__ xz, const float* __restrict__ cw,
+                                                         const float* __restrict__ cb, float* __restrict__ du,
+                                                         int rows, int rows_per, float* __restrict__ part) {
   __shared__ float sh[5][16][17];
   const int dlc = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int d = blockIdx.x * 16 + dlc;
-  const long r0 = (long)blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
+  const int L = fL.div;
+  const int r0 = blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if (d < D) {
-    for (long r = r0 + rl; r < r1; r += 16) {
-      const int t = r % L;
-      const int s = r / L;
-      const int k = s / B, b = s % B;
-      const float g = dpre[r * D + d];
-      acc[4] += g;
+    float w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = cw[d * 4 + j];
+    const float bias = cb[d];
+    for (int r = r0 + rl; r < r1; r += 16) {
+      int t, b;
+      const int s = fdivmod(r, fL, t);
+      const int k = fdivmod(s, fB, b);
+      const int* ord = order + k * L;
+      const float* xb = xz + (long)b * L * (2 * D) + d;
+      float x[4];
+      float pre = bias;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int tau = t - 3 + j;
-        if (tau >= 0) acc[j] += g * xz[((long)b * L + order[k * L + tau]) * (2L * D) + d];
+        x[j] = tau >= 0 ? xb[ord[tau] * (2 * D)] : 0.f;
+        pre += w[j] * x[j];
       }
+      const float sg = sigmoid_f(pre);
+      float* gp = du + (long)r * D + d;
+      const float g = *gp * sg * (1.f + pre * (1.f - sg));
+      *gp = g;
+      acc[4] += g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += g * x[j];
     }
   }
 #pragma unroll
   for (int j = 0; j < 5; ++j) sh[j][rl][dlc] = acc[j];
   __syncthreads();
   if (threadIdx.x < 80) {
-    const int j = threadIdx.x / 16, dd = threadIdx.x % 16, dg = blockIdx.x * 16 + dd;
+    const int j = threadIdx.x >> 4, dd = threadIdx.x & 15, dg = blockIdx.x * 16 + dd;
     if (dg < D) {
       float v = 0.f;
 #pragma unroll
@@ -414,8 +411,10 @@ VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order,
   VC_REQUIRE(B >= 0 && L > 0 && D > 0 && ndir > 0);
   long total = (long)ndir * B * L * D;
   if (total == 0) return VC_OK;
-  hipLaunchKernelGGL(dirconv_fwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, B, L, D, ndir, order, xz, conv_w,
-                     conv_b, u);
+  VC_REQUIRE_I32(total);
+  VC_REQUIRE_I32((long)B * L * 2 * D);
+  hipLaunchKernelGGL(dirconv_fwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(D),
+                     make_fastdiv(L), make_fastdiv(B), order, xz, conv_w, conv_b, u);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -445,8 +444,9 @@ VC_API int vc_mamba_combine_fwd(int B, int L, int D, int ndir, const int* inv_or
   VC_REQUIRE(B >= 0 && L > 0 && D > 0 && ndir > 0 && ndir <= 64);
   long total = (long)B * L * D;
   if (total == 0) return VC_OK;
-  hipLaunchKernelGGL(combine_fwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, B, L, D, ndir, inv_order,
-                     gate_logits, y, ysum);
+  VC_REQUIRE_I32((long)ndir * total);
+  hipLaunchKernelGGL(combine_fwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(D),
+                     make_fastdiv(L), B, ndir, inv_order, gate_logits, y, ysum);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -478,8 +478,9 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   hipLaunchKernelGGL(scan_bwd, dim3(nseq, nchunk), dim3(256), sm, stream, a, ndir, gate_logits, dysum, o);
   VC_CHECK_LAUNCH();
   const int XW = R + 2 * NST;
-  hipLaunchKernelGGL(sum_bc_chunks, dim3(vc_cdiv(rows * 2 * NST, 256)), dim3(256), 0, stream, rows, nchunk, XW, R,
-                     p_bc, dxdbl);
+  VC_REQUIRE_I32(rows * 2 * NST);
+  hipLaunchKernelGGL(sum_bc_chunks, dim3(vc_cdiv(rows * 2 * NST, 256)), dim3(256), 0, stream, (int)rows, nchunk, XW,
+                     R, p_bc, dxdbl);
   VC_CHECK_LAUNCH();
   int rc = vc_colsum(nseq, D * NST, p_a, (long)D * NST, dA_log, 0.f, p_rest, rest, stream);
   if (rc) return rc;
@@ -498,19 +499,16 @@ VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order,
                                 float* dconv_w, float* dconv_b, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(B > 0 && L > 0 && D > 0 && ndir > 0);
   const long rows = (long)ndir * B * L;
-  const long total = rows * D;
-  hipLaunchKernelGGL(dirconv_bwd_pre, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, B, L, D, order, xz, conv_w,
-                     conv_b, du, total);
-  VC_CHECK_LAUNCH();
-  const long tot2 = (long)B * L * 2 * D;
-  hipLaunchKernelGGL(dirconv_bwd_gather, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, B, L, D, ndir, inv_order,
-                     conv_w, du, dz, dxz);
-  VC_CHECK_LAUNCH();
+  VC_REQUIRE_I32(rows * D);
   int rows_per = std::max<long>(64, (rows + 255) / 256);
   while ((long)vc_cdiv(rows, rows_per) * D * 5 > ws_floats) rows_per *= 2;
   const int P = vc_cdiv(rows, rows_per);
-  hipLaunchKernelGGL(dirconv_bwd_wgrad, dim3(vc_cdiv(D, 16), P), dim3(256), 0, stream, B, L, D, order, xz, du, rows,
-                     rows_per, ws);
+  hipLaunchKernelGGL(dirconv_bwd_wgrad, dim3(vc_cdiv(D, 16), P), dim3(256), 0, stream, D, make_fastdiv(L),
+                     make_fastdiv(B), order, xz, conv_w, conv_b, du, (int)rows, rows_per, ws);
+  VC_CHECK_LAUNCH();
+  const long tot2 = (long)B * L * 2 * D;
+  hipLaunchKernelGGL(dirconv_bwd_gather, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, (int)tot2,
+                     make_fastdiv(2 * D), make_fastdiv(L), B, ndir, inv_order, conv_w, du, dz, dxz);
   VC_CHECK_LAUNCH();
   int rc = launch_sum_rows(P, 4 * D, ws, 5L * D, 0L, dconv_w, 0.f, stream);
   if (rc) return rc;

@@ -11,13 +11,12 @@
 
 namespace {
 
-__global__ void cat2_fwd(long M, int C1, int C2, const float* __restrict__ x1, long ld1, const float* __restrict__ x2,
-                         long ld2, int exchange, float* __restrict__ out) {
-  const int Ct = C1 + C2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * Ct) return;
-  const long m = idx / Ct;
-  const int c = idx % Ct;
+__global__ void cat2_fwd(int total, FastDiv fCt, int C1, const float* __restrict__ x1, long ld1,
+                         const float* __restrict__ x2, long ld2, int exchange, float* __restrict__ out) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c;
+  const long m = fdivmod(idx, fCt, c);
   float v;
   if (c < C1) v = (exchange && (c & 1) == 0) ? x2[m * ld2 + c] : x1[m * ld1 + c];
   else {
@@ -27,13 +26,12 @@ __global__ void cat2_fwd(long M, int C1, int C2, const float* __restrict__ x1, l
   out[idx] = v;
 }
 
-__global__ void cat2_bwd(long M, int C1, int C2, const float* __restrict__ dout, int exchange, float* __restrict__ dx1,
-                         long ld1, float beta1, float* __restrict__ dx2, long ld2, float beta2) {
-  const int Cm = C1 > C2 ? C1 : C2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * Cm) return;
-  const long m = idx / Cm;
-  const int c = idx % Cm;
+__global__ void cat2_bwd(int total, FastDiv fCm, int C1, int C2, const float* __restrict__ dout, int exchange,
+                         float* __restrict__ dx1, long ld1, float beta1, float* __restrict__ dx2, long ld2, float beta2) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c;
+  const long m = fdivmod(idx, fCm, c);
   const float* dr = dout + m * (C1 + C2);
   const bool sw = exchange && (c & 1) == 0;
   if (dx1 && c < C1) {
@@ -48,26 +46,27 @@ __global__ void cat2_bwd(long M, int C1, int C2, const float* __restrict__ dout,
   }
 }
 
-__global__ void glf_combine_fwd(long M, int C, const float* __restrict__ wpre, const float* __restrict__ mean,
+__global__ void glf_combine_fwd(int total, FastDiv fC, const float* __restrict__ wpre, const float* __restrict__ mean,
                                 const float* __restrict__ invstd, const float* __restrict__ gam,
                                 const float* __restrict__ bet, const float* __restrict__ fc,
                                 const float* __restrict__ fl, float* __restrict__ out) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * C) return;
-  const long m = idx / C;
-  const int c = idx % C;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int C = fC.div;
+  int c;
+  const long m = fdivmod(idx, fC, c);
   const float wy = (wpre[idx] - mean[c]) * invstd[c] * gam[c] + bet[c];
   const float z = fc[idx], x2 = fl[idx];
   out[m * 2 * C + c] = (wy + z) + x2;
   out[m * 2 * C + C + c] = x2 + z;
 }
 
-__global__ void add2_2d(long M, int C, const float* __restrict__ a, long lda, const float* __restrict__ b, long ldb,
-                        float* __restrict__ out, long ldo, float beta) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * C) return;
-  const long m = idx / C;
-  const int c = idx % C;
+__global__ void add2_2d(int total, FastDiv fC, const float* __restrict__ a, long lda, const float* __restrict__ b,
+                        long ldb, float* __restrict__ out, long ldo, float beta) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c;
+  const long m = fdivmod(idx, fC, c);
   float v = a[m * lda + c];
   if (b) v += b[m * ldb + c];
   float* p = out + m * ldo + c;
@@ -79,17 +78,26 @@ __global__ __launch_bounds__(256) void head_fwd(int S1, int S2, int C, int ncls,
                                                 const float* __restrict__ f2, const float* __restrict__ W,
                                                 const float* __restrict__ bias, float* __restrict__ feat,
                                                 float* __restrict__ logits) {
-  extern __shared__ float fs[];
+  extern __shared__ float fs[];  // [C] feat, then [4][64] partials
+  float* red = fs + C;
   const int b = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += 256) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + cl;
     float s1 = 0.f, s2 = 0.f;
-    for (int p = 0; p < S1; ++p) s1 += f1[((long)b * S1 + p) * C + c];
-    for (int q = 0; q < S2; ++q) s2 += f2[((long)b * S2 + q) * C + c];
-    const float v = s1 / (float)S1 + s2 / (float)S2;
-    fs[c] = v;
-    feat[(long)b * C + c] = v;
+    if (c < C) {
+      for (int p = rg; p < S1; p += 4) s1 += f1[((long)b * S1 + p) * C + c];
+      for (int q = rg; q < S2; q += 4) s2 += f2[((long)b * S2 + q) * C + c];
+    }
+    red[rg * 64 + cl] = s1 / (float)S1 + s2 / (float)S2;
+    __syncthreads();
+    if (rg == 0 && c < C) {
+      const float v = red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl];
+      fs[c] = v;
+      feat[(long)b * C + c] = v;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int k = wave; k < ncls; k += 4) {
     float acc = 0.f;
@@ -112,18 +120,23 @@ __global__ __launch_bounds__(256) void head_bwd_x(int S1, int S2, int C, int ncl
   }
 }
 
-__global__ void head_bwd_w(int B, int C, int ncls, const float* __restrict__ dlog, const float* __restrict__ feat,
-                           float* __restrict__ dW, float* __restrict__ db) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ncls * (C + 1)) return;
-  const int k = i / (C + 1), c = i % (C + 1);
+// grid (ncls, ceil((C+1)/64)): 64 columns x 4 batch groups per block, fixed-order LDS combine;
+// column C is the bias gradient (sum over b of dlogits)
+__global__ __launch_bounds__(256) void head_bwd_w(int B, int C, int ncls, const float* __restrict__ dlog,
+                                                  const float* __restrict__ feat, float* __restrict__ dW,
+                                                  float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int k = blockIdx.x, cl = threadIdx.x & 63, bg = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
   float acc = 0.f;
-  if (c < C) {
-    for (int b = 0; b < B; ++b) acc += dlog[(long)b * ncls + k] * feat[(long)b * C + c];
-    dW[(long)k * C + c] = acc;
-  } else {
-    for (int b = 0; b < B; ++b) acc += dlog[(long)b * ncls + k];
-    db[k] = acc;
+  if (c <= C)
+    for (int b = bg; b < B; b += 4) acc += dlog[(long)b * ncls + k] * (c < C ? feat[(long)b * C + c] : 1.f);
+  red[bg][cl] = acc;
+  __syncthreads();
+  if (bg == 0 && c <= C) {
+    const float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    if (c < C) dW[(long)k * C + c] = v;
+    else db[k] = v;
   }
 }
 
@@ -192,27 +205,53 @@ __global__ __launch_bounds__(256) void ce_bwd(int B, int ncls, const float* __re
   }
 }
 
-__global__ void step_inc(float* step) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) step[0] += 1.f;
+// step[0] = t (incremented), step[1] = 1 - beta1^t, step[2] = sqrt(1 - beta2^t)
+__global__ void step_inc(float* step, const float* __restrict__ hyper) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float t = step[0] + 1.f;
+    step[0] = t;
+    step[1] = 1.f - powf(hyper[1], t);
+    step[2] = sqrtf(1.f - powf(hyper[2], t));
+  }
+}
+
+struct AdamHyper {
+  float lr, b1, b2, eps, wd, gs, bc1, sbc2;
+};
+
+__device__ __forceinline__ void adamw_elem(const AdamHyper& h, float& p, float g, float& m, float& v) {
+  const float gi = g * h.gs;
+  const float pi = p * (1.f - h.lr * h.wd);
+  m = m + (gi - m) * (1.f - h.b1);
+  v = v * h.b2 + (1.f - h.b2) * gi * gi;
+  const float denom = sqrtf(v) / h.sbc2 + h.eps;
+  p = pi - (h.lr / h.bc1) * (m / denom);
 }
 
 // hyper = [lr, beta1, beta2, eps, weight_decay, grad_scale]; torch.optim.AdamW (amsgrad=False);
 // grad_scale folds the 1/world_size of a data-parallel gradient SUM into the update
+// 4 elements per thread (16-B loads/stores) over [0, n4*4), scalar tail after
 __global__ void adamw(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                       float* __restrict__ v, const float* __restrict__ hyper, const float* __restrict__ step) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
-  const float t = step[0];
-  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
-  const float gi = g[i] * hyper[5];
-  float pi = p[i] * (1.f - lr * wd);
-  const float mi = m[i] + (gi - m[i]) * (1.f - b1);
-  const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-  m[i] = mi;
-  v[i] = vi;
-  const float denom = sqrtf(vi) / sqrtf(bc2) + eps;
-  p[i] = pi - (lr / bc1) * (mi / denom);
+  const AdamHyper h{hyper[0], hyper[1], hyper[2], hyper[3], hyper[4], hyper[5], step[1], step[2]};
+  const long n4 = n >> 2;
+  if (i < n4) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adamw_elem(h, pv.x, gv.x, mv.x, vv.x);
+    adamw_elem(h, pv.y, gv.y, mv.y, vv.y);
+    adamw_elem(h, pv.z, gv.z, mv.z, vv.z);
+    adamw_elem(h, pv.w, gv.w, mv.w, vv.w);
+    reinterpret_cast<float4*>(p)[i] = pv;
+    reinterpret_cast<float4*>(m)[i] = mv;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  } else {
+    const long j = n4 * 4 + (i - n4);
+    if (j < n) adamw_elem(h, p[j], g[j], m[j], v[j]);
+  }
 }
 
 __global__ void index_add_i64(int n, const int* __restrict__ idx, long long* __restrict__ ptr, long long val) {
@@ -236,8 +275,9 @@ VC_API int vc_cat2_fwd(long M, int C1, int C2, const float* x1, long ld1, const 
                        float* out, hipStream_t stream) {
   VC_REQUIRE(M >= 0 && C1 > 0 && C2 > 0 && (!exchange || C1 == C2));
   if (M == 0) return VC_OK;
-  hipLaunchKernelGGL(cat2_fwd, dim3(vc_cdiv(M * (C1 + C2), 256)), dim3(256), 0, stream, M, C1, C2, x1, ld1, x2, ld2,
-                     exchange, out);
+  VC_REQUIRE_I32(M * (C1 + C2));
+  hipLaunchKernelGGL(cat2_fwd, dim3(vc_cdiv(M * (C1 + C2), 256)), dim3(256), 0, stream, (int)(M * (C1 + C2)),
+                     make_fastdiv(C1 + C2), C1, x1, ld1, x2, ld2, exchange, out);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -247,8 +287,9 @@ VC_API int vc_cat2_bwd(long M, int C1, int C2, const float* dout, int exchange, 
   VC_REQUIRE(M >= 0 && C1 > 0 && C2 > 0 && (!exchange || C1 == C2));
   if (M == 0) return VC_OK;
   const int Cm = C1 > C2 ? C1 : C2;
-  hipLaunchKernelGGL(cat2_bwd, dim3(vc_cdiv(M * Cm, 256)), dim3(256), 0, stream, M, C1, C2, dout, exchange, dx1, ld1,
-                     beta1, dx2, ld2, beta2);
+  VC_REQUIRE_I32(M * (C1 + C2));
+  hipLaunchKernelGGL(cat2_bwd, dim3(vc_cdiv(M * Cm, 256)), dim3(256), 0, stream, (int)(M * Cm), make_fastdiv(Cm), C1,
+                     C2, dout, exchange, dx1, ld1, beta1, dx2, ld2, beta2);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -258,8 +299,9 @@ VC_API int vc_glf_combine_fwd(long M, int C, const float* w_pre, const float* bn
                               hipStream_t stream) {
   VC_REQUIRE(M >= 0 && C > 0);
   if (M == 0) return VC_OK;
-  hipLaunchKernelGGL(glf_combine_fwd, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, M, C, w_pre, bn_mean,
-                     bn_invstd, bn_w, bn_b, fc, fl, out);
+  VC_REQUIRE_I32(M * 2 * C);
+  hipLaunchKernelGGL(glf_combine_fwd, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C),
+                     w_pre, bn_mean, bn_invstd, bn_w, bn_b, fc, fl, out);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -269,7 +311,9 @@ VC_API int vc_add2_2d(long M, int C, const float* a, long lda, const float* b, l
                       float beta, hipStream_t stream) {
   VC_REQUIRE(M >= 0 && C > 0);
   if (M == 0) return VC_OK;
-  hipLaunchKernelGGL(add2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, M, C, a, lda, b, ldb, out, ldo, beta);
+  VC_REQUIRE_I32(M * C);
+  hipLaunchKernelGGL(add2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C), a, lda,
+                     b, ldb, out, ldo, beta);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -277,8 +321,8 @@ VC_API int vc_add2_2d(long M, int C, const float* a, long lda, const float* b, l
 VC_API int vc_head_fwd(int B, int S1, int S2, int C, int ncls, const float* f1, const float* f2, const float* W,
                        const float* bias, float* feat, float* logits, hipStream_t stream) {
   VC_REQUIRE(B > 0 && S1 > 0 && S2 > 0 && C > 0 && ncls > 0);
-  hipLaunchKernelGGL(head_fwd, dim3(B), dim3(256), sizeof(float) * C, stream, S1, S2, C, ncls, f1, f2, W, bias, feat,
-                     logits);
+  hipLaunchKernelGGL(head_fwd, dim3(B), dim3(256), sizeof(float) * (C + 256), stream, S1, S2, C, ncls, f1, f2, W,
+                     bias, feat, logits);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -288,7 +332,7 @@ VC_API int vc_head_bwd(int B, int S1, int S2, int C, int ncls, const float* dlog
   VC_REQUIRE(B > 0 && S1 > 0 && S2 > 0 && C > 0 && ncls > 0);
   hipLaunchKernelGGL(head_bwd_x, dim3(B), dim3(256), 0, stream, S1, S2, C, ncls, dlogits, W, df1, df2);
   VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(head_bwd_w, dim3(vc_cdiv(ncls * (C + 1), 256)), dim3(256), 0, stream, B, C, ncls, dlogits, feat,
+  hipLaunchKernelGGL(head_bwd_w, dim3(ncls, vc_cdiv(C + 1, 64)), dim3(256), 0, stream, B, C, ncls, dlogits, feat,
                      dW, db);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -316,11 +360,13 @@ VC_API int vc_ce_bwd(int B, int ncls, const float* logits, const long long* targ
 VC_API int vc_adamw(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, const float* hyper,
                     float* step, hipStream_t stream) {
   VC_REQUIRE(n >= 0);
-  hipLaunchKernelGGL(step_inc, dim3(1), dim3(64), 0, stream, step);
+  VC_REQUIRE(((uintptr_t)params | (uintptr_t)grads | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0);
+  hipLaunchKernelGGL(step_inc, dim3(1), dim3(64), 0, stream, step, hyper);
   VC_CHECK_LAUNCH();
   if (n == 0) return VC_OK;
-  hipLaunchKernelGGL(adamw, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, params, grads, exp_avg, exp_avg_sq, hyper,
-                     step);
+  const long threads = (n >> 2) + (n & 3);
+  hipLaunchKernelGGL(adamw, dim3(vc_cdiv(threads, 256)), dim3(256), 0, stream, n, params, grads, exp_avg, exp_avg_sq,
+                     hyper, step);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

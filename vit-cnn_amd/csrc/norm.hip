@@ -182,13 +182,13 @@ __global__ void bn_eval_prep(int C, const float* __restrict__ run_mean, const fl
   save_invstd[c] = rsqrtf(run_var[c] + eps);
 }
 
-__global__ void bn_apply(long M, int C, const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+__global__ void bn_apply(int total, FastDiv fC, const float* __restrict__ x, long ldx, const float* __restrict__ mean,
                          const float* __restrict__ invstd, const float* __restrict__ w, const float* __restrict__ b,
                          int relu, float* __restrict__ y, long ldy) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * C) return;
-  const long r = idx / C;
-  const int c = idx % C;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c;
+  const long r = fdivmod(idx, fC, c);
   float v = (x[r * ldx + c] - mean[c]) * invstd[c] * w[c] + b[c];
   if (relu) v = fmaxf(v, 0.f);
   y[r * ldy + c] = v;
@@ -235,20 +235,21 @@ __global__ void bn_bwd_finish(int C, const double* __restrict__ sums, float* __r
 }
 
 // train: dx = w*invstd*(dyv - s1/M - xhat*s2/M);  eval (sums == null): dx = w*invstd*dyv
-__global__ void bn_bwd_apply(long M, int C, const float* __restrict__ dy, long lddy, const float* __restrict__ x,
+__global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, long lddy, const float* __restrict__ x,
                              long ldx, const float* __restrict__ relu_out, long ldo, const float* __restrict__ mean,
                              const float* __restrict__ invstd, const float* __restrict__ w,
                              const double* __restrict__ sums, float* __restrict__ dx, long lddx, float beta_dx,
                              const double* __restrict__ red, float* __restrict__ dw, float* __restrict__ db,
                              float beta_w) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int C = fC.div;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < C) {
     if (dw) dw[idx] = (beta_w != 0.f ? beta_w * dw[idx] : 0.f) + (float)red[C + idx];
     if (db) db[idx] = (beta_w != 0.f ? beta_w * db[idx] : 0.f) + (float)red[idx];
   }
   if (idx >= M * C) return;
-  const long r = idx / C;
-  const int c = idx % C;
+  int c;
+  const long r = fdivmod(idx, fC, c);
   float d = dy[r * lddy + c];
   if (relu_out && !(relu_out[r * ldo + c] > 0.f)) d = 0.f;
   const float is = invstd[c];
@@ -336,7 +337,9 @@ VC_EXPORT int vc_bn_apply(long M, int C, const float* x, long ldx, const float* 
                           const float* w, const float* b, int relu, float* y, long ldy, hipStream_t stream) {
   VC_REQUIRE(C > 0 && M >= 0);
   if (M == 0) return VC_OK;
-  hipLaunchKernelGGL(bn_apply, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, M, C, x, ldx, mean, invstd, w, b,
+  VC_REQUIRE_I32(M * C);
+  hipLaunchKernelGGL(bn_apply, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C), x, ldx,
+                     mean, invstd, w, b,
                      relu, y, ldy);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -364,7 +367,9 @@ VC_EXPORT int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, co
                      sums);
   VC_CHECK_LAUNCH();
   if (dx) {
-    hipLaunchKernelGGL(bn_bwd_apply, dim3(vc_cdiv(std::max<long>(M * C, C), 256)), dim3(256), 0, stream, M, C, dy,
+    VC_REQUIRE_I32(M * C);
+    hipLaunchKernelGGL(bn_bwd_apply, dim3(vc_cdiv(std::max<long>(M * C, C), 256)), dim3(256), 0, stream, (int)M,
+                       make_fastdiv(C), dy,
                        lddy, x, ldx, relu_out, ldo, mean, invstd, w, train ? sums : (const double*)nullptr, dx, lddx,
                        beta_dx, sums, dw, db, beta_w);
     VC_CHECK_LAUNCH();

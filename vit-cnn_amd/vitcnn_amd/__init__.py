@@ -6,5 +6,6 @@ over hand-written gfx950 HIP kernels behind the C ABI in include/vitcnn.h.
 from .model import Multimodality_Mamba  # noqa: F401
 from .losses import CrossEntropyLoss  # noqa: F401
 from .optim import AdamW  # noqa: F401
+from .step import fused_train_step  # noqa: F401
 
-__all__ = ["Multimodality_Mamba", "CrossEntropyLoss", "AdamW"]
+__all__ = ["Multimodality_Mamba", "CrossEntropyLoss", "AdamW", "fused_train_step"]

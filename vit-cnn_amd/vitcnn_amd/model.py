@@ -18,7 +18,9 @@ MI355X-first design:
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 import weakref
 from typing import Dict
 
@@ -34,6 +36,10 @@ LN_EPS = 1e-6
 BN_EPS = 1e-5
 BN_MOM = 0.1
 NDIR = 10
+N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
+SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
+
+_LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
 
 UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
                    "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
@@ -258,6 +264,18 @@ class Multimodality_Mamba(nn.Module):
             self._device_tables(device)[key] = t
         return t
 
+    def _side_lanes(self, device):
+        """Side streams of the step's branch-level concurrency, each with its own scratch (split-K
+        slabs, reduction partials) so concurrent kernels never share a workspace.  The hsiMamba
+        scan (the only large scratch user) always runs on the caller's stream."""
+        tab = self._device_tables(device)
+        lanes = tab.get("lanes")
+        if lanes is None:
+            lanes = [(torch.cuda.Stream(device), torch.empty(SIDE_SCRATCH, dtype=torch.float32, device=device))
+                     for _ in range(N_SIDE)]
+            tab["lanes"] = lanes
+        return lanes
+
     def _scratch_floats(self, B):
         need = 1 << 22
         for blk in (self.hsi1, self.hsi2):
@@ -302,7 +320,12 @@ class _VitCnnFunction(torch.autograd.Function):
         if prog.ws.generation != ctx.gen:
             raise RuntimeError("ViT-CNN MI355X path: another training forward of the same batch size overwrote "
                                "the saved activations before this backward; call backward before the next forward")
-        grad = prog.backward(dlogits.detach().to(torch.float32).contiguous())
+        # The autograd engine runs this on its device thread.  Forking side streams from that thread
+        # inside a hipGraph capture (opened on the user's thread) breaks capture_end on this ROCm
+        # release, so a captured autograd backward runs on one stream; `fused_train_step`
+        # (step.py) captures the multi-stream backward from the caller's thread instead.
+        grad = prog.backward(dlogits.detach().to(torch.float32).contiguous(),
+                             lanes=not torch.cuda.is_current_stream_capturing())
         return None, None, None, grad, None
 
 
@@ -316,11 +339,77 @@ class _Program:
         self.train = 1 if train else 0
         self.ws = model._workspace(device, B, ("train" if train else "eval", mode))
         self.tab = model._device_tables(device)
-        self.scr = model._scratch(device, B)
-        self.scr_p, self.scr_n = self.scr.data_ptr(), self.scr.numel()
+        scr = model._scratch(device, B)
+        lanes = model._side_lanes(device)
+        self.streams = [torch.cuda.current_stream(device)] + [st for st, _ in lanes]
+        self._raw = [st.cuda_stream for st in self.streams]
+        self._scr = [(scr.data_ptr(), scr.numel())] + [(t.data_ptr(), t.numel()) for _, t in lanes]
+        self.cur = 0
+        self._ev_i = 0
+        self._ev_lane = {}
+        self.lanes_on = _LANES
         _, self.P, self.BUF, self.I64 = model._ptrs()
-        self.s = torch.cuda.current_stream(device).cuda_stream
         self.device = device
+
+    # ---------------------------------------------------------------- lanes (stream-level concurrency)
+    # Lane 0 is the caller's stream; independent branches of the network run on side lanes that
+    # fork from / join back to it through events (captured as graph edges under hipGraph capture).
+    @property
+    def s(self):
+        return self._raw[self.cur]
+
+    @property
+    def scr_p(self):
+        return self._scr[self.cur][0]
+
+    @property
+    def scr_n(self):
+        return self._scr[self.cur][1]
+
+    def _event(self):
+        """next event of the model's per-device pool.  Events are reused step after step instead of
+        created and destroyed: an event destroyed while a hipGraph capture is still open leaves the
+        capture referring to a dead object."""
+        pool = self.m._device_tables(self.device).setdefault("events", [])
+        if self._ev_i == len(pool):
+            pool.append(torch.cuda.Event())
+        e = pool[self._ev_i]
+        self._ev_i += 1
+        return e
+
+    def mark(self):
+        """event recorded on the current lane"""
+        e = self._event()
+        e.record(self.streams[self.cur])
+        self._ev_lane[id(e)] = self.cur
+        return e
+
+    def wait(self, *events):
+        """The current lane waits for the given events.  Capture rules this ROCm release needs
+        (tools/graph_probe*.py): a side lane is forked by waiting on a lane-0 event before it waits
+        on another side lane's event, and a lane never waits on its own event (a no-op anyway)."""
+        for e in events:
+            if self._ev_lane.get(id(e)) == self.cur:
+                continue
+            self.streams[self.cur].wait_event(e)
+
+    @contextlib.contextmanager
+    def lane(self, i, *after):
+        prev = self.cur
+        self.cur = i if self.lanes_on else 0
+        self.wait(*after)
+        try:
+            yield
+        finally:
+            self.cur = prev
+
+    def join_lanes(self):
+        """lane 0 waits for everything issued on the side lanes"""
+        assert self.cur == 0
+        for i in range(1, len(self.streams)):
+            e = self._event()
+            e.record(self.streams[i])
+            self.streams[0].wait_event(e)
 
     # ---------------------------------------------------------------- gemm wrappers
     def mm_nt(self, M, N, K, A, lda, W, ldw, C, ldc, bias=0, alpha=1.0, beta=0.0, add=0, add_ld=0, add_mod=0,
@@ -410,7 +499,9 @@ class _Program:
         rows = B * L_
         gv, mx = pfx + ".global_view", pfx + ".global_view.layers.0"
         order, inv = self.tab[("order", H)].data_ptr(), self.tab[("inv", H)].data_ptr()
-        # --- hsiMamba global view (Mutimodality_Mamba7.py:419-701, :983-1017)
+        M = B * S
+        FM, e_fm = self.block_local_branch(blk, pfx, X, H)
+        # --- hsiMamba global view (Mutimodality_Mamba7.py:419-701, :983-1017), on lane 0
         T = ws.f(pfx + ".T", rows * E)
         self.mm_nt(rows, E, Cin, X, Cin, P[gv + ".patch_embed.projection.weight"], Cin, T, E,
                    add=P[gv + ".pos_embed"], add_ld=E, add_mod=L_)
@@ -435,15 +526,37 @@ class _Program:
         self.mm_nt(rows, Cout, E, G, E, P[pfx + ".change_dim.weight"], E, CD, Cout, bias=P[pfx + ".change_dim.bias"])
         Zg = self.token_learner(pfx + ".global_feature", CD, L_, Cout, S)
         Fg = self.layernorm(pfx + ".ln3", Zg, B * S, Cout, pfx + ".Fg")
+        self.wait(e_fm)
+        # --- fusionBlock(global, fused) with ChannelExchange
+        return self.fusion(pfx + ".fusion", Fg, Cout, FM, Cout, M, Cout)
+
+    def block_local_branch(self, blk, pfx, X, H):
+        """local feature (lane 1) || channel feature (lane 2), then the GLfusionBlock on lane 1;
+        returns (FM, event on lane 1 after FM)."""
+        B, ws, P = self.B, self.ws, self.P
+        Cin, Cout = blk.cin, blk.cout
+        L_, Hs = H * H, H - 2
+        S, Ci, Pk = Hs * Hs, Cout // 2, (Hs // 2) * (Hs // 2)
+        rows = B * L_
+        e0 = self.mark()
         # --- local feature: BN -> conv3x3 -> ReLU
-        Fl = self.conv_bn_relu3(pfx + ".local_feature", X, H, Cin, Cout)
+        with self.lane(1, e0):
+            Fl = self.conv_bn_relu3(pfx + ".local_feature", X, H, Cin, Cout)
         # --- channel feature: conv1x1 -> TokenLearner -> ln4
-        CF = ws.f(pfx + ".CF", rows * Cout)
-        self.mm_nt(rows, Cout, Cin, X, Cin, P[pfx + ".channel_feature.weight"], Cin, CF, Cout,
-                   bias=P[pfx + ".channel_feature.bias"])
-        Zc = self.token_learner(pfx + ".channel_token", CF, L_, Cout, S)
-        Fc = self.layernorm(pfx + ".ln4", Zc, B * S, Cout, pfx + ".Fc")
-        # --- GLfusionBlock(x1 = channel, x2 = local): non-local cross attention (:140-159, :1107-1117)
+        with self.lane(2, e0):
+            CF = ws.f(pfx + ".CF", rows * Cout)
+            self.mm_nt(rows, Cout, Cin, X, Cin, P[pfx + ".channel_feature.weight"], Cin, CF, Cout,
+                       bias=P[pfx + ".channel_feature.bias"])
+            Zc = self.token_learner(pfx + ".channel_token", CF, L_, Cout, S)
+            Fc = self.layernorm(pfx + ".ln4", Zc, B * S, Cout, pfx + ".Fc")
+            e_fc = self.mark()
+        with self.lane(1, e_fc):
+            FM = self.glfusion(pfx, Fl, Fc, Cout, S, Ci, Pk, Hs)
+            return FM, self.mark()
+
+    def glfusion(self, pfx, Fl, Fc, Cout, S, Ci, Pk, Hs):
+        """GLfusionBlock(x1 = channel, x2 = local): non-local cross attention (:140-159, :1107-1117)"""
+        B, ws, P = self.B, self.ws, self.P
         nl = pfx + ".FusionLayer.cross_attention"
         M = B * S
         TH = ws.f(pfx + ".TH", M * Ci)
@@ -462,31 +575,37 @@ class _Program:
         CAT1 = ws.f(pfx + ".CAT1", M * 2 * Cout)
         self.L.vc_glf_combine_fwd(M, Cout, WP, wm, wi, P[nl + ".W.1.weight"], P[nl + ".W.1.bias"], Fc, Fl, CAT1,
                                   self.s)
-        FM = self.conv1x1_bn_relu(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout)
-        # --- fusionBlock(global, fused) with ChannelExchange
-        return self.fusion(pfx + ".fusion", Fg, Cout, FM, Cout, M, Cout)
+        return self.conv1x1_bn_relu(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout)
 
     def forward(self, hsi, lidar):
         m, B, ws = self.m, self.B, self.ws
         ws.generation += 1
         Pp = m.patch
         X0 = ws.f("x0", B * Pp * Pp * m.c1)
+        S1, S2 = (Pp - 2) ** 2, (Pp - 4) ** 2
+        e_in = self.mark()
+        # LiDAR branch on lane 3 (independent of the HSI blocks until fusion1 / fusion2)
+        with self.lane(3, e_in):
+            if m.c2 == 1:
+                ws.t["lidar_in"] = lidar  # keep alive for the backward
+                LX = lidar.data_ptr()
+            else:
+                LX = ws.f("lx0", B * Pp * Pp * m.c2)
+                self.L.vc_nchw_to_nhwc(B, m.c2, Pp * Pp, lidar.data_ptr(), LX, self.s)
+            L1 = self.conv_bn_relu3("lidar1", LX, Pp, m.c2, 16)
+            L2 = self.conv_bn_relu3("lidar2", L1, Pp - 2, 16, 32)
         self.L.vc_nchw_to_nhwc(B, m.c1, Pp * Pp, hsi.data_ptr(), X0, self.s)
-        if m.c2 == 1:
-            ws.t["lidar_in"] = lidar  # keep alive for the backward
-            LX = lidar.data_ptr()
-        else:
-            LX = ws.f("lx0", B * Pp * Pp * m.c2)
-            self.L.vc_nchw_to_nhwc(B, m.c2, Pp * Pp, lidar.data_ptr(), LX, self.s)
         ws.t["hsi_in"] = hsi
         self.X0, self.LX = X0, LX
         H1 = self.block(m.hsi1, "hsi1", X0, Pp)
+        e_h1 = self.mark()
+        with self.lane(3, e_h1):
+            F1 = self.fusion("fusion1", H1, m.hsi1.cout, L1, 16, B * S1, 128)
+            e_f1 = self.mark()
         H2 = self.block(m.hsi2, "hsi2", H1, Pp - 2)
-        L1 = self.conv_bn_relu3("lidar1", LX, Pp, m.c2, 16)
-        L2 = self.conv_bn_relu3("lidar2", L1, Pp - 2, 16, 32)
-        S1, S2 = (Pp - 2) ** 2, (Pp - 4) ** 2
-        F1 = self.fusion("fusion1", H1, m.hsi1.cout, L1, 16, B * S1, 128)
+        self.wait(e_f1)
         F2 = self.fusion("fusion2", H2, m.hsi2.cout, L2, 32, B * S2, 128)
+        self.join_lanes()
         logits = torch.empty(B, m.ncls, dtype=torch.float32, device=self.device)
         feat = ws.f("feat", B * 128)
         self.L.vc_head_fwd(B, S1, S2, 128, m.ncls, F1, F2, self.P["classifier.weight"], self.P["classifier.bias"],
@@ -560,8 +679,13 @@ class _Program:
                               self.G[pfx + ".tokenizers.0.conv.0.weight"], self.s)
         self.L.vc_tl_pixel_bwd(rows, C, S, df, par, ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), dX, C, self.s)
 
-    def block_bwd(self, blk, pfx, X, H, dOut, dX):
-        """dX (accumulated, beta=1) = gradient w.r.t. the block input, or None to skip input grads."""
+    def block_bwd(self, blk, pfx, X, H, dOut, dX, dx_ready):
+        """dX (accumulated, beta=1) = gradient w.r.t. the block input, or None to skip input grads;
+        dx_ready = event after which dX holds its initial value (None: already ordered on lane 0).
+        Lane 0 runs the global (hsiMamba) chain, lane 1 the GLfusion/non-local, local-conv and channel
+        chains; the accumulations into dX are ordered local -> channel (lane 1) -> global (lane 0).
+        Side lanes only ever wait on lane-0 events and lane 0 joins them (a star): the one cross-
+        stream topology this ROCm release's graph capture handles in a backward (tools/graph_probe.py)."""
         B, ws, P, G = self.B, self.ws, self.P, self.G
         Cin, Cout, E = blk.cin, blk.cout, blk.embed
         D, R = E // 2, math.ceil(E / 16)
@@ -578,36 +702,45 @@ class _Program:
         # fusionBlock(Fg, FM)
         dFg, dFM = f(pfx + ".dFg", M * Cout), f(pfx + ".dFM", M * Cout)
         self.fusion_bwd(pfx + ".fusion", Fg, Cout, FMo, Cout, M, Cout, dOut, dFg, 0.0, dFM, 0.0)
-        # GLfusionBlock FusionLayer
-        CAT1, dCAT1 = f(pfx + ".CAT1", M * 2 * Cout), f(pfx + ".dCAT1", M * 2 * Cout)
-        self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout, dFM, dCAT1, 0.0)
-        dFc, dFl = f(pfx + ".dFc", M * Cout), f(pfx + ".dFl", M * Cout)
-        self.L.vc_add2_2d(M, Cout, dCAT1, 2 * Cout, dCAT1 + F32 * Cout, 2 * Cout, dFc, Cout, 0.0, self.s)
-        self.L.vc_add2_2d(M, Cout, dFc, Cout, 0, 0, dFl, Cout, 0.0, self.s)
-        # localf = BN(W o) + Fc + Fl  ->  non-local branch
-        WP, dWP = f(pfx + ".WP", M * Cout), f(pfx + ".dWP", M * Cout)
-        self.bn_bwd(nl + ".W.1", pfx + ".W1", dCAT1, 2 * Cout, WP, Cout, 0, M, Cout, dWP, Cout, 0.0)
-        O, dO = f(pfx + ".O", M * Ci), f(pfx + ".dO", M * Ci)
-        self.linear_bwd(nl + ".W.0.weight", nl + ".W.0.bias", dWP, M, Cout, Ci, O, Ci, dO, 0.0)
-        TH, PP, ATT = f(pfx + ".TH", M * Ci), f(pfx + ".PP", B * Pk * 2 * Ci), f(pfx + ".ATT", M * Pk)
-        dTH, dPP = f(pfx + ".dTH", M * Ci), f(pfx + ".dPP", B * Pk * 2 * Ci)
-        self.L.vc_nonlocal_attn_bwd(B, S, Pk, Ci, TH, PP, ATT, dO, dTH, dPP, self.s)
-        dPG = f(pfx + ".dPG", M * 2 * Ci)
-        self.L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dPP, ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr(),
-                               dPG, 2 * Ci, self.s)
-        self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, Ci, Cout, Fc, Cout, dFc, 1.0, lddy=2 * Ci)
-        self.linear_bwd(nl + ".g.0.weight", nl + ".g.0.bias", dPG + F32 * Ci, M, Ci, Cout, Fc, Cout, dFc, 1.0,
-                        lddy=2 * Ci)
-        self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
-        # local feature
-        self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0)
-        # channel feature: ln4 -> TokenLearner -> conv1x1
-        Zc, dZc = f(pfx + ".channel_token.Z", M * Cout), f(pfx + ".dZc", M * Cout)
-        self.ln_bwd(pfx + ".ln4", pfx + ".Fc", dFc, Zc, M, Cout, dZc, 0.0)
-        CF, dCF = f(pfx + ".CF", rows * Cout), f(pfx + ".dCF", rows * Cout)
-        self.token_learner_bwd(pfx + ".channel_token", CF, L_, Cout, S, dZc, dCF)
-        self.linear_bwd(pfx + ".channel_feature.weight", pfx + ".channel_feature.bias", dCF, rows, Cout, Cin, X, Cin,
-                        dX or 0, 1.0)
+        if dX and dx_ready is not None:
+            self.wait(dx_ready)  # lane 1 accumulates into dX: order it after dX's producer
+        e0 = self.mark()
+        with self.lane(1, e0):
+            # GLfusionBlock FusionLayer + non-local branch (lane 1) -> dFc, dFl
+            CAT1, dCAT1 = f(pfx + ".CAT1", M * 2 * Cout), f(pfx + ".dCAT1", M * 2 * Cout)
+            self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout, dFM, dCAT1, 0.0)
+            dFc, dFl = f(pfx + ".dFc", M * Cout), f(pfx + ".dFl", M * Cout)
+            self.L.vc_add2_2d(M, Cout, dCAT1, 2 * Cout, dCAT1 + F32 * Cout, 2 * Cout, dFc, Cout, 0.0, self.s)
+            self.L.vc_add2_2d(M, Cout, dFc, Cout, 0, 0, dFl, Cout, 0.0, self.s)
+            # localf = BN(W o) + Fc + Fl  ->  non-local branch
+            WP, dWP = f(pfx + ".WP", M * Cout), f(pfx + ".dWP", M * Cout)
+            self.bn_bwd(nl + ".W.1", pfx + ".W1", dCAT1, 2 * Cout, WP, Cout, 0, M, Cout, dWP, Cout, 0.0)
+            O, dO = f(pfx + ".O", M * Ci), f(pfx + ".dO", M * Ci)
+            self.linear_bwd(nl + ".W.0.weight", nl + ".W.0.bias", dWP, M, Cout, Ci, O, Ci, dO, 0.0)
+            TH, PP, ATT = f(pfx + ".TH", M * Ci), f(pfx + ".PP", B * Pk * 2 * Ci), f(pfx + ".ATT", M * Pk)
+            dTH, dPP = f(pfx + ".dTH", M * Ci), f(pfx + ".dPP", B * Pk * 2 * Ci)
+            self.L.vc_nonlocal_attn_bwd(B, S, Pk, Ci, TH, PP, ATT, dO, dTH, dPP, self.s)
+            dPG = f(pfx + ".dPG", M * 2 * Ci)
+            self.L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dPP,
+                                   ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr(), dPG, 2 * Ci, self.s)
+            self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, Ci, Cout, Fc, Cout, dFc, 1.0,
+                            lddy=2 * Ci)
+            self.linear_bwd(nl + ".g.0.weight", nl + ".g.0.bias", dPG + F32 * Ci, M, Ci, Cout, Fc, Cout, dFc, 1.0,
+                            lddy=2 * Ci)
+            self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
+            # local feature: BN -> conv3x3 -> ReLU backward (first accumulation into dX)
+            self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0)
+            # channel feature: ln4 -> TokenLearner -> conv1x1
+            Zc, dZc = f(pfx + ".channel_token.Z", M * Cout), f(pfx + ".dZc", M * Cout)
+            self.ln_bwd(pfx + ".ln4", pfx + ".Fc", dFc, Zc, M, Cout, dZc, 0.0)
+            CF, dCF = f(pfx + ".CF", rows * Cout), f(pfx + ".dCF", rows * Cout)
+            self.token_learner_bwd(pfx + ".channel_token", CF, L_, Cout, S, dZc, dCF)
+            self.linear_bwd(pfx + ".channel_feature.weight", pfx + ".channel_feature.bias", dCF, rows, Cout, Cin, X,
+                            Cin, 0, 0.0)
+            if dX:
+                self.mm_nn(rows, Cin, Cout, dCF, Cout, self.P[pfx + ".channel_feature.weight"], Cin, dX, Cin,
+                           beta=1.0)
+            e_ch = self.mark()
         # global feature: ln3 -> TokenLearner -> change_dim
         Zg, dZg = f(pfx + ".global_feature.Z", M * Cout), f(pfx + ".dZg", M * Cout)
         self.ln_bwd(pfx + ".ln3", pfx + ".Fg", dFg, Zg, M, Cout, dZg, 0.0)
@@ -643,10 +776,14 @@ class _Program:
         T = f(pfx + ".T", rows * E)
         self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dT, 1.0)   # dT = residual + LN grad
         self.colsum(B, L_ * E, dT, L_ * E, G[gv + ".pos_embed"])
-        self.linear_bwd(gv + ".patch_embed.projection.weight", None, dT, rows, E, Cin, X, Cin, dX or 0, 1.0)
+        self.linear_bwd(gv + ".patch_embed.projection.weight", None, dT, rows, E, Cin, X, Cin, 0, 0.0)
+        if dX:
+            self.wait(e_ch)
+            self.mm_nn(rows, Cin, E, dT, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
 
-    def backward(self, dlogits):
+    def backward(self, dlogits, lanes=True):
         m, B, ws = self.m, self.B, self.ws
+        self.lanes_on = lanes and _LANES and os.environ.get("VITCNN_LANES_BWD", "1") != "0"
         grad = torch.empty(m._n_params, dtype=torch.float32, device=self.device)
         if m._n_params > m._n_active:  # parameters the reference forward never uses get no gradient
             self.L.vc_fill(m._n_params - m._n_active, grad.data_ptr() + F32 * m._n_active, 0.0, self.s)
@@ -660,10 +797,14 @@ class _Program:
                            dF2, self.G["classifier.weight"], self.G["classifier.bias"], self.s)
         dH1, dH2 = ws.f("dH1", B * S1 * C1o), ws.f("dH2", B * S2 * C2o)
         dL1, dL2 = ws.f("dL1", B * S1 * 16), ws.f("dL2", B * S2 * 32)
-        self.fusion_bwd("fusion1", self.H1, C1o, self.L1, 16, B * S1, 128, dF1, dH1, 0.0, dL1, 0.0)
         self.fusion_bwd("fusion2", self.H2, C2o, self.L2, 32, B * S2, 128, dF2, dH2, 0.0, dL2, 0.0)
-        self.conv_bn_relu3_bwd("lidar2", self.L1, Pp - 2, 16, 32, dL2, dL1, 1.0)
-        self.conv_bn_relu3_bwd("lidar1", self.LX, Pp, m.c2, 16, dL1, 0, 0.0)
-        self.block_bwd(m.hsi2, "hsi2", self.H1, Pp - 2, dH2, dH1)
-        self.block_bwd(m.hsi1, "hsi1", self.X0, Pp, dH1, None)
+        e_f2 = self.mark()
+        with self.lane(3, e_f2):  # fusion1 + LiDAR branch on lane 3
+            self.fusion_bwd("fusion1", self.H1, C1o, self.L1, 16, B * S1, 128, dF1, dH1, 0.0, dL1, 0.0)
+            e_f1 = self.mark()
+            self.conv_bn_relu3_bwd("lidar2", self.L1, Pp - 2, 16, 32, dL2, dL1, 1.0)
+            self.conv_bn_relu3_bwd("lidar1", self.LX, Pp, m.c2, 16, dL1, 0, 0.0)
+        self.block_bwd(m.hsi2, "hsi2", self.H1, Pp - 2, dH2, dH1, e_f1)
+        self.block_bwd(m.hsi1, "hsi1", self.X0, Pp, dH1, None, None)
+        self.join_lanes()
         return grad

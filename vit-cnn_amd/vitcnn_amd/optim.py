@@ -34,7 +34,7 @@ class AdamW(torch.optim.Optimizer):
         if st is None or st["m"].device != flat.device:
             n = self._owner()._n_active
             st = dict(m=torch.zeros(n, device=flat.device), v=torch.zeros(n, device=flat.device),
-                      step=torch.zeros(1, device=flat.device), hyper=torch.zeros(6, device=flat.device))
+                      step=torch.zeros(3, device=flat.device), hyper=torch.zeros(6, device=flat.device))
             self._dev = st
             self._hyper_vals = None
         return st
