@@ -48,6 +48,16 @@ VC_API int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
                    float beta, float* C, long ldc, long strideC, int batch,
                    const float* bias, const float* addend, long add_ld, int add_mod, int flags,
                    float* bias_grad, float* ws, long ws_floats, hipStream_t stream);
+/* vc_gemm with an in-launch split-K combine: tile_counters (n_counters >= the output tile count) is
+ * a caller-owned unsigned array that is zero on entry and left zero; when split-K is chosen the
+ * last-arriving slice of each tile sums the slices (same fixed order as vc_gemm's separate reduce
+ * kernel: bit-identical results) instead of a second launch.  Counters must not be shared by
+ * concurrently running calls (one array per stream).  NULL counters = vc_gemm. */
+VC_API int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha, const float* A, long lda,
+                      long strideA, const float* B, long ldb, long strideB, float beta, float* C, long ldc,
+                      long strideC, int batch, const float* bias, const float* addend, long add_ld, int add_mod,
+                      int flags, float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                      int n_counters, hipStream_t stream);
 
 /* out[c] = beta*out[c] + sum_r X[r*ldx + c]  (bias gradients; fixed-order two-stage) */
 VC_API int vc_colsum(int R, int C, const float* X, long ldx, float* out, float beta,
@@ -104,28 +114,32 @@ VC_API int vc_maxpool2_bwd(int B, int H, int W, int C, const float* dy, const un
  * u [ndir*B*L, D] = SiLU(causal dwconv1d_k4(x-part) + bias). */
 VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order, const float* xz,
                                 const float* conv_w, const float* conv_b, float* u, hipStream_t stream);
-/* selective scan (fp32 state, N = 16) + D skip + SiLU(z) gate; dt = softplus(dt_w @ xdbl[:, :R] + dt_b)
- * computed in-kernel; xdbl = x_proj(u) [ndir*B*L, R+32]; y [ndir*B*L, D]  (modeling_mamba.py:175-283) */
+/* selective scan of every direction's sequence (modeling_mamba.py:175-283), ungated:
+ * yp[k,b,t,d] = sum_n C_t[n] h_t[d,n] + D_d u_t[d]; h_t = exp(dt A) h_{t-1} + dt B_t u_t,
+ * dt = softplus(W_dt dtr_t + b_dt).  u/xdbl/yp are [ndir*B*L, D] / [.., R+32] / [.., D]. */
 VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
-                             const float* xz, const int* order, const float* dt_w, const float* dt_b,
-                             const float* A_log, const float* Dskip, float* y, hipStream_t stream);
-/* ysum[b,l,:] = sum_k softmax(gate_logits)_k y[k, b, inv_k(l), :]  (un-permute + gate, :694-701) */
+                             const int* order, const float* dt_w, const float* dt_b, const float* A_log,
+                             const float* Dskip, float* yp, hipStream_t stream);
+/* ypsum[b,l,:] = sum_k softmax(gate_logits)_k yp[k, b, inv_k(l), :]  (un-permute + gate, :694-701);
+ * ysum = ypsum * SiLU(z[b,l,:]) — the token-wise SiLU(z) gate of modeling_mamba.py:274 applied
+ * once after the combine (it commutes with the permutation and the gated sum) */
 VC_API int vc_mamba_combine_fwd(int B, int L, int D, int ndir, const int* inv_order, const float* gate_logits,
-                                const float* y, float* ysum, hipStream_t stream);
-/* backward of scan + combine: du, ddt_lin (pre-softplus), dz per sequence position; the B/C
- * columns of dxdbl (ld R+32); dA_log [D,16], dDskip [D], dgate_logits [ndir] (all overwritten) */
+                                const float* yp, const float* xz, float* ypsum, float* ysum, hipStream_t stream);
+/* backward of the SiLU(z) gate: dyp = dysum * SiLU(z); the z half of dxz (ld 2D) = dysum * ypsum * SiLU'(z) */
+VC_API int vc_mamba_gate_bwd(int B, int L, int D, const float* xz, const float* ypsum, const float* dysum,
+                             float* dyp, float* dxz, hipStream_t stream);
+/* backward of scan + gated combine given dyp: du, ddt_lin (pre-softplus) per sequence position;
+ * the B/C columns of dxdbl (ld R+32); dA_log [D,16], dDskip [D], dgate_logits [ndir] (all overwritten) */
 VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
-                             const float* xz, const int* order, const float* dt_w, const float* dt_b,
-                             const float* A_log, const float* Dskip, const float* gate_logits,
-                             const float* dysum, float* du, float* ddt_lin, float* dz, float* dxdbl,
-                             float* dA_log, float* dDskip, float* dgate_logits, float* ws, long ws_floats,
-                             hipStream_t stream);
-/* backward of gather + conv1d + SiLU: du is turned into dpre in place; dxz [B*L, 2D] overwritten
- * (both halves, summed over the directions); conv weight [D,1,4] / bias [D] grads overwritten */
+                             const int* order, const float* dt_w, const float* dt_b, const float* A_log,
+                             const float* Dskip, const float* gate_logits, const float* yp, const float* dyp,
+                             float* du, float* ddt_lin, float* dxdbl, float* dA_log, float* dDskip,
+                             float* dgate_logits, float* ws, long ws_floats, hipStream_t stream);
+/* backward of gather + conv1d + SiLU: du is turned into dpre in place; the x half of dxz [B*L, 2D]
+ * is overwritten (summed over the directions); conv weight [D,1,4] / bias [D] grads overwritten */
 VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order, const int* inv_order,
-                                const float* xz, const float* conv_w, const float* conv_b, float* du,
-                                const float* dz, float* dxz, float* dconv_w, float* dconv_b, float* ws,
-                                long ws_floats, hipStream_t stream);
+                                const float* xz, const float* conv_w, const float* conv_b, float* du, float* dxz,
+                                float* dconv_w, float* dconv_b, float* ws, long ws_floats, hipStream_t stream);
 
 /* ---------------------------------------------------------------- TokenLearner
  * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64).  params: S x 5 floats

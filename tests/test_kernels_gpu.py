@@ -174,3 +174,34 @@ def test_batchnorm_train_fwd_bwd(L, ws, M, C, relu):
     assert rel_err(dx.cpu().numpy(), xr.grad.numpy()) < 1e-4
     assert rel_err(dw.cpu().numpy(), wr.grad.numpy()) < 1e-4
     assert rel_err(db.cpu().numpy(), br.grad.numpy()) < 1e-4
+
+
+@pytest.mark.parametrize("ta,tb,M,N,K,bgrad", [(1, 0, 72, 9, 51840, True), (1, 0, 256, 1296, 3136, True),
+                                               (0, 1, 3136, 256, 1296, False), (1, 0, 41, 72, 51840, False),
+                                               (0, 0, 3136, 256, 512, False)])
+def test_gemm_ex_in_launch_splitk_is_bit_identical(L, ws, ta, tb, M, N, K, bgrad):
+    """vc_gemm_ex (last-arriving slice combines) == vc_gemm (separate reduce kernel), bit for bit,
+    and the tile counters are left zero for the next call."""
+    A = (rnd(K, M, seed=31) if ta else rnd(M, K, seed=31)).to(DEV)
+    B = (rnd(N, K, seed=32) if tb else rnd(K, N, seed=32)).to(DEV)
+    lda, ldb = (M if ta else K), (K if tb else N)
+    outs = []
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    for ex in (False, True):
+        C = torch.full((M, N), float("nan"), device=DEV)
+        bg = torch.full((M,), float("nan"), device=DEV) if bgrad else None
+        args = (ta, tb, M, N, K, 1.0, P(A), lda, 0, P(B), ldb, 0, 0.0, P(C), N, 0, 1, None, None, 0, 0, 0, P(bg),
+                P(ws), ws.numel())
+        for _ in range(2):  # twice: the counters must be back at zero after the first call
+            if ex:
+                L.vc_gemm_ex(*args, P(cnt), cnt.numel(), S())
+            else:
+                L.vc_gemm(*args, S())
+        torch.cuda.synchronize()
+        outs.append((C.cpu(), bg.cpu() if bg is not None else None))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if bgrad:
+        assert torch.equal(outs[0][1], outs[1][1])
+    assert int(cnt.abs().sum()) == 0
+    ref = (A.t() if ta else A).cpu() @ (B.t() if tb else B).cpu()
+    assert rel_err(outs[1][0].numpy(), ref.numpy()) < 1e-5

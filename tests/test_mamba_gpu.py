@@ -87,21 +87,23 @@ def test_mamba_kernels_vs_float64(L, D, E):
     lib.vc_mamba_dirconv_fwd(B, L, D, ndir, P(o32), P(xz_d), P(cw_d), P(cb_d), P(U), s)
     lib.vc_gemm(0, 1, rows, XW, D, 1.0, P(U), D, 0, P(wx_d), D, 0, 0.0, P(XD), XW, 0, 1, None, None, 0, 0, 0, None,
                 P(ws), ws.numel(), s)
-    lib.vc_mamba_scan_fwd(B, L, D, R, ndir, P(U), P(XD), P(xz_d), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
-                          P(Y), s)
-    lib.vc_mamba_combine_fwd(B, L, D, ndir, P(inv32), P(gate_d), P(Y), P(YS), s)
+    lib.vc_mamba_scan_fwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d), P(Y), s)
+    YP = torch.empty(B * L, D, device=DEV)
+    lib.vc_mamba_combine_fwd(B, L, D, ndir, P(inv32), P(gate_d), P(Y), P(xz_d), P(YP), P(YS), s)
     torch.cuda.synchronize()
     ref = ys_ref.detach().reshape(B * L, D)
     err = float((YS.cpu().double() - ref).abs().max() / ref.abs().max())
     assert err < 1e-5, ("forward", err)
 
     dys_d = d(dys)
-    dU, dDTL, dZ = (torch.empty(rows, D, device=DEV) for _ in range(3))
+    dU, dDTL = (torch.empty(rows, D, device=DEV) for _ in range(2))
     dXD = torch.empty(rows, XW, device=DEV)
+    dXZ = torch.full((B * L, 2 * D), float("nan"), device=DEV)
+    dYP = torch.empty(B * L, D, device=DEV)
     dA, dDs, dG = torch.empty(D, N, device=DEV), torch.empty(D, device=DEV), torch.empty(ndir, device=DEV)
-    lib.vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(xz_d), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
-                          P(gate_d), P(dys_d), P(dU), P(dDTL), P(dZ), P(dXD), P(dA), P(dDs), P(dG), P(ws), ws.numel(),
-                          s)
+    lib.vc_mamba_gate_bwd(B, L, D, P(xz_d), P(YP), P(dys_d), P(dYP), P(dXZ), s)
+    lib.vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
+                          P(gate_d), P(Y), P(dYP), P(dU), P(dDTL), P(dXD), P(dA), P(dDs), P(dG), P(ws), ws.numel(), s)
     dWdt, dbdt = torch.empty(D, R, device=DEV), torch.empty(D, device=DEV)
     lib.vc_gemm(0, 0, rows, R, D, 1.0, P(dDTL), D, 0, P(wdt_d), R, 0, 0.0, P(dXD), XW, 0, 1, None, None, 0, 0, 0,
                 None, P(ws), ws.numel(), s)
@@ -112,9 +114,8 @@ def test_mamba_kernels_vs_float64(L, D, E):
                 P(ws), ws.numel(), s)
     lib.vc_gemm(0, 0, rows, D, XW, 1.0, P(dXD), XW, 0, P(wx_d), D, 0, 1.0, P(dU), D, 0, 1, None, None, 0, 0, 0, None,
                 P(ws), ws.numel(), s)
-    dXZ = torch.empty(B * L, 2 * D, device=DEV)
     dCW, dCB = torch.empty(D, 4, device=DEV), torch.empty(D, device=DEV)
-    lib.vc_mamba_dirconv_bwd(B, L, D, ndir, P(o32), P(inv32), P(xz_d), P(cw_d), P(cb_d), P(dU), P(dZ), P(dXZ),
+    lib.vc_mamba_dirconv_bwd(B, L, D, ndir, P(o32), P(inv32), P(xz_d), P(cw_d), P(cb_d), P(dU), P(dXZ),
                              P(dCW), P(dCB), P(ws), ws.numel(), s)
     torch.cuda.synchronize()
     names = ["xz", "conv_w", "conv_b", "x_proj", "dt_w", "dt_b", "A_log", "D", "gate"]

@@ -1,0 +1,63 @@
+"""GPU tool: every vc_gemm_ex call of one training step (B=64), re-timed in isolation with HIP events.
+Prints shape, layout, split, time and TFLOP/s per call, sorted by time.
+usage: python tools/gemm_census.py [reps]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "vit-cnn_amd"))
+import torch  # noqa: E402
+
+from vitcnn_amd import CrossEntropyLoss, Multimodality_Mamba, fused_train_step  # noqa: E402
+from vitcnn_amd._lib import lib  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    dev = torch.device("cuda", 0)
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16).to(dev).train()
+    crit = CrossEntropyLoss(weight=torch.ones(16, device=dev))
+    hsi, lidar = torch.rand(64, 144, 9, 9, device=dev), torch.rand(64, 1, 9, 9, device=dev)
+    tgt = torch.randint(1, 16, (64,), device=dev)
+    fused_train_step(m, crit, hsi, lidar, tgt)
+    torch.cuda.synchronize()
+    L = lib()
+    calls = []
+    orig = L.vc_gemm_ex
+
+    def spy(*a):
+        calls.append(a)
+        return orig(*a)
+
+    L.vc_gemm_ex = spy
+    fused_train_step(m, crit, hsi, lidar, tgt)
+    torch.cuda.synchronize()
+    L.vc_gemm_ex = orig
+    raw = L.raw["vc_gemm_ex"]
+    st = torch.cuda.Stream(dev)
+    rows = []
+    for a in calls:
+        ta, tb, M, N, K = a[0], a[1], a[2], a[3], a[4]
+        batch = a[16]
+        args = list(a[:-1]) + [st.cuda_stream]
+        for _ in range(3):
+            raw(*args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            raw(*args)
+        e1.record(st)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) / reps * 1e3
+        fl = 2.0 * M * N * K * batch
+        rows.append((us, ta, tb, M, N, K, batch, a[22] is not None, fl / us * 1e-6))
+    rows.sort(reverse=True)
+    tot = sum(r[0] for r in rows)
+    print(f"{len(rows)} GEMMs, isolated sum {tot:.1f} us, {sum(2.0*r[3]*r[4]*r[5]*r[6] for r in rows)/tot*1e-6:.1f} TFLOP/s")
+    print("   us   tA tB      M      N      K  batch bgrad  TFLOP/s")
+    for r in rows:
+        print("%7.1f  %d  %d %6d %6d %6d %5d %5s %8.1f" % r)
+
+
+if __name__ == "__main__":
+    main()

@@ -94,6 +94,19 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// sum over the 4 rows of a wave for every column (lane & 15): v + v^16 + v^32 + v^48, all lanes get
+// the result.  gfx950 v_permlane16_swap / v_permlane32_swap are VALU half-exchanges, so this costs
+// two VALU swaps + adds instead of two ds_bpermute round trips through the LDS crossbar.  Summation
+// order equals __shfl_xor(16) then __shfl_xor(32) (bit-identical).
+__device__ __forceinline__ float cross_row_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = __builtin_bit_cast(float, (unsigned)p[0]) + __builtin_bit_cast(float, (unsigned)p[1]);
+  const unsigned w = __builtin_bit_cast(unsigned, v);
+  const auto q = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return __builtin_bit_cast(float, (unsigned)q[0]) + __builtin_bit_cast(float, (unsigned)q[1]);
+}
+
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
 

@@ -9,12 +9,17 @@
 //
 //   u[k,b,t,:]  = SiLU(causal depthwise conv1d_k4(xz[b, order_k(t), :D]) + bias)      (dirconv)
 //   xdbl        = u x_proj^T                                                          (vc_gemm)
-//   y[k,b,t,d]  = (sum_n C_t[n] h_t[d,n] + D_d u_t[d]) * SiLU(z[b, order_k(t), d])    (scan)
+//   yp[k,b,t,d] = sum_n C_t[n] h_t[d,n] + D_d u_t[d]                                   (scan)
 //                 h_t = exp(dt*A) h_{t-1} + dt*B_t*u_t,  dt = softplus(W_dt dtr_t + b_dt)
-//   ysum[b,l,:] = sum_k softmax(gate)_k y[k, b, inv_k(l), :]                          (combine)
+//   YP[b,l,:]   = sum_k softmax(gate)_k yp[k, b, inv_k(l), :]                          (combine)
+//   ysum[b,l,:] = YP[b,l,:] * SiLU(z[b,l,:])
+// The SiLU(z) gate of each direction's output, y_k = yp_k * SiLU(z(token)), is token-wise, so
+// it commutes with the un-permute and the gated sum: it is applied once per token after the
+// combine, and its backward (dz, and d(yp) = g_k dysum SiLU(z)) is an elementwise pass outside
+// the sequential scan (gate_bwd) instead of 10 x 16 redundant evaluations inside it.
 //
 // The scan keeps its 16-wide state in fp32 registers: one wave = 4 channels x 16 states,
-// state reductions are 16-lane shuffles.  The backward re-runs the recurrence from 16-step
+// state reductions are 16-lane DPP sums.  The backward re-runs the recurrence from 16-step
 // LDS checkpoints (nothing of size [seq, D, L, N] is ever stored) and reduces dB / dC over
 // channels through per-wave LDS slabs, so every reduction is fixed-order.
 #include "common.h"
@@ -51,7 +56,6 @@ struct ScanArgs {
   int B, L, D, R;
   const float* u;      // [nseq*L, D]
   const float* xdbl;   // [nseq*L, R+2N]
-  const float* xz;     // [B*L, 2D]
   const int* order;    // [ndir*L]
   const float* wdt;    // [D, R]
   const float* bdt;    // [D]
@@ -68,13 +72,15 @@ __device__ __forceinline__ float gate_softmax(const float* logits, int ndir, int
 }
 
 // Stage one sequence (seq s = k*B + b, channels d0..d0+15) into LDS:
-//   xs [L][XW] x_proj output rows (dt-rank | B | C), us [L][16] u, zs [L][16] z gathered through
-//   the direction order, dr [L][16] (bwd only) d(ysum) gathered through the order,
-//   dts [L][16] dt = softplus(W_dt xs[:R] + b_dt) and dsp [L][16] softplus' (bwd only).
-// Everything the sequential loop touches afterwards is LDS or registers.
+//   xs [L][XW] x_proj output rows (dt-rank | B | C), wsm [16][R] W_dt rows, us [L][16] u,
+//   dts [L][16] dt = softplus(W_dt xs[:R] + b_dt), and (bwd only) dr [L][16] = g_k d(yp), the
+//   gradient of this direction's yp gathered through the order.  The bwd staging also folds the
+//   token-wise partial sums dD += d(yp) u and dgate_k += dyp yp into (dd_acc, dg_acc).
+//   softplus'(dt_lin) is recomputed in the backward as -expm1(-dt) instead of being stored.
 template <bool BWD>
 __device__ __forceinline__ void scan_stage(const ScanArgs& a, int s, int d0, float* xs, float* wsm, float* dts,
-                                           float* dsp, float* us, float* zs, float* dr, const float* dysum) {
+                                           float* us, float* dr, float g, const float* dyp, const float* yp,
+                                           float& dd_acc, float& dg_acc) {
   const int XW = a.R + 2 * NST;
   const int k = s / a.B, b = s % a.B;
   const int tid = threadIdx.x;
@@ -86,15 +92,18 @@ __device__ __forceinline__ void scan_stage(const ScanArgs& a, int s, int d0, flo
   }
   for (int i = tid; i < a.L * DPB; i += 256) {
     const int t = i / DPB, d = d0 + i % DPB;
-    float uv = 0.f, zv = 0.f, gv = 0.f;
+    float uv = 0.f, gv = 0.f;
     if (d < a.D) {
-      const long tok = (long)b * a.L + a.order[k * a.L + t];
-      uv = a.u[((long)s * a.L + t) * a.D + d];
-      zv = a.xz[tok * (2L * a.D) + a.D + d];
-      if (BWD) gv = dysum[tok * a.D + d];
+      const long pos = ((long)s * a.L + t) * a.D + d;
+      uv = a.u[pos];
+      if (BWD) {
+        const float dv = dyp[((long)b * a.L + a.order[k * a.L + t]) * a.D + d];
+        gv = g * dv;
+        dd_acc += gv * uv;
+        dg_acc += dv * yp[pos];
+      }
     }
     us[i] = uv;
-    zs[i] = BWD ? zv : silu_f(zv);
     if (BWD) dr[i] = gv;
   }
   __syncthreads();
@@ -105,7 +114,6 @@ __device__ __forceinline__ void scan_stage(const ScanArgs& a, int s, int d0, flo
     const float* w = wsm + dl * a.R;
     for (int r = 0; r < a.R; ++r) dtl += w[r] * row[r];
     dts[i] = softplus_f(dtl);
-    if (BWD) dsp[i] = dtl > 20.f ? 1.f : sigmoid_f(dtl);
   }
   __syncthreads();
 }
@@ -117,23 +125,29 @@ __global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ 
   float* wsm = xs + a.L * XW;          // [16][R]
   float* dts = wsm + DPB * a.R;        // [L][16]
   float* us = dts + a.L * DPB;         // [L][16]
-  float* zs = us + a.L * DPB;          // [L][16] silu(z)
-  float* yb = zs + a.L * DPB;          // [L][16]
+  float* yb = us + a.L * DPB;          // [L][16]
   const int s = blockIdx.x, d0 = blockIdx.y * DPB;
   const int tid = threadIdx.x, dl = tid >> 4, n = tid & 15;
   const int d = d0 + dl;
   const bool valid = d < a.D;
-  scan_stage<false>(a, s, d0, xs, wsm, dts, nullptr, us, zs, nullptr, nullptr);
+  float unused0 = 0.f, unused1 = 0.f;
+  scan_stage<false>(a, s, d0, xs, wsm, dts, us, nullptr, 0.f, nullptr, nullptr, unused0, unused1);
   const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
   const float Dd = valid ? a.dskip[d] : 0.f;
   float h = 0.f;
-  for (int t = 0; t < a.L; ++t) {
-    const float* row = xs + t * XW;
-    const float dt = dts[t * DPB + dl];
-    const float ut = us[t * DPB + dl];
-    h = __expf(dt * A) * h + dt * row[a.R + n] * ut;
-    const float ys = row16_sum(h * row[a.R + NST + n]);
-    if (n == 0) yb[t * DPB + dl] = (ys + Dd * ut) * zs[t * DPB + dl];
+  for (int t0 = 0; t0 < a.L; t0 += CK) {
+#pragma unroll
+    for (int i = 0; i < CK; ++i) {
+      const int t = t0 + i;
+      if (t < a.L) {
+        const float* row = xs + t * XW + a.R;
+        const float dt = dts[t * DPB + dl];
+        const float ut = us[t * DPB + dl];
+        h = __expf(dt * A) * h + dt * row[n] * ut;
+        const float ys = row16_sum(h * row[NST + n]);
+        if (n == 0) yb[t * DPB + dl] = ys + Dd * ut;
+      }
+    }
   }
   __syncthreads();
   for (int i = tid; i < a.L * DPB; i += 256) {
@@ -145,59 +159,66 @@ __global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ 
 struct ScanBwdOut {
   float* du;        // [nseq*L, D]
   float* ddtl;      // [nseq*L, D]  grad of W_dt dtr + b_dt (pre-softplus)
-  float* dz;        // [nseq*L, D]  grad of z at sequence position
   float* dbc_part;  // [gridDim.y][nseq*L][2N]
   float* da_part;   // [nseq][D*N]
-  float* dd_part;   // [nseq][D]
+  float* dd_part;   // [nseq][D]  (only columns of this block's chunk written)
   float* dg_part;   // [nseq][gridDim.y]
 };
 
 __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
-                                                const float* __restrict__ dysum, ScanBwdOut o) {
+                                                const float* __restrict__ yp, const float* __restrict__ dyp,
+                                                ScanBwdOut o) {
   extern __shared__ float smem[];
   const int XW = a.R + 2 * NST;
   const int nck = (a.L + CK - 1) / CK;
   float* xs = smem;                       // [L][XW]
   float* wsm = xs + a.L * XW;             // [16][R]
   float* dts = wsm + DPB * a.R;           // [L][16]
-  float* dsp = dts + a.L * DPB;           // [L][16]
-  float* us = dsp + a.L * DPB;            // [L][16]
-  float* zs = us + a.L * DPB;             // [L][16]
-  float* dr = zs + a.L * DPB;             // [L][16]
+  float* us = dts + a.L * DPB;            // [L][16]
+  float* dr = us + a.L * DPB;             // [L][16]  d(yp) of this direction
   float* ck = dr + a.L * DPB;             // [nck][256]
   float* bc = ck + nck * 256;             // [4][CK][32]
-  float* red = bc + 4 * CK * 32;          // [4]
+  float* red = bc + 4 * CK * 32;          // [256] dD partials, then [4] dg partials
   const int s = blockIdx.x, k = s / a.B, d0 = blockIdx.y * DPB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, dl = tid >> 4, n = tid & 15;
   const int d = d0 + dl;
   const bool valid = d < a.D;
-  scan_stage<true>(a, s, d0, xs, wsm, dts, dsp, us, zs, dr, dysum);
+  const float g = gate_softmax(gate_logits, ndir, k);
+  float dD_stage = 0.f, dg_acc = 0.f;
+  scan_stage<true>(a, s, d0, xs, wsm, dts, us, dr, g, dyp, yp, dD_stage, dg_acc);
   const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
   const float Dd = valid ? a.dskip[d] : 0.f;
-  const float g = gate_softmax(gate_logits, ndir, k);
 
   // phase 1: forward recurrence, checkpoint the state entering every CK-step chunk
   float h = 0.f;
-  for (int t = 0; t < a.L; ++t) {
-    if (t % CK == 0) ck[(t / CK) * 256 + tid] = h;
-    const float dt = dts[t * DPB + dl];
-    h = __expf(dt * A) * h + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
+  for (int c = 0; c < nck; ++c) {
+    ck[c * 256 + tid] = h;
+#pragma unroll
+    for (int i = 0; i < CK; ++i) {
+      const int t = c * CK + i;
+      if (t < a.L) {
+        const float dt = dts[t * DPB + dl];
+        h = __expf(dt * A) * h + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
+      }
+    }
   }
 
   // phase 2: reverse sweep, one checkpoint chunk at a time
-  float dh_carry = 0.f, dA_acc = 0.f, dD_acc = 0.f, dg_acc = 0.f;
+  float dh_carry = 0.f, dA_acc = 0.f;
   float* dst = o.dbc_part + ((long)blockIdx.y * gridDim.x + s) * a.L * 2 * NST;
   for (int c = nck - 1; c >= 0; --c) {
     const int t0 = c * CK;
     const float hin = ck[c * 256 + tid];
-    float hreg[CK];
+    float hreg[CK], dAr[CK];
     float hh = hin;
 #pragma unroll
     for (int i = 0; i < CK; ++i) {
       const int t = t0 + i;
+      dAr[i] = 0.f;
       if (t < a.L) {
         const float dt = dts[t * DPB + dl];
-        hh = __expf(dt * A) * hh + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
+        dAr[i] = __expf(dt * A);
+        hh = dAr[i] * hh + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
       }
       hreg[i] = hh;
     }
@@ -207,27 +228,18 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
       if (t >= a.L) continue;
       const int ti = t * DPB + dl;
       const float dt = dts[ti];
-      const float dA = __expf(dt * A);
+      const float dA = dAr[i];
       const float Bn = xs[t * XW + a.R + n], Cn = xs[t * XW + a.R + NST + n];
       const float ht = hreg[i];
       const float hp = i > 0 ? hreg[i > 0 ? i - 1 : 0] : hin;
-      const float ut = us[ti], zt = zs[ti], draw = dr[ti];
-      const float dout = g * draw;
-      const float ypre = row16_sum(ht * Cn) + Dd * ut;
-      const float sg = sigmoid_f(zt);
-      const float sz = zt * sg;
-      const float dy = dout * sz;
+      const float ut = us[ti], dy = dr[ti];
       const float dh = dh_carry + Cn * dy;
       const float ddA = dh * hp;
       dA_acc += ddA * dA * dt * A;
       const float ddt = row16_sum(ddA * dA * A + dh * Bn * ut);
       const float dus = row16_sum(dh * dt * Bn);
       dh_carry = dh * dA;
-      float vb = dh * dt * ut, vc = dy * ht;
-      vb += __shfl_xor(vb, 16, 64);
-      vb += __shfl_xor(vb, 32, 64);
-      vc += __shfl_xor(vc, 16, 64);
-      vc += __shfl_xor(vc, 32, 64);
+      const float vb = cross_row_sum(dh * dt * ut), vc = cross_row_sum(dy * ht);
       if (lane < 16) {
         bc[(wave * CK + i) * 32 + lane] = vb;
         bc[(wave * CK + i) * 32 + 16 + lane] = vc;
@@ -235,10 +247,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
       if (n == 0 && valid) {
         const long o_idx = ((long)s * a.L + t) * a.D + d;
         o.du[o_idx] = dus + dy * Dd;
-        o.ddtl[o_idx] = ddt * dsp[ti];
-        o.dz[o_idx] = dout * ypre * sg * (1.f + zt * (1.f - sg));
-        dD_acc += dy * ut;
-        dg_acc += draw * ypre * sz;
+        o.ddtl[o_idx] = ddt * (dt > 20.f ? 1.f : -expm1f(-dt));  // softplus'(dt_lin) = 1 - exp(-dt)
       }
     }
     __syncthreads();
@@ -250,19 +259,42 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
     }
     __syncthreads();
   }
-  if (valid) {
-    o.da_part[(long)s * a.D * NST + d * NST + n] = dA_acc;
-    if (n == 0) o.dd_part[(long)s * a.D + d] = dD_acc;
-  }
+  if (valid) o.da_part[(long)s * a.D * NST + d * NST + n] = dA_acc;
+  // staging partials: thread i of the staging loop handled (t, dl = i % 16) -> dl = tid & 15 here
+  float* rd = red;            // [16][16]: rows = tid >> 4 (16 row groups), cols = dl
+  rd[(tid >> 4) * 16 + (tid & 15)] = dD_stage;
   float v = wave_sum(dg_acc);
+  __syncthreads();
+  if (tid < 16 && d0 + tid < a.D) {
+    float sacc = 0.f;
+    for (int r = 0; r < 16; ++r) sacc += rd[r * 16 + tid];
+    o.dd_part[(long)s * a.D + d0 + tid] = sacc;
+  }
+  __syncthreads();
   if (lane == 0) red[wave] = v;
   __syncthreads();
   if (tid == 0) o.dg_part[(long)s * gridDim.y + blockIdx.y] = red[0] + red[1] + red[2] + red[3];
 }
 
+// token-wise SiLU(z) gate of the combined output, backward:
+//   dyp = dysum * SiLU(z);   dz = dysum * YP * SiLU'(z)  -> the z half of dxz (ld 2D)
+__global__ void gate_bwd(int total, FastDiv fD, const float* __restrict__ xz, const float* __restrict__ ypsum,
+                         const float* __restrict__ dysum, float* __restrict__ dyp, float* __restrict__ dxz) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int D = fD.div;
+  int d;
+  const int r = fdivmod(idx, fD, d);
+  const float z = xz[(long)r * 2 * D + D + d];
+  const float sg = sigmoid_f(z);
+  const float g = dysum[idx];
+  dyp[idx] = g * z * sg;
+  dxz[(long)r * 2 * D + D + d] = g * ypsum[idx] * sg * (1.f + z * (1.f - sg));
+}
 
 __global__ void combine_fwd(int total, FastDiv fD, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
-                            const float* __restrict__ logits, const float* __restrict__ y, float* __restrict__ out) {
+                            const float* __restrict__ logits, const float* __restrict__ y,
+                            const float* __restrict__ xz, float* __restrict__ ypsum, float* __restrict__ out) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int D = fD.div, L = fL.div;
@@ -279,7 +311,8 @@ __global__ void combine_fwd(int total, FastDiv fD, FastDiv fL, int B, int ndir, 
     const float gk = __expf(logits[kk] - mx) * rden;
     acc += gk * y[((long)(kk * B + b) * L + inv[kk * L + l]) * D + d];
   }
-  out[idx] = acc;
+  ypsum[idx] = acc;
+  out[idx] = acc * silu_f(xz[(long)bl * 2 * D + D + d]);
 }
 
 // dlogit_j = g_j (dg_j - sum_k g_k dg_k),  dg_k = sum over the k-th direction's partials
@@ -315,37 +348,30 @@ __global__ void sum_bc_chunks(int rows, int nchunk, int XW, int R, const float* 
   dxdbl[(long)r * XW + R + j] = s;
 }
 
-// dxz[b,l,d]   = sum_k sum_j w[d,j] dpre[k,b,inv_k(l)+3-j,d]
-// dxz[b,l,D+d] = sum_k dz[k,b,inv_k(l),d]
-__global__ void dirconv_bwd_gather(int total, FastDiv f2D, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
+// dxz[b,l,d] = sum_k sum_j w[d,j] dpre[k,b,inv_k(l)+3-j,d]   (the x half; gate_bwd writes the z half)
+__global__ void dirconv_bwd_gather(int total, FastDiv fD, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
                                    const float* __restrict__ cw, const float* __restrict__ dpre,
-                                   const float* __restrict__ dz, float* __restrict__ dxz) {
+                                   float* __restrict__ dxz) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int D = f2D.div >> 1, L = fL.div;
-  int col, l;
-  const int bl = fdivmod(idx, f2D, col);
+  const int D = fD.div, L = fL.div;
+  int d, l;
+  const int bl = fdivmod(idx, fD, d);
   const int b = fdivmod(bl, fL, l);
+  float w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = cw[d * 4 + j];
   float acc = 0.f;
-  if (col < D) {
-    const int d = col;
-    float w[4];
+  for (int kk = 0; kk < ndir; ++kk) {
+    const int tk = inv[kk * L + l];
+    const float* base = dpre + (long)(kk * B + b) * L * D + d;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = cw[d * 4 + j];
-    for (int kk = 0; kk < ndir; ++kk) {
-      const int tk = inv[kk * L + l];
-      const float* base = dpre + (long)(kk * B + b) * L * D + d;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int t = tk + 3 - j;
-        if (t < L) acc += w[j] * base[t * D];
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int t = tk + 3 - j;
+      if (t < L) acc += w[j] * base[t * D];
     }
-  } else {
-    const int d = col - D;
-    for (int kk = 0; kk < ndir; ++kk) acc += dz[((long)(kk * B + b) * L + inv[kk * L + l]) * D + d];
   }
-  dxz[idx] = acc;
+  dxz[(long)bl * 2 * D + d] = acc;
 }
 
 // Fused SiLU backward + conv1d weight/bias partial sums over a chunk of (seq, t) rows:
@@ -420,44 +446,57 @@ VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order,
 }
 
 static size_t scan_fwd_smem(int L, int R) {
-  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 4 * (size_t)L * DPB);
+  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 3 * (size_t)L * DPB);
 }
 static size_t scan_bwd_smem(int L, int R) {
   const int nck = (L + CK - 1) / CK;
-  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 5 * (size_t)L * DPB + nck * 256 + 4 * CK * 32 + 4);
+  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 3 * (size_t)L * DPB + nck * 256 + 4 * CK * 32 + 256);
 }
 
-VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl, const float* xz,
+VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                              const int* order, const float* dt_w, const float* dt_b, const float* A_log,
                              const float* Dskip, float* y, hipStream_t stream) {
   VC_REQUIRE(B > 0 && L > 0 && D > 0 && R > 0 && R <= 64 && ndir > 0);
   const size_t sm = scan_fwd_smem(L, R);
   VC_REQUIRE(sm <= 160 * 1024);
-  ScanArgs a{B, L, D, R, u, xdbl, xz, order, dt_w, dt_b, A_log, Dskip};
+  ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
   hipLaunchKernelGGL(scan_fwd, dim3(ndir * B, vc_cdiv(D, DPB)), dim3(256), sm, stream, a, y);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
 
 VC_API int vc_mamba_combine_fwd(int B, int L, int D, int ndir, const int* inv_order, const float* gate_logits,
-                                const float* y, float* ysum, hipStream_t stream) {
+                                const float* y, const float* xz, float* ypsum, float* ysum, hipStream_t stream) {
   VC_REQUIRE(B >= 0 && L > 0 && D > 0 && ndir > 0 && ndir <= 64);
   long total = (long)B * L * D;
   if (total == 0) return VC_OK;
   VC_REQUIRE_I32((long)ndir * total);
   hipLaunchKernelGGL(combine_fwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(D),
-                     make_fastdiv(L), B, ndir, inv_order, gate_logits, y, ysum);
+                     make_fastdiv(L), B, ndir, inv_order, gate_logits, y, xz, ypsum, ysum);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
 
-// Backward of scan + gated combine.  Writes du, ddt_lin, dz (per sequence position), the
-// B/C columns of dxdbl (ld R+2N), and dA_log / dD / d(gate logits) (overwrite).
+VC_API int vc_mamba_gate_bwd(int B, int L, int D, const float* xz, const float* ypsum, const float* dysum, float* dyp,
+                             float* dxz, hipStream_t stream) {
+  VC_REQUIRE(B >= 0 && L > 0 && D > 0);
+  long total = (long)B * L * D;
+  if (total == 0) return VC_OK;
+  VC_REQUIRE_I32(2 * total);
+  hipLaunchKernelGGL(gate_bwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(D), xz,
+                     ypsum, dysum, dyp, dxz);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// Backward of scan + gate-weighted combine, given dyp = d(YP) per token (vc_mamba_gate_bwd).
+// Writes du, ddt_lin (per sequence position), the B/C columns of dxdbl (ld R+2N), and
+// dA_log / dD / d(gate logits) (overwrite).
 // ws needs (ceil(D/16) * nseq*L*2N + nseq*D*N + nseq*D + nseq*ceil(D/16) + D*N) floats.
-VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl, const float* xz,
+VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                              const int* order, const float* dt_w, const float* dt_b, const float* A_log,
-                             const float* Dskip, const float* gate_logits, const float* dysum, float* du,
-                             float* ddt_lin, float* dz, float* dxdbl, float* dA_log, float* dDskip,
+                             const float* Dskip, const float* gate_logits, const float* y, const float* dyp,
+                             float* du, float* ddt_lin, float* dxdbl, float* dA_log, float* dDskip,
                              float* dgate_logits, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(B > 0 && L > 0 && D > 0 && R > 0 && R <= 64 && ndir > 0 && ndir <= 64);
   const int nseq = ndir * B, nchunk = vc_cdiv(D, DPB);
@@ -473,9 +512,9 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   float* p_g = p_d + need_d;
   float* p_rest = p_g + need_g;
   long rest = ws_floats - (need_bc + need_a + need_d + need_g);
-  ScanArgs a{B, L, D, R, u, xdbl, xz, order, dt_w, dt_b, A_log, Dskip};
-  ScanBwdOut o{du, ddt_lin, dz, p_bc, p_a, p_d, p_g};
-  hipLaunchKernelGGL(scan_bwd, dim3(nseq, nchunk), dim3(256), sm, stream, a, ndir, gate_logits, dysum, o);
+  ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
+  ScanBwdOut o{du, ddt_lin, p_bc, p_a, p_d, p_g};
+  hipLaunchKernelGGL(scan_bwd, dim3(nseq, nchunk), dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
   VC_CHECK_LAUNCH();
   const int XW = R + 2 * NST;
   VC_REQUIRE_I32(rows * 2 * NST);
@@ -493,9 +532,10 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
 }
 
 // Backward of the direction gather + causal conv1d + SiLU.  dpre overwrites du in place;
-// dxz (overwritten) = both halves of the in_proj output gradient; conv grads overwritten.
+// the x half of dxz (ld 2D) is overwritten (vc_mamba_gate_bwd writes the z half); conv grads
+// overwritten.
 VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order, const int* inv_order, const float* xz,
-                                const float* conv_w, const float* conv_b, float* du, const float* dz, float* dxz,
+                                const float* conv_w, const float* conv_b, float* du, float* dxz,
                                 float* dconv_w, float* dconv_b, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(B > 0 && L > 0 && D > 0 && ndir > 0);
   const long rows = (long)ndir * B * L;
@@ -506,10 +546,11 @@ VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order,
   hipLaunchKernelGGL(dirconv_bwd_wgrad, dim3(vc_cdiv(D, 16), P), dim3(256), 0, stream, D, make_fastdiv(L),
                      make_fastdiv(B), order, xz, conv_w, conv_b, du, (int)rows, rows_per, ws);
   VC_CHECK_LAUNCH();
-  const long tot2 = (long)B * L * 2 * D;
+  const long tot2 = (long)B * L * D;
   hipLaunchKernelGGL(dirconv_bwd_gather, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, (int)tot2,
-                     make_fastdiv(2 * D), make_fastdiv(L), B, ndir, inv_order, conv_w, du, dz, dxz);
+                     make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, conv_w, du, dxz);
   VC_CHECK_LAUNCH();
+  if (dconv_b == dconv_w + 4L * D) return launch_sum_rows(P, 5 * D, ws, 5L * D, 0L, dconv_w, 0.f, stream);
   int rc = launch_sum_rows(P, 4 * D, ws, 5L * D, 0L, dconv_w, 0.f, stream);
   if (rc) return rc;
   rc = launch_sum_rows(P, D, ws, 5L * D, 4L * D, dconv_b, 0.f, stream);

@@ -294,6 +294,7 @@ VC_EXPORT int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const f
   hipLaunchKernelGGL(ln_bwd, dim3(P), dim3(256), 0, stream, R, C, rows_per, dy, lddy, x, ldx, w, mean, rstd, dx,
                      lddx, beta_dx, ws);
   VC_CHECK_LAUNCH();
+  if (dw && db == dw + C) return launch_sum_rows(P, 2 * C, ws, (long)2 * C, 0L, dw, beta_w, stream);  // adjacent
   if (dw) {
     int rc = launch_sum_rows(P, C, ws, (long)2 * C, 0L, dw, beta_w, stream);
     if (rc) return rc;

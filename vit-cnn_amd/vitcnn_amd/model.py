@@ -38,6 +38,7 @@ BN_MOM = 0.1
 NDIR = 10
 N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
+N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 _LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
 
@@ -276,6 +277,15 @@ class Multimodality_Mamba(nn.Module):
             tab["lanes"] = lanes
         return lanes
 
+    def _tile_counters(self, device):
+        """one zeroed split-K arrival-counter array per lane (vc_gemm_ex; kernels leave them zero)"""
+        tab = self._device_tables(device)
+        c = tab.get("tile_counters")
+        if c is None:
+            c = [torch.zeros(N_COUNTERS, dtype=torch.int32, device=device) for _ in range(N_SIDE + 1)]
+            tab["tile_counters"] = c
+        return c
+
     def _scratch_floats(self, B):
         need = 1 << 22
         for blk in (self.hsi1, self.hsi2):
@@ -344,6 +354,7 @@ class _Program:
         self.streams = [torch.cuda.current_stream(device)] + [st for st, _ in lanes]
         self._raw = [st.cuda_stream for st in self.streams]
         self._scr = [(scr.data_ptr(), scr.numel())] + [(t.data_ptr(), t.numel()) for _, t in lanes]
+        self._cnt = [t.data_ptr() for t in model._tile_counters(device)]
         self.cur = 0
         self._ev_i = 0
         self._ev_lane = {}
@@ -376,6 +387,11 @@ class _Program:
         e = pool[self._ev_i]
         self._ev_i += 1
         return e
+
+    def gemm(self, *args):
+        """vc_gemm_ex on the current lane with its scratch and split-K tile counters; args are
+        vc_gemm's up to bias_grad"""
+        self.L.vc_gemm_ex(*args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
 
     def mark(self):
         """event recorded on the current lane"""
@@ -415,19 +431,19 @@ class _Program:
     def mm_nt(self, M, N, K, A, lda, W, ldw, C, ldc, bias=0, alpha=1.0, beta=0.0, add=0, add_ld=0, add_mod=0,
               relu=0):
         """C[M,N] = alpha * A[M,K] W[N,K]^T + beta*C + bias + addend"""
-        self.L.vc_gemm(0, 1, M, N, K, alpha, A, lda, 0, W, ldw, 0, beta, C, ldc, 0, 1, bias or None, add or None,
-                       add_ld, add_mod, relu, None, self.scr_p, self.scr_n, self.s)
+        self.gemm(0, 1, M, N, K, alpha, A, lda, 0, W, ldw, 0, beta, C, ldc, 0, 1, bias or None, add or None,
+                       add_ld, add_mod, relu, None)
 
     def mm_nn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0):
         """C[M,N] = alpha * A[M,K] B[K,N] + beta*C"""
-        self.L.vc_gemm(0, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
-                       None, self.scr_p, self.scr_n, self.s)
+        self.gemm(0, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
+                       None)
 
     def mm_tn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0, bias_grad=0):
         """C[M,N] = alpha * A^T B, A stored [K, M] (weight gradients: M,N small, K = rows);
         bias_grad[M] (optional) = alpha * column sums of A, fused into the same GEMM"""
-        self.L.vc_gemm(1, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
-                       bias_grad or None, self.scr_p, self.scr_n, self.s)
+        self.gemm(1, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
+                       bias_grad or None)
 
     def colsum(self, R, C, X, ldx, out, beta=0.0):
         self.L.vc_colsum(R, C, X, ldx, out, beta, self.scr_p, self.scr_n, self.s)
@@ -485,8 +501,8 @@ class _Program:
         self.L.vc_tl_attn_fwd(self.train, B, L_, S, mx, avg, self.P[pfx + ".tokenizers.0.conv.0.weight"],
                               self.BUF[pfx + ".tokenizers.0.conv.1.running_mean"], BN_EPS, BN_MOM, st, a, self.s)
         Z = ws.f(pfx + ".Z", B * S * C)
-        self.L.vc_gemm(0, 0, S, C, L_, 1.0 / L_, a, L_, S * L_, X, C, L_ * C, 0.0, Z, C, S * C, B, None, None, 0, 0, 0,
-                       None, self.scr_p, self.scr_n, self.s)
+        self.gemm(0, 0, S, C, L_, 1.0 / L_, a, L_, S * L_, X, C, L_ * C, 0.0, Z, C, S * C, B, None, None, 0, 0, 0,
+                       None)
         return Z
 
     def block(self, blk, pfx, X, H):
@@ -514,10 +530,10 @@ class _Program:
         XD = ws.f(pfx + ".XD", NDIR * rows * XW)
         self.mm_nt(NDIR * rows, XW, D, U, D, P[mx + ".x_proj.weight"], D, XD, XW)
         Y = ws.f(pfx + ".Y", NDIR * rows * D)
-        self.L.vc_mamba_scan_fwd(B, L_, D, R, NDIR, U, XD, XZ, order, P[mx + ".dt_proj.weight"],
+        self.L.vc_mamba_scan_fwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
                                  P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], Y, self.s)
-        YS = ws.f(pfx + ".YS", rows * D)
-        self.L.vc_mamba_combine_fwd(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, YS, self.s)
+        YP, YS = ws.f(pfx + ".YP", rows * D), ws.f(pfx + ".YS", rows * D)
+        self.L.vc_mamba_combine_fwd(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, XZ, YP, YS, self.s)
         T2 = ws.f(pfx + ".T2", rows * E)
         self.mm_nt(rows, E, D, YS, D, P[mx + ".out_proj.weight"], D, T2, E, add=T, add_ld=E, add_mod=rows)
         G = self.layernorm(gv + ".ln1", T2, rows, E, pfx + ".G")
@@ -669,10 +685,10 @@ class _Program:
         rows = B * L_
         a, st = ws.f(pfx + ".a", B * S * L_), ws.get(pfx + ".st", 2 * S, torch.float64).data_ptr()
         da = ws.f(pfx + ".da", B * S * L_)
-        self.L.vc_gemm(0, 1, S, L_, C, 1.0 / L_, dZ, C, S * C, X, C, L_ * C, 0.0, da, L_, S * L_, B, None, None, 0, 0,
-                       0, None, self.scr_p, self.scr_n, self.s)
-        self.L.vc_gemm(1, 0, L_, C, S, 1.0 / L_, a, L_, S * L_, dZ, C, S * C, 0.0, dX, C, L_ * C, B, None, None, 0, 0,
-                       0, None, self.scr_p, self.scr_n, self.s)
+        self.gemm(0, 1, S, L_, C, 1.0 / L_, dZ, C, S * C, X, C, L_ * C, 0.0, da, L_, S * L_, B, None, None, 0, 0,
+                       0, None)
+        self.gemm(1, 0, L_, C, S, 1.0 / L_, a, L_, S * L_, dZ, C, S * C, 0.0, dX, C, L_ * C, B, None, None, 0, 0,
+                       0, None)
         df = ws.f(pfx + ".df", S * rows)
         par = self.P[pfx + ".tokenizers.0.conv.0.weight"]
         self.L.vc_tl_attn_bwd(self.train, B, L_, S, ws.f(pfx + ".mx", rows), ws.f(pfx + ".avg", rows), par, st, da, df,
@@ -754,12 +770,14 @@ class _Program:
         YS, dYS = f(pfx + ".YS", rows * D), f(pfx + ".dYS", rows * D)
         self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0)
         U, XD, XZ = f(pfx + ".U", NDIR * rows * D), f(pfx + ".XD", NDIR * rows * XW), f(pfx + ".XZ", rows * 2 * D)
-        dU, dDTL, dZ = f(pfx + ".dU", NDIR * rows * D), f(pfx + ".dDTL", NDIR * rows * D), f(pfx + ".dZ",
-                                                                                                NDIR * rows * D)
-        dXD = f(pfx + ".dXD", NDIR * rows * XW)
-        self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, XZ, order, P[mx + ".dt_proj.weight"],
-                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], dYS, dU,
-                                 dDTL, dZ, dXD, G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"], self.scr_p,
+        Y, YP = f(pfx + ".Y", NDIR * rows * D), f(pfx + ".YP", rows * D)
+        dU, dDTL = f(pfx + ".dU", NDIR * rows * D), f(pfx + ".dDTL", NDIR * rows * D)
+        dXD, dXZ, dYP = f(pfx + ".dXD", NDIR * rows * XW), f(pfx + ".dXZ", rows * 2 * D), f(pfx + ".dYP", rows * D)
+        # SiLU(z) gate (token-wise): dyp and the z half of dxz
+        self.L.vc_mamba_gate_bwd(B, L_, D, XZ, YP, dYS, dYP, dXZ, self.s)
+        self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
+                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], Y, dYP,
+                                 dU, dDTL, dXD, G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"], self.scr_p,
                                  self.scr_n, self.s)
         nr = NDIR * rows
         # dt_proj: dt_lin = xdbl[:, :R] W_dt^T + b_dt
@@ -767,9 +785,8 @@ class _Program:
         self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, bias_grad=G[mx + ".dt_proj.bias"])
         # x_proj: xdbl = u W_x^T
         self.linear_bwd(mx + ".x_proj.weight", None, dXD, nr, XW, D, U, D, dU, 1.0)
-        dXZ = f(pfx + ".dXZ", rows * 2 * D)
         self.L.vc_mamba_dirconv_bwd(B, L_, D, NDIR, order, inv, XZ, P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"],
-                                    dU, dZ, dXZ, G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"], self.scr_p,
+                                    dU, dXZ, G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"], self.scr_p,
                                     self.scr_n, self.s)
         Xn, dXn = f(pfx + ".Xn", rows * E), f(pfx + ".dXn", rows * E)
         self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0)
