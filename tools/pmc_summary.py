@@ -1,36 +1,55 @@
-"""Per-kernel PMC counter averages from a rocprofv3 --pmc database.  usage: pmc_summary.py DIR [name-filter]"""
+"""Per-kernel PMC counter values per dispatch from rocprofv3 --pmc databases (counters_collection).
+usage: pmc_summary.py DIR [DIR...] [--filter NAME]
+Groups dispatches by (kernel, grid size); prints the mean per-dispatch value of every counter."""
+import argparse
 import glob
 import os
 import sqlite3
-import sys
 from collections import defaultdict
 
 
-def main():
-    d = sys.argv[1]
-    flt = sys.argv[2] if len(sys.argv) > 2 else ""
-    dbs = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
-    for db in dbs:
+def load(d, flt):
+    out = defaultdict(lambda: defaultdict(list))   # (kernel, grid) -> counter -> [per-dispatch values]
+    dur = defaultdict(list)
+    for db in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
         con = sqlite3.connect(db)
-        tabs = [r[0] for r in con.execute("select name from sqlite_master where type in ('table','view')")]
-        pmc = [t for t in tabs if t.startswith("counters") or t == "pmc_events" or "counter" in t.lower()]
-        print(db, pmc)
-        if "counters" not in tabs:
-            continue
-        cols = [r[1] for r in con.execute("pragma table_info(counters)")]
-        print(cols)
-        rows = con.execute("select * from counters").fetchall()
-        agg = defaultdict(lambda: defaultdict(list))
-        ci = {c: i for i, c in enumerate(cols)}
-        for r in rows:
-            name = r[ci.get("kernel_name", ci.get("name", 0))]
-            if flt and flt not in str(name):
+        rows = con.execute("select dispatch_id, kernel_name, grid_size, counter_name, value, duration "
+                           "from counters_collection").fetchall()
+        per = defaultdict(float)
+        meta = {}
+        for disp, name, grid, ctr, val, du in rows:
+            if flt and flt not in name:
                 continue
-            agg[str(name).split("(")[0][-40:]][r[ci["counter_name"]]].append(r[ci["value"]])
-        for k, v in agg.items():
-            print(k)
-            for c, vals in sorted(v.items()):
-                print("   %-28s mean %.4g  (n=%d)" % (c, sum(vals) / len(vals), len(vals)))
+            per[(disp, ctr)] += val
+            meta[disp] = (name, grid, du)
+        for (disp, ctr), v in per.items():
+            name, grid, du = meta[disp]
+            short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+            out[(short, grid)][ctr].append(v)
+        for disp, (name, grid, du) in meta.items():
+            short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+            dur[(short, grid)].append(du)
+    return out, dur
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--filter", default="")
+    a = ap.parse_args()
+    merged = defaultdict(dict)
+    durs = {}
+    for d in a.dirs:
+        out, dur = load(d, a.filter)
+        for k, v in out.items():
+            for c, vals in v.items():
+                merged[k][c] = sum(vals) / len(vals)
+        for k, v in dur.items():
+            durs[k] = sum(v) / len(v)
+    for k in sorted(merged, key=lambda k: -durs.get(k, 0)):
+        print(f"{k[0]}  grid={k[1]}  avg duration {durs.get(k, 0) / 1e3:.1f} us")
+        for c, v in sorted(merged[k].items()):
+            print(f"    {c:24s} {v:.6g}")
 
 
 if __name__ == "__main__":

@@ -75,20 +75,21 @@ __device__ __forceinline__ float gate_softmax(const float* logits, int ndir, int
 //   xs [L][XW] x_proj output rows (dt-rank | B | C), wsm [16][R] W_dt rows, us [L][16] u,
 //   dts [L][16] dt = softplus(W_dt xs[:R] + b_dt), and (bwd only) dr [L][16] = g_k d(yp), the
 //   gradient of this direction's yp gathered through the order.  The bwd staging also folds the
-//   token-wise partial sums dD += d(yp) u and dgate_k += dyp yp into (dd_acc, dg_acc).
-//   softplus'(dt_lin) is recomputed in the backward as -expm1(-dt) instead of being stored.
-template <bool BWD>
+//   token-wise partial sums dD += d(yp) u and dgate_k += dyp yp into (dd_acc, dg_acc), and
+//   stages dsp [L][16] = softplus'(dt_lin).
+template <bool BWD, int RT>
 __device__ __forceinline__ void scan_stage(const ScanArgs& a, int s, int d0, float* xs, float* wsm, float* dts,
-                                           float* us, float* dr, float g, const float* dyp, const float* yp,
-                                           float& dd_acc, float& dg_acc) {
-  const int XW = a.R + 2 * NST;
+                                           float* dsp, float* us, float* dr, float g, const float* dyp,
+                                           const float* yp, float& dd_acc, float& dg_acc) {
+  const int R = RT ? RT : a.R;  // dt rank (compile-time for the two block shapes: 9, 16)
+  const int XW = R + 2 * NST;
   const int k = s / a.B, b = s % a.B;
   const int tid = threadIdx.x;
   const float* xsrc = a.xdbl + (long)s * a.L * XW;
   for (int i = tid; i < a.L * XW; i += 256) xs[i] = xsrc[i];
-  for (int i = tid; i < DPB * a.R; i += 256) {
-    const int dd = d0 + i / a.R;
-    wsm[i] = dd < a.D ? a.wdt[(long)dd * a.R + i % a.R] : 0.f;
+  for (int i = tid; i < DPB * R; i += 256) {
+    const int dd = d0 + i / R;
+    wsm[i] = dd < a.D ? a.wdt[(long)dd * R + i % R] : 0.f;
   }
   for (int i = tid; i < a.L * DPB; i += 256) {
     const int t = i / DPB, d = d0 + i % DPB;
@@ -111,19 +112,22 @@ __device__ __forceinline__ void scan_stage(const ScanArgs& a, int s, int d0, flo
     const int t = i / DPB, dl = i % DPB, d = d0 + dl;
     float dtl = d < a.D ? a.bdt[d] : 0.f;
     const float* row = xs + t * XW;
-    const float* w = wsm + dl * a.R;
-    for (int r = 0; r < a.R; ++r) dtl += w[r] * row[r];
+    const float* w = wsm + dl * R;
+    for (int r = 0; r < R; ++r) dtl += w[r] * row[r];
     dts[i] = softplus_f(dtl);
+    if (BWD) dsp[i] = dtl > 20.f ? 1.f : sigmoid_f(dtl);  // softplus'(dt_lin)
   }
   __syncthreads();
 }
 
+template <int RT>
 __global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ y) {
   extern __shared__ float smem[];
-  const int XW = a.R + 2 * NST;
+  const int R = RT ? RT : a.R;
+  const int XW = R + 2 * NST;
   float* xs = smem;                    // [L][XW]
   float* wsm = xs + a.L * XW;          // [16][R]
-  float* dts = wsm + DPB * a.R;        // [L][16]
+  float* dts = wsm + DPB * R;        // [L][16]
   float* us = dts + a.L * DPB;         // [L][16]
   float* yb = us + a.L * DPB;          // [L][16]
   const int s = blockIdx.x, d0 = blockIdx.y * DPB;
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ 
   const int d = d0 + dl;
   const bool valid = d < a.D;
   float unused0 = 0.f, unused1 = 0.f;
-  scan_stage<false>(a, s, d0, xs, wsm, dts, us, nullptr, 0.f, nullptr, nullptr, unused0, unused1);
+  scan_stage<false, RT>(a, s, d0, xs, wsm, dts, nullptr, us, nullptr, 0.f, nullptr, nullptr, unused0, unused1);
   const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
   const float Dd = valid ? a.dskip[d] : 0.f;
   float h = 0.f;
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ 
     for (int i = 0; i < CK; ++i) {
       const int t = t0 + i;
       if (t < a.L) {
-        const float* row = xs + t * XW + a.R;
+        const float* row = xs + t * XW + R;
         const float dt = dts[t * DPB + dl];
         const float ut = us[t * DPB + dl];
         h = __expf(dt * A) * h + dt * row[n] * ut;
@@ -165,17 +169,24 @@ struct ScanBwdOut {
   float* dg_part;   // [nseq][gridDim.y]
 };
 
+template <int RT>
 __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
                                                 const float* __restrict__ yp, const float* __restrict__ dyp,
                                                 ScanBwdOut o) {
   extern __shared__ float smem[];
-  const int XW = a.R + 2 * NST;
+  const int R = RT ? RT : a.R;
+  const int XW = R + 2 * NST;
   const int nck = (a.L + CK - 1) / CK;
   float* xs = smem;                       // [L][XW]
   float* wsm = xs + a.L * XW;             // [16][R]
-  float* dts = wsm + DPB * a.R;           // [L][16]
-  float* us = dts + a.L * DPB;            // [L][16]
+  float* dts = wsm + DPB * R;           // [L][16]
+  float* dsp = dts + a.L * DPB;           // [L][16]  softplus'(dt_lin)
+  float* us = dsp + a.L * DPB;            // [L][16]
   float* dr = us + a.L * DPB;             // [L][16]  d(yp) of this direction
+  // the reverse sweep consumes us[t] / dr[t] at step t and never again, so the (t, d) results
+  // du / ddt_lin overwrite them in place and are flushed once, coalesced, after the sweep
+  float* dub = us;
+  float* ddb = dr;
   float* ck = dr + a.L * DPB;             // [nck][256]
   float* bc = ck + nck * 256;             // [4][CK][32]
   float* red = bc + 4 * CK * 32;          // [256] dD partials, then [4] dg partials
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
   const bool valid = d < a.D;
   const float g = gate_softmax(gate_logits, ndir, k);
   float dD_stage = 0.f, dg_acc = 0.f;
-  scan_stage<true>(a, s, d0, xs, wsm, dts, us, dr, g, dyp, yp, dD_stage, dg_acc);
+  scan_stage<true, RT>(a, s, d0, xs, wsm, dts, dsp, us, dr, g, dyp, yp, dD_stage, dg_acc);
   const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
   const float Dd = valid ? a.dskip[d] : 0.f;
 
@@ -198,7 +209,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
       const int t = c * CK + i;
       if (t < a.L) {
         const float dt = dts[t * DPB + dl];
-        h = __expf(dt * A) * h + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
+        h = __expf(dt * A) * h + dt * xs[t * XW + R + n] * us[t * DPB + dl];
       }
     }
   }
@@ -218,7 +229,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
       if (t < a.L) {
         const float dt = dts[t * DPB + dl];
         dAr[i] = __expf(dt * A);
-        hh = dAr[i] * hh + dt * xs[t * XW + a.R + n] * us[t * DPB + dl];
+        hh = dAr[i] * hh + dt * xs[t * XW + R + n] * us[t * DPB + dl];
       }
       hreg[i] = hh;
     }
@@ -229,7 +240,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
       const int ti = t * DPB + dl;
       const float dt = dts[ti];
       const float dA = dAr[i];
-      const float Bn = xs[t * XW + a.R + n], Cn = xs[t * XW + a.R + NST + n];
+      const float Bn = xs[t * XW + R + n], Cn = xs[t * XW + R + NST + n];
       const float ht = hreg[i];
       const float hp = i > 0 ? hreg[i > 0 ? i - 1 : 0] : hin;
       const float ut = us[ti], dy = dr[ti];
@@ -244,10 +255,9 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
         bc[(wave * CK + i) * 32 + lane] = vb;
         bc[(wave * CK + i) * 32 + 16 + lane] = vc;
       }
-      if (n == 0 && valid) {
-        const long o_idx = ((long)s * a.L + t) * a.D + d;
-        o.du[o_idx] = dus + dy * Dd;
-        o.ddtl[o_idx] = ddt * (dt > 20.f ? 1.f : -expm1f(-dt));  // softplus'(dt_lin) = 1 - exp(-dt)
+      if (n == 0) {
+        dub[ti] = dus + dy * Dd;
+        ddb[ti] = ddt * dsp[ti];
       }
     }
     __syncthreads();
@@ -258,6 +268,14 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
                                   bc[(2 * CK + i) * 32 + col] + bc[(3 * CK + i) * 32 + col];
     }
     __syncthreads();
+  }
+  for (int i = tid; i < a.L * DPB; i += 256) {  // coalesced flush of du / ddt_lin
+    const int t = i / DPB, dd = d0 + i % DPB;
+    if (dd < a.D) {
+      const long o_idx = ((long)s * a.L + t) * a.D + dd;
+      o.du[o_idx] = dub[i];
+      o.ddtl[o_idx] = ddb[i];
+    }
   }
   if (valid) o.da_part[(long)s * a.D * NST + d * NST + n] = dA_acc;
   // staging partials: thread i of the staging loop handled (t, dl = i % 16) -> dl = tid & 15 here
@@ -450,7 +468,7 @@ static size_t scan_fwd_smem(int L, int R) {
 }
 static size_t scan_bwd_smem(int L, int R) {
   const int nck = (L + CK - 1) / CK;
-  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 3 * (size_t)L * DPB + nck * 256 + 4 * CK * 32 + 256);
+  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 4 * (size_t)L * DPB + nck * 256 + 4 * CK * 32 + 256);
 }
 
 VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
@@ -460,7 +478,10 @@ VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* 
   const size_t sm = scan_fwd_smem(L, R);
   VC_REQUIRE(sm <= 160 * 1024);
   ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
-  hipLaunchKernelGGL(scan_fwd, dim3(ndir * B, vc_cdiv(D, DPB)), dim3(256), sm, stream, a, y);
+  const dim3 grid(ndir * B, vc_cdiv(D, DPB));
+  if (R == 9) hipLaunchKernelGGL(scan_fwd<9>, grid, dim3(256), sm, stream, a, y);
+  else if (R == 16) hipLaunchKernelGGL(scan_fwd<16>, grid, dim3(256), sm, stream, a, y);
+  else hipLaunchKernelGGL(scan_fwd<0>, grid, dim3(256), sm, stream, a, y);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -514,7 +535,10 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   long rest = ws_floats - (need_bc + need_a + need_d + need_g);
   ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
   ScanBwdOut o{du, ddt_lin, p_bc, p_a, p_d, p_g};
-  hipLaunchKernelGGL(scan_bwd, dim3(nseq, nchunk), dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
+  const dim3 grid(nseq, nchunk);
+  if (R == 9) hipLaunchKernelGGL(scan_bwd<9>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
+  else if (R == 16) hipLaunchKernelGGL(scan_bwd<16>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
+  else hipLaunchKernelGGL(scan_bwd<0>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
   VC_CHECK_LAUNCH();
   const int XW = R + 2 * NST;
   VC_REQUIRE_I32(rows * 2 * NST);
