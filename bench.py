@@ -63,12 +63,67 @@ def time_kernel(fn, reps, stream):
     return s.elapsed_time(e) / reps * 1e-3
 
 
-def dominant_kernel_roofline(model, batch, reps):
-    """Re-launch the step's dominant kernel on its live workspace buffers and time it with events.
+def _traffic_from_profile(kernel_key):
+    """HBM bytes per launch of `kernel_key` from the committed PMC profile (rocprofv3 --pmc
+    FETCH_SIZE and WRITE_SIZE, separate passes; tools/pmc_collect.sh -> profiles/r01_pmc.json),
+    or None when no profile of this kernel is committed."""
+    path = os.path.join(REPO, "profiles", "r01_pmc.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        prof = json.load(f)
+    k = prof.get("kernels", {}).get(kernel_key)
+    return None if k is None else k.get("hbm_bytes_per_launch")
 
-    Dominant kernel (profiles/): the fp32 MFMA GEMM of hsi1.local_feature (im2col'ed 3x3 conv,
-    M = B*49, N = 256, K = 9*144) — roofline bound: MFMA (fp32 peak).  Algorithmic work per
-    launch = 2*M*N*K flop."""
+
+def dominant_kernel_roofline(model, batch, reps):
+    """Re-launch the step's dominant kernel on its live workspace buffers and time it with HIP events
+    on the stream it is launched on.
+
+    Dominant kernel (profiles/r01_*_kernel_stats.md): the hsiMamba selective-scan backward of
+    block hsi1 (`scan_bwd<9>`, grid 640 sequences x 5 channel chunks), the longest single launch
+    of the step.  It is a sequential recurrence over 81 tokens with no matrix work, so its roofline
+    is HBM.  Algorithmic bytes per launch = compulsory reads of u, x_proj rows, yp (each
+    [10*B*L, *]) and d(yp) [B*L, D] + writes of du, d(dt_lin) and the dB/dC columns
+    (DESIGN.md section 4)."""
+    from vitcnn_amd._lib import lib
+    from vitcnn_amd.model import NDIR, _Program
+    dev = model.flat_params.device
+    prog = _Program(model, dev, batch, True, "grad")
+    L = lib()
+    blk, pfx, H = model.hsi1, "hsi1", model.patch
+    E = blk.embed
+    D, R, Lt = E // 2, -(-E // 16), H * H
+    XW = R + 32
+    rows, nr = batch * Lt, NDIR * batch * Lt
+    f = prog.ws.f
+    mx, gv = pfx + ".global_view.layers.0", pfx + ".global_view"
+    P = prog.P
+    order = prog.tab[("order", H)].data_ptr()
+    outs = torch.empty(D * 16 + D + NDIR, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def fn():
+        L.vc_mamba_scan_bwd(batch, Lt, D, R, NDIR, f(pfx + ".U", nr * D), f(pfx + ".XD", nr * XW), order,
+                            P[mx + ".dt_proj.weight"], P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"],
+                            P[gv + ".weights"], f(pfx + ".Y", nr * D), f(pfx + ".dYP", rows * D),
+                            f(pfx + ".dU", nr * D), f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW),
+                            outs.data_ptr(), outs.data_ptr() + 4 * D * 16, outs.data_ptr() + 4 * (D * 16 + D),
+                            prog.scr_p, prog.scr_n, stream.cuda_stream)
+
+    t = time_kernel(fn, reps, stream)
+    algo = 4.0 * (nr * D * 2 + nr * XW + rows * D + nr * D * 2 + nr * 32)
+    achieved = algo / t / 1e9
+    traffic = _traffic_from_profile("scan_bwd<9>")
+    return {"kernel": "scan_bwd<9> (hsi1 selective-scan backward, 640 seq x 81 tokens x 72 ch x 16 states)",
+            "bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic, "avg_launch_us": round(t * 1e6, 2),
+            "algorithmic_bytes_per_launch": algo}
+
+
+def gemm_roofline(model, batch, reps):
+    """The largest GEMM of the step (hsi1.local_feature im2col'ed 3x3 conv, M = B*49, N = 256,
+    K = 9*144) timed the same way; MFMA-bound (fp32 peak).  Reported beside the dominant kernel."""
     from vitcnn_amd._lib import lib
     from vitcnn_amd.model import _Program
     dev = model.flat_params.device
@@ -89,8 +144,8 @@ def dominant_kernel_roofline(model, batch, reps):
     achieved = flops / t / 1e12
     return {"kernel": "gemm_f32_mfma<false,true> (hsi1.local_feature conv3x3, M=%d N=%d K=%d)" % (M, N, K),
             "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
-            "avg_launch_us": round(t * 1e6, 2), "flop_per_launch": flops}
+            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "avg_launch_us": round(t * 1e6, 2),
+            "flop_per_launch": flops}
 
 
 def cpu_baseline(steps):
@@ -143,9 +198,11 @@ def main():
         # step's side streams are captured with it
         holder["loss"] = fused_train_step(model, crit, hsi, lidar, target)
 
+    from vitcnn_amd import parallel
+
     def allreduce():
-        if world > 1:
-            dist.all_reduce(model.flat_params.grad, op=dist.ReduceOp.SUM)
+        # one RCCL all-reduce of the flat gradient (active parameters); 1/world folded into AdamW
+        parallel.allreduce_gradients(model, opt)
 
     def eager_step():
         opt.zero_grad(set_to_none=True)
@@ -210,6 +267,7 @@ def main():
     ms_sync = (time.perf_counter() - t1) / nsync * 1e3
 
     roof = dominant_kernel_roofline(model, args.batch, args.kernel_reps)
+    roof_gemm = gemm_roofline(model, args.batch, args.kernel_reps)
     patches = world * args.batch * args.steps
     value = patches / elapsed
     out = {
@@ -228,6 +286,7 @@ def main():
                              "peak_tflops_fp32_mfma": PEAK_FP32_MFMA_TFLOPS,
                              "frac": round(value / world * GFLOP_PER_PATCH * 1e-3 / PEAK_FP32_MFMA_TFLOPS, 5)},
         "roofline": roof,
+        "roofline_gemm": roof_gemm,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_steps)

@@ -53,7 +53,7 @@ __global__ void dirconv_fwd(int total, FastDiv fD, FastDiv fL, FastDiv fB, const
 }
 
 struct ScanArgs {
-  int B, L, D, R;
+  int B, L, D, R, nchunk;
   const float* u;      // [nseq*L, D]
   const float* xdbl;   // [nseq*L, R+2N]
   const int* order;    // [ndir*L]
@@ -62,6 +62,18 @@ struct ScanArgs {
   const float* alog;   // [D, N]
   const float* dskip;  // [D]
 };
+
+// Block -> (sequence, channel chunk) for a 1-D grid of nseq * nchunk blocks.  Workgroups are dealt
+// to the 8 XCDs round-robin by dispatch order, so the identity map would spread the nchunk blocks
+// of one sequence (which all stage the same x_proj rows and gathered tokens) over different L2s.
+// Folding the id XCD-major keeps them on one XCD and adjacent in time (L2 reuse); when the grid
+// is not a multiple of 8 the identity map is used.
+__device__ __forceinline__ void seq_chunk(int nchunk, int& s, int& chunk) {
+  const int nb = gridDim.x, h = blockIdx.x;
+  const int l = (nb & 7) ? h : (h & 7) * (nb >> 3) + (h >> 3);
+  s = l / nchunk;
+  chunk = l - s * nchunk;
+}
 
 __device__ __forceinline__ float gate_softmax(const float* logits, int ndir, int k) {
   float mx = logits[0];
@@ -130,7 +142,9 @@ __global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ 
   float* dts = wsm + DPB * R;        // [L][16]
   float* us = dts + a.L * DPB;         // [L][16]
   float* yb = us + a.L * DPB;          // [L][16]
-  const int s = blockIdx.x, d0 = blockIdx.y * DPB;
+  int s, chunk;
+  seq_chunk(a.nchunk, s, chunk);
+  const int d0 = chunk * DPB;
   const int tid = threadIdx.x, dl = tid >> 4, n = tid & 15;
   const int d = d0 + dl;
   const bool valid = d < a.D;
@@ -163,10 +177,10 @@ __global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ 
 struct ScanBwdOut {
   float* du;        // [nseq*L, D]
   float* ddtl;      // [nseq*L, D]  grad of W_dt dtr + b_dt (pre-softplus)
-  float* dbc_part;  // [gridDim.y][nseq*L][2N]
+  float* dbc_part;  // [nchunk][nseq*L][2N]
   float* da_part;   // [nseq][D*N]
   float* dd_part;   // [nseq][D]  (only columns of this block's chunk written)
-  float* dg_part;   // [nseq][gridDim.y]
+  float* dg_part;   // [nseq][nchunk]
 };
 
 template <int RT>
@@ -190,7 +204,10 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
   float* ck = dr + a.L * DPB;             // [nck][256]
   float* bc = ck + nck * 256;             // [4][CK][32]
   float* red = bc + 4 * CK * 32;          // [256] dD partials, then [4] dg partials
-  const int s = blockIdx.x, k = s / a.B, d0 = blockIdx.y * DPB;
+  int s, chunk;
+  seq_chunk(a.nchunk, s, chunk);
+  const int k = s / a.B, d0 = chunk * DPB;
+  const int nseq = gridDim.x / a.nchunk;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, dl = tid >> 4, n = tid & 15;
   const int d = d0 + dl;
   const bool valid = d < a.D;
@@ -216,7 +233,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
 
   // phase 2: reverse sweep, one checkpoint chunk at a time
   float dh_carry = 0.f, dA_acc = 0.f;
-  float* dst = o.dbc_part + ((long)blockIdx.y * gridDim.x + s) * a.L * 2 * NST;
+  float* dst = o.dbc_part + ((long)chunk * nseq + s) * a.L * 2 * NST;
   for (int c = nck - 1; c >= 0; --c) {
     const int t0 = c * CK;
     const float hin = ck[c * 256 + tid];
@@ -291,7 +308,7 @@ __global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const floa
   __syncthreads();
   if (lane == 0) red[wave] = v;
   __syncthreads();
-  if (tid == 0) o.dg_part[(long)s * gridDim.y + blockIdx.y] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) o.dg_part[(long)s * a.nchunk + chunk] = red[0] + red[1] + red[2] + red[3];
 }
 
 // token-wise SiLU(z) gate of the combined output, backward:
@@ -477,8 +494,8 @@ VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* 
   VC_REQUIRE(B > 0 && L > 0 && D > 0 && R > 0 && R <= 64 && ndir > 0);
   const size_t sm = scan_fwd_smem(L, R);
   VC_REQUIRE(sm <= 160 * 1024);
-  ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
-  const dim3 grid(ndir * B, vc_cdiv(D, DPB));
+  ScanArgs a{B, L, D, R, vc_cdiv(D, DPB), u, xdbl, order, dt_w, dt_b, A_log, Dskip};
+  const dim3 grid(ndir * B * vc_cdiv(D, DPB));
   if (R == 9) hipLaunchKernelGGL(scan_fwd<9>, grid, dim3(256), sm, stream, a, y);
   else if (R == 16) hipLaunchKernelGGL(scan_fwd<16>, grid, dim3(256), sm, stream, a, y);
   else hipLaunchKernelGGL(scan_fwd<0>, grid, dim3(256), sm, stream, a, y);
@@ -533,9 +550,9 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   float* p_g = p_d + need_d;
   float* p_rest = p_g + need_g;
   long rest = ws_floats - (need_bc + need_a + need_d + need_g);
-  ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
+  ScanArgs a{B, L, D, R, nchunk, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
   ScanBwdOut o{du, ddt_lin, p_bc, p_a, p_d, p_g};
-  const dim3 grid(nseq, nchunk);
+  const dim3 grid(nseq * nchunk);
   if (R == 9) hipLaunchKernelGGL(scan_bwd<9>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
   else if (R == 16) hipLaunchKernelGGL(scan_bwd<16>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
   else hipLaunchKernelGGL(scan_bwd<0>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
