@@ -84,8 +84,10 @@ def dominant_kernel_roofline(model, batch, reps):
     block hsi1 (`scan_bwd<9>`, grid 640 sequences x 5 channel chunks), the longest single launch
     of the step.  It is a sequential recurrence over 81 tokens with no matrix work, so its roofline
     is HBM.  Algorithmic bytes per launch = compulsory reads of u, x_proj rows, yp (each
-    [10*B*L, *]) and d(yp) [B*L, D] + writes of du, d(dt_lin) and the dB/dC columns
-    (DESIGN.md section 4)."""
+    [10*B*L, *]), d(yp) [B*L, D] and the forward's 8-token state checkpoints
+    [10*B][ceil(L/8)][16][D] + writes of du, d(dt_lin) and the dB/dC columns (DESIGN.md
+    section 4).  The timed call is the whole vc_mamba_scan_bwd entry point (scan_bwd + its two
+    small column sums + gate gradient)."""
     from vitcnn_amd._lib import lib
     from vitcnn_amd.model import NDIR, _Program
     dev = model.flat_params.device
@@ -101,18 +103,20 @@ def dominant_kernel_roofline(model, batch, reps):
     P = prog.P
     order = prog.tab[("order", H)].data_ptr()
     outs = torch.empty(D * 16 + D + NDIR, device=dev)
+    ckpt = L.vc_mamba_scan_ckpt_floats(batch, Lt, D, NDIR)
     stream = torch.cuda.current_stream(dev)
 
     def fn():
         L.vc_mamba_scan_bwd(batch, Lt, D, R, NDIR, f(pfx + ".U", nr * D), f(pfx + ".XD", nr * XW), order,
                             P[mx + ".dt_proj.weight"], P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"],
                             P[gv + ".weights"], f(pfx + ".Y", nr * D), f(pfx + ".dYP", rows * D),
+                            f(pfx + ".CKP", ckpt),
                             f(pfx + ".dU", nr * D), f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW),
                             outs.data_ptr(), outs.data_ptr() + 4 * D * 16, outs.data_ptr() + 4 * (D * 16 + D),
                             prog.scr_p, prog.scr_n, stream.cuda_stream)
 
     t = time_kernel(fn, reps, stream)
-    algo = 4.0 * (nr * D * 2 + nr * XW + rows * D + nr * D * 2 + nr * 32)
+    algo = 4.0 * (nr * D * 2 + nr * XW + rows * D + ckpt + nr * D * 2 + nr * 32)
     achieved = algo / t / 1e9
     traffic = _traffic_from_profile("scan_bwd<9>")
     return {"kernel": "scan_bwd<9> (hsi1 selective-scan backward, 640 seq x 81 tokens x 72 ch x 16 states)",

@@ -117,9 +117,12 @@ VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order,
 /* selective scan of every direction's sequence (modeling_mamba.py:175-283), ungated:
  * yp[k,b,t,d] = sum_n C_t[n] h_t[d,n] + D_d u_t[d]; h_t = exp(dt A) h_{t-1} + dt B_t u_t,
  * dt = softplus(W_dt dtr_t + b_dt).  u/xdbl/yp are [ndir*B*L, D] / [.., R+32] / [.., D]. */
+/* ckpt (nullable): [ndir*B][ceil(L/8)][16][D] fp32 states entering every 8-token segment, saved
+ * for vc_mamba_scan_bwd; vc_mamba_scan_ckpt_floats gives its size (-1 on bad arguments) */
+VC_API int vc_mamba_scan_ckpt_floats(int B, int L, int D, int ndir);
 VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                              const int* order, const float* dt_w, const float* dt_b, const float* A_log,
-                             const float* Dskip, float* yp, hipStream_t stream);
+                             const float* Dskip, float* yp, float* ckpt, hipStream_t stream);
 /* ypsum[b,l,:] = sum_k softmax(gate_logits)_k yp[k, b, inv_k(l), :]  (un-permute + gate, :694-701);
  * ysum = ypsum * SiLU(z[b,l,:]) — the token-wise SiLU(z) gate of modeling_mamba.py:274 applied
  * once after the combine (it commutes with the permutation and the gated sum) */
@@ -129,12 +132,13 @@ VC_API int vc_mamba_combine_fwd(int B, int L, int D, int ndir, const int* inv_or
 VC_API int vc_mamba_gate_bwd(int B, int L, int D, const float* xz, const float* ypsum, const float* dysum,
                              float* dyp, float* dxz, hipStream_t stream);
 /* backward of scan + gated combine given dyp: du, ddt_lin (pre-softplus) per sequence position;
- * the B/C columns of dxdbl (ld R+32); dA_log [D,16], dDskip [D], dgate_logits [ndir] (all overwritten) */
+ * the B/C columns of dxdbl (ld R+32); dA_log [D,16], dDskip [D], dgate_logits [ndir] (all overwritten).
+ * ckpt: the states vc_mamba_scan_fwd saved (nullable: recomputed into ws) */
 VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                              const int* order, const float* dt_w, const float* dt_b, const float* A_log,
                              const float* Dskip, const float* gate_logits, const float* yp, const float* dyp,
-                             float* du, float* ddt_lin, float* dxdbl, float* dA_log, float* dDskip,
-                             float* dgate_logits, float* ws, long ws_floats, hipStream_t stream);
+                             const float* ckpt, float* du, float* ddt_lin, float* dxdbl, float* dA_log,
+                             float* dDskip, float* dgate_logits, float* ws, long ws_floats, hipStream_t stream);
 /* backward of gather + conv1d + SiLU: du is turned into dpre in place; the x half of dxz [B*L, 2D]
  * is overwritten (summed over the directions); conv weight [D,1,4] / bias [D] grads overwritten */
 VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order, const int* inv_order,
@@ -153,6 +157,10 @@ VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, cons
                           float* bn_buffers, float eps, float momentum, double* stats, float* a, hipStream_t stream);
 VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
                           const double* stats, const float* da, float* df, float* dparams, hipStream_t stream);
+/* mask [B, S, HW] uint8 = the ReLU decisions (BN(1) output > 0) attn_fwd / attn_bwd take, from the
+ * same stats (test instrumentation: the float64 parity yardstick follows the HIP path's fp32 ties) */
+VC_API int vc_tl_relu_mask(int B, int HW, int S, const float* mx, const float* avg, const float* params,
+                           const double* stats, unsigned char* mask, hipStream_t stream);
 /* dx[i,:] += d(avg)/C, dx[i, argmax] += d(max), summed over the S tokens (accumulates) */
 VC_API int vc_tl_pixel_bwd(long M, int C, int S, const float* df, const float* params, const int* amx, float* dx,
                            long lddx, hipStream_t stream);

@@ -66,6 +66,18 @@ def relu_masks_from_workspace(model, B):
         grab(blk + ".local_feature", S, cout)
         grab(blk + ".FusionLayer.FusionLayer", S, cout)
         grab(blk + ".fusion.FusionLayer", S, cout)
+    # TokenLearner BN(1) ReLUs: recomputed by the HIP path's own expression (vc_tl_relu_mask)
+    from vitcnn_amd._lib import lib
+    params = model._ptrs()[1]
+    for blk, H, cout in (("hsi1", P, model.hsi1.cout), ("hsi2", P - 2, model.hsi2.cout)):
+        S, HW = (H - 2) ** 2, H * H
+        for tl in (".global_feature", ".channel_token"):
+            pfx = blk + tl
+            mask = torch.empty(B * S * HW, dtype=torch.uint8, device=ws.device)
+            lib().vc_tl_relu_mask(B, HW, S, ws.tensor(pfx + ".mx").data_ptr(), ws.tensor(pfx + ".avg").data_ptr(),
+                                  params[pfx + ".tokenizers.0.conv.0.weight"], ws.tensor(pfx + ".st").data_ptr(),
+                                  mask.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            masks[pfx] = mask.view(B, S, H, H).cpu().bool()
     grab("lidar1", P - 2, 16)
     grab("lidar2", P - 4, 32)
     grab("fusion1.FusionLayer", P - 2, 128)
@@ -73,12 +85,37 @@ def relu_masks_from_workspace(model, B):
     return masks
 
 
-def masked_oracle_step(O, state, hsi, lidar, target, weight, masks):
+def tl_pooled_from_workspace(model, B):
+    """The HIP path's TokenLearner pooled inputs per TokenLearner prefix: (channel max [B,1,H,H]
+    float64, its channel index [B,1,H,H] int64, channel mean [B,1,H,H] float64), read from the
+    saved `<pfx>.mx / .amx / .avg` rows of the training workspace."""
+    ws = next(v for k, v in model._ws.items() if k[2][0] == "train")
+    P = model.patch
+    out = {}
+    for blk, H in (("hsi1", P), ("hsi2", P - 2)):
+        n = B * H * H
+        for tl in (".global_feature", ".channel_token"):
+            pfx = blk + tl
+            mx = ws.tensor(pfx + ".mx")[:n].view(B, 1, H, H).cpu().double()
+            amx = ws.tensor(pfx + ".amx")[:n].view(B, 1, H, H).cpu().long()
+            avg = ws.tensor(pfx + ".avg")[:n].view(B, 1, H, H).cpu().double()
+            out[pfx] = (mx, amx, avg)
+    return out
+
+
+def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None):
     """oracle train step in which the conv/fusion ReLUs use the given masks (pre * mask) instead of
     their own sign test.  A pre-activation within rounding distance of zero is an fp32 tie that the
     HIP path and the CPU reference may resolve differently; evaluating the float64 yardstick with the
-    HIP path's decisions keeps such a tie from being scored as a gradient error."""
-    orig = (O.bn_conv3_relu, O.conv_bn_relu_1x1)
+    HIP path's decisions keeps such a tie from being scored as a gradient error.
+
+    `pooled` ({prefix: (max, argmax, mean)} from tl_pooled_from_workspace): TokenLearner BN(1)
+    normalises a 2->1 conv of the pooled channel max / mean whose spread is a tiny fraction of its
+    mean, so the fp32 rounding of the pooled values is amplified by 1/std.  The yardstick then takes
+    the HIP path's pooled VALUES (gradients still flow to the argmax channel and to every channel
+    through the mean, exactly as in the reference)."""
+    orig = (O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner)
+    F = torch.nn.functional
 
     def bn_conv3(P, pfx, x):
         pre = O.conv2d(P, pfx + ".conv", O.batchnorm(P, pfx + ".bn", x))
@@ -88,8 +125,28 @@ def masked_oracle_step(O, state, hsi, lidar, target, weight, masks):
         pre = O.batchnorm(P, pfx + ".1", O.conv2d(P, pfx + ".0", x))
         return pre * masks[pfx].to(pre.dtype) if pfx in masks else torch.relu(pre)
 
-    O.bn_conv3_relu, O.conv_bn_relu_1x1 = bn_conv3, conv1x1
+    def token_learner(P, pfx, x, S):   # oracle token_learner with the HIP path's decisions / pooling
+        given = pooled is not None and pfx in pooled
+        if pfx not in masks and not given:
+            return orig[2](P, pfx, x, S)
+        if given:
+            mx_h, amx_h, avg_h = (t.to(x.dtype) if t.is_floating_point() else t for t in pooled[pfx])
+            g = torch.gather(x, 1, amx_h)
+            m = x.mean(dim=1, keepdim=True)
+            pool = torch.cat([mx_h + (g - g.detach()), avg_h + (m - m.detach())], dim=1)
+        else:
+            pool = torch.cat([x.max(dim=1, keepdim=True)[0], x.mean(dim=1, keepdim=True)], dim=1)
+        toks = []
+        for i in range(S):
+            t = f"{pfx}.tokenizers.{i}.conv"
+            f = F.conv2d(pool, P[t + ".0.weight"], P[t + ".0.bias"])
+            pre = O.batchnorm(P, t + ".1", f)
+            a = torch.sigmoid(pre * masks[pfx][:, i:i + 1].to(pre.dtype) if pfx in masks else torch.relu(pre))
+            toks.append((x * a).mean(dim=(-2, -1)))
+        return torch.stack(toks, dim=1)
+
+    O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner = bn_conv3, conv1x1, token_learner
     try:
         return O.train_step(state, hsi, lidar, target, weight)
     finally:
-        O.bn_conv3_relu, O.conv_bn_relu_1x1 = orig
+        O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner = orig

@@ -49,8 +49,12 @@ def _ref(xz, order, cw, cb, wx, wdt, bdt, alog, dsk, gate, B, L, D, R, ndir):
     return ys, leaves
 
 
-@pytest.mark.parametrize("L,D,E", [(81, 72, 144), (49, 128, 256)])
-def test_mamba_kernels_vs_float64(L, D, E):
+@pytest.mark.parametrize("L,D,E,use_ckpt", [(81, 72, 144, True), (49, 128, 256, True), (81, 72, 144, False),
+                                            (121, 72, 144, True), (25, 40, 80, True)])
+def test_mamba_kernels_vs_float64(L, D, E, use_ckpt):
+    """(121, 72): the MUUFL-shape hsi1 (11x11 patches); (25, 40): an odd channel count and a
+    sequence shorter than 5 checkpoint segments; use_ckpt=False recomputes the states in the
+    backward."""
     lib = _lib()
     torch.manual_seed(0)
     B, ndir, N = 2, 10, 16
@@ -87,7 +91,9 @@ def test_mamba_kernels_vs_float64(L, D, E):
     lib.vc_mamba_dirconv_fwd(B, L, D, ndir, P(o32), P(xz_d), P(cw_d), P(cb_d), P(U), s)
     lib.vc_gemm(0, 1, rows, XW, D, 1.0, P(U), D, 0, P(wx_d), D, 0, 0.0, P(XD), XW, 0, 1, None, None, 0, 0, 0, None,
                 P(ws), ws.numel(), s)
-    lib.vc_mamba_scan_fwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d), P(Y), s)
+    CKP = torch.empty(lib.vc_mamba_scan_ckpt_floats(B, L, D, ndir), device=DEV)
+    lib.vc_mamba_scan_fwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d), P(Y),
+                          P(CKP), s)
     YP = torch.empty(B * L, D, device=DEV)
     lib.vc_mamba_combine_fwd(B, L, D, ndir, P(inv32), P(gate_d), P(Y), P(xz_d), P(YP), P(YS), s)
     torch.cuda.synchronize()
@@ -103,7 +109,8 @@ def test_mamba_kernels_vs_float64(L, D, E):
     dA, dDs, dG = torch.empty(D, N, device=DEV), torch.empty(D, device=DEV), torch.empty(ndir, device=DEV)
     lib.vc_mamba_gate_bwd(B, L, D, P(xz_d), P(YP), P(dys_d), P(dYP), P(dXZ), s)
     lib.vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
-                          P(gate_d), P(Y), P(dYP), P(dU), P(dDTL), P(dXD), P(dA), P(dDs), P(dG), P(ws), ws.numel(), s)
+                          P(gate_d), P(Y), P(dYP), P(CKP) if use_ckpt else None, P(dU), P(dDTL), P(dXD), P(dA),
+                          P(dDs), P(dG), P(ws), ws.numel(), s)
     dWdt, dbdt = torch.empty(D, R, device=DEV), torch.empty(D, device=DEV)
     lib.vc_gemm(0, 0, rows, R, D, 1.0, P(dDTL), D, 0, P(wdt_d), R, 0, 0.0, P(dXD), XW, 0, 1, None, None, 0, 0, 0,
                 None, P(ws), ws.numel(), s)

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from helpers import (golden_batch, hash_state_dict, load_npz, masked_oracle_step, rel_err,
-                     relu_masks_from_workspace)
+                     relu_masks_from_workspace, tl_pooled_from_workspace)
 from oracle import vitcnn_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -76,7 +76,8 @@ def b4():
     sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
     st64 = O.make_state(sd64)
     masks = relu_masks_from_workspace(m, 4)
-    masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(), masks)
+    masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(), masks,
+                       pooled=tl_pooled_from_workspace(m, 4))
     ref64 = {k: st64[k].grad for k in O.param_names(st64)}
     # fp32 reference's own error is measured against its own ReLU decisions
     st64r = O.make_state(sd64)

@@ -18,7 +18,7 @@ step() {  # step NAME SECONDS CMD...
   esac
 }
 
-step test 600 python -m pytest tests/ -m gpu -q -rf
+step test 600 python -u -m pytest tests/ -m gpu -q -rf --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 100 --warmup 10 ${BENCH_ARGS}
 step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline

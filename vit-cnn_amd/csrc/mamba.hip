@@ -18,17 +18,14 @@
 // combine, and its backward (dz, and d(yp) = g_k dysum SiLU(z)) is an elementwise pass outside
 // the sequential scan (gate_bwd) instead of 10 x 16 redundant evaluations inside it.
 //
-// The scan keeps its 16-wide state in fp32 registers: one wave = 4 channels x 16 states,
-// state reductions are 16-lane DPP sums.  The backward re-runs the recurrence from 16-step
-// LDS checkpoints (nothing of size [seq, D, L, N] is ever stored) and reduces dB / dC over
-// channels through per-wave LDS slabs, so every reduction is fixed-order.
+// The scan runs one lane per channel with the 16-wide state in fp32 registers (see scan_fwd);
+// the backward re-runs the recurrence from the forward's segment checkpoints (nothing of size
+// [seq, D, L, N] is ever stored), and every reduction is fixed-order.
 #include "common.h"
 
 namespace {
 
 constexpr int NST = 16;     // ssm state size (config state_size=16, Mutimodality_Mamba7.py:316)
-constexpr int CK = 16;      // checkpoint interval of the backward recompute
-constexpr int DPB = 16;     // channels per block (4 waves x 4 channels)
 
 // one thread per (k, b, t, d); index decomposition with launch-time FastDivs (no integer divide)
 __global__ void dirconv_fwd(int total, FastDiv fD, FastDiv fL, FastDiv fB, const int* __restrict__ order,
@@ -52,8 +49,16 @@ __global__ void dirconv_fwd(int total, FastDiv fD, FastDiv fL, FastDiv fB, const
   u[idx] = silu_f(pre);
 }
 
+__device__ __forceinline__ float gate_softmax(const float* logits, int ndir, int k) {
+  float mx = logits[0];
+  for (int i = 1; i < ndir; ++i) mx = fmaxf(mx, logits[i]);
+  float den = 0.f;
+  for (int i = 0; i < ndir; ++i) den += __expf(logits[i] - mx);
+  return __expf(logits[k] - mx) / den;
+}
+
 struct ScanArgs {
-  int B, L, D, R, nchunk;
+  int B, L, D, R;
   const float* u;      // [nseq*L, D]
   const float* xdbl;   // [nseq*L, R+2N]
   const int* order;    // [ndir*L]
@@ -63,252 +68,333 @@ struct ScanArgs {
   const float* dskip;  // [D]
 };
 
-// Block -> (sequence, channel chunk) for a 1-D grid of nseq * nchunk blocks.  Workgroups are dealt
-// to the 8 XCDs round-robin by dispatch order, so the identity map would spread the nchunk blocks
-// of one sequence (which all stage the same x_proj rows and gathered tokens) over different L2s.
-// Folding the id XCD-major keeps them on one XCD and adjacent in time (L2 reuse); when the grid
-// is not a multiple of 8 the identity map is used.
-__device__ __forceinline__ void seq_chunk(int nchunk, int& s, int& chunk) {
-  const int nb = gridDim.x, h = blockIdx.x;
-  const int l = (nb & 7) ? h : (h & 7) * (nb >> 3) + (h >> 3);
-  s = l / nchunk;
-  chunk = l - s * nchunk;
+// Selective scan.  Block = one sequence s = k*B + b (all channels); wave = 16 channels x 4 state
+// groups: lane = q * 16 + c, row q holds states n = 4q..4q+3 of channel 16*wave + c.
+//
+// gfx950 issues one wave64 VALU instruction per 4 cycles (an exp per 8) and the scan has little
+// else to do, so it is bounded by VALU issue; the mapping decides how much work is redundant and
+// how many waves hide latency.  Per (token, channel) work (dt*u, du, ddt, the dt lookup) is repeated
+// 4x (once per row) instead of 16x in a lane-per-state mapping, each lane's 4 states give 4
+// independent chains, and 4x more waves than a lane-per-channel mapping keep every SIMD busy.
+// Sums over the 16 states are 4 in-register terms plus one cross-row sum (two VALU half swaps);
+// the backward's dB_t / dC_t (sums over channels) are a reduce-scatter inside each 16-lane row
+// (DPP) and a fixed-order combine of the waves' partials in LDS.
+//
+// dt = softplus(W_dt x_t + b_dt) depends on the token only through x_t, so it is computed for all
+// (token, channel) pairs up front into LDS, a pass without serial dependence.  The forward stores
+// the state entering every SCK-token segment ([nseq][nseg][16][D]); the backward re-runs one
+// segment at a time from those checkpoints (the segment's states stay in registers) and sweeps it
+// in reverse, so nothing of size [seq, L, D, 16] is ever stored.
+constexpr int SCK = 8;                  // tokens per checkpoint segment
+constexpr int NQ = 4;                   // states per lane
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ int seg_count(int L) { return (L + SCK - 1) / SCK; }
+
+// softplus(beta = 1, threshold = 20) with an accurate log1p: log1p(e) = log(1 + e) * e / ((1 + e) - 1)
+__device__ __forceinline__ float softplus_c(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * LOG2E);
+  const float u = 1.f + e;
+  const float lp = u == 1.f ? e : __builtin_amdgcn_logf(u) * LN2 * (e * __builtin_amdgcn_rcpf(u - 1.f));
+  return x > 20.f ? x : lp;
 }
 
-__device__ __forceinline__ float gate_softmax(const float* logits, int ndir, int k) {
-  float mx = logits[0];
-  for (int i = 1; i < ndir; ++i) mx = fmaxf(mx, logits[i]);
-  float den = 0.f;
-  for (int i = 0; i < ndir; ++i) den += __expf(logits[i] - mx);
-  return __expf(logits[k] - mx) / den;
+// exp(x) - 1 without cancellation near 0: a degree-6 Taylor polynomial for |x| < 1/4 (truncation
+// < 5e-8 relative), exp(x) - 1 elsewhere
+__device__ __forceinline__ float expm1_c(float x) {
+  const float p = x * (1.f + x * (0.5f + x * (1.f / 6 + x * (1.f / 24 + x * (1.f / 120 + x * (1.f / 720))))));
+  return fabsf(x) < 0.25f ? p : __builtin_amdgcn_exp2f(x * LOG2E) - 1.f;
 }
 
-// Stage one sequence (seq s = k*B + b, channels d0..d0+15) into LDS:
-//   xs [L][XW] x_proj output rows (dt-rank | B | C), wsm [16][R] W_dt rows, us [L][16] u,
-//   dts [L][16] dt = softplus(W_dt xs[:R] + b_dt), and (bwd only) dr [L][16] = g_k d(yp), the
-//   gradient of this direction's yp gathered through the order.  The bwd staging also folds the
-//   token-wise partial sums dD += d(yp) u and dgate_k += dyp yp into (dd_acc, dg_acc), and
-//   stages dsp [L][16] = softplus'(dt_lin).
-template <bool BWD, int RT>
-__device__ __forceinline__ void scan_stage(const ScanArgs& a, int s, int d0, float* xs, float* wsm, float* dts,
-                                           float* dsp, float* us, float* dr, float g, const float* dyp,
-                                           const float* yp, float& dd_acc, float& dg_acc) {
-  const int R = RT ? RT : a.R;  // dt rank (compile-time for the two block shapes: 9, 16)
-  const int XW = R + 2 * NST;
-  const int k = s / a.B, b = s % a.B;
-  const int tid = threadIdx.x;
-  const float* xsrc = a.xdbl + (long)s * a.L * XW;
-  for (int i = tid; i < a.L * XW; i += 256) xs[i] = xsrc[i];
-  for (int i = tid; i < DPB * R; i += 256) {
-    const int dd = d0 + i / R;
-    wsm[i] = dd < a.D ? a.wdt[(long)dd * R + i % R] : 0.f;
+// LDS image of one sequence (Lp = SCK * segments tokens; rows L..Lp-1 zero):
+//   Bs [Lp][16], Cs [Lp][16] (lane (q, c) reads its 4 states of a token as one ds_read_b128),
+//   dts [Lp][Dp] dt per (token, channel), Dp = 16 * waves; xr [Lp][R] the dt-rank columns.
+struct SeqLds {
+  float *Bs, *Cs, *dts, *xr;
+  __device__ SeqLds(float* base, int Lp, int R, int Dp) {
+    Bs = base;
+    Cs = Bs + Lp * NST;
+    dts = Cs + Lp * NST;
+    xr = dts + Lp * Dp;
   }
-  for (int i = tid; i < a.L * DPB; i += 256) {
-    const int t = i / DPB, d = d0 + i % DPB;
-    float uv = 0.f, gv = 0.f;
-    if (d < a.D) {
-      const long pos = ((long)s * a.L + t) * a.D + d;
-      uv = a.u[pos];
-      if (BWD) {
-        const float dv = dyp[((long)b * a.L + a.order[k * a.L + t]) * a.D + d];
-        gv = g * dv;
-        dd_acc += gv * uv;
-        dg_acc += dv * yp[pos];
-      }
-    }
-    us[i] = uv;
-    if (BWD) dr[i] = gv;
-  }
-  __syncthreads();
-  for (int i = tid; i < a.L * DPB; i += 256) {
-    const int t = i / DPB, dl = i % DPB, d = d0 + dl;
-    float dtl = d < a.D ? a.bdt[d] : 0.f;
-    const float* row = xs + t * XW;
-    const float* w = wsm + dl * R;
-    for (int r = 0; r < R; ++r) dtl += w[r] * row[r];
-    dts[i] = softplus_f(dtl);
-    if (BWD) dsp[i] = dtl > 20.f ? 1.f : sigmoid_f(dtl);  // softplus'(dt_lin)
-  }
-  __syncthreads();
+};
+static size_t seq_lds_floats(int L, int R, int Dp) {
+  const size_t Lp = (size_t)((L + SCK - 1) / SCK) * SCK;
+  return Lp * (2 * NST + Dp + R);
 }
 
 template <int RT>
-__global__ __launch_bounds__(256) void scan_fwd(ScanArgs a, float* __restrict__ y) {
-  extern __shared__ float smem[];
+__device__ __forceinline__ void stage_seq(const ScanArgs& a, int s, const SeqLds& m, int Lp, int Dp) {
   const int R = RT ? RT : a.R;
   const int XW = R + 2 * NST;
-  float* xs = smem;                    // [L][XW]
-  float* wsm = xs + a.L * XW;          // [16][R]
-  float* dts = wsm + DPB * R;        // [L][16]
-  float* us = dts + a.L * DPB;         // [L][16]
-  float* yb = us + a.L * DPB;          // [L][16]
-  int s, chunk;
-  seq_chunk(a.nchunk, s, chunk);
-  const int d0 = chunk * DPB;
-  const int tid = threadIdx.x, dl = tid >> 4, n = tid & 15;
-  const int d = d0 + dl;
-  const bool valid = d < a.D;
-  float unused0 = 0.f, unused1 = 0.f;
-  scan_stage<false, RT>(a, s, d0, xs, wsm, dts, nullptr, us, nullptr, 0.f, nullptr, nullptr, unused0, unused1);
-  const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
-  const float Dd = valid ? a.dskip[d] : 0.f;
-  float h = 0.f;
-  for (int t0 = 0; t0 < a.L; t0 += CK) {
+  const float* src = a.xdbl + (long)s * a.L * XW;
+  const int n = a.L * XW, tot = Lp * XW;
+  const int nt = blockDim.x;
+  constexpr int SB = 8;
+  for (int base = 0; base < tot; base += SB * nt) {
+    float v[SB];
 #pragma unroll
-    for (int i = 0; i < CK; ++i) {
-      const int t = t0 + i;
-      if (t < a.L) {
-        const float* row = xs + t * XW + R;
-        const float dt = dts[t * DPB + dl];
-        const float ut = us[t * DPB + dl];
-        h = __expf(dt * A) * h + dt * row[n] * ut;
-        const float ys = row16_sum(h * row[NST + n]);
-        if (n == 0) yb[t * DPB + dl] = ys + Dd * ut;
+    for (int j = 0; j < SB; ++j) {
+      const int i = base + j * nt + threadIdx.x;
+      v[j] = i < n ? src[i] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < SB; ++j) {
+      const int i = base + j * nt + threadIdx.x;
+      if (i < tot) {
+        const int t = i / XW, col = i - t * XW;
+        if (col < R) m.xr[t * R + col] = v[j];
+        else if (col < R + NST) m.Bs[t * NST + col - R] = v[j];
+        else m.Cs[t * NST + col - R - NST] = v[j];
       }
     }
   }
+  // dt for every (token, channel): the block has 4 * Dp threads, so thread i handles channel
+  // c = i % Dp of tokens i / Dp, i / Dp + 4, ...; its W_dt row and bias are loaded once
+  const int c = threadIdx.x % Dp;
+  const bool valid = c < a.D;
+  const int cc = valid ? c : 0;
+  float w[RT ? RT : 64];
+#pragma unroll
+  for (int r = 0; r < R; ++r) w[r] = valid ? a.wdt[(long)cc * R + r] : 0.f;
+  const float bias = valid ? a.bdt[cc] : 0.f;
   __syncthreads();
-  for (int i = tid; i < a.L * DPB; i += 256) {
-    const int t = i / DPB, dd = d0 + i % DPB;
-    if (dd < a.D) y[((long)s * a.L + t) * a.D + dd] = yb[i];
+  for (int t = threadIdx.x / Dp; t < Lp; t += nt / Dp) {
+    const float* row = m.xr + t * R;
+    float dtl = bias;
+#pragma unroll
+    for (int r = 0; r < R; ++r) dtl += w[r] * row[r];
+    m.dts[t * Dp + c] = softplus_c(dtl);
   }
+  __syncthreads();
+}
+
+// sum over the 4 rows of a wave (cross_row_sum, common.h) of 4 in-lane terms
+__device__ __forceinline__ float state_sum(float a0, float a1, float a2, float a3) {
+  return cross_row_sum((a0 + a1) + (a2 + a3));
+}
+
+template <int RT>
+__global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ y, float* __restrict__ ckpt) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int R = RT ? RT : a.R;
+  const int nseg = seg_count(a.L), Lp = nseg * SCK;
+  const int Dp = (blockDim.x >> 6) * 16;
+  const SeqLds m(smem, Lp, R, Dp);
+  const int s = blockIdx.x, lane = threadIdx.x & 63, q = lane >> 4;
+  const int d = (threadIdx.x >> 6) * 16 + (lane & 15);
+  const bool valid = d < a.D;
+  const int dc = valid ? d : 0;
+  float A2[NQ];
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) A2[j] = valid ? -__expf(a.alog[dc * NST + NQ * q + j]) * LOG2E : 0.f;
+  const float Dd = valid ? a.dskip[dc] : 0.f;
+  stage_seq<RT>(a, s, m, Lp, Dp);
+  const float* ub = a.u + (long)s * a.L * a.D + dc;
+  float h[NQ] = {0.f, 0.f, 0.f, 0.f};
+  float un[SCK];
+#pragma unroll
+  for (int i = 0; i < SCK; ++i) un[i] = valid && i < a.L ? ub[(long)i * a.D] : 0.f;
+  for (int c = 0; c < nseg; ++c) {
+    const int t0 = c * SCK;
+    if (ckpt && valid) {
+      float* cp = ckpt + ((long)(s * nseg + c) * NST + NQ * q) * a.D + d;
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) cp[(long)j * a.D] = h[j];
+    }
+    float uc[SCK];
+#pragma unroll
+    for (int i = 0; i < SCK; ++i) {
+      uc[i] = un[i];
+      const int tn = t0 + SCK + i;
+      un[i] = valid && tn < a.L ? ub[(long)tn * a.D] : 0.f;   // prefetch the next segment
+    }
+#pragma unroll
+    for (int i = 0; i < SCK; ++i) {
+      const int t = t0 + i;
+      const float4 bv = *reinterpret_cast<const float4*>(m.Bs + t * NST + NQ * q);
+      const float4 cv = *reinterpret_cast<const float4*>(m.Cs + t * NST + NQ * q);
+      const float dt = m.dts[t * Dp + d];
+      const float dtu = dt * uc[i];
+      h[0] = __builtin_amdgcn_exp2f(dt * A2[0]) * h[0] + dtu * bv.x;
+      h[1] = __builtin_amdgcn_exp2f(dt * A2[1]) * h[1] + dtu * bv.y;
+      h[2] = __builtin_amdgcn_exp2f(dt * A2[2]) * h[2] + dtu * bv.z;
+      h[3] = __builtin_amdgcn_exp2f(dt * A2[3]) * h[3] + dtu * bv.w;
+      const float yt = state_sum(h[0] * cv.x, h[1] * cv.y, h[2] * cv.z, h[3] * cv.w) + Dd * uc[i];
+      // the 4 rows hold the same value: an unconditional store of identical bytes
+      if (y && valid && t < a.L) y[((long)s * a.L + t) * a.D + d] = yt;
+    }
+  }
+}
+
+// Sum of 8 per-lane values over the 16 lanes of each row, scattered: lane l of the row returns the
+// total of value (l & 15) >> 1.  Partners: row_mirror (15 - l), row_half_mirror (7 - l within 8),
+// quad_perm xor 2, xor 1 — each stage pairs lanes that hold the same value set, so the contributor
+// sets stay disjoint; fixed order, deterministic.
+__device__ __forceinline__ float reduce_scatter8_row(const float (&v)[8]) {
+  const int l = threadIdx.x & 15;
+  const bool b3 = l & 8, b2 = l & 4, b1 = l & 2;
+  float y4[4], z[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float keep = b3 ? v[j + 4] : v[j], send = b3 ? v[j] : v[j + 4];
+    y4[j] = keep + dpp_mov<0x140>(send);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float keep = b2 ? y4[j + 2] : y4[j], send = b2 ? y4[j] : y4[j + 2];
+    z[j] = keep + dpp_mov<0x141>(send);
+  }
+  const float keep = b1 ? z[1] : z[0], send = b1 ? z[0] : z[1];
+  const float w = keep + dpp_mov<0x4E>(send);
+  return w + dpp_mov<0xB1>(w);
 }
 
 struct ScanBwdOut {
   float* du;        // [nseq*L, D]
   float* ddtl;      // [nseq*L, D]  grad of W_dt dtr + b_dt (pre-softplus)
-  float* dbc_part;  // [nchunk][nseq*L][2N]
+  float* dxdbl;     // [nseq*L, XW] B / C columns written
   float* da_part;   // [nseq][D*N]
-  float* dd_part;   // [nseq][D]  (only columns of this block's chunk written)
-  float* dg_part;   // [nseq][nchunk]
+  float* dd_part;   // [nseq][D]
+  float* dg_part;   // [nseq]
 };
 
 template <int RT>
-__global__ __launch_bounds__(256) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
+__global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
                                                 const float* __restrict__ yp, const float* __restrict__ dyp,
-                                                ScanBwdOut o) {
-  extern __shared__ float smem[];
+                                                const float* __restrict__ ckpt, ScanBwdOut o) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // SeqLds, red [nw][SCK][32], [nw]
   const int R = RT ? RT : a.R;
   const int XW = R + 2 * NST;
-  const int nck = (a.L + CK - 1) / CK;
-  float* xs = smem;                       // [L][XW]
-  float* wsm = xs + a.L * XW;             // [16][R]
-  float* dts = wsm + DPB * R;           // [L][16]
-  float* dsp = dts + a.L * DPB;           // [L][16]  softplus'(dt_lin)
-  float* us = dsp + a.L * DPB;            // [L][16]
-  float* dr = us + a.L * DPB;             // [L][16]  d(yp) of this direction
-  // the reverse sweep consumes us[t] / dr[t] at step t and never again, so the (t, d) results
-  // du / ddt_lin overwrite them in place and are flushed once, coalesced, after the sweep
-  float* dub = us;
-  float* ddb = dr;
-  float* ck = dr + a.L * DPB;             // [nck][256]
-  float* bc = ck + nck * 256;             // [4][CK][32]
-  float* red = bc + 4 * CK * 32;          // [256] dD partials, then [4] dg partials
-  int s, chunk;
-  seq_chunk(a.nchunk, s, chunk);
-  const int k = s / a.B, d0 = chunk * DPB;
-  const int nseq = gridDim.x / a.nchunk;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, dl = tid >> 4, n = tid & 15;
-  const int d = d0 + dl;
+  const int nseg = seg_count(a.L), Lp = nseg * SCK;
+  const int nw = blockDim.x >> 6, Dp = nw * 16;
+  const SeqLds m(smem, Lp, R, Dp);
+  float* red = m.xr + Lp * R;
+  int* ord = reinterpret_cast<int*>(red + nw * SCK * 32 + nw);   // [L] this direction's order
+  const int s = blockIdx.x, k = s / a.B, b = s - k * a.B;
+  for (int t = threadIdx.x; t < a.L; t += blockDim.x) ord[t] = a.order[k * a.L + t];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, cl = lane & 15;
+  const int d = wave * 16 + cl;
   const bool valid = d < a.D;
+  const int dc = valid ? d : 0;
   const float g = gate_softmax(gate_logits, ndir, k);
-  float dD_stage = 0.f, dg_acc = 0.f;
-  scan_stage<true, RT>(a, s, d0, xs, wsm, dts, dsp, us, dr, g, dyp, yp, dD_stage, dg_acc);
-  const float A = valid ? -__expf(a.alog[d * NST + n]) : 0.f;
-  const float Dd = valid ? a.dskip[d] : 0.f;
-
-  // phase 1: forward recurrence, checkpoint the state entering every CK-step chunk
-  float h = 0.f;
-  for (int c = 0; c < nck; ++c) {
-    ck[c * 256 + tid] = h;
+  float A2[NQ];
 #pragma unroll
-    for (int i = 0; i < CK; ++i) {
-      const int t = c * CK + i;
-      if (t < a.L) {
-        const float dt = dts[t * DPB + dl];
-        h = __expf(dt * A) * h + dt * xs[t * XW + R + n] * us[t * DPB + dl];
+  for (int j = 0; j < NQ; ++j) A2[j] = valid ? -__expf(a.alog[dc * NST + NQ * q + j]) * LOG2E : 0.f;
+  const float Dd = valid ? a.dskip[dc] : 0.f;
+  stage_seq<RT>(a, s, m, Lp, Dp);
+  const long base = (long)s * a.L;
+  // the dB/dC column this lane's reduce-scatter total belongs to
+  const int vi = cl >> 1;
+  const int col = vi < 4 ? NQ * q + vi : NST + NQ * q + vi - 4;
+  float dh[NQ] = {0.f, 0.f, 0.f, 0.f}, dAacc[NQ] = {0.f, 0.f, 0.f, 0.f};
+  float dD_acc = 0.f, dg_acc = 0.f;
+  // global operands of a segment: the entering state, u, the gathered d(yp) and yp (for the gate
+  // gradient); the next segment's are loaded while this one is computed
+  float hn[NQ], un[SCK], dn[SCK], yn[SCK];
+  auto load_seg = [&](int c) {
+    const int t0 = c * SCK;
+    const float* cp = ckpt + ((long)(s * nseg + c) * NST + NQ * q) * a.D + dc;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) hn[j] = valid ? cp[(long)j * a.D] : 0.f;
+#pragma unroll
+    for (int i = 0; i < SCK; ++i) {
+      const int t = t0 + i;
+      const bool in = valid && t < a.L;
+      un[i] = in ? a.u[(base + t) * a.D + dc] : 0.f;
+      dn[i] = in ? dyp[((long)b * a.L + ord[t]) * a.D + dc] : 0.f;
+      yn[i] = in ? yp[(base + t) * a.D + dc] : 0.f;
+    }
+  };
+  __syncthreads();   // ord
+  load_seg(nseg - 1);
+  for (int c = nseg - 1; c >= 0; --c) {
+    const int t0 = c * SCK;
+    float hs[SCK + 1][NQ];   // hs[i] = state entering token t0 + i
+    float uc[SCK], dyr[SCK];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) hs[0][j] = hn[j];
+#pragma unroll
+    for (int i = 0; i < SCK; ++i) {
+      uc[i] = un[i];
+      dyr[i] = dn[i];
+      dg_acc += dyr[i] * yn[i];
+    }
+    if (c > 0) load_seg(c - 1);
+    // recompute the segment's states (and keep exp(dt A) for the reverse sweep)
+    float dAs[SCK][NQ];
+#pragma unroll
+    for (int i = 0; i < SCK; ++i) {
+      const int t = t0 + i;
+      const float4 bv = *reinterpret_cast<const float4*>(m.Bs + t * NST + NQ * q);
+      const float dt = m.dts[t * Dp + d];
+      const float dtu = dt * uc[i];
+      const float bb[NQ] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        dAs[i][j] = __builtin_amdgcn_exp2f(dt * A2[j]);
+        hs[i + 1][j] = dAs[i][j] * hs[i][j] + dtu * bb[j];
       }
     }
-  }
-
-  // phase 2: reverse sweep, one checkpoint chunk at a time
-  float dh_carry = 0.f, dA_acc = 0.f;
-  float* dst = o.dbc_part + ((long)chunk * nseq + s) * a.L * 2 * NST;
-  for (int c = nck - 1; c >= 0; --c) {
-    const int t0 = c * CK;
-    const float hin = ck[c * 256 + tid];
-    float hreg[CK], dAr[CK];
-    float hh = hin;
+    // reverse sweep
 #pragma unroll
-    for (int i = 0; i < CK; ++i) {
+    for (int i = SCK - 1; i >= 0; --i) {
       const int t = t0 + i;
-      dAr[i] = 0.f;
-      if (t < a.L) {
-        const float dt = dts[t * DPB + dl];
-        dAr[i] = __expf(dt * A);
-        hh = dAr[i] * hh + dt * xs[t * XW + R + n] * us[t * DPB + dl];
+      const float4 b4 = *reinterpret_cast<const float4*>(m.Bs + t * NST + NQ * q);
+      const float4 c4 = *reinterpret_cast<const float4*>(m.Cs + t * NST + NQ * q);
+      const float bv[NQ] = {b4.x, b4.y, b4.z, b4.w}, cv[NQ] = {c4.x, c4.y, c4.z, c4.w};
+      const float dt = m.dts[t * Dp + d], ut = uc[i], dy = g * dyr[i];
+      const float dtu = dt * ut;
+      float Sp[NQ], qp[NQ], v[8];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const float dhn = dh[j] + cv[j] * dy;                  // dL/dh_t
+        const float dA = dAs[i][j];
+        const float qq = dhn * hs[i][j] * dA;                  // dL/d(dA_t) * dA_t
+        dAacc[j] += qq * dt;
+        qp[j] = qq * A2[j];
+        Sp[j] = dhn * bv[j];
+        v[j] = dhn * dtu;                                      // dL/dB_t[n], this channel
+        v[4 + j] = dy * hs[i + 1][j];                          // dL/dC_t[n], this channel
+        dh[j] = dhn * dA;                                      // carried to t - 1
       }
-      hreg[i] = hh;
+      const float S = state_sum(Sp[0], Sp[1], Sp[2], Sp[3]);
+      const float qa = state_sum(qp[0], qp[1], qp[2], qp[3]);
+      if (valid && t < a.L) {   // the 4 rows store identical values
+        o.du[(base + t) * a.D + d] = dt * S + Dd * dy;
+        // softplus'(dt_lin) = sigmoid(dt_lin) = 1 - exp(-softplus(dt_lin))
+        o.ddtl[(base + t) * a.D + d] = (qa * LN2 + ut * S) * -expm1_c(-dt);
+      }
+      if (q == 0) dD_acc += dy * ut;
+      red[(wave * SCK + i) * 32 + col] = reduce_scatter8_row(v);   // lanes 2j, 2j+1 store the same
     }
-#pragma unroll
-    for (int i = CK - 1; i >= 0; --i) {
-      const int t = t0 + i;
-      if (t >= a.L) continue;
-      const int ti = t * DPB + dl;
-      const float dt = dts[ti];
-      const float dA = dAr[i];
-      const float Bn = xs[t * XW + R + n], Cn = xs[t * XW + R + NST + n];
-      const float ht = hreg[i];
-      const float hp = i > 0 ? hreg[i > 0 ? i - 1 : 0] : hin;
-      const float ut = us[ti], dy = dr[ti];
-      const float dh = dh_carry + Cn * dy;
-      const float ddA = dh * hp;
-      dA_acc += ddA * dA * dt * A;
-      const float ddt = row16_sum(ddA * dA * A + dh * Bn * ut);
-      const float dus = row16_sum(dh * dt * Bn);
-      dh_carry = dh * dA;
-      const float vb = cross_row_sum(dh * dt * ut), vc = cross_row_sum(dy * ht);
-      if (lane < 16) {
-        bc[(wave * CK + i) * 32 + lane] = vb;
-        bc[(wave * CK + i) * 32 + 16 + lane] = vc;
-      }
-      if (n == 0) {
-        dub[ti] = dus + dy * Dd;
-        ddb[ti] = ddt * dsp[ti];
+    __syncthreads();
+    for (int j = threadIdx.x; j < SCK * 32; j += blockDim.x) {
+      const int i = j >> 5, cc = j & 31, t = t0 + i;
+      if (t < a.L) {
+        float sum = 0.f;
+        for (int ww = 0; ww < nw; ++ww) sum += red[(ww * SCK + i) * 32 + cc];
+        o.dxdbl[(base + t) * XW + R + cc] = sum;
       }
     }
     __syncthreads();
-    for (int j = tid; j < CK * 32; j += 256) {
-      const int i = j >> 5, col = j & 31, t = t0 + i;
-      if (t < a.L)
-        dst[(long)t * 32 + col] = bc[(0 * CK + i) * 32 + col] + bc[(1 * CK + i) * 32 + col] +
-                                  bc[(2 * CK + i) * 32 + col] + bc[(3 * CK + i) * 32 + col];
-    }
-    __syncthreads();
   }
-  for (int i = tid; i < a.L * DPB; i += 256) {  // coalesced flush of du / ddt_lin
-    const int t = i / DPB, dd = d0 + i % DPB;
-    if (dd < a.D) {
-      const long o_idx = ((long)s * a.L + t) * a.D + dd;
-      o.du[o_idx] = dub[i];
-      o.ddtl[o_idx] = ddb[i];
-    }
+  if (valid) {
+    float* dap = o.da_part + ((long)s * a.D + d) * NST + NQ * q;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) dap[j] = dAacc[j] * A2[j] * LN2;   // dL/dA_log = dL/dA * A
+    if (q == 0) o.dd_part[(long)s * a.D + d] = dD_acc;
   }
-  if (valid) o.da_part[(long)s * a.D * NST + d * NST + n] = dA_acc;
-  // staging partials: thread i of the staging loop handled (t, dl = i % 16) -> dl = tid & 15 here
-  float* rd = red;            // [16][16]: rows = tid >> 4 (16 row groups), cols = dl
-  rd[(tid >> 4) * 16 + (tid & 15)] = dD_stage;
-  float v = wave_sum(dg_acc);
+  const float v = wave_sum(q == 0 ? dg_acc : 0.f);
+  float* rg = red + nw * SCK * 32;
+  if (lane == 0) rg[wave] = v;
   __syncthreads();
-  if (tid < 16 && d0 + tid < a.D) {
-    float sacc = 0.f;
-    for (int r = 0; r < 16; ++r) sacc += rd[r * 16 + tid];
-    o.dd_part[(long)s * a.D + d0 + tid] = sacc;
+  if (threadIdx.x == 0) {
+    float sum = 0.f;
+    for (int ww = 0; ww < nw; ++ww) sum += rg[ww];
+    o.dg_part[s] = sum;
   }
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  if (tid == 0) o.dg_part[(long)s * a.nchunk + chunk] = red[0] + red[1] + red[2] + red[3];
 }
 
 // token-wise SiLU(z) gate of the combined output, backward:
@@ -372,16 +458,6 @@ __global__ __launch_bounds__(256) void gate_grad(int ndir, int per_dir, const fl
   }
 }
 
-
-__global__ void sum_bc_chunks(int rows, int nchunk, int XW, int R, const float* __restrict__ part,
-                              float* __restrict__ dxdbl) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * 2 * NST) return;
-  const int r = idx >> 5, j = idx & 31;  // 2 * NST == 32
-  float s = 0.f;
-  for (int c = 0; c < nchunk; ++c) s += part[(long)c * rows * 2 * NST + idx];
-  dxdbl[(long)r * XW + R + j] = s;
-}
 
 // dxz[b,l,d] = sum_k sum_j w[d,j] dpre[k,b,inv_k(l)+3-j,d]   (the x half; gate_bwd writes the z half)
 __global__ void dirconv_bwd_gather(int total, FastDiv fD, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
@@ -480,25 +556,27 @@ VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order,
   return VC_OK;
 }
 
-static size_t scan_fwd_smem(int L, int R) {
-  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 3 * (size_t)L * DPB);
-}
-static size_t scan_bwd_smem(int L, int R) {
-  const int nck = (L + CK - 1) / CK;
-  return sizeof(float) * ((size_t)L * (R + 2 * NST) + DPB * R + 4 * (size_t)L * DPB + nck * 256 + 4 * CK * 32 + 256);
+static int seg_count_h(int L) { return (L + SCK - 1) / SCK; }
+
+VC_API int vc_mamba_scan_ckpt_floats(int B, int L, int D, int ndir) {
+  if (B <= 0 || L <= 0 || D <= 0 || ndir <= 0) return -1;
+  const long n = (long)ndir * B * seg_count_h(L) * NST * D;
+  return n < (1L << 31) ? (int)n : -1;
 }
 
 VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                              const int* order, const float* dt_w, const float* dt_b, const float* A_log,
-                             const float* Dskip, float* y, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && L > 0 && D > 0 && R > 0 && R <= 64 && ndir > 0);
-  const size_t sm = scan_fwd_smem(L, R);
+                             const float* Dskip, float* y, float* ckpt, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && L > 0 && D > 0 && D <= 128 && R > 0 && R <= 64 && ndir > 0);
+  const dim3 grid(ndir * B), block(vc_cdiv(D, 16) * 64);
+  VC_REQUIRE(block.x <= 512);
+  const size_t sm = sizeof(float) * seq_lds_floats(L, R, block.x / 4);
   VC_REQUIRE(sm <= 160 * 1024);
-  ScanArgs a{B, L, D, R, vc_cdiv(D, DPB), u, xdbl, order, dt_w, dt_b, A_log, Dskip};
-  const dim3 grid(ndir * B * vc_cdiv(D, DPB));
-  if (R == 9) hipLaunchKernelGGL(scan_fwd<9>, grid, dim3(256), sm, stream, a, y);
-  else if (R == 16) hipLaunchKernelGGL(scan_fwd<16>, grid, dim3(256), sm, stream, a, y);
-  else hipLaunchKernelGGL(scan_fwd<0>, grid, dim3(256), sm, stream, a, y);
+  VC_REQUIRE_I32((long)ndir * B * L * (R + 2 * NST));
+  ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
+  if (R == 9) hipLaunchKernelGGL(scan_fwd<9>, grid, block, sm, stream, a, y, ckpt);
+  else if (R == 16) hipLaunchKernelGGL(scan_fwd<16>, grid, block, sm, stream, a, y, ckpt);
+  else hipLaunchKernelGGL(scan_fwd<0>, grid, block, sm, stream, a, y, ckpt);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -529,45 +607,57 @@ VC_API int vc_mamba_gate_bwd(int B, int L, int D, const float* xz, const float* 
 
 // Backward of scan + gate-weighted combine, given dyp = d(YP) per token (vc_mamba_gate_bwd).
 // Writes du, ddt_lin (per sequence position), the B/C columns of dxdbl (ld R+2N), and
-// dA_log / dD / d(gate logits) (overwrite).
-// ws needs (ceil(D/16) * nseq*L*2N + nseq*D*N + nseq*D + nseq*ceil(D/16) + D*N) floats.
+// dA_log / dD / d(gate logits) (overwrite).  ckpt: the segment states vc_mamba_scan_fwd stored
+// (null: they are recomputed into ws first).
+// ws needs (nseq*D*N + nseq*D + nseq + 2048*ceil(D*N/64)*64) floats (+ vc_mamba_scan_ckpt_floats
+// without ckpt).
 VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                              const int* order, const float* dt_w, const float* dt_b, const float* A_log,
                              const float* Dskip, const float* gate_logits, const float* y, const float* dyp,
-                             float* du, float* ddt_lin, float* dxdbl, float* dA_log, float* dDskip,
-                             float* dgate_logits, float* ws, long ws_floats, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && L > 0 && D > 0 && R > 0 && R <= 64 && ndir > 0 && ndir <= 64);
-  const int nseq = ndir * B, nchunk = vc_cdiv(D, DPB);
-  const long rows = (long)nseq * L;
-  const long need_bc = (long)nchunk * rows * 2 * NST;
-  const long need_a = (long)nseq * D * NST, need_d = (long)nseq * D, need_g = (long)nseq * nchunk;
-  VC_REQUIRE(need_bc + need_a + need_d + need_g <= ws_floats);
-  const size_t sm = scan_bwd_smem(L, R);
+                             const float* ckpt, float* du, float* ddt_lin, float* dxdbl, float* dA_log,
+                             float* dDskip, float* dgate_logits, float* ws, long ws_floats, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && L > 0 && D > 0 && D <= 128 && R > 0 && R <= 64 && ndir > 0 && ndir <= 64);
+  const int nseq = ndir * B;
+  const long need_a = (long)nseq * D * NST, need_d = (long)nseq * D, need_g = nseq;
+  long need_ck = 0;
+  if (!ckpt) {
+    const int n = vc_mamba_scan_ckpt_floats(B, L, D, ndir);
+    VC_REQUIRE(n > 0);
+    need_ck = n;
+  }
+  VC_REQUIRE(need_a + need_d + need_g + need_ck <= ws_floats);
+  const int nw = vc_cdiv(D, 16);
+  VC_REQUIRE(nw <= 8);
+  const size_t sm = sizeof(float) * (seq_lds_floats(L, R, nw * 16) + nw * SCK * 32 + nw + L);
   VC_REQUIRE(sm <= 160 * 1024);
-  float* p_bc = ws;
-  float* p_a = p_bc + need_bc;
+  VC_REQUIRE_I32((long)nseq * L * (R + 2 * NST));
+  float* p_a = ws;
   float* p_d = p_a + need_a;
   float* p_g = p_d + need_d;
-  float* p_rest = p_g + need_g;
-  long rest = ws_floats - (need_bc + need_a + need_d + need_g);
-  ScanArgs a{B, L, D, R, nchunk, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
-  ScanBwdOut o{du, ddt_lin, p_bc, p_a, p_d, p_g};
-  const dim3 grid(nseq * nchunk);
-  if (R == 9) hipLaunchKernelGGL(scan_bwd<9>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
-  else if (R == 16) hipLaunchKernelGGL(scan_bwd<16>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
-  else hipLaunchKernelGGL(scan_bwd<0>, grid, dim3(256), sm, stream, a, ndir, gate_logits, y, dyp, o);
-  VC_CHECK_LAUNCH();
-  const int XW = R + 2 * NST;
-  VC_REQUIRE_I32(rows * 2 * NST);
-  hipLaunchKernelGGL(sum_bc_chunks, dim3(vc_cdiv(rows * 2 * NST, 256)), dim3(256), 0, stream, (int)rows, nchunk, XW,
-                     R, p_bc, dxdbl);
+  float* p_ck = p_g + need_g;
+  float* p_rest = p_ck + need_ck;
+  long rest = ws_floats - (need_a + need_d + need_g + need_ck);
+  ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
+  const dim3 grid(nseq), block(nw * 64);
+  if (!ckpt) {
+    const size_t smf = sizeof(float) * seq_lds_floats(L, R, nw * 16);
+    if (R == 9) hipLaunchKernelGGL(scan_fwd<9>, grid, block, smf, stream, a, nullptr, p_ck);
+    else if (R == 16) hipLaunchKernelGGL(scan_fwd<16>, grid, block, smf, stream, a, nullptr, p_ck);
+    else hipLaunchKernelGGL(scan_fwd<0>, grid, block, smf, stream, a, nullptr, p_ck);
+    VC_CHECK_LAUNCH();
+    ckpt = p_ck;
+  }
+  ScanBwdOut o{du, ddt_lin, dxdbl, p_a, p_d, p_g};
+  if (R == 9) hipLaunchKernelGGL(scan_bwd<9>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
+  else if (R == 16) hipLaunchKernelGGL(scan_bwd<16>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
+  else hipLaunchKernelGGL(scan_bwd<0>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
   VC_CHECK_LAUNCH();
   int rc = vc_colsum(nseq, D * NST, p_a, (long)D * NST, dA_log, 0.f, p_rest, rest, stream);
   if (rc) return rc;
   rc = vc_colsum(nseq, D, p_d, (long)D, dDskip, 0.f, p_rest, rest, stream);
   if (rc) return rc;
-  // dg partials are laid out [k][b][chunk]: per direction B*nchunk contiguous values
-  hipLaunchKernelGGL(gate_grad, dim3(1), dim3(256), 0, stream, ndir, B * nchunk, gate_logits, p_g, dgate_logits);
+  // dg partials are laid out [k][b]: per direction B contiguous values
+  hipLaunchKernelGGL(gate_grad, dim3(1), dim3(256), 0, stream, ndir, B, gate_logits, p_g, dgate_logits);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

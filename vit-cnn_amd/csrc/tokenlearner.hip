@@ -68,6 +68,22 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return r;
 }
 
+// the token's 2->1 conv output for pixel i, in fp64: BN(1) normalises values with a tiny spread
+// around a large mean, so the fp32 rounding of the conv would be amplified by 1/std
+__device__ __forceinline__ double tl_f(const float* __restrict__ mx, const float* __restrict__ avg, long i, float w0,
+                                       float w1, float bc) {
+  return (double)w0 * mx[i] + (double)w1 * avg[i] + (double)bc;
+}
+
+// the token's BN(1) output for pixel i: forward, backward and vc_tl_relu_mask share this one
+// expression, so they take identical ReLU decisions
+__device__ __forceinline__ float tl_bn(const float* __restrict__ mx, const float* __restrict__ avg, long i, float w0,
+                                       float w1, float bc, double mean, double invstd, float gam, float bet,
+                                       double& xh) {
+  xh = (tl_f(mx, avg, i, w0, w1, bc) - mean) * invstd;
+  return (float)xh * gam + bet;
+}
+
 // one block per token s; a[(b*S + s)*HW + p]
 __global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S, const float* __restrict__ mx,
                                                 const float* __restrict__ avg, const float* __restrict__ par,
@@ -81,11 +97,11 @@ __global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S
   double mean, invstd;
   if (train) {
     double acc = 0.0;
-    for (long i = threadIdx.x; i < n; i += TLT) acc += (double)(w0 * mx[i] + w1 * avg[i] + bc);
+    for (long i = threadIdx.x; i < n; i += TLT) acc += tl_f(mx, avg, i, w0, w1, bc);
     mean = block_sum(acc, red) / (double)n;
     double q = 0.0;
     for (long i = threadIdx.x; i < n; i += TLT) {
-      const double d = (double)(w0 * mx[i] + w1 * avg[i] + bc) - mean;
+      const double d = tl_f(mx, avg, i, w0, w1, bc) - mean;
       q += d * d;
     }
     const double m2 = block_sum(q, red);
@@ -107,8 +123,8 @@ __global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S
     stats[2 * s + 1] = invstd;
   }
   for (long i = threadIdx.x; i < n; i += TLT) {
-    const float f = w0 * mx[i] + w1 * avg[i] + bc;
-    const float bn = (float)(((double)f - mean) * invstd) * gam + bet;
+    double xh;
+    const float bn = tl_bn(mx, avg, i, w0, w1, bc, mean, invstd, gam, bet, xh);
     const long b = i / HW, q = i % HW;
     a[((long)b * S + s) * HW + q] = sigmoid_f(fmaxf(bn, 0.f));
   }
@@ -127,8 +143,8 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S
   const long n = (long)B * HW;
   double s1 = 0.0, s2 = 0.0;
   for (long i = threadIdx.x; i < n; i += TLT) {
-    const double xh = ((double)(w0 * mx[i] + w1 * avg[i] + bc) - mean) * invstd;
-    const float bn = (float)xh * gam + bet;
+    double xh;
+    const float bn = tl_bn(mx, avg, i, w0, w1, bc, mean, invstd, gam, bet, xh);
     const long b = i / HW, q = i % HW;
     float g1 = 0.f;
     if (bn > 0.f) {
@@ -142,8 +158,8 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S
   s2 = block_sum(s2, red);
   double gw0 = 0.0, gw1 = 0.0, gb = 0.0;
   for (long i = threadIdx.x; i < n; i += TLT) {
-    const double xh = ((double)(w0 * mx[i] + w1 * avg[i] + bc) - mean) * invstd;
-    const float bn = (float)xh * gam + bet;
+    double xh;
+    const float bn = tl_bn(mx, avg, i, w0, w1, bc, mean, invstd, gam, bet, xh);
     const long b = i / HW, q = i % HW;
     float g1 = 0.f;
     if (bn > 0.f) {
@@ -167,6 +183,19 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S
     g[3] = (float)s2;
     g[4] = (float)s1;
   }
+}
+
+// mask[(b*S + s)*HW + q] = (BN(1) output > 0): the ReLU decisions attn_fwd / attn_bwd took
+__global__ __launch_bounds__(256) void attn_mask(int B, int HW, int S, const float* __restrict__ mx,
+                                                 const float* __restrict__ avg, const float* __restrict__ par,
+                                                 const double* __restrict__ stats, unsigned char* __restrict__ mask) {
+  const int s = blockIdx.y;
+  const long n = (long)B * HW, i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float* p = par + (long)s * TPAR;
+  double xh;
+  const float bn = tl_bn(mx, avg, i, p[0], p[1], p[2], stats[2 * s], stats[2 * s + 1], p[3], p[4], xh);
+  mask[((i / HW) * S + s) * HW + i % HW] = bn > 0.f ? 1 : 0;
 }
 
 // dx[i, c] += davg/C + (c == argmax ? dmx : 0),  dmx / davg summed over the S tokens
@@ -214,6 +243,15 @@ VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, cons
   VC_REQUIRE(B > 0 && HW > 0 && S > 0);
   hipLaunchKernelGGL(attn_bwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, S, mx, avg, params, stats, da, df,
                      dparams);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_tl_relu_mask(int B, int HW, int S, const float* mx, const float* avg, const float* params,
+                           const double* stats, unsigned char* mask, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && HW > 0 && S > 0);
+  hipLaunchKernelGGL(attn_mask, dim3(vc_cdiv((long)B * HW, 256), S), dim3(256), 0, stream, B, HW, S, mx, avg, params,
+                     stats, mask);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

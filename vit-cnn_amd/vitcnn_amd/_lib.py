@@ -71,7 +71,19 @@ class _Lib:
             fn.argtypes = types
             fn.restype = ctypes.c_int
             self.raw[name] = fn
-            setattr(self, name, self._checked(name, fn))
+            setattr(self, name, self._size(name, fn) if name.endswith("_floats") else self._checked(name, fn))
+
+    @staticmethod
+    def _size(name, fn):
+        """`vc_*_floats` entry points are size queries: they return a count, negative on bad arguments"""
+        def call(*args):
+            n = fn(*args)
+            if n < 0:
+                raise RuntimeError(f"{name}{args}: invalid shape/argument")
+            return n
+
+        call.__name__ = name
+        return call
 
     @staticmethod
     def _checked(name, fn):

@@ -348,6 +348,7 @@ class _Program:
         self.B = int(B)
         self.train = 1 if train else 0
         self.ws = model._workspace(device, B, ("train" if train else "eval", mode))
+        self.ws_grad = mode == "grad"
         self.tab = model._device_tables(device)
         scr = model._scratch(device, B)
         lanes = model._side_lanes(device)
@@ -530,8 +531,10 @@ class _Program:
         XD = ws.f(pfx + ".XD", NDIR * rows * XW)
         self.mm_nt(NDIR * rows, XW, D, U, D, P[mx + ".x_proj.weight"], D, XD, XW)
         Y = ws.f(pfx + ".Y", NDIR * rows * D)
+        # segment checkpoints of the scan state, kept for the backward (training with grad only)
+        CKP = ws.f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR)) if self.ws_grad else None
         self.L.vc_mamba_scan_fwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
-                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], Y, self.s)
+                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], Y, CKP, self.s)
         YP, YS = ws.f(pfx + ".YP", rows * D), ws.f(pfx + ".YS", rows * D)
         self.L.vc_mamba_combine_fwd(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, XZ, YP, YS, self.s)
         T2 = ws.f(pfx + ".T2", rows * E)
@@ -777,6 +780,7 @@ class _Program:
         self.L.vc_mamba_gate_bwd(B, L_, D, XZ, YP, dYS, dYP, dXZ, self.s)
         self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
                                  P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], Y, dYP,
+                                 f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR)),
                                  dU, dDTL, dXD, G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"], self.scr_p,
                                  self.scr_n, self.s)
         nr = NDIR * rows
