@@ -84,8 +84,8 @@ def dominant_kernel_roofline(model, batch, reps):
     block hsi1 (`scan_bwd<9>`, grid 640 sequences x 5 channel chunks), the longest single launch
     of the step.  It is a sequential recurrence over 81 tokens with no matrix work, so its roofline
     is HBM.  Algorithmic bytes per launch = compulsory reads of u, x_proj rows, yp (each
-    [10*B*L, *]), d(yp) [B*L, D] and the forward's 8-token state checkpoints
-    [10*B][ceil(L/8)][16][D] + writes of du, d(dt_lin) and the dB/dC columns (DESIGN.md
+    [10*B*L, *]), d(yp) [B*L, D] and the forward's 4-token state checkpoints
+    [10*B][ceil(L/4)][16][D] + writes of du, d(dt_lin) and the dB/dC columns (DESIGN.md
     section 4).  The timed call is the whole vc_mamba_scan_bwd entry point (scan_bwd + its two
     small column sums + gate gradient)."""
     from vitcnn_amd._lib import lib

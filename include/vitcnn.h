@@ -117,7 +117,7 @@ VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order,
 /* selective scan of every direction's sequence (modeling_mamba.py:175-283), ungated:
  * yp[k,b,t,d] = sum_n C_t[n] h_t[d,n] + D_d u_t[d]; h_t = exp(dt A) h_{t-1} + dt B_t u_t,
  * dt = softplus(W_dt dtr_t + b_dt).  u/xdbl/yp are [ndir*B*L, D] / [.., R+32] / [.., D]. */
-/* ckpt (nullable): [ndir*B][ceil(L/8)][16][D] fp32 states entering every 8-token segment, saved
+/* ckpt (nullable): [ndir*B][ceil(L/4)][16][D] fp32 states entering every 4-token segment, saved
  * for vc_mamba_scan_bwd; vc_mamba_scan_ckpt_floats gives its size (-1 on bad arguments) */
 VC_API int vc_mamba_scan_ckpt_floats(int B, int L, int D, int ndir);
 VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
@@ -229,5 +229,13 @@ VC_API int vc_patch_gather(int W, int H, int C, int P, const float* cube, const 
  * mode of model_utils.py:1126-1128; windows are distinct, so no two i share a centre) */
 VC_API int vc_center_accumulate(int W, int H, int P, int ncls, const int* corners, long k0, int step, int n,
                                 const float* logits, double* probs, hipStream_t stream);
+
+/* ---------------------------------------------------------------- classification metrics
+ * Confusion matrix of a prediction map (utils.py:585-663 metrics(), counting step :596-611):
+ * cm[t * n_classes + p] += number of pixels with target t, prediction p, both in
+ * [0, n_classes), target not flagged in ignored[n_classes] (uint8).  cm (uint64) is
+ * accumulated into: zero it first.  n_classes <= 64. */
+VC_API int vc_confusion_matrix(long n, const long long* target, const long long* pred, int n_classes,
+                               const unsigned char* ignored, unsigned long long* cm, hipStream_t stream);
 
 #endif /* VITCNN_H */

@@ -85,7 +85,11 @@ struct ScanArgs {
 // the state entering every SCK-token segment ([nseq][nseg][16][D]); the backward re-runs one
 // segment at a time from those checkpoints (the segment's states stay in registers) and sweeps it
 // in reverse, so nothing of size [seq, L, D, 16] is ever stored.
-constexpr int SCK = 8;                  // tokens per checkpoint segment
+// 4 tokens per segment (measured on MI355X): the backward's per-segment registers (states, cached
+// exp(dt A), prefetched operands) fit 128 VGPRs, i.e. 4 waves per SIMD, so all 640 sequence blocks
+// of a launch are resident at once (8 tokens: 182 VGPRs, 2 waves per SIMD, 3 rounds of blocks;
+// hsi1 backward 211 -> 156 us).  The checkpoints cost 16 * D floats per segment of HBM traffic.
+constexpr int SCK = 4;
 constexpr int NQ = 4;                   // states per lane
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
