@@ -205,3 +205,26 @@ def test_gemm_ex_in_launch_splitk_is_bit_identical(L, ws, ta, tb, M, N, K, bgrad
     assert int(cnt.abs().sum()) == 0
     ref = (A.t() if ta else A).cpu() @ (B.t() if tb else B).cpu()
     assert rel_err(outs[1][0].numpy(), ref.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("B,ncls", [(64, 16), (4, 12), (100, 40), (3, 1)])
+def test_weighted_cross_entropy(L, B, ncls):
+    """vc_ce_fwd / vc_ce_bwd (16-lane row per sample, several passes when B > 64 or ncls > 16)
+    vs torch's weighted CrossEntropyLoss (model_utils.py:311) including an ignore_index target."""
+    logits = rnd(B, ncls, seed=41, scale=4.0)
+    g = torch.Generator().manual_seed(42)
+    target = torch.randint(0, ncls, (B,), generator=g)
+    target[0] = -100
+    w = torch.rand(ncls, generator=g) + 0.5
+    lr = logits.clone().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, target, weight=w, ignore_index=-100)
+    ref.backward(torch.tensor(0.75))
+    ld, td, wd = logits.to(DEV), target.to(DEV), w.to(DEV)
+    loss = torch.empty(1, device=DEV)
+    gout = torch.full((1,), 0.75, device=DEV)
+    dl = torch.empty(B, ncls, device=DEV)
+    L.vc_ce_fwd(B, ncls, P(ld), P(td), P(wd), -100, P(loss), S())
+    L.vc_ce_bwd(B, ncls, P(ld), P(td), P(wd), -100, P(gout), P(dl), S())
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+    assert rel_err(dl.cpu().numpy(), lr.grad.numpy()) < 1e-5

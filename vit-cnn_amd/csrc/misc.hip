@@ -85,8 +85,10 @@ __global__ __launch_bounds__(256) void head_fwd(int S1, int S2, int C, int ncls,
   for (int c0 = 0; c0 < C; c0 += 64) {
     const int c = c0 + cl;
     float s1 = 0.f, s2 = 0.f;
-    if (c < C) {
+    if (c < C) {   // unrolled: a thread's loads of the chunk are in flight together
+#pragma unroll 4
       for (int p = rg; p < S1; p += 4) s1 += f1[((long)b * S1 + p) * C + c];
+#pragma unroll 4
       for (int q = rg; q < S2; q += 4) s2 += f2[((long)b * S2 + q) * C + c];
     }
     red[rg * 64 + cl] = s1 / (float)S1 + s2 / (float)S2;
@@ -98,12 +100,15 @@ __global__ __launch_bounds__(256) void head_fwd(int S1, int S2, int C, int ncls,
     }
     __syncthreads();
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int k = wave; k < ncls; k += 4) {
+  // logits: a 16-lane row per class (16 classes per pass), DPP row sums instead of LDS shuffles
+  const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
+  for (int k0 = 0; k0 < ncls; k0 += 16) {
+    const int k = k0 + g;
     float acc = 0.f;
-    for (int c = lane; c < C; c += 64) acc += fs[c] * W[(long)k * C + c];
-    acc = wave_sum(acc);
-    if (lane == 0) logits[(long)b * ncls + k] = acc + bias[k];
+    if (k < ncls)
+      for (int c = l; c < C; c += 16) acc += fs[c] * W[(long)k * C + c];
+    acc = row16_sum(acc);
+    if (l == 0 && k < ncls) logits[(long)b * ncls + k] = acc + bias[k];
   }
 }
 
@@ -140,67 +145,91 @@ __global__ __launch_bounds__(256) void head_bwd_w(int B, int C, int ncls, const 
   }
 }
 
+// Weighted cross entropy, every sample at once: one 1024-thread block, a 16-lane row per sample
+// (lane l holds logits l, l+16, ...), row max / sum by DPP within the row, the target's logit
+// picked from the row's own registers.  64 samples per pass: one global round trip for B <= 64.
 // loss = sum_b w[y_b] * (lse_b - logit[b, y_b]) / sum_b w[y_b]   (targets == ignore_index contribute 0)
-__global__ __launch_bounds__(256) void ce_fwd(int B, int ncls, const float* __restrict__ logits,
+constexpr int CET = 1024;
+
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  return v;
+}
+
+// per sample row: max, sum of exp(logit - max) and the target's logit, in every lane of the row
+__device__ __forceinline__ void ce_row(const float* __restrict__ lr, int ncls, long long y, int l, float& mx, float& se,
+                                       float& ly) {
+  mx = -INFINITY;
+  float t = 0.f;
+  for (int k = l; k < ncls; k += 16) {
+    const float v = lr[k];
+    mx = fmaxf(mx, v);
+    if (k == y) t = v;
+  }
+  mx = row16_max(mx);
+  ly = row16_sum(t);
+  se = 0.f;
+  for (int k = l; k < ncls; k += 16) se += __expf(lr[k] - mx);
+  se = row16_sum(se);
+}
+
+__device__ __forceinline__ float block_sum1024(float v, float* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < CET / 64; ++i) r += red[i];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(CET) void ce_fwd(int B, int ncls, const float* __restrict__ logits,
                                               const long long* __restrict__ target, const float* __restrict__ w,
                                               long long ignore_index, float* __restrict__ loss) {
-  __shared__ float r1[4], r2[4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float red[CET / 64];
+  const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   float num = 0.f, den = 0.f;
-  for (int b = wave; b < B; b += 4) {
-    const float* lr = logits + (long)b * ncls;
-    float mx = -INFINITY;
-    for (int k = lane; k < ncls; k += 64) mx = fmaxf(mx, lr[k]);
-    mx = wave_max(mx);
-    float se = 0.f;
-    for (int k = lane; k < ncls; k += 64) se += __expf(lr[k] - mx);
-    se = wave_sum(se);
+  for (int b = g; b < B; b += CET / 16) {
     const long long y = target[b];
-    if (lane == 0 && y != ignore_index) {
+    float mx, se, ly;
+    ce_row(logits + (long)b * ncls, ncls, y, l, mx, se, ly);
+    if (l == 0 && y != ignore_index) {
       const float wy = w ? w[y] : 1.f;
-      num += wy * (logf(se) + mx - lr[y]);
+      num += wy * (logf(se) + mx - ly);
       den += wy;
     }
   }
-  num = wave_sum(num);
-  den = wave_sum(den);
-  if (lane == 0) {
-    r1[wave] = num;
-    r2[wave] = den;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) loss[0] = (r1[0] + r1[1] + r1[2] + r1[3]) / (r2[0] + r2[1] + r2[2] + r2[3]);
+  num = block_sum1024(num, red);
+  den = block_sum1024(den, red);
+  if (threadIdx.x == 0) loss[0] = num / den;
 }
 
-__global__ __launch_bounds__(256) void ce_bwd(int B, int ncls, const float* __restrict__ logits,
+__global__ __launch_bounds__(CET) void ce_bwd(int B, int ncls, const float* __restrict__ logits,
                                               const long long* __restrict__ target, const float* __restrict__ w,
                                               long long ignore_index, const float* __restrict__ gout,
                                               float* __restrict__ dlogits) {
-  __shared__ float r2[4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float red[CET / 64];
   float den = 0.f;
-  for (int b = threadIdx.x; b < B; b += 256) {
+  for (int b = threadIdx.x; b < B; b += CET) {
     const long long y = target[b];
     if (y != ignore_index) den += w ? w[y] : 1.f;
   }
-  den = wave_sum(den);
-  if (lane == 0) r2[wave] = den;
-  __syncthreads();
-  den = r2[0] + r2[1] + r2[2] + r2[3];
-  const float g = (gout ? gout[0] : 1.f) / den;
-  for (int b = wave; b < B; b += 4) {
-    const float* lr = logits + (long)b * ncls;
-    float mx = -INFINITY;
-    for (int k = lane; k < ncls; k += 64) mx = fmaxf(mx, lr[k]);
-    mx = wave_max(mx);
-    float se = 0.f;
-    for (int k = lane; k < ncls; k += 64) se += __expf(lr[k] - mx);
-    se = wave_sum(se);
+  den = block_sum1024(den, red);
+  const float gs = (gout ? gout[0] : 1.f) / den;
+  const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
+  for (int b = g; b < B; b += CET / 16) {
     const long long y = target[b];
+    float mx, se, ly;
+    ce_row(logits + (long)b * ncls, ncls, y, l, mx, se, ly);
     const float wy = (y == ignore_index) ? 0.f : (w ? w[y] : 1.f);
-    for (int k = lane; k < ncls; k += 64) {
+    const float* lr = logits + (long)b * ncls;
+    for (int k = l; k < ncls; k += 16) {
       const float p = __expf(lr[k] - mx) / se;
-      dlogits[(long)b * ncls + k] = g * wy * (p - (k == y ? 1.f : 0.f));
+      dlogits[(long)b * ncls + k] = gs * wy * (p - (k == y ? 1.f : 0.f));
     }
   }
 }
@@ -341,7 +370,7 @@ VC_API int vc_head_bwd(int B, int S1, int S2, int C, int ncls, const float* dlog
 VC_API int vc_ce_fwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
                      long long ignore_index, float* loss, hipStream_t stream) {
   VC_REQUIRE(B > 0 && ncls > 0);
-  hipLaunchKernelGGL(ce_fwd, dim3(1), dim3(256), 0, stream, B, ncls, logits, target, weight, ignore_index, loss);
+  hipLaunchKernelGGL(ce_fwd, dim3(1), dim3(CET), 0, stream, B, ncls, logits, target, weight, ignore_index, loss);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -349,7 +378,7 @@ VC_API int vc_ce_fwd(int B, int ncls, const float* logits, const long long* targ
 VC_API int vc_ce_bwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
                      long long ignore_index, const float* grad_out, float* dlogits, hipStream_t stream) {
   VC_REQUIRE(B > 0 && ncls > 0);
-  hipLaunchKernelGGL(ce_bwd, dim3(1), dim3(256), 0, stream, B, ncls, logits, target, weight, ignore_index, grad_out,
+  hipLaunchKernelGGL(ce_bwd, dim3(1), dim3(CET), 0, stream, B, ncls, logits, target, weight, ignore_index, grad_out,
                      dlogits);
   VC_CHECK_LAUNCH();
   return VC_OK;
