@@ -1,0 +1,79 @@
+"""MUUFL-shape parity (SURVEY.md section 8, row A-MUUFL / config C4): 64 HSI + 2 LiDAR bands,
+11x11 patches, 12 classes (11 + Unclassified).  The reference has no MUUFL behaviour of its own for
+this model (its scan-order tables and TokenLearner sizes are written for 9x9 / 7x7); the
+generalisation in SURVEY.md A-MUUFL (generator-rule scan orders, S = (P-2)^2 / (P-4)^2 tokens) is
+checked for self-consistency: the HIP path against the CPU oracle on hash-filled parameters of that
+architecture and a synthetic batch.  Tolerances as for the Houston2013 shape (tests/test_model_gpu.py):
+logits / loss within 1e-3 relative; every gradient element against a float64 evaluation of the same
+step (with the HIP path's ReLU decisions and TokenLearner pooled values), within 1e-3 of the tensor
+scale or 3x the fp32 oracle's own error, plus 1e-5 of the largest gradient."""
+import pytest
+import torch
+
+from helpers import masked_oracle_step, rel_err, relu_masks_from_workspace, tl_pooled_from_workspace
+from oracle import vitcnn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+B, BANDS, LIDAR, P, NCLS = 4, 64, 2, 11, 12
+
+
+@pytest.fixture(scope="module")
+def muufl():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vitcnn_amd import CrossEntropyLoss, Multimodality_Mamba
+    from vitcnn_amd.hashinit import fill_module_, synthetic_batch
+    m = Multimodality_Mamba(P, 1, 1, BANDS, LIDAR, 32, NCLS, "multi_clock_gate")
+    fill_module_(m)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    hsi, lidar, target = (torch.from_numpy(a) for a in synthetic_batch("muufl.b4", B, BANDS, LIDAR, P, NCLS))
+    w = O.ce_class_weights(NCLS)
+    state = O.make_state(sd)
+    ref_logits, ref_loss = O.train_step(state, hsi, lidar, target, w)
+    m = m.to("cuda").train()
+    crit = CrossEntropyLoss(weight=w.to("cuda"))
+    logits = m(hsi.to("cuda"), lidar.to("cuda"))
+    loss = crit(logits, target.to("cuda"))
+    loss.backward()
+    torch.cuda.synchronize()
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    st64 = O.make_state(sd64)
+    masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(), relu_masks_from_workspace(m, B),
+                       pooled=tl_pooled_from_workspace(m, B))
+    st64r = O.make_state(sd64)
+    O.train_step(st64r, hsi.double(), lidar.double(), target, w.double())
+    names = O.param_names(state)
+    return dict(m=m, logits=logits.detach().cpu(), loss=float(loss.detach()), ref_logits=ref_logits, ref_loss=float(ref_loss),
+                ref=({k: state[k].grad for k in names}), ref64={k: st64[k].grad for k in names},
+                ref64_own={k: st64r[k].grad for k in names})
+
+
+def test_muufl_logits_loss(muufl):
+    assert muufl["logits"].shape == (B, NCLS)
+    assert rel_err(muufl["logits"].numpy(), muufl["ref_logits"].numpy()) < 1e-3
+    assert abs(muufl["loss"] - muufl["ref_loss"]) < 1e-3 * abs(muufl["ref_loss"])
+
+
+def test_muufl_gradients(muufl):
+    m, ref, ref64, own = muufl["m"], muufl["ref"], muufl["ref64"], muufl["ref64_own"]
+    flat = m.flat_params.grad.detach().cpu()
+    named = dict(m.named_parameters())
+    gmax = max(float(g.abs().max()) for g in ref64.values() if g is not None)
+    floor = 1e-5 * gmax
+    bad, checked = [], 0
+    for n, off in m._poff.items():
+        p = named[n]
+        got = flat[off:off + p.numel()].view(p.shape).double()
+        r64 = ref64.get(n)
+        if r64 is None:
+            assert float(got.abs().max()) == 0.0, n
+            continue
+        err = float((got - r64).abs().max())
+        err32 = float((ref[n].double() - own[n]).abs().max())
+        scale = float(r64.abs().max())
+        checked += 1
+        if not (err <= 1e-3 * scale + floor or err <= 3.0 * err32 + floor):
+            bad.append((n, err, err32, scale))
+    assert checked > 1000
+    assert not bad, bad[:5]
