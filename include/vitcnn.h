@@ -132,7 +132,8 @@ VC_API int vc_mamba_combine_fwd(int B, int L, int D, int ndir, const int* inv_or
 VC_API int vc_mamba_gate_bwd(int B, int L, int D, const float* xz, const float* ypsum, const float* dysum,
                              float* dyp, float* dxz, hipStream_t stream);
 /* backward of scan + gated combine given dyp: du, ddt_lin (pre-softplus) per sequence position;
- * the B/C columns of dxdbl (ld R+32); dA_log [D,16], dDskip [D], dgate_logits [ndir] (all overwritten).
+ * the B/C columns of dxdbl (ld R+32); dA_log [D,16], dDskip [D], dgate_logits [ndir] (all overwritten;
+ * each may be NULL, its cross-sequence reduction is then skipped).
  * ckpt: the states vc_mamba_scan_fwd saved (nullable: recomputed into ws) */
 VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                              const int* order, const float* dt_w, const float* dt_b, const float* A_log,

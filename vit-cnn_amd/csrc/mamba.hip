@@ -656,10 +656,12 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   else if (R == 16) hipLaunchKernelGGL(scan_bwd<16>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
   else hipLaunchKernelGGL(scan_bwd<0>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
   VC_CHECK_LAUNCH();
-  int rc = vc_colsum(nseq, D * NST, p_a, (long)D * NST, dA_log, 0.f, p_rest, rest, stream);
+  // the three parameter-gradient outputs are optional (the per-sequence partials stay in ws)
+  int rc = dA_log ? vc_colsum(nseq, D * NST, p_a, (long)D * NST, dA_log, 0.f, p_rest, rest, stream) : 0;
   if (rc) return rc;
-  rc = vc_colsum(nseq, D, p_d, (long)D, dDskip, 0.f, p_rest, rest, stream);
+  rc = dDskip ? vc_colsum(nseq, D, p_d, (long)D, dDskip, 0.f, p_rest, rest, stream) : 0;
   if (rc) return rc;
+  if (!dgate_logits) return VC_OK;
   // dg partials are laid out [k][b]: per direction B contiguous values
   hipLaunchKernelGGL(gate_grad, dim3(1), dim3(256), 0, stream, ndir, B, gate_logits, p_g, dgate_logits);
   VC_CHECK_LAUNCH();
