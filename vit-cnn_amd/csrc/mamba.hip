@@ -268,14 +268,14 @@ template <int RT>
 __global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
                                                 const float* __restrict__ yp, const float* __restrict__ dyp,
                                                 const float* __restrict__ ckpt, ScanBwdOut o) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // SeqLds, red [nw][SCK][32], [nw]
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // SeqLds, red [2][nw][SCK][32], [nw]
   const int R = RT ? RT : a.R;
   const int XW = R + 2 * NST;
   const int nseg = seg_count(a.L), Lp = nseg * SCK;
   const int nw = blockDim.x >> 6, Dp = nw * 16;
   const SeqLds m(smem, Lp, R, Dp);
   float* red = m.xr + Lp * R;
-  int* ord = reinterpret_cast<int*>(red + nw * SCK * 32 + nw);   // [L] this direction's order
+  int* ord = reinterpret_cast<int*>(red + 2 * nw * SCK * 32 + nw);   // [L] this direction's order
   const int s = blockIdx.x, k = s / a.B, b = s - k * a.B;
   for (int t = threadIdx.x; t < a.L; t += blockDim.x) ord[t] = a.order[k * a.L + t];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, cl = lane & 15;
@@ -342,6 +342,7 @@ __global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const floa
       }
     }
     // reverse sweep
+    float* rb = red + (c & 1) * nw * SCK * 32;
 #pragma unroll
     for (int i = SCK - 1; i >= 0; --i) {
       const int t = t0 + i;
@@ -371,18 +372,20 @@ __global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const floa
         o.ddtl[(base + t) * a.D + d] = (qa * LN2 + ut * S) * -expm1_c(-dt);
       }
       if (q == 0) dD_acc += dy * ut;
-      red[(wave * SCK + i) * 32 + col] = reduce_scatter8_row(v);   // lanes 2j, 2j+1 store the same
+      rb[(wave * SCK + i) * 32 + col] = reduce_scatter8_row(v);   // lanes 2j, 2j+1 store the same
     }
+    // one barrier per segment: the partials alternate between two buffers, so the next segment's
+    // stores (other buffer) need no barrier behind this combine; the one after them orders the
+    // reuse of this buffer two segments later
     __syncthreads();
     for (int j = threadIdx.x; j < SCK * 32; j += blockDim.x) {
       const int i = j >> 5, cc = j & 31, t = t0 + i;
       if (t < a.L) {
         float sum = 0.f;
-        for (int ww = 0; ww < nw; ++ww) sum += red[(ww * SCK + i) * 32 + cc];
+        for (int ww = 0; ww < nw; ++ww) sum += rb[(ww * SCK + i) * 32 + cc];
         o.dxdbl[(base + t) * XW + R + cc] = sum;
       }
     }
-    __syncthreads();
   }
   if (valid) {
     float* dap = o.da_part + ((long)s * a.D + d) * NST + NQ * q;
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const floa
     if (q == 0) o.dd_part[(long)s * a.D + d] = dD_acc;
   }
   const float v = wave_sum(q == 0 ? dg_acc : 0.f);
-  float* rg = red + nw * SCK * 32;
+  float* rg = red + 2 * nw * SCK * 32;
   if (lane == 0) rg[wave] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -632,7 +635,7 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   VC_REQUIRE(need_a + need_d + need_g + need_ck <= ws_floats);
   const int nw = vc_cdiv(D, 16);
   VC_REQUIRE(nw <= 8);
-  const size_t sm = sizeof(float) * (seq_lds_floats(L, R, nw * 16) + nw * SCK * 32 + nw + L);
+  const size_t sm = sizeof(float) * (seq_lds_floats(L, R, nw * 16) + 2 * nw * SCK * 32 + nw + L);
   VC_REQUIRE(sm <= 160 * 1024);
   VC_REQUIRE_I32((long)nseq * L * (R + 2 * NST));
   float* p_a = ws;
