@@ -239,4 +239,31 @@ VC_API int vc_center_accumulate(int W, int H, int P, int ncls, const int* corner
 VC_API int vc_confusion_matrix(long n, const long long* target, const long long* pred, int n_classes,
                                const unsigned char* ignored, unsigned long long* cm, hipStream_t stream);
 
+/* ---------------------------------------------------------------- S2EFT (config 5)
+ * model/compare_method/S2EFT.py.  Token rows are [B, T, D] row-major, T = N + 1 (cls first).
+ * vc_s2eft_gate_fwd: spectral gate :134-143 (x [B,N,C]; w = conv1d weight [1,2,7] (mean, max),
+ *   bias [1]): mask[b,t] = sigmoid(conv1d_k7_pad3([mean_c x, max_c x]))[t] >= beta; xg = x * mask
+ *   (the reference thresholds `.data`: no gradient reaches the gate).
+ * vc_s2eft_cls_rows: X[b,0,:] = cls + pos[0] (:150-152); vc_s2eft_strip_cls: dE = dX[:,1:,:].
+ * vc_s2eft_attn_fwd/bwd: Attention :45-74 core, dim_head 16, softmax(q k^T * scale) v over
+ *   qkv [B*T, 3*H*16] (to_qkv output, q|k|v blocks); out [B*T, H*16]; lse [B,H,T] saved; T <= 256.
+ * vc_gelu_fwd/bwd: nn.GELU (erf form, FeedForward :25).
+ * vc_s2eft_skip_pack/unpack/bias_grad: CAF skipcat Conv2d(T, T, [1,2]) (:88-106) as a GEMM with the
+ *   weight viewed [T, 2T] over Z[b] = interleave(x, last) [2T, D]; biasmat [T, D] = bias broadcast. */
+VC_API int vc_s2eft_gate_fwd(int B, int N, int C, const float* x, const float* w, const float* bias, float beta,
+                             float* xg, float* mask, hipStream_t stream);
+VC_API int vc_s2eft_cls_rows(int B, int T, int D, const float* cls, const float* pos, float* X, hipStream_t stream);
+VC_API int vc_s2eft_strip_cls(int B, int N, int D, const float* dX, float* dE, hipStream_t stream);
+VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale, float* out, float* lse,
+                             hipStream_t stream);
+VC_API int vc_s2eft_attn_bwd(int B, int T, int H, const float* qkv, const float* out, const float* dout,
+                             const float* lse, float scale, float* dqkv, hipStream_t stream);
+VC_API int vc_gelu_fwd(long n, const float* x, float* y, hipStream_t stream);
+VC_API int vc_gelu_bwd(long n, const float* dy, const float* x, float* dx, hipStream_t stream);
+VC_API int vc_s2eft_skip_pack(int B, int T, int D, const float* x, const float* last, const float* bias, float* Z,
+                              float* biasmat, hipStream_t stream);
+VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx, int acc_x, float* dlast,
+                                hipStream_t stream);
+VC_API int vc_s2eft_skip_bias_grad(int B, int T, int D, const float* dY, float* db, hipStream_t stream);
+
 #endif /* VITCNN_H */

@@ -1,0 +1,320 @@
+// S2EFT comparison model (config 5): the ops vc_gemm / vc_layernorm do
+// not already cover.  Reference: model/compare_method/S2EFT.py
+//   spectral gate            :134-143  sigmoid(conv1d_k7([mean_c, max_c])) >= 0.4 -> hard 0/1 mask
+//   embedding + cls + pos    :146-153
+//   4-head attention core    :45-74    softmax(q k^T * dim_head^-0.5) v, dim_head 16
+//   GELU MLP                 :21-32    nn.GELU (erf form)
+//   CAF skipcat              :88-106   Conv2d(T, T, [1, 2]) over cat(x, last_output[nl-2]) on a new axis
+// Token rows are [B, T, D] row-major (token-major, the reference's [b, n, dim] layout); the qkv
+// projection output is [B*T, 3*H*16] (q | k | v column blocks, head h at columns h*16.. of each).
+#include "common.h"
+
+namespace {
+
+// ------------------------------------------------------------------ spectral gate
+// One block per sample.  Per token row: mean and max over C (one wave per row), then the k=7 conv over
+// the token axis (zero padded), sigmoid, threshold; xg = x * mask (the mask is `.data`: no gradient).
+__global__ __launch_bounds__(256) void gate_fwd(int N, int C, const float* __restrict__ x,
+                                                const float* __restrict__ w, const float* __restrict__ bias,
+                                                float beta, float* __restrict__ xg, float* __restrict__ mask) {
+  extern __shared__ float sh[];
+  float* avg = sh;
+  float* mx = sh + N;
+  float* msk = sh + 2 * N;
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* xb = x + (long)b * N * C;
+  for (int r = wave; r < N; r += 4) {
+    float s = 0.f, m = -INFINITY;
+    for (int c = lane; c < C; c += 64) {
+      const float v = xb[(long)r * C + c];
+      s += v;
+      m = fmaxf(m, v);
+    }
+    s = wave_sum(s);
+    m = wave_max(m);
+    if (lane == 0) {
+      avg[r] = s / (float)C;
+      mx[r] = m;
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < N; t += 256) {
+    float v = bias[0];
+    for (int k = 0; k < 7; ++k) {
+      const int j = t + k - 3;
+      if (j >= 0 && j < N) v += w[k] * avg[j] + w[7 + k] * mx[j];
+    }
+    const float s = 1.0f / (1.0f + expf(-v));
+    const float m = s >= beta ? 1.0f : 0.0f;
+    msk[t] = m;
+    mask[(long)b * N + t] = m;
+  }
+  __syncthreads();
+  float* xgb = xg + (long)b * N * C;
+  for (int i = threadIdx.x; i < N * C; i += 256) xgb[i] = xb[i] * msk[i / C];
+}
+
+// X[b, 0, :] = cls + pos[0]  (the other rows come from the embedding GEMM with pos fused as addend)
+__global__ void cls_rows(int B, int T, int D, const float* __restrict__ cls, const float* __restrict__ pos,
+                         float* __restrict__ X) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * D) return;
+  const int b = i / D, d = i % D;
+  X[(long)b * T * D + d] = cls[d] + pos[d];
+}
+
+// dE[b, t, :] = dX[b, 1 + t, :]
+__global__ void strip_cls(int B, int N, int D, const float* __restrict__ dX, float* __restrict__ dE) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * N * D) return;
+  const long b = i / ((long)N * D), r = i % ((long)N * D);
+  dE[i] = dX[b * (N + 1) * D + D + r];
+}
+
+// ------------------------------------------------------------------ attention core (dim_head 16)
+// One block per (sample, head), one thread per query row; K/V of the head staged in LDS and read as
+// broadcasts.  Saves the log-sum-exp per row for the backward (P is never stored).
+__global__ __launch_bounds__(256) void attn_fwd(int T, int H, const float* __restrict__ qkv, float scale,
+                                                float* __restrict__ out, float* __restrict__ lse) {
+  __shared__ f32x4 Ks[256 * 4], Vs[256 * 4];
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int ld = 3 * H * 16, ldo = H * 16;
+  const float* base = qkv + (long)b * T * ld;
+  for (int i = threadIdx.x; i < T * 4; i += 256) {
+    const int t = i >> 2, q4 = i & 3;
+    Ks[i] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
+    Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
+  }
+  __syncthreads();
+  const int i = threadIdx.x;
+  if (i >= T) return;
+  f32x4 q[4];
+  for (int k = 0; k < 4; ++k) q[k] = *(const f32x4*)(base + (long)i * ld + h * 16 + k * 4);
+  float m = -INFINITY;
+  for (int j = 0; j < T; ++j) {
+    f32x4 a = q[0] * Ks[j * 4] + q[1] * Ks[j * 4 + 1] + q[2] * Ks[j * 4 + 2] + q[3] * Ks[j * 4 + 3];
+    m = fmaxf(m, (a.x + a.y + a.z + a.w) * scale);
+  }
+  float l = 0.f;
+  f32x4 acc[4] = {};
+  for (int j = 0; j < T; ++j) {
+    f32x4 a = q[0] * Ks[j * 4] + q[1] * Ks[j * 4 + 1] + q[2] * Ks[j * 4 + 2] + q[3] * Ks[j * 4 + 3];
+    const float p = expf((a.x + a.y + a.z + a.w) * scale - m);
+    l += p;
+    for (int k = 0; k < 4; ++k) acc[k] += p * Vs[j * 4 + k];
+  }
+  const float r = 1.0f / l;
+  float* o = out + ((long)b * T + i) * ldo + h * 16;
+  for (int k = 0; k < 4; ++k) *(f32x4*)(o + k * 4) = acc[k] * r;
+  lse[((long)b * H + h) * T + i] = m + logf(l);
+}
+
+// dS = P * (dP - rowsum(dO * O)); pass 1 (thread per query) -> dq, pass 2 (thread per key) -> dk, dv.
+__global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __restrict__ qkv,
+                                                const float* __restrict__ out, const float* __restrict__ dout,
+                                                const float* __restrict__ lse, float scale,
+                                                float* __restrict__ dqkv) {
+  __shared__ f32x4 Qs[256 * 4], Ks[256 * 4], Vs[256 * 4], dOs[256 * 4];
+  __shared__ float Ls[256], Ds[256];
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int ld = 3 * H * 16, ldo = H * 16;
+  const float* base = qkv + (long)b * T * ld;
+  for (int i = threadIdx.x; i < T * 4; i += 256) {
+    const int t = i >> 2, q4 = i & 3;
+    Qs[i] = *(const f32x4*)(base + (long)t * ld + h * 16 + q4 * 4);
+    Ks[i] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
+    Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
+    dOs[i] = *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4);
+  }
+  const int i = threadIdx.x;
+  if (i < T) {
+    const float* o = out + ((long)b * T + i) * ldo + h * 16;
+    const float* g = dout + ((long)b * T + i) * ldo + h * 16;
+    float s = 0.f;
+    for (int d = 0; d < 16; ++d) s += o[d] * g[d];
+    Ds[i] = s;
+    Ls[i] = lse[((long)b * H + h) * T + i];
+  }
+  __syncthreads();
+  if (i >= T) return;
+  {  // dq_i
+    f32x4 q[4], go[4], dq[4] = {};
+    for (int k = 0; k < 4; ++k) {
+      q[k] = Qs[i * 4 + k];
+      go[k] = dOs[i * 4 + k];
+    }
+    const float li = Ls[i], di = Ds[i];
+    for (int j = 0; j < T; ++j) {
+      f32x4 a = q[0] * Ks[j * 4] + q[1] * Ks[j * 4 + 1] + q[2] * Ks[j * 4 + 2] + q[3] * Ks[j * 4 + 3];
+      f32x4 c = go[0] * Vs[j * 4] + go[1] * Vs[j * 4 + 1] + go[2] * Vs[j * 4 + 2] + go[3] * Vs[j * 4 + 3];
+      const float p = expf((a.x + a.y + a.z + a.w) * scale - li);
+      const float ds = p * ((c.x + c.y + c.z + c.w) - di);
+      for (int k = 0; k < 4; ++k) dq[k] += ds * Ks[j * 4 + k];
+    }
+    float* w = dqkv + ((long)b * T + i) * ld + h * 16;
+    for (int k = 0; k < 4; ++k) *(f32x4*)(w + k * 4) = dq[k] * scale;
+  }
+  {  // dk_j, dv_j with j = this thread
+    const int j = i;
+    f32x4 kk[4], vv[4], dk[4] = {}, dv[4] = {};
+    for (int k = 0; k < 4; ++k) {
+      kk[k] = Ks[j * 4 + k];
+      vv[k] = Vs[j * 4 + k];
+    }
+    for (int r = 0; r < T; ++r) {
+      f32x4 a = Qs[r * 4] * kk[0] + Qs[r * 4 + 1] * kk[1] + Qs[r * 4 + 2] * kk[2] + Qs[r * 4 + 3] * kk[3];
+      f32x4 c = dOs[r * 4] * vv[0] + dOs[r * 4 + 1] * vv[1] + dOs[r * 4 + 2] * vv[2] + dOs[r * 4 + 3] * vv[3];
+      const float p = expf((a.x + a.y + a.z + a.w) * scale - Ls[r]);
+      const float ds = p * ((c.x + c.y + c.z + c.w) - Ds[r]);
+      for (int k = 0; k < 4; ++k) {
+        dv[k] += p * dOs[r * 4 + k];
+        dk[k] += ds * Qs[r * 4 + k];
+      }
+    }
+    float* w = dqkv + ((long)b * T + j) * ld + h * 16;
+    for (int k = 0; k < 4; ++k) {
+      *(f32x4*)(w + H * 16 + k * 4) = dk[k] * scale;
+      *(f32x4*)(w + 2 * H * 16 + k * 4) = dv[k];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ GELU (erf form, nn.GELU default)
+__global__ void gelu_fwd(long n, const float* __restrict__ x, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = x[i];
+  y[i] = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+}
+
+__global__ void gelu_bwd(long n, const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = x[i];
+  const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * expf(-0.5f * v * v);
+  dx[i] = dy[i] * (cdf + v * pdf);
+}
+
+// ------------------------------------------------------------------ CAF skipcat
+// Z[b, i, k, :] = (k == 0 ? x : last)[b, i, :]  (the Conv2d(T, T, [1, 2]) input as a [2T, D] matrix
+// whose row i*2+k meets weight column i*2+k); biasmat[o, :] = bias[o] (the GEMM's row addend).
+__global__ void skip_pack(int B, int T, int D, const float* __restrict__ x, const float* __restrict__ last,
+                          const float* __restrict__ bias, float* __restrict__ Z, float* __restrict__ biasmat) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)B * T * D;
+  if (i < (long)T * D) biasmat[i] = bias[i / D];
+  if (i >= n) return;
+  const long row = i / D, d = i % D;  // row = b*T + t
+  Z[(row * 2) * D + d] = x[i];
+  Z[(row * 2 + 1) * D + d] = last[i];
+}
+
+// dx (=/+=) dZ[:, :, 0, :]; dlast += dZ[:, :, 1, :]
+__global__ void skip_unpack(int B, int T, int D, const float* __restrict__ dZ, float* __restrict__ dx, int acc_x,
+                            float* __restrict__ dlast) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * T * D) return;
+  const long row = i / D, d = i % D;
+  const float a = dZ[(row * 2) * D + d];
+  dx[i] = acc_x ? dx[i] + a : a;
+  dlast[i] += dZ[(row * 2 + 1) * D + d];
+}
+
+// dbias[o] = sum_{b, d} dY[b, o, d]  (one block per o)
+__global__ __launch_bounds__(256) void skip_bias_grad(int B, int T, int D, const float* __restrict__ dY,
+                                                      float* __restrict__ db) {
+  __shared__ float sh[8];
+  const int o = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < B * D; i += 256) {
+    const int b = i / D, d = i % D;
+    s += dY[((long)b * T + o) * D + d];
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) db[o] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+}  // namespace
+
+VC_API int vc_s2eft_gate_fwd(int B, int N, int C, const float* x, const float* w, const float* bias, float beta,
+                             float* xg, float* mask, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && N > 0 && C > 0 && N <= 4096);
+  VC_REQUIRE_I32((long)N * C);
+  hipLaunchKernelGGL(gate_fwd, dim3(B), dim3(256), 3 * N * sizeof(float), stream, N, C, x, w, bias, beta, xg, mask);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_s2eft_cls_rows(int B, int T, int D, const float* cls, const float* pos, float* X, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && T > 0 && D > 0);
+  hipLaunchKernelGGL(cls_rows, dim3(vc_cdiv((long)B * D, 256)), dim3(256), 0, stream, B, T, D, cls, pos, X);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_s2eft_strip_cls(int B, int N, int D, const float* dX, float* dE, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && N > 0 && D > 0);
+  hipLaunchKernelGGL(strip_cls, dim3(vc_cdiv((long)B * N * D, 256)), dim3(256), 0, stream, B, N, D, dX, dE);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale, float* out, float* lse,
+                             hipStream_t stream) {
+  VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
+  hipLaunchKernelGGL(attn_fwd, dim3(B * H), dim3(256), 0, stream, T, H, qkv, scale, out, lse);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_s2eft_attn_bwd(int B, int T, int H, const float* qkv, const float* out, const float* dout,
+                             const float* lse, float scale, float* dqkv, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
+  hipLaunchKernelGGL(attn_bwd, dim3(B * H), dim3(256), 0, stream, T, H, qkv, out, dout, lse, scale, dqkv);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_gelu_fwd(long n, const float* x, float* y, hipStream_t stream) {
+  VC_REQUIRE(n >= 0);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(gelu_fwd, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, x, y);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_gelu_bwd(long n, const float* dy, const float* x, float* dx, hipStream_t stream) {
+  VC_REQUIRE(n >= 0);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(gelu_bwd, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, dy, x, dx);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_s2eft_skip_pack(int B, int T, int D, const float* x, const float* last, const float* bias, float* Z,
+                              float* biasmat, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && T > 0 && D > 0);
+  hipLaunchKernelGGL(skip_pack, dim3(vc_cdiv((long)B * T * D, 256)), dim3(256), 0, stream, B, T, D, x, last, bias,
+                     Z, biasmat);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx, int acc_x, float* dlast,
+                                hipStream_t stream) {
+  VC_REQUIRE(B > 0 && T > 0 && D > 0);
+  hipLaunchKernelGGL(skip_unpack, dim3(vc_cdiv((long)B * T * D, 256)), dim3(256), 0, stream, B, T, D, dZ, dx, acc_x,
+                     dlast);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_s2eft_skip_bias_grad(int B, int T, int D, const float* dY, float* db, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && T > 0 && D > 0);
+  hipLaunchKernelGGL(skip_bias_grad, dim3(T), dim3(256), 0, stream, B, T, D, dY, db);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}

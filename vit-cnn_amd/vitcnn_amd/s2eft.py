@@ -1,0 +1,385 @@
+"""S2EFT comparison model (config 5) on the MI355X path.
+
+Reference: `model/compare_method/S2EFT.py` (class `ViT` :110-162, `Transformer` :76-108,
+`Attention` :34-74, `FeedForward` :21-32), built by `model_utils.py:400-423`
+(image_size 7, near_band 3, num_patches = n_bands, dim 64, depth 5, heads 4, mlp_dim 8,
+dim_head 16, mode 'CAF', Adam lr 5e-4).
+
+The module keeps the reference's parameter tree, so `state_dict()` has the reference's key names
+and `.pth` files interchange.  Forward and backward are one hand-written program of HIP kernels
+(`csrc/s2eft.hip` + `vc_gemm` + `vc_layernorm_*`) over token rows [B, T, D] (T = N + 1); the
+parameters live in one flat fp32 buffer whose `.grad` the backward fills (the fused optimizer of
+`optim.py` then updates it in one pass; Adam = `AdamW(weight_decay=0)`).
+
+Deviations, stated: dropout (p = 0.1 in `get_model`) is not applied — the path runs the p = 0
+network (the reference's eval-mode function) in both modes and warns once when p > 0 in training;
+the `mask` argument is unsupported (the reference's mask path references an un-imported `F`,
+:58, and raises too).
+"""
+from __future__ import annotations
+
+import math
+import warnings
+import weakref
+
+import torch
+import torch.nn as nn
+
+from ._lib import lib
+
+F32 = 4
+LN_EPS = 1e-5  # nn.LayerNorm default (PreNorm :13-19, mlp_head :125-128)
+
+
+# ---------------------------------------------------------------- parameter tree (reference names)
+class Residual(nn.Module):
+    def __init__(self, fn):
+        super().__init__()
+        self.fn = fn
+
+
+class PreNorm(nn.Module):
+    def __init__(self, dim, fn):
+        super().__init__()
+        self.norm = nn.LayerNorm(dim)
+        self.fn = fn
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, hidden_dim, dropout=0.0):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(dim, hidden_dim), nn.GELU(), nn.Dropout(dropout),
+                                 nn.Linear(hidden_dim, dim), nn.Dropout(dropout))
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, heads, dim_head, dropout):
+        super().__init__()
+        inner = dim_head * heads
+        self.heads = heads
+        self.scale = dim_head ** -0.5
+        self.to_qkv = nn.Linear(dim, inner * 3, bias=False)
+        self.to_out = nn.Sequential(nn.Linear(inner, dim), nn.Dropout(dropout))
+
+
+class Transformer(nn.Module):
+    def __init__(self, dim, depth, heads, dim_head, mlp_head, dropout, num_channel, mode):
+        super().__init__()
+        self.layers = nn.ModuleList([])
+        for _ in range(depth):
+            self.layers.append(nn.ModuleList([
+                Residual(PreNorm(dim, Attention(dim, heads=heads, dim_head=dim_head, dropout=dropout))),
+                Residual(PreNorm(dim, FeedForward(dim, mlp_head, dropout=dropout)))]))
+        self.mode = mode
+        self.skipcat = nn.ModuleList([])
+        for _ in range(depth - 2):
+            self.skipcat.append(nn.Conv2d(num_channel + 1, num_channel + 1, [1, 2], 1, 0))
+
+
+class ViT(nn.Module):
+    """Same constructor as the reference `ViT` (S2EFT.py:110-131); forward(x [B, N, C]) -> logits."""
+
+    def __init__(self, image_size, near_band, num_patches, num_classes, dim, depth, heads, mlp_dim, pool="cls",
+                 channels=1, dim_head=16, dropout=0.0, emb_dropout=0.0, mode="ViT"):
+        super().__init__()
+        if dim_head != 16:
+            raise ValueError("S2EFT MI355X path: the attention kernel is written for dim_head 16 (the reference's)")
+        if mode not in ("ViT", "CAF"):
+            raise ValueError(f"unknown transformer mode {mode!r}")
+        patch_dim = image_size ** 2 * near_band
+        # creation order = the reference's, so the default initialisation draws the same numbers
+        self.conv2d = nn.Conv1d(in_channels=2, out_channels=1, kernel_size=7, stride=1, padding=3)
+        self.pos_embedding = nn.Parameter(torch.randn(1, num_patches + 2, dim))
+        self.patch_to_embedding = nn.Linear(patch_dim, dim)
+        self.cls_token = nn.Parameter(torch.randn(1, 1, dim))
+        self.dropout = nn.Dropout(emb_dropout)
+        self.transformer = Transformer(dim, depth, heads, dim_head, mlp_dim, dropout, num_patches + 1, mode)
+        self.pool = pool
+        self.mlp_head = nn.Sequential(nn.LayerNorm(dim), nn.Linear(dim, num_classes))
+        # tokens in: num_patches + 1 (HSI bands + the LiDAR band), so that T = N + 1 matches the skipcat
+        # Conv2d(num_patches + 2) channels and pos_embedding's num_patches + 2 rows (S2EFT.py:88, :117)
+        self.N, self.C, self.D, self.depth, self.heads = num_patches + 1, patch_dim, dim, depth, heads
+        self.hidden, self.ncls, self.mode = mlp_dim, num_classes, mode
+        self.p_drop = max(dropout, emb_dropout)
+        self._warned = False
+        self._build_flat()
+
+    # ------------------------------------------------------------ flat parameter buffer
+    def _build_flat(self):
+        named = list(nn.Module.named_parameters(self))
+        self._poff, off = {}, 0
+        for n, p in named:
+            self._poff[n] = off
+            off += p.numel()
+        self._n_params = self._n_active = off
+        flat = torch.empty(off, dtype=torch.float32, device=named[0][1].device)
+        for n, p in named:
+            flat[self._poff[n]:self._poff[n] + p.numel()].copy_(p.detach().reshape(-1))
+        self._pmods = {}
+        for mn, m in nn.Module.named_modules(self):
+            for pn, p in m._parameters.items():
+                if p is None:
+                    continue
+                self._pmods[(mn + "." if mn else "") + pn] = (m, pn)
+        self._rebind(flat)
+        me = weakref.ref(self)
+        for _, p in named:
+            p._vc_owner = me
+
+    def _rebind(self, flat):
+        object.__setattr__(self, "_flat_store", flat.detach().requires_grad_(True))
+        base = self._flat_store.detach()
+        for n, (m, pn) in self._pmods.items():
+            p = m._parameters[pn]
+            o = self._poff[n]
+            p.data = base[o:o + p.numel()].view(p.shape)
+
+    def _apply(self, fn, recurse=True):
+        flat = fn(self._flat_store.detach())
+        if flat.dtype != torch.float32:
+            raise RuntimeError("S2EFT MI355X path computes in fp32; dtype casts are not supported")
+        self._rebind(flat)
+        return self
+
+    def _ensure_flat(self):
+        base = self._flat_store.data_ptr()
+        for n, (m, pn) in self._pmods.items():
+            if m._parameters[pn].data_ptr() != base + F32 * self._poff[n]:
+                flat = torch.empty(self._n_params, dtype=torch.float32, device=self._flat_store.device)
+                for n2, (m2, pn2) in self._pmods.items():
+                    o = self._poff[n2]
+                    flat[o:o + m2._parameters[pn2].numel()].copy_(m2._parameters[pn2].detach().reshape(-1))
+                self._rebind(flat)
+                return
+
+    @property
+    def flat_params(self) -> torch.Tensor:
+        return self._flat_store
+
+    @property
+    def n_active_params(self) -> int:
+        return self._n_active
+
+    def zero_grad(self, set_to_none: bool = True):
+        super().zero_grad(set_to_none=set_to_none)
+        if set_to_none:
+            self._flat_store.grad = None
+        elif self._flat_store.grad is not None:
+            self._flat_store.grad.zero_()
+
+    # ------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, mask=None) -> torch.Tensor:
+        if mask is not None:
+            raise NotImplementedError("S2EFT mask path is not supported (the reference's raises NameError, :58)")
+        if x.device.type != "cuda":
+            raise RuntimeError("S2EFT MI355X path: input must be on a ROCm (cuda) device; no CPU fallback")
+        if x.dim() != 3 or x.shape[1] != self.N or x.shape[2] != self.C:
+            raise RuntimeError(f"expected x [B, {self.N}, {self.C}], got {list(x.shape)}")
+        if self.training and self.p_drop > 0 and not self._warned:
+            warnings.warn("S2EFT MI355X path: dropout is not applied (p = 0 network)")
+            self._warned = True
+        self._ensure_flat()
+        if self._flat_store.device != x.device:
+            raise RuntimeError("model and input are on different devices")
+        x = x.detach().to(torch.float32).contiguous()
+        needs_grad = torch.is_grad_enabled() and self._flat_store.requires_grad
+        return _S2EFTFunction.apply(self, x, self._flat_store, needs_grad)
+
+
+class _S2EFTFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, x, flat, needs_grad):
+        prog = _Program(model, x)
+        logits = prog.forward()
+        ctx.prog = prog if needs_grad else None
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        if ctx.prog is None:
+            raise RuntimeError("S2EFT: backward through a forward run without grad")
+        grad = ctx.prog.backward(dlogits.detach().to(torch.float32).contiguous())
+        ctx.prog = None
+        return None, None, grad, None
+
+
+class _Program:
+    """One forward (saving what the backward reads) and its hand-written backward."""
+
+    SCRATCH = 1 << 22
+
+    def __init__(self, m: ViT, x: torch.Tensor):
+        self.m, self.x, self.L = m, x, lib()
+        self.dev = x.device
+        self.s = torch.cuda.current_stream(self.dev).cuda_stream
+        self.B = x.shape[0]
+        self.T = m.N + 1
+        base = m._flat_store.data_ptr()
+        self.P = {n: base + F32 * o for n, o in m._poff.items()}
+        self.scr = self.new(self.SCRATCH)
+        self.keep = []
+
+    def new(self, *shape):
+        return torch.empty(*shape, dtype=torch.float32, device=self.dev)
+
+    def gemm(self, tA, tB, M, N, K, A, lda, sA, Bm, ldb, sB, beta, C, ldc, sC, batch=1, bias=None, add=None,
+             add_ld=0, add_mod=0, bias_grad=None, alpha=1.0):
+        self.L.vc_gemm(tA, tB, M, N, K, alpha, A, lda, sA, Bm, ldb, sB, beta, C, ldc, sC, batch, bias, add, add_ld,
+                       add_mod, 0, bias_grad, self.scr.data_ptr(), self.SCRATCH, self.s)
+
+    def ln(self, pfx, X, R, ldx):
+        D = self.m.D
+        Y, mu, rs = self.new(R, D), self.new(R), self.new(R)
+        self.L.vc_layernorm_fwd(R, D, X, ldx, self.P[pfx + ".weight"], self.P[pfx + ".bias"], LN_EPS, Y.data_ptr(), D,
+                                mu.data_ptr(), rs.data_ptr(), self.s)
+        return Y, mu, rs
+
+    def forward(self):
+        m, L, B, T, N, C, D, Hh = self.m, self.L, self.B, self.T, self.m.N, self.m.C, self.m.D, self.m.heads
+        R = B * T
+        P = self.P
+        xg, mask = self.new(B, N, C), self.new(B, N)
+        L.vc_s2eft_gate_fwd(B, N, C, self.x.data_ptr(), P["conv2d.weight"], P["conv2d.bias"], 0.4, xg.data_ptr(),
+                            mask.data_ptr(), self.s)
+        X = self.new(B, T, D)
+        L.vc_s2eft_cls_rows(B, T, D, P["cls_token"], P["pos_embedding"], X.data_ptr(), self.s)
+        # rows 1..N of every sample: xg W^T + b + pos[1 + t]  (pos fused as the GEMM's row addend)
+        self.gemm(0, 1, N, D, C, xg.data_ptr(), C, N * C, P["patch_to_embedding.weight"], C, 0, 0.0,
+                  X.data_ptr() + F32 * D, D, T * D, batch=B, bias=P["patch_to_embedding.bias"],
+                  add=P["pos_embedding"] + F32 * D, add_ld=D, add_mod=N)
+        self.xg = xg
+        self.saved = []
+        xin = []
+        for li in range(m.depth):
+            pre = f"transformer.layers.{li}"
+            st = {"xin": X}
+            xin.append(X)
+            if m.mode == "CAF" and li > 1:
+                sk = f"transformer.skipcat.{li - 2}"
+                Z, bm, Xs = self.new(B, 2 * T, D), self.new(T, D), self.new(B, T, D)
+                L.vc_s2eft_skip_pack(B, T, D, X.data_ptr(), xin[li - 2].data_ptr(), P[sk + ".bias"], Z.data_ptr(),
+                                     bm.data_ptr(), self.s)
+                self.gemm(0, 0, T, D, 2 * T, P[sk + ".weight"], 2 * T, 0, Z.data_ptr(), D, 2 * T * D, 0.0,
+                          Xs.data_ptr(), D, T * D, batch=B, add=bm.data_ptr(), add_ld=D, add_mod=T)
+                st["Z"] = Z
+                X = Xs
+            st["xs"] = X
+            # attention sub-block
+            Y, mu, rs = self.ln(pre + ".0.fn.norm", X.data_ptr(), R, D)
+            qkv = self.new(R, 3 * Hh * 16)
+            self.gemm(0, 1, R, 3 * Hh * 16, D, Y.data_ptr(), D, 0, P[pre + ".0.fn.fn.to_qkv.weight"], D, 0, 0.0,
+                      qkv.data_ptr(), 3 * Hh * 16, 0)
+            O, lse = self.new(R, Hh * 16), self.new(B, Hh, T)
+            L.vc_s2eft_attn_fwd(B, T, Hh, qkv.data_ptr(), 16 ** -0.5, O.data_ptr(), lse.data_ptr(), self.s)
+            X2 = self.new(B, T, D)
+            self.gemm(0, 1, R, D, Hh * 16, O.data_ptr(), Hh * 16, 0, P[pre + ".0.fn.fn.to_out.0.weight"], Hh * 16, 0,
+                      0.0, X2.data_ptr(), D, 0, bias=P[pre + ".0.fn.fn.to_out.0.bias"], add=X.data_ptr(), add_ld=D)
+            # feed-forward sub-block
+            Y2, mu2, rs2 = self.ln(pre + ".1.fn.norm", X2.data_ptr(), R, D)
+            Hd = self.new(R, m.hidden)
+            self.gemm(0, 1, R, m.hidden, D, Y2.data_ptr(), D, 0, P[pre + ".1.fn.fn.net.0.weight"], D, 0, 0.0,
+                      Hd.data_ptr(), m.hidden, 0, bias=P[pre + ".1.fn.fn.net.0.bias"])
+            G = self.new(R, m.hidden)
+            L.vc_gelu_fwd(R * m.hidden, Hd.data_ptr(), G.data_ptr(), self.s)
+            X3 = self.new(B, T, D)
+            self.gemm(0, 1, R, D, m.hidden, G.data_ptr(), m.hidden, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0,
+                      0.0, X3.data_ptr(), D, 0, bias=P[pre + ".1.fn.fn.net.3.bias"], add=X2.data_ptr(), add_ld=D)
+            st.update(Y=Y, mu=mu, rs=rs, qkv=qkv, O=O, lse=lse, X2=X2, Y2=Y2, mu2=mu2, rs2=rs2, Hd=Hd, G=G)
+            self.saved.append(st)
+            X = X3
+        self.Xout = X
+        # head on the cls rows (ld T*D)
+        Yc, muc, rsc = self.ln("mlp_head.0", X.data_ptr(), B, T * D)
+        logits = self.new(B, m.ncls)
+        self.gemm(0, 1, B, m.ncls, D, Yc.data_ptr(), D, 0, P["mlp_head.1.weight"], D, 0, 0.0, logits.data_ptr(),
+                  m.ncls, 0, bias=P["mlp_head.1.bias"])
+        self.head = (Yc, muc, rsc)
+        return logits
+
+    def backward(self, dlogits):
+        m, L, B, T, N, C, D, Hh = self.m, self.L, self.B, self.T, self.m.N, self.m.C, self.m.D, self.m.heads
+        R = B * T
+        P = self.P
+        grad = self.new(m._n_params)
+        L.vc_fill(m._n_params, grad.data_ptr(), 0.0, self.s)
+        gb = grad.data_ptr()
+        G = {n: gb + F32 * o for n, o in m._poff.items()}
+        scr, ns = self.scr.data_ptr(), self.SCRATCH
+        # head
+        Yc, muc, rsc = self.head
+        self.gemm(1, 0, m.ncls, D, B, dlogits.data_ptr(), m.ncls, 0, Yc.data_ptr(), D, 0, 0.0, G["mlp_head.1.weight"],
+                  D, 0, bias_grad=G["mlp_head.1.bias"])
+        dYc = self.new(B, D)
+        self.gemm(0, 0, B, D, m.ncls, dlogits.data_ptr(), m.ncls, 0, P["mlp_head.1.weight"], D, 0, 0.0, dYc.data_ptr(),
+                  D, 0)
+        dX = self.new(B, T, D)
+        L.vc_fill(R * D, dX.data_ptr(), 0.0, self.s)
+        L.vc_layernorm_bwd(B, D, dYc.data_ptr(), D, self.Xout.data_ptr(), T * D, P["mlp_head.0.weight"], muc.data_ptr(),
+                           rsc.data_ptr(), dX.data_ptr(), T * D, 0.0, G["mlp_head.0.weight"], G["mlp_head.0.bias"], 0.0,
+                           scr, ns, self.s)
+        dlast = {}
+        for li in reversed(range(m.depth)):
+            pre = f"transformer.layers.{li}"
+            st = self.saved[li]
+            # feed-forward: X3 = X2 + W2 gelu(W1 LN(X2) + b1) + b2 ; dX holds dX3, becomes dX2 in place
+            dG = self.new(R, m.hidden)
+            self.gemm(1, 0, D, m.hidden, R, dX.data_ptr(), D, 0, st["G"].data_ptr(), m.hidden, 0, 0.0,
+                      G[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0, bias_grad=G[pre + ".1.fn.fn.net.3.bias"])
+            self.gemm(0, 0, R, m.hidden, D, dX.data_ptr(), D, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0, 0.0,
+                      dG.data_ptr(), m.hidden, 0)
+            dH = self.new(R, m.hidden)
+            L.vc_gelu_bwd(R * m.hidden, dG.data_ptr(), st["Hd"].data_ptr(), dH.data_ptr(), self.s)
+            self.gemm(1, 0, m.hidden, D, R, dH.data_ptr(), m.hidden, 0, st["Y2"].data_ptr(), D, 0, 0.0,
+                      G[pre + ".1.fn.fn.net.0.weight"], D, 0, bias_grad=G[pre + ".1.fn.fn.net.0.bias"])
+            dY2 = self.new(R, D)
+            self.gemm(0, 0, R, D, m.hidden, dH.data_ptr(), m.hidden, 0, P[pre + ".1.fn.fn.net.0.weight"], D, 0, 0.0,
+                      dY2.data_ptr(), D, 0)
+            L.vc_layernorm_bwd(R, D, dY2.data_ptr(), D, st["X2"].data_ptr(), D, P[pre + ".1.fn.norm.weight"],
+                               st["mu2"].data_ptr(), st["rs2"].data_ptr(), dX.data_ptr(), D, 1.0,
+                               G[pre + ".1.fn.norm.weight"], G[pre + ".1.fn.norm.bias"], 0.0, scr, ns, self.s)
+            # attention: X2 = Xs + Wo attn(Wqkv LN(Xs)) + bo ; dX becomes dXs in place
+            E = Hh * 16
+            self.gemm(1, 0, D, E, R, dX.data_ptr(), D, 0, st["O"].data_ptr(), E, 0, 0.0,
+                      G[pre + ".0.fn.fn.to_out.0.weight"], E, 0, bias_grad=G[pre + ".0.fn.fn.to_out.0.bias"])
+            dO = self.new(R, E)
+            self.gemm(0, 0, R, E, D, dX.data_ptr(), D, 0, P[pre + ".0.fn.fn.to_out.0.weight"], E, 0, 0.0,
+                      dO.data_ptr(), E, 0)
+            dqkv = self.new(R, 3 * E)
+            L.vc_s2eft_attn_bwd(B, T, Hh, st["qkv"].data_ptr(), st["O"].data_ptr(), dO.data_ptr(), st["lse"].data_ptr(),
+                                16 ** -0.5, dqkv.data_ptr(), self.s)
+            self.gemm(1, 0, 3 * E, D, R, dqkv.data_ptr(), 3 * E, 0, st["Y"].data_ptr(), D, 0, 0.0,
+                      G[pre + ".0.fn.fn.to_qkv.weight"], D, 0)
+            dY = self.new(R, D)
+            self.gemm(0, 0, R, D, 3 * E, dqkv.data_ptr(), 3 * E, 0, P[pre + ".0.fn.fn.to_qkv.weight"], D, 0, 0.0,
+                      dY.data_ptr(), D, 0)
+            L.vc_layernorm_bwd(R, D, dY.data_ptr(), D, st["xs"].data_ptr(), D, P[pre + ".0.fn.norm.weight"],
+                               st["mu"].data_ptr(), st["rs"].data_ptr(), dX.data_ptr(), D, 1.0,
+                               G[pre + ".0.fn.norm.weight"], G[pre + ".0.fn.norm.bias"], 0.0, scr, ns, self.s)
+            # skipcat: Xs[b] = Wm Z[b] + bias  (Wm = weight viewed [T, 2T])
+            if "Z" in st:
+                sk = f"transformer.skipcat.{li - 2}"
+                dWb = self.new(B, T * 2 * T)
+                self.gemm(0, 1, T, 2 * T, D, dX.data_ptr(), D, T * D, st["Z"].data_ptr(), D, 2 * T * D, 0.0,
+                          dWb.data_ptr(), 2 * T, T * 2 * T, batch=B)
+                L.vc_colsum(B, T * 2 * T, dWb.data_ptr(), T * 2 * T, G[sk + ".weight"], 0.0, scr, ns, self.s)
+                L.vc_s2eft_skip_bias_grad(B, T, D, dX.data_ptr(), G[sk + ".bias"], self.s)
+                dZ = self.new(B, 2 * T, D)
+                self.gemm(1, 0, 2 * T, D, T, P[sk + ".weight"], 2 * T, 0, dX.data_ptr(), D, T * D, 0.0, dZ.data_ptr(),
+                          D, 2 * T * D, batch=B)
+                if li - 2 not in dlast:
+                    dl = self.new(B, T, D)
+                    L.vc_fill(R * D, dl.data_ptr(), 0.0, self.s)
+                    dlast[li - 2] = dl
+                dXin = self.new(B, T, D)
+                L.vc_s2eft_skip_unpack(B, T, D, dZ.data_ptr(), dXin.data_ptr(), 0, dlast[li - 2].data_ptr(), self.s)
+                dX = dXin
+            if li in dlast:  # this layer's input is also last_output[li] of layer li + 2
+                L.vc_add2_2d(R, D, dX.data_ptr(), D, dlast[li].data_ptr(), D, dX.data_ptr(), D, 0.0, self.s)
+        # embedding: X0 = cat(cls, xg W^T + b) + pos
+        L.vc_colsum(B, T * D, dX.data_ptr(), T * D, G["pos_embedding"], 0.0, scr, ns, self.s)
+        L.vc_colsum(B, D, dX.data_ptr(), T * D, G["cls_token"], 0.0, scr, ns, self.s)
+        dE = self.new(B * N, D)
+        L.vc_s2eft_strip_cls(B, N, D, dX.data_ptr(), dE.data_ptr(), self.s)
+        self.gemm(1, 0, D, C, B * N, dE.data_ptr(), D, 0, self.xg.data_ptr(), C, 0, 0.0,
+                  G["patch_to_embedding.weight"], C, 0, bias_grad=G["patch_to_embedding.bias"])
+        return grad
