@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-s2eft", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
@@ -207,6 +208,76 @@ def cpu_baseline(steps):
                       f"torch CPU with {threads} threads; {dt / steps:.2f} s/step"}
 
 
+def s2eft_leg(dev, steps, cpu_steps):
+    """Config 5: S2EFT train step (forward, weighted CE, backward, Adam)
+    at B = 64 on [64, 145, 147] synthetic tokens, eager launches; plus the CPU oracle on the same
+    shape (oracle/s2eft_oracle.py, autograd, torch CPU threads) as its baseline."""
+    from vitcnn_amd import CrossEntropyLoss
+    from vitcnn_amd.optim import AdamW
+    from vitcnn_amd.s2eft import ViT
+    torch.manual_seed(0)
+    kw = dict(image_size=7, near_band=3, num_patches=144, num_classes=16, dim=64, depth=5, heads=4, mlp_dim=8,
+              dropout=0.0, emb_dropout=0.0, mode="CAF")
+    m = ViT(**kw).to(dev).train()
+    opt = AdamW(m.parameters(), lr=5e-4, weight_decay=0.0)
+    w = torch.ones(16)
+    w[0] = 0.0
+    crit = CrossEntropyLoss(weight=w.to(dev))
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(64, 145, 147, generator=g)
+    t = torch.randint(1, 16, (64,), generator=g)
+    xd, td = x.to(dev), t.to(dev)
+
+    def eager_step():
+        opt.zero_grad(set_to_none=True)
+        crit(m(xd), td).backward()
+        opt.step()
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(5):
+            eager_step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    # the whole step (forward, CE, hand-written backward, fused Adam) as one hipGraph
+    launch = "hipGraph"
+    try:
+        graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            crit(m(xd), td).backward()
+            opt.step()
+        step = graph.replay
+    except RuntimeError as e:  # reported in the line, never silent
+        launch = f"eager (graph capture failed: {str(e)[:80]})"
+        step = eager_step
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    out = {"workload": "S2EFT (CAF, depth 5, 4 heads x 16, dim 64) train step, x [64,145,147], 16 classes",
+           "value": round(64 / ms * 1e3, 1), "unit": "patches/s", "ms_per_step": round(ms, 4), "dtype": "fp32",
+           "launch": launch}
+    if cpu_steps > 0:
+        from oracle import s2eft_oracle as O
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        O.train_step(sd, x, t, w)
+        t0 = time.perf_counter()
+        for _ in range(cpu_steps):
+            O.train_step(sd, x, t, w)
+        dt = (time.perf_counter() - t0) / cpu_steps
+        out["cpu_baseline"] = {"value": round(64 / dt, 2), "unit": "patches/s", "cores": threads, "kind": "port",
+                               "sample": f"{cpu_steps} B=64 fwd+bwd steps of oracle/s2eft_oracle.py"}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -334,6 +405,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_steps)
+    if world == 1 and not args.no_s2eft:
+        out["config5_s2eft"] = s2eft_leg(dev, min(args.steps, 50), 0 if args.no_cpu_baseline else 5)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -153,3 +153,41 @@ def test_s2eft_gpu_adam_step_and_eval():
     with torch.no_grad():
         final = float(crit(m(x), t))
     assert final < l0
+
+
+def test_get_model_s2eft_defaults():
+    from vitcnn_amd.model_utils import get_model
+    m, opt, crit, kw = get_model("S2EFT", n_classes=16, n_bands=(144, 1), ignored_labels=[0], dataset="Houston2013",
+                                 device=torch.device("cpu"))
+    assert kw["patch_size"] == 7 and kw["lr"] == 0.0005 and kw["epoch"] == 600 and kw["batch_size"] == 64
+    assert opt.param_groups[0]["weight_decay"] == 0.0
+    assert m.N == 145 and m.C == 147 and m.transformer.skipcat[0].weight.shape == (146, 146, 1, 2)
+
+
+@pytest.mark.gpu
+def test_s2eft_gpu_pca30_vit_mode():
+    """applyPCA branch (num_patches 30 -> 31 tokens + cls, model_utils.py:403-405) and the plain 'ViT'
+    transformer mode (no skipcat, S2EFT.py:94-97): HIP vs oracle, hash-free seeded init"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vitcnn_amd.s2eft import ViT
+    for mode in ("ViT", "CAF"):
+        torch.manual_seed(3)
+        kw = dict(KW, num_patches=30, num_classes=7, mode=mode)
+        sd = {k: v.clone() for k, v in ViT(**kw).state_dict().items()}
+        g = torch.Generator().manual_seed(9)
+        x = torch.rand(8, 31, 147, generator=g)
+        t = torch.randint(1, 7, (8,), generator=g)
+        w = torch.ones(7)
+        w[0] = 0
+        ol, oloss, og = O.train_step(sd, x, t, w, mode=mode)
+        m = ViT(**kw)
+        m.load_state_dict(sd)
+        m = m.to("cuda")
+        from vitcnn_amd.losses import CrossEntropyLoss
+        logits = m(x.cuda())
+        CrossEntropyLoss(weight=w.cuda())(logits, t.cuda()).backward()
+        assert _rel(logits.detach().cpu(), ol) < 1e-3
+        flat = m.flat_params.grad.cpu()
+        gref = torch.cat([og[n].reshape(-1) for n in m._poff])
+        assert float((flat - gref).norm()) <= 1e-3 * float(gref.norm())

@@ -12,9 +12,9 @@
 namespace {
 
 // ------------------------------------------------------------------ spectral gate
-// One block per sample.  Per token row: mean and max over C (one wave per row), then the k=7 conv over
+// Blocks (sample, 1/8 of its rows): each recomputes the sample's statistics (L2-resident).  Per token row: mean and max over C (one wave per row), then the k=7 conv over
 // the token axis (zero padded), sigmoid, threshold; xg = x * mask (the mask is `.data`: no gradient).
-__global__ __launch_bounds__(256) void gate_fwd(int N, int C, const float* __restrict__ x,
+__global__ __launch_bounds__(512) void gate_fwd(int N, int C, const float* __restrict__ x,
                                                 const float* __restrict__ w, const float* __restrict__ bias,
                                                 float beta, float* __restrict__ xg, float* __restrict__ mask) {
   extern __shared__ float sh[];
@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void gate_fwd(int N, int C, const float* __res
   float* msk = sh + 2 * N;
   const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* xb = x + (long)b * N * C;
-  for (int r = wave; r < N; r += 4) {
+  for (int r = wave; r < N; r += 8) {
     float s = 0.f, m = -INFINITY;
     for (int c = lane; c < C; c += 64) {
       const float v = xb[(long)r * C + c];
@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void gate_fwd(int N, int C, const float* __res
     }
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < N; t += 256) {
+  for (int t = threadIdx.x; t < N; t += 512) {
     float v = bias[0];
     for (int k = 0; k < 7; ++k) {
       const int j = t + k - 3;
@@ -47,11 +47,13 @@ __global__ __launch_bounds__(256) void gate_fwd(int N, int C, const float* __res
     const float s = 1.0f / (1.0f + expf(-v));
     const float m = s >= beta ? 1.0f : 0.0f;
     msk[t] = m;
-    mask[(long)b * N + t] = m;
+    if (blockIdx.y == 0) mask[(long)b * N + t] = m;
   }
   __syncthreads();
   float* xgb = xg + (long)b * N * C;
-  for (int i = threadIdx.x; i < N * C; i += 256) xgb[i] = xb[i] * msk[i / C];
+  const int per = (N * C + gridDim.y - 1) / gridDim.y;
+  const int end = min(N * C, per * ((int)blockIdx.y + 1));
+  for (int i = per * blockIdx.y + threadIdx.x; i < end; i += 512) xgb[i] = xb[i] * msk[i / C];
 }
 
 // X[b, 0, :] = cls + pos[0]  (the other rows come from the embedding GEMM with pos fused as addend)
@@ -72,12 +74,31 @@ __global__ void strip_cls(int B, int N, int D, const float* __restrict__ dX, flo
 }
 
 // ------------------------------------------------------------------ attention core (dim_head 16)
-// One block per (sample, head), one thread per query row; K/V of the head staged in LDS and read as
-// broadcasts.  Saves the log-sum-exp per row for the backward (P is never stored).
+// Block = 256 lanes = 64 rows x 4 key-quarters: lane (row, part) walks keys j = part, part+4, ...; the four
+// partial softmax states / gradient sums of a row meet by lane shuffles.  Grid B*H*ceil(T/64) (768
+// blocks, 3072 waves at config 5).  The head's K/V (and for the backward Q, dO, lse, rowsum(dO*O)) sit in
+// LDS sized to T and are read as 4-way broadcasts.  P is never stored: the forward saves lse per row.
+constexpr int kParts = 4;
+
+__device__ __forceinline__ float dot16(const f32x4* q, const f32x4* k) {
+  f32x4 a = q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3];
+  return (a.x + a.y + a.z + a.w);
+}
+
+__device__ __forceinline__ float part_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void attn_fwd(int T, int H, const float* __restrict__ qkv, float scale,
                                                 float* __restrict__ out, float* __restrict__ lse) {
-  __shared__ f32x4 Ks[256 * 4], Vs[256 * 4];
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  extern __shared__ f32x4 lds4[];  // 2 * T * 64 B
+  f32x4* Ks = lds4;
+  f32x4* Vs = lds4 + T * 4;
+  const int nq = (T + 63) >> 6;
+  const int bh = blockIdx.x / nq, chunk = blockIdx.x % nq;
+  const int b = bh / H, h = bh % H;
   const int ld = 3 * H * 16, ldo = H * 16;
   const float* base = qkv + (long)b * T * ld;
   for (int i = threadIdx.x; i < T * 4; i += 256) {
@@ -86,37 +107,55 @@ __global__ __launch_bounds__(256) void attn_fwd(int T, int H, const float* __res
     Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
   }
   __syncthreads();
-  const int i = threadIdx.x;
-  if (i >= T) return;
+  const int part = threadIdx.x & (kParts - 1);
+  const int i = chunk * 64 + (threadIdx.x >> 2);
+  const bool valid = i < T;
+  const int ii = valid ? i : T - 1;  // idle lanes shadow the last row so the shuffles stay uniform
   f32x4 q[4];
-  for (int k = 0; k < 4; ++k) q[k] = *(const f32x4*)(base + (long)i * ld + h * 16 + k * 4);
+  for (int k = 0; k < 4; ++k) q[k] = *(const f32x4*)(base + (long)ii * ld + h * 16 + k * 4);
   float m = -INFINITY;
-  for (int j = 0; j < T; ++j) {
-    f32x4 a = q[0] * Ks[j * 4] + q[1] * Ks[j * 4 + 1] + q[2] * Ks[j * 4 + 2] + q[3] * Ks[j * 4 + 3];
-    m = fmaxf(m, (a.x + a.y + a.z + a.w) * scale);
-  }
+  for (int j = part; j < T; j += kParts) m = fmaxf(m, dot16(q, Ks + j * 4) * scale);
   float l = 0.f;
   f32x4 acc[4] = {};
-  for (int j = 0; j < T; ++j) {
-    f32x4 a = q[0] * Ks[j * 4] + q[1] * Ks[j * 4 + 1] + q[2] * Ks[j * 4 + 2] + q[3] * Ks[j * 4 + 3];
-    const float p = expf((a.x + a.y + a.z + a.w) * scale - m);
+  for (int j = part; j < T; j += kParts) {
+    const float p = expf(dot16(q, Ks + j * 4) * scale - m);
     l += p;
     for (int k = 0; k < 4; ++k) acc[k] += p * Vs[j * 4 + k];
   }
+  // merge the four partial states of the row
+  float M = fmaxf(m, __shfl_xor(m, 1, 64));
+  M = fmaxf(M, __shfl_xor(M, 2, 64));
+  const float f = (m == -INFINITY) ? 0.f : expf(m - M);
+  l = part_sum(l * f);
+  for (int k = 0; k < 4; ++k) {
+    acc[k] *= f;
+    acc[k].x = part_sum(acc[k].x);
+    acc[k].y = part_sum(acc[k].y);
+    acc[k].z = part_sum(acc[k].z);
+    acc[k].w = part_sum(acc[k].w);
+  }
+  if (!valid) return;
   const float r = 1.0f / l;
   float* o = out + ((long)b * T + i) * ldo + h * 16;
-  for (int k = 0; k < 4; ++k) *(f32x4*)(o + k * 4) = acc[k] * r;
-  lse[((long)b * H + h) * T + i] = m + logf(l);
+  *(f32x4*)(o + part * 4) = acc[part] * r;
+  if (part == 0) lse[((long)b * H + h) * T + i] = M + logf(l);
 }
 
-// dS = P * (dP - rowsum(dO * O)); pass 1 (thread per query) -> dq, pass 2 (thread per key) -> dk, dv.
+// dS = P * (dP - rowsum(dO * O)); pass 1 (lane group per query row) -> dq, pass 2 (per key row) -> dk, dv.
 __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __restrict__ qkv,
                                                 const float* __restrict__ out, const float* __restrict__ dout,
                                                 const float* __restrict__ lse, float scale,
                                                 float* __restrict__ dqkv) {
-  __shared__ f32x4 Qs[256 * 4], Ks[256 * 4], Vs[256 * 4], dOs[256 * 4];
-  __shared__ float Ls[256], Ds[256];
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  extern __shared__ f32x4 lds4[];  // 4 * T * 64 B + 2 * T * 4 B (37.9 KB at T = 146)
+  f32x4* Qs = lds4;
+  f32x4* Ks = lds4 + T * 4;
+  f32x4* Vs = lds4 + 2 * T * 4;
+  f32x4* dOs = lds4 + 3 * T * 4;
+  float* Ls = (float*)(lds4 + 4 * T * 4);
+  float* Ds = Ls + T;
+  const int nq = (T + 63) >> 6;
+  const int bh = blockIdx.x / nq, chunk = blockIdx.x % nq;
+  const int b = bh / H, h = bh % H;
   const int ld = 3 * H * 16, ldo = H * 16;
   const float* base = qkv + (long)b * T * ld;
   for (int i = threadIdx.x; i < T * 4; i += 256) {
@@ -126,55 +165,71 @@ __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __res
     Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
     dOs[i] = *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4);
   }
-  const int i = threadIdx.x;
-  if (i < T) {
-    const float* o = out + ((long)b * T + i) * ldo + h * 16;
-    const float* g = dout + ((long)b * T + i) * ldo + h * 16;
-    float s = 0.f;
-    for (int d = 0; d < 16; ++d) s += o[d] * g[d];
-    Ds[i] = s;
-    Ls[i] = lse[((long)b * H + h) * T + i];
+  // rowsum(dO * O): 16 lanes per row, coalesced
+  for (int i0 = 0; i0 < T * 16; i0 += 256) {
+    const int idx = i0 + threadIdx.x;
+    const int r = idx >> 4, d = idx & 15;
+    float v = 0.f;
+    if (idx < T * 16) v = out[((long)b * T + r) * ldo + h * 16 + d] * dout[((long)b * T + r) * ldo + h * 16 + d];
+    v = group16_sum(v);
+    if (d == 0 && idx < T * 16) {
+      Ds[r] = v;
+      Ls[r] = lse[((long)b * H + h) * T + r];
+    }
   }
   __syncthreads();
-  if (i >= T) return;
-  {  // dq_i
+  const int part = threadIdx.x & (kParts - 1);
+  const int i = chunk * 64 + (threadIdx.x >> 2);
+  const bool valid = i < T;
+  const int ii = valid ? i : T - 1;
+  {  // dq of row ii
     f32x4 q[4], go[4], dq[4] = {};
     for (int k = 0; k < 4; ++k) {
-      q[k] = Qs[i * 4 + k];
-      go[k] = dOs[i * 4 + k];
+      q[k] = Qs[ii * 4 + k];
+      go[k] = dOs[ii * 4 + k];
     }
-    const float li = Ls[i], di = Ds[i];
-    for (int j = 0; j < T; ++j) {
-      f32x4 a = q[0] * Ks[j * 4] + q[1] * Ks[j * 4 + 1] + q[2] * Ks[j * 4 + 2] + q[3] * Ks[j * 4 + 3];
-      f32x4 c = go[0] * Vs[j * 4] + go[1] * Vs[j * 4 + 1] + go[2] * Vs[j * 4 + 2] + go[3] * Vs[j * 4 + 3];
-      const float p = expf((a.x + a.y + a.z + a.w) * scale - li);
-      const float ds = p * ((c.x + c.y + c.z + c.w) - di);
+    const float li = Ls[ii], di = Ds[ii];
+    for (int j = part; j < T; j += kParts) {
+      const float p = expf(dot16(q, Ks + j * 4) * scale - li);
+      const float ds = p * (dot16(go, Vs + j * 4) - di);
       for (int k = 0; k < 4; ++k) dq[k] += ds * Ks[j * 4 + k];
     }
-    float* w = dqkv + ((long)b * T + i) * ld + h * 16;
-    for (int k = 0; k < 4; ++k) *(f32x4*)(w + k * 4) = dq[k] * scale;
+    for (int k = 0; k < 4; ++k) {
+      dq[k].x = part_sum(dq[k].x);
+      dq[k].y = part_sum(dq[k].y);
+      dq[k].z = part_sum(dq[k].z);
+      dq[k].w = part_sum(dq[k].w);
+    }
+    if (valid) *(f32x4*)(dqkv + ((long)b * T + i) * ld + h * 16 + part * 4) = dq[part] * scale;
   }
-  {  // dk_j, dv_j with j = this thread
-    const int j = i;
+  {  // dk, dv of key row ii
     f32x4 kk[4], vv[4], dk[4] = {}, dv[4] = {};
     for (int k = 0; k < 4; ++k) {
-      kk[k] = Ks[j * 4 + k];
-      vv[k] = Vs[j * 4 + k];
+      kk[k] = Ks[ii * 4 + k];
+      vv[k] = Vs[ii * 4 + k];
     }
-    for (int r = 0; r < T; ++r) {
-      f32x4 a = Qs[r * 4] * kk[0] + Qs[r * 4 + 1] * kk[1] + Qs[r * 4 + 2] * kk[2] + Qs[r * 4 + 3] * kk[3];
-      f32x4 c = dOs[r * 4] * vv[0] + dOs[r * 4 + 1] * vv[1] + dOs[r * 4 + 2] * vv[2] + dOs[r * 4 + 3] * vv[3];
-      const float p = expf((a.x + a.y + a.z + a.w) * scale - Ls[r]);
-      const float ds = p * ((c.x + c.y + c.z + c.w) - Ds[r]);
+    for (int r = part; r < T; r += kParts) {
+      const float p = expf(dot16(kk, Qs + r * 4) * scale - Ls[r]);
+      const float ds = p * (dot16(vv, dOs + r * 4) - Ds[r]);
       for (int k = 0; k < 4; ++k) {
         dv[k] += p * dOs[r * 4 + k];
         dk[k] += ds * Qs[r * 4 + k];
       }
     }
-    float* w = dqkv + ((long)b * T + j) * ld + h * 16;
     for (int k = 0; k < 4; ++k) {
-      *(f32x4*)(w + H * 16 + k * 4) = dk[k] * scale;
-      *(f32x4*)(w + 2 * H * 16 + k * 4) = dv[k];
+      dk[k].x = part_sum(dk[k].x);
+      dk[k].y = part_sum(dk[k].y);
+      dk[k].z = part_sum(dk[k].z);
+      dk[k].w = part_sum(dk[k].w);
+      dv[k].x = part_sum(dv[k].x);
+      dv[k].y = part_sum(dv[k].y);
+      dv[k].z = part_sum(dv[k].z);
+      dv[k].w = part_sum(dv[k].w);
+    }
+    if (valid) {
+      float* w = dqkv + ((long)b * T + i) * ld + h * 16;
+      *(f32x4*)(w + H * 16 + part * 4) = dk[part] * scale;
+      *(f32x4*)(w + 2 * H * 16 + part * 4) = dv[part];
     }
   }
 }
@@ -243,7 +298,7 @@ VC_API int vc_s2eft_gate_fwd(int B, int N, int C, const float* x, const float* w
                              float* xg, float* mask, hipStream_t stream) {
   VC_REQUIRE(B > 0 && N > 0 && C > 0 && N <= 4096);
   VC_REQUIRE_I32((long)N * C);
-  hipLaunchKernelGGL(gate_fwd, dim3(B), dim3(256), 3 * N * sizeof(float), stream, N, C, x, w, bias, beta, xg, mask);
+  hipLaunchKernelGGL(gate_fwd, dim3(B, 8), dim3(512), 3 * N * sizeof(float), stream, N, C, x, w, bias, beta, xg, mask);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -265,7 +320,8 @@ VC_API int vc_s2eft_strip_cls(int B, int N, int D, const float* dX, float* dE, h
 VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale, float* out, float* lse,
                              hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_fwd, dim3(B * H), dim3(256), 0, stream, T, H, qkv, scale, out, lse);
+  hipLaunchKernelGGL(attn_fwd, dim3(B * H * ((T + 63) / 64)), dim3(256), 2 * T * 64, stream, T, H, qkv, scale, out,
+                     lse);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -273,7 +329,8 @@ VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale,
 VC_API int vc_s2eft_attn_bwd(int B, int T, int H, const float* qkv, const float* out, const float* dout,
                              const float* lse, float scale, float* dqkv, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_bwd, dim3(B * H), dim3(256), 0, stream, T, H, qkv, out, dout, lse, scale, dqkv);
+  hipLaunchKernelGGL(attn_bwd, dim3(B * H * ((T + 63) / 64)), dim3(256), 4 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
+                     dout, lse, scale, dqkv);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

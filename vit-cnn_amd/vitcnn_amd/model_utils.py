@@ -10,9 +10,9 @@ replaces, so `main.py`-style drivers switch by changing one import:
 * `test(run, net, img1, img2, hyperparams) -> probs[W, H, n_classes]` — :1067-1132.
 * `val(net, data_loader, device, supervision) -> accuracy` — :1135-1158.
 
-Only "Multimodality_Mamba" (the README's "ViT-CNN (ours)") is registered: the reference's other
-branches import modules that are absent from the reference tree and
-are out of scope for this path.
+Registered: "Multimodality_Mamba" (the README's "ViT-CNN (ours)") and "S2EFT" (config 5, :400-423).
+The reference's other branches import modules absent from the reference tree (SURVEY.md section 2a
+row 22) and are out of scope for this path.
 
 Data parallelism: when a torch.distributed process group with more than
 one rank is initialised, `train` all-reduces the flat gradient after every backward (one RCCL
@@ -35,7 +35,7 @@ from .model import Multimodality_Mamba
 from .optim import AdamW
 from .window import SlidingWindowInference
 
-REGISTERED = ("Multimodality_Mamba",)
+REGISTERED = ("Multimodality_Mamba", "S2EFT")
 
 
 def camel_to_snake(name: str) -> str:
@@ -60,6 +60,8 @@ def get_model(name, **kwargs):
     weights[torch.LongTensor(list(kwargs["ignored_labels"]))] = 0.0
     weights = weights.to(device)
     weights = kwargs.setdefault("weights", weights)
+    if name == "S2EFT":
+        return _get_s2eft(n_bands, n_classes, device, kwargs)
     kwargs.setdefault("patch_size", 9)
     patch_size = kwargs["patch_size"]
     center_pixel = True
@@ -83,6 +85,28 @@ def get_model(name, **kwargs):
     kwargs.setdefault("radiation_augmentation", False)
     kwargs.setdefault("mixture_augmentation", False)
     kwargs["center_pixel"] = center_pixel
+    return model, optimizer, criterion, kwargs
+
+
+def _get_s2eft(n_bands, n_classes, device, kwargs):
+    """S2EFT branch of model_utils.py:400-423 (config 5): ViT(image_size=patch_size, near_band 3,
+    num_patches=n_bands, dim 64, depth 5, heads 4, mlp_dim 8, dropout 0.1, mode 'CAF'), Adam(lr 5e-4),
+    weighted CE, epoch 600, batch 64.  Adam = the fused AdamW kernel with weight_decay 0.  The model
+    takes x [B, n_bands + 1, patch_size**2 * 3]."""
+    from .s2eft import ViT
+    kwargs.setdefault("patch_size", 7)
+    kwargs.setdefault("applyPCA", False)
+    if kwargs["applyPCA"]:
+        n_bands = 30
+    model = ViT(image_size=kwargs["patch_size"], near_band=3, num_patches=n_bands, num_classes=n_classes, dim=64,
+                depth=5, heads=4, mlp_dim=8, dropout=0.1, emb_dropout=0.1, mode="CAF").to(device)
+    lr = kwargs.setdefault("lr", 0.0005)
+    optimizer = AdamW(model.parameters(), lr=lr, weight_decay=0.0)
+    criterion = CrossEntropyLoss(weight=kwargs["weights"])
+    kwargs.setdefault("epoch", 600)
+    kwargs.setdefault("batch_size", 64)
+    kwargs.setdefault("supervision", "full")
+    kwargs["center_pixel"] = True
     return model, optimizer, criterion, kwargs
 
 
