@@ -266,4 +266,18 @@ VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx,
                                 hipStream_t stream);
 VC_API int vc_s2eft_skip_bias_grad(int B, int T, int D, const float* dY, float* db, hipStream_t stream);
 
+/* ---------------------------------------------------------------- FusAtNet forward (config 5)
+ * model/compare_method/FusAtNet.py over channels-last [B,H,W,C] rows.
+ * vc_im2col3x3_pad: col[(b,oh,ow), c*9+kh*3+kw] of a 3x3 conv with padding pad (0: ConvUnit_NP :19-27,
+ *   1: ConvUnit / Residual units :9-17, :29-62); OH = H + 2 pad - 2; GEMM against weight [O, C*9].
+ * vc_mul2_2d: out = a * b elementwise (Mt = spatial_am(x2) * Fhs, Fss = Fm * Am, :178-183).
+ * vc_pool_scale: out[b,hw,c] = mean_p pooled[b,p,c] * F[b,hw,c] (AdaptiveAvgPool2d(1) of the spectral
+ *   attention map times Fhs, :100-101, :178). */
+VC_API int vc_im2col3x3_pad(int B, int H, int W, int C, int pad, const float* x, long ldx, float* col,
+                            hipStream_t stream);
+VC_API int vc_mul2_2d(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
+                      hipStream_t stream);
+VC_API int vc_pool_scale(int B, int HW, int HWp, int C, const float* pooled, const float* F, long ldf, float* out,
+                         long ldo, hipStream_t stream);
+
 #endif /* VITCNN_H */

@@ -1,0 +1,96 @@
+"""FusAtNet (config 5): forward parity.
+
+CPU: the oracle (oracle/fusat_oracle.py) reproduces the reference module's train-mode logits, its BN
+running-statistic updates and its eval-mode logits (tests/golden/fusat_b4.npz from
+tests/golden/gen_fusat_golden.py); the product module, seeded alike, has the reference's state_dict
+names and initial values (per-tensor sums).
+GPU: the HIP forward (im2col3x3_pad + vc_gemm, BN, pools, products) vs the oracle: logits within
+1e-3 relative (north_star fp32), argmax bit-exact, in train mode (B = 4 golden batch, B = 16) and
+in eval mode after the running statistics were updated.  No backward: the reference's raises.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fusat_oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _golden():
+    return np.load(os.path.join(HERE, "golden", "fusat_b4.npz"))
+
+
+def _seeded():
+    from vitcnn_amd.fusatnet import FusAtNet
+    torch.manual_seed(0)
+    return FusAtNet(144, 1, 16)
+
+
+def _rel(a, b):
+    return float((a - b).norm() / float(b.norm()))
+
+
+def test_fusat_state_dict_and_oracle_match_reference():
+    z = _golden()
+    m = _seeded()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    for k, v in sd.items():
+        if v.is_floating_point():
+            assert abs(float(v.double().sum()) - float(z["s:" + k])) <= 1e-9 * max(1.0, abs(float(z["s:" + k]))), k
+    x1, x2 = torch.from_numpy(z["x1"]), torch.from_numpy(z["x2"])
+    with torch.no_grad():
+        lt = O.forward(sd, x1, x2, train=True)
+        assert _rel(lt, torch.from_numpy(z["logits_train"])) < 1e-5
+        for k, v in sd.items():
+            if "running" in k:
+                assert abs(float(v.double().sum()) - float(z["r:" + k])) <= 1e-4 * max(1.0, abs(float(z["r:" + k]))), k
+        le = O.forward(sd, x1, x2, train=False)
+        assert _rel(le, torch.from_numpy(z["logits_eval"])) < 1e-5
+
+
+def test_fusat_cpu_input_raises():
+    m = _seeded()
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(2, 144, 11, 11), torch.zeros(2, 1, 11, 11))
+
+
+def _gpu(B, seed):
+    m = _seeded()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    if B == 4:
+        z = _golden()
+        x1, x2 = torch.from_numpy(z["x1"]), torch.from_numpy(z["x2"])
+    else:
+        g = torch.Generator().manual_seed(seed)
+        x1, x2 = torch.rand(B, 144, 11, 11, generator=g), torch.rand(B, 1, 11, 11, generator=g)
+    m = m.to("cuda").train()
+    with torch.no_grad():
+        ref_t = O.forward(sd, x1, x2, train=True)
+        ref_e = O.forward(sd, x1, x2, train=False)
+    lt = m(x1.cuda(), x2.cuda()).cpu()
+    m.eval()
+    le = m(x1.cuda(), x2.cuda()).cpu()
+    assert _rel(lt, ref_t) < 1e-3, _rel(lt, ref_t)
+    assert torch.equal(lt.argmax(-1), ref_t.argmax(-1))
+    assert _rel(le, ref_e) < 1e-3, _rel(le, ref_e)
+    assert torch.equal(le.argmax(-1), ref_e.argmax(-1))
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            assert torch.allclose(v.cpu(), sd[k], rtol=1e-3, atol=1e-4), k
+
+
+@pytest.mark.gpu
+def test_fusat_gpu_golden_b4():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _gpu(4, 0)
+
+
+@pytest.mark.gpu
+def test_fusat_gpu_b16():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _gpu(16, 11)

@@ -1,0 +1,95 @@
+// FusAtNet comparison model (config 5), forward: the ops the existing
+// kernels (vc_gemm, vc_bn_*, vc_maxpool2_fwd, vc_add2_2d) do not cover.
+// Reference: model/compare_method/FusAtNet.py (ConvUnit :9-17 3x3 pad 1, ConvUnit_NP :19-27 valid,
+// Spectral_Attention_Module :85-101 maxpool + AdaptiveAvgPool2d(1), FusAtNet.forward :176-184 products).
+// Activations are channels-last [B, H, W, C] rows.
+#include "common.h"
+
+namespace {
+
+// col[(b, oh, ow), c*9 + kh*3 + kw] = x[b, oh + kh - pad, ow + kw - pad, c] (zero outside), OH = H + 2 pad - 2.
+// One thread per (row, c): 9 taps, writes 9 consecutive columns.
+__global__ void im2col3x3_pad(int total, FastDiv fC, FastDiv fOW, FastDiv fOH, int H, int W, int pad,
+                              const float* __restrict__ x, long ldx, float* __restrict__ col) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c, ow, oh;
+  const int row = fdivmod(idx, fC, c);
+  const int r2 = fdivmod(row, fOW, ow);
+  const int b = fdivmod(r2, fOH, oh);
+  const int C = (int)fC.div;
+  float* out = col + (long)row * C * 9 + c * 9;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int ih = oh + kh - pad;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int iw = ow + kw - pad;
+      float v = 0.f;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = x[((long)(b * H + ih) * W + iw) * ldx + c];
+      out[kh * 3 + kw] = v;
+    }
+  }
+}
+
+// out[m, c] = a[m, c] * b[m, c]  (strided rows)
+__global__ void mul2_2d(int total, FastDiv fC, const float* __restrict__ a, long lda, const float* __restrict__ b,
+                        long ldb, float* __restrict__ out, long ldo) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c;
+  const long m = fdivmod(idx, fC, c);
+  out[m * ldo + c] = a[m * lda + c] * b[m * ldb + c];
+}
+
+// out[b, hw, c] = mean_{p < HWp} pooled[b, p, c] * F[b, hw, c]   (AdaptiveAvgPool2d(1) then broadcast product)
+__global__ void pool_scale(int total, FastDiv fC, FastDiv fHW, int HWp, const float* __restrict__ pooled,
+                           const float* __restrict__ F, long ldf, float* __restrict__ out, long ldo) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c, hw;
+  const int m = fdivmod(idx, fC, c);
+  const int b = fdivmod(m, fHW, hw);
+  const int C = (int)fC.div;
+  float s = 0.f;
+  for (int p = 0; p < HWp; ++p) s += pooled[((long)b * HWp + p) * C + c];
+  out[(long)m * ldo + c] = (s / (float)HWp) * F[(long)m * ldf + c];
+}
+
+}  // namespace
+
+VC_API int vc_im2col3x3_pad(int B, int H, int W, int C, int pad, const float* x, long ldx, float* col,
+                            hipStream_t stream) {
+  VC_REQUIRE(B > 0 && C > 0 && (pad == 0 || pad == 1) && ldx >= C);
+  const int OH = H + 2 * pad - 2, OW = W + 2 * pad - 2;
+  VC_REQUIRE(OH > 0 && OW > 0);
+  const long total = (long)B * OH * OW * C;
+  VC_REQUIRE_I32(total);
+  VC_REQUIRE_I32(total * 9);
+  hipLaunchKernelGGL(im2col3x3_pad, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
+                     make_fastdiv(OW), make_fastdiv(OH), H, W, pad, x, ldx, col);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_mul2_2d(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
+                      hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && C > 0);
+  if (M == 0) return VC_OK;
+  VC_REQUIRE_I32(M * C);
+  hipLaunchKernelGGL(mul2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C), a, lda,
+                     b, ldb, out, ldo);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_pool_scale(int B, int HW, int HWp, int C, const float* pooled, const float* F, long ldf, float* out,
+                         long ldo, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && HW > 0 && HWp > 0 && C > 0);
+  const long total = (long)B * HW * C;
+  VC_REQUIRE_I32(total);
+  hipLaunchKernelGGL(pool_scale, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
+                     make_fastdiv(HW), HWp, pooled, F, ldf, out, ldo);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}

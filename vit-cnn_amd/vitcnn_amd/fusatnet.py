@@ -1,0 +1,270 @@
+"""FusAtNet comparison model (config 5): forward on the MI355X path.
+
+Reference: `model/compare_method/FusAtNet.py` (`FusAtNet` :168-186), built by `model_utils.py:109-118`
+(patch 11, Adam lr 1e-3).  The module keeps the reference's parameter tree and state_dict names.
+Forward (train-mode BatchNorm with running-stat updates, or eval-mode) is a program of HIP kernels
+over channels-last [B, H, W, C] rows: every 3x3 conv is `vc_im2col3x3_pad` + `vc_gemm` (bias fused),
+BatchNorm `vc_bn_stats` + `vc_bn_apply` (ReLU fused), residual adds `vc_add2_2d`, pools
+`vc_maxpool2_fwd` / `vc_pool_scale`, products `vc_mul2_2d`, the concatenation is written in place.
+
+Backward: not provided.  The reference's own backward raises (the in-place `x += identity` on a
+saved ReLU output, :44, :61), so the pinned behaviour is the forward; the
+logits returned here carry no autograd graph, and `loss.backward()` raises RuntimeError as the
+reference's does.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ._lib import lib
+
+F32 = 4
+BN_EPS, BN_MOMENTUM = 1e-5, 0.1
+
+
+class ConvUnit(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, kernel_size=3, padding=1, bias=True)
+        self.bn = nn.BatchNorm2d(cout)
+        self.activation = nn.ReLU()
+
+
+class ConvUnit_NP(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, kernel_size=3, bias=True)
+        self.bn = nn.BatchNorm2d(cout)
+        self.activation = nn.ReLU()
+
+
+class Residual_Unit1(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, kernel_size=3, padding=1, bias=True)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, kernel_size=3, padding=1, bias=True)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.activation = nn.ReLU()
+        self.max_pool = nn.MaxPool2d(kernel_size=2, stride=2)
+
+
+class Residual_Unit2(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, kernel_size=3, padding=1, bias=True)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, kernel_size=3, padding=1, bias=True)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.activation = nn.ReLU()
+
+
+class _SixConv(nn.Module):
+    """Hyper_Feature_Extractor / Modality_Feature_Extractor (:64-83, :103-122)"""
+
+    def __init__(self, cin, cout=1024):
+        super().__init__()
+        self.conv1 = ConvUnit(cin, 256)
+        self.conv2 = ConvUnit(256, 256)
+        self.conv3 = ConvUnit(256, 256)
+        self.conv4 = ConvUnit(256, 256)
+        self.conv5 = ConvUnit(256, 256)
+        self.conv6 = ConvUnit(256, cout)
+
+
+class Hyper_Feature_Extractor(_SixConv):
+    pass
+
+
+class Modality_Feature_Extractor(_SixConv):
+    pass
+
+
+class Spectral_Attention_Module(nn.Module):
+    def __init__(self, cin, cout=1024):
+        super().__init__()
+        self.res1 = Residual_Unit1(cin, 256)
+        self.res2 = Residual_Unit1(256, 256)
+        self.conv1 = ConvUnit(256, 256)
+        self.conv2 = ConvUnit(256, cout)
+        self.max_pool = nn.MaxPool2d(kernel_size=2, stride=2)
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+
+
+class _ResAttention(nn.Module):
+    """Spatial_Attention_module / Modality_Attention_Module (:103-117, :124-138)"""
+
+    def __init__(self, cin, cout=1024):
+        super().__init__()
+        self.res1 = Residual_Unit2(cin, 128)
+        self.res2 = Residual_Unit2(128, 256)
+        self.conv1 = ConvUnit(256, 256)
+        self.conv2 = ConvUnit(256, cout)
+
+
+class Spatial_Attention_module(_ResAttention):
+    pass
+
+
+class Modality_Attention_Module(_ResAttention):
+    pass
+
+
+class Classification_Module(nn.Module):
+    def __init__(self, cin, num_classes):
+        super().__init__()
+        self.conv1 = ConvUnit_NP(cin, 256)
+        self.conv2 = ConvUnit_NP(256, 256)
+        self.conv3 = ConvUnit_NP(256, 256)
+        self.conv4 = ConvUnit_NP(256, 256)
+        self.conv5 = ConvUnit_NP(256, 1024)
+        self.conv6 = nn.Conv2d(1024, num_classes, kernel_size=1, bias=True)
+
+
+class FusAtNet(nn.Module):
+    """Same constructor as the reference (FusAtNet.py:168-176); forward(x1 [B,C1,P,P], x2 [B,C2,P,P])."""
+
+    def __init__(self, input_channels, input_channels2, num_classes):
+        super().__init__()
+        self.hfe = Hyper_Feature_Extractor(input_channels, 1024)
+        self.spectral_am = Spectral_Attention_Module(input_channels, 1024)
+        self.spatial_am = Spatial_Attention_module(input_channels2, 1024)
+        self.mfe = Modality_Feature_Extractor(1024 * 2 + input_channels + input_channels2, 1024)
+        self.mam = Modality_Attention_Module(1024 * 2 + input_channels + input_channels2, 1024)
+        self.cm = Classification_Module(1024, num_classes)
+        self.c1, self.c2, self.ncls = input_channels, input_channels2, num_classes
+
+    def forward(self, x1: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+        if x1.device.type != "cuda":
+            raise RuntimeError("FusAtNet MI355X path: inputs must be on a ROCm (cuda) device; no CPU fallback")
+        if x1.dim() != 4 or x1.shape[1] != self.c1 or x1.shape[2] != x1.shape[3]:
+            raise RuntimeError(f"expected x1 [B, {self.c1}, P, P], got {list(x1.shape)}")
+        if x2.dim() != 4 or x2.shape[0] != x1.shape[0] or x2.shape[1] != self.c2 or x2.shape[2:] != x1.shape[2:]:
+            raise RuntimeError(f"expected x2 [B, {self.c2}, P, P] matching x1, got {list(x2.shape)}")
+        if x1.shape[2] < 11:
+            raise RuntimeError("FusAtNet needs patch >= 11 (five valid 3x3 convs + two 2x2 pools)")
+        with torch.no_grad():
+            return _Program(self, x1.detach().float().contiguous(), x2.detach().float().contiguous()).run()
+
+
+class _Program:
+    SCRATCH = 1 << 22
+
+    def __init__(self, m: FusAtNet, x1, x2):
+        self.m, self.L, self.dev = m, lib(), x1.device
+        self.s = torch.cuda.current_stream(self.dev).cuda_stream
+        self.B, self.P = x1.shape[0], x1.shape[2]
+        self.x1, self.x2 = x1, x2
+        self.scr = torch.empty(self.SCRATCH, dtype=torch.float32, device=self.dev)
+        self.train = m.training
+
+    def new(self, *shape):
+        return torch.empty(*shape, dtype=torch.float32, device=self.dev)
+
+    def nhwc(self, x):
+        B, C, H, W = x.shape
+        y = self.new(B, H, W, C)
+        self.L.vc_nchw_to_nhwc(B, C, H * W, x.data_ptr(), y.data_ptr(), self.s)
+        return y
+
+    def conv3(self, x, ldx, H, C, conv, pad):
+        """x [B,H,H,C] rows (ld ldx) -> conv3x3 + bias, [B,OH,OH,O] contiguous"""
+        B, O = self.B, conv.out_channels
+        OH = H + 2 * pad - 2
+        M, K = B * OH * OH, C * 9
+        col = self.new(M, K)
+        self.L.vc_im2col3x3_pad(B, H, H, C, pad, x.data_ptr(), ldx, col.data_ptr(), self.s)
+        y = self.new(B, OH, OH, O)
+        self.L.vc_gemm(0, 1, M, O, K, 1.0, col.data_ptr(), K, 0, conv.weight.data_ptr(), K, 0, 0.0, y.data_ptr(), O, 0,
+                       1, conv.bias.data_ptr(), None, 0, 0, 0, None, self.scr.data_ptr(), self.SCRATCH, self.s)
+        del col
+        return y, OH
+
+    def bn_relu(self, y, M, C, bn, relu=1):
+        mean, invstd = self.new(C), self.new(C)
+        self.L.vc_bn_stats(1 if self.train else 0, M, C, y.data_ptr(), C, bn.eps, bn.momentum if bn.momentum is not None
+                           else BN_MOMENTUM, mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(),
+                           bn.running_var.data_ptr(), self.scr.data_ptr(), self.SCRATCH, self.s)
+        if self.train:
+            bn.num_batches_tracked.add_(1)
+        self.L.vc_bn_apply(M, C, y.data_ptr(), C, mean.data_ptr(), invstd.data_ptr(), bn.weight.data_ptr(),
+                           bn.bias.data_ptr(), relu, y.data_ptr(), C, self.s)
+        return y
+
+    def unit(self, x, ldx, H, C, u, pad=1):
+        y, OH = self.conv3(x, ldx, H, C, u.conv, pad)
+        return self.bn_relu(y, self.B * OH * OH, u.conv.out_channels, u.bn), OH
+
+    def residual(self, x, ldx, H, C, r, pool):
+        a, _ = self.conv3(x, ldx, H, C, r.conv1, 1)
+        O = r.conv1.out_channels
+        M = self.B * H * H
+        self.bn_relu(a, M, O, r.bn1)
+        b, _ = self.conv3(a, O, H, O, r.conv2, 1)
+        self.bn_relu(b, M, O, r.bn2)
+        self.L.vc_add2_2d(M, O, b.data_ptr(), O, a.data_ptr(), O, b.data_ptr(), O, 0.0, self.s)  # x += identity
+        if not pool:
+            return b, H
+        return self.maxpool(b, H, O), H // 2
+
+    def maxpool(self, x, H, C):
+        y = self.new(self.B, H // 2, H // 2, C)
+        arg = torch.empty(y.numel(), dtype=torch.uint8, device=self.dev)
+        self.L.vc_maxpool2_fwd(self.B, H, H, C, x.data_ptr(), C, y.data_ptr(), arg.data_ptr(), self.s)
+        return y
+
+    def six(self, x, ldx, H, C, mod):
+        for u in (mod.conv1, mod.conv2, mod.conv3, mod.conv4, mod.conv5, mod.conv6):
+            x, _ = self.unit(x, ldx, H, C, u)
+            C = ldx = u.conv.out_channels
+        return x
+
+    def res_attention(self, x, ldx, H, C, mod):
+        x, _ = self.residual(x, ldx, H, C, mod.res1, False)
+        x, _ = self.residual(x, 128, H, 128, mod.res2, False)
+        x, _ = self.unit(x, 256, H, 256, mod.conv1)
+        x, _ = self.unit(x, 256, H, 256, mod.conv2)
+        return x
+
+    def run(self):
+        m, L, B, P = self.m, self.L, self.B, self.P
+        c1, c2 = m.c1, m.c2
+        x1, x2 = self.nhwc(self.x1), self.nhwc(self.x2)
+        HW = P * P
+        M = B * HW
+        Fhs = self.six(x1, c1, P, c1, m.hfe)                                  # [B,P,P,1024]
+        # spectral attention: two pooled residual units, two units, maxpool, global average
+        sa = m.spectral_am
+        t, H = self.residual(x1, c1, P, c1, sa.res1, True)
+        t, H = self.residual(t, 256, H, 256, sa.res2, True)
+        t, _ = self.unit(t, 256, H, 256, sa.conv1)
+        t, _ = self.unit(t, 256, H, 256, sa.conv2)
+        t = self.maxpool(t, H, 1024)
+        Hp = H // 2
+        Ct = c1 + c2 + 2048
+        cat = self.new(B, P, P, Ct)                                           # cat([x1, x2, Ms, Mt], 1)
+        L.vc_add2_2d(M, c1, x1.data_ptr(), c1, None, 0, cat.data_ptr(), Ct, 0.0, self.s)
+        L.vc_add2_2d(M, c2, x2.data_ptr(), c2, None, 0, cat.data_ptr() + F32 * c1, Ct, 0.0, self.s)
+        L.vc_pool_scale(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024, cat.data_ptr() + F32 * (c1 + c2), Ct,
+                        self.s)                                               # Ms
+        Sp = self.res_attention(x2, c2, P, c2, m.spatial_am)
+        L.vc_mul2_2d(M, 1024, Sp.data_ptr(), 1024, Fhs.data_ptr(), 1024, cat.data_ptr() + F32 * (c1 + c2 + 1024), Ct,
+                     self.s)                                                  # Mt
+        del Sp, Fhs, t
+        Fm = self.six(cat, Ct, P, Ct, m.mfe)
+        Am = self.res_attention(cat, Ct, P, Ct, m.mam)
+        del cat
+        L.vc_mul2_2d(M, 1024, Fm.data_ptr(), 1024, Am.data_ptr(), 1024, Fm.data_ptr(), 1024, self.s)  # Fss
+        x, H, C = Fm, P, 1024
+        for u in (m.cm.conv1, m.cm.conv2, m.cm.conv3, m.cm.conv4, m.cm.conv5):
+            x, H = self.unit(x, C, H, C, u, pad=0)
+            C = u.conv.out_channels
+        Mo = B * H * H
+        logits = self.new(Mo, m.ncls)
+        L.vc_gemm(0, 1, Mo, m.ncls, C, 1.0, x.data_ptr(), C, 0, m.cm.conv6.weight.data_ptr(), C, 0, 0.0,
+                  logits.data_ptr(), m.ncls, 0, 1, m.cm.conv6.bias.data_ptr(), None, 0, 0, 0, None,
+                  self.scr.data_ptr(), self.SCRATCH, self.s)
+        if H == 1:
+            return logits.view(B, m.ncls).squeeze()                          # torch.squeeze (:165)
+        return logits.view(B, H, H, m.ncls).permute(0, 3, 1, 2).squeeze()
