@@ -278,6 +278,47 @@ def s2eft_leg(dev, steps, cpu_steps):
     return out
 
 
+FUSAT_GFLOP_PER_PATCH = 6.92  # SURVEY.md section 8(d), FusAtNet forward
+
+
+def fusat_leg(dev, steps, cpu):
+    """Config 5: FusAtNet train-mode forward (batch-statistics BN with
+    running-stat updates) at B = 64 on [64,144,11,11] + [64,1,11,11]; forward only (the reference's
+    backward raises).  CPU baseline: oracle/fusat_oracle.py forward at B = 4."""
+    from vitcnn_amd.fusatnet import FusAtNet
+    torch.manual_seed(0)
+    m = FusAtNet(144, 1, 16).to(dev).train()
+    g = torch.Generator().manual_seed(3)
+    x1, x2 = torch.rand(64, 144, 11, 11, generator=g), torch.rand(64, 1, 11, 11, generator=g)
+    a, b = x1.to(dev), x2.to(dev)
+    for _ in range(2):
+        m(a, b)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m(a, b)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    tf = 64 / ms * 1e3 * FUSAT_GFLOP_PER_PATCH * 1e-3
+    out = {"workload": "FusAtNet train-mode forward, [64,144,11,11] + [64,1,11,11], 16 classes",
+           "value": round(64 / ms * 1e3, 1), "unit": "patches/s (forward)", "ms_per_batch": round(ms, 3),
+           "dtype": "fp32", "achieved_tflops": round(tf, 2),
+           "mfma_frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4)}
+    if cpu:
+        from oracle import fusat_oracle as O
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        with torch.no_grad():
+            O.forward(sd, x1[:4], x2[:4])
+            t0 = time.perf_counter()
+            O.forward(sd, x1[:4], x2[:4])
+            dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(4 / dt, 2), "unit": "patches/s (forward)", "cores": threads,
+                               "kind": "port", "sample": "1 B=4 train-mode forward of oracle/fusat_oracle.py"}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -407,6 +448,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.cpu_steps)
     if world == 1 and not args.no_s2eft:
         out["config5_s2eft"] = s2eft_leg(dev, min(args.steps, 50), 0 if args.no_cpu_baseline else 5)
+        out["config5_fusatnet"] = fusat_leg(dev, 5, not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -10,7 +10,8 @@ replaces, so `main.py`-style drivers switch by changing one import:
 * `test(run, net, img1, img2, hyperparams) -> probs[W, H, n_classes]` — :1067-1132.
 * `val(net, data_loader, device, supervision) -> accuracy` — :1135-1158.
 
-Registered: "Multimodality_Mamba" (the README's "ViT-CNN (ours)") and "S2EFT" (config 5, :400-423).
+Registered: "Multimodality_Mamba" (the README's "ViT-CNN (ours)"), "S2EFT" (config 5, :400-423) and
+"FusAtNet" (config 5, :109-118, forward only).
 The reference's other branches import modules absent from the reference tree (SURVEY.md section 2a
 row 22) and are out of scope for this path.
 
@@ -35,7 +36,7 @@ from .model import Multimodality_Mamba
 from .optim import AdamW
 from .window import SlidingWindowInference
 
-REGISTERED = ("Multimodality_Mamba", "S2EFT")
+REGISTERED = ("Multimodality_Mamba", "S2EFT", "FusAtNet")
 
 
 def camel_to_snake(name: str) -> str:
@@ -62,6 +63,8 @@ def get_model(name, **kwargs):
     weights = kwargs.setdefault("weights", weights)
     if name == "S2EFT":
         return _get_s2eft(n_bands, n_classes, device, kwargs)
+    if name == "FusAtNet":
+        return _get_fusatnet(n_bands, n_bands2, n_classes, device, kwargs)
     kwargs.setdefault("patch_size", 9)
     patch_size = kwargs["patch_size"]
     center_pixel = True
@@ -105,6 +108,25 @@ def _get_s2eft(n_bands, n_classes, device, kwargs):
     criterion = CrossEntropyLoss(weight=kwargs["weights"])
     kwargs.setdefault("epoch", 600)
     kwargs.setdefault("batch_size", 64)
+    kwargs.setdefault("supervision", "full")
+    kwargs["center_pixel"] = True
+    return model, optimizer, criterion, kwargs
+
+
+def _get_fusatnet(n_bands, n_bands2, n_classes, device, kwargs):
+    """FusAtNet branch of model_utils.py:109-118: FusAtNet(n_bands, n_bands2, n_classes), patch 11,
+    torch.optim.Adam(lr 1e-3) as in the reference, weighted CE, epoch 150, batch 64, applyPCA False.
+    Forward only on this path (the reference's backward raises), so no gradient
+    ever reaches the optimizer."""
+    from .fusatnet import FusAtNet
+    kwargs.setdefault("patch_size", 11)
+    model = FusAtNet(n_bands, n_bands2, n_classes).to(device)
+    lr = kwargs.setdefault("lr", 0.001)
+    optimizer = torch.optim.Adam(model.parameters(), lr=lr)
+    criterion = CrossEntropyLoss(weight=kwargs["weights"])
+    kwargs.setdefault("epoch", 150)
+    kwargs.setdefault("batch_size", 64)
+    kwargs.setdefault("applyPCA", False)
     kwargs.setdefault("supervision", "full")
     kwargs["center_pixel"] = True
     return model, optimizer, criterion, kwargs
