@@ -279,5 +279,12 @@ VC_API int vc_mul2_2d(long M, int C, const float* a, long lda, const float* b, l
                       hipStream_t stream);
 VC_API int vc_pool_scale(int B, int HW, int HWp, int C, const float* pooled, const float* F, long ldf, float* out,
                          long ldo, hipStream_t stream);
+/* backward (out-of-place residual semantics): gradient of vc_im2col3x3_pad
+ * (gather form; dx rows of ld lddx, overwritten or accumulated), and of vc_pool_scale
+ * (dF += mean_p(pooled) * dout; dpooled[b,p,c] = sum_hw dout*F / HWp). */
+VC_API int vc_col2im3x3_pad(int B, int H, int W, int C, int pad, const float* dcol, float* dx, long lddx,
+                            int accumulate, hipStream_t stream);
+VC_API int vc_pool_scale_bwd(int B, int HW, int HWp, int C, const float* pooled, const float* F, long ldf,
+                             const float* dout, long lddo, float* dF, long lddf, float* dpooled, hipStream_t stream);
 
 #endif /* VITCNN_H */

@@ -6,7 +6,9 @@ tests/golden/gen_fusat_golden.py); the product module, seeded alike, has the ref
 names and initial values (per-tensor sums).
 GPU: the HIP forward (im2col3x3_pad + vc_gemm, BN, pools, products) vs the oracle: logits within
 1e-3 relative (north_star fp32), argmax bit-exact, in train mode (B = 4 golden batch, B = 16) and
-in eval mode after the running statistics were updated.  No backward: the reference's raises.
+in eval mode after the running statistics were updated; and the backward (out-of-place residual
+semantics, the reference's own autograd raises) against torch autograd over the oracle: every
+parameter gradient within 1e-3 of its norm (+1e-5 of the largest).
 """
 import os
 
@@ -94,3 +96,31 @@ def test_fusat_gpu_b16():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _gpu(16, 11)
+
+
+@pytest.mark.gpu
+def test_fusat_gpu_backward_b4():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vitcnn_amd.losses import CrossEntropyLoss
+    z = _golden()
+    m = _seeded()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x1, x2 = torch.from_numpy(z["x1"]), torch.from_numpy(z["x2"])
+    t = torch.tensor([3, 7, 1, 12])
+    w = torch.ones(16)
+    w[0] = 0
+    params = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    ref = O.forward(params, x1, x2, train=True)
+    torch.nn.functional.cross_entropy(ref, t, weight=w).backward()
+    m = m.to("cuda").train()
+    logits = m(x1.cuda(), x2.cuda())
+    loss = CrossEntropyLoss(weight=w.cuda())(logits, t.cuda())
+    loss.backward()
+    assert _rel(logits.detach().cpu(), ref.detach()) < 1e-3
+    named = dict(m.named_parameters())
+    gmax = max(float(params[k].grad.norm()) for k in named)
+    for k, p in named.items():
+        g = params[k].grad
+        err = float((p.grad.cpu() - g).norm())
+        assert err <= 1e-3 * float(g.norm()) + 1e-5 * gmax, (k, err, float(g.norm()))

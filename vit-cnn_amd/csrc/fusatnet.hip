@@ -56,7 +56,74 @@ __global__ void pool_scale(int total, FastDiv fC, FastDiv fHW, int HWp, const fl
   out[(long)m * ldo + c] = (s / (float)HWp) * F[(long)m * ldf + c];
 }
 
+// gradient of im2col3x3_pad, gather form: dx[b, ih, iw, c] (= or +=) sum over taps of dcol
+__global__ void col2im3x3_pad(int total, FastDiv fC, FastDiv fW, FastDiv fH, int pad, const float* __restrict__ dcol,
+                              float* __restrict__ dx, long lddx, int accumulate) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int c, iw, ih;
+  const int p = fdivmod(idx, fC, c);
+  const int q = fdivmod(p, fW, iw);
+  const int b = fdivmod(q, fH, ih);
+  const int C = (int)fC.div, H = (int)fH.div, W = (int)fW.div;
+  const int OH = H + 2 * pad - 2, OW = W + 2 * pad - 2;
+  float v = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int oh = ih - kh + pad;
+    if (oh < 0 || oh >= OH) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int ow = iw - kw + pad;
+      if (ow < 0 || ow >= OW) continue;
+      v += dcol[((long)(b * OH + oh) * OW + ow) * C * 9 + c * 9 + kh * 3 + kw];
+    }
+  }
+  float* o = dx + (long)p * lddx + c;
+  *o = accumulate ? *o + v : v;
+}
+
+// backward of pool_scale: one thread per (b, c): s = mean_p pooled; dF (+)= s * dout; dpooled = sum_hw dout*F / HWp
+__global__ void pool_scale_bwd(int B, int HW, int HWp, int C, const float* __restrict__ pooled,
+                               const float* __restrict__ F, long ldf, const float* __restrict__ dout, long lddo,
+                               float* __restrict__ dF, long lddf, float* __restrict__ dpooled) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * C) return;
+  const int b = idx / C, c = idx % C;
+  float s = 0.f;
+  for (int p = 0; p < HWp; ++p) s += pooled[((long)b * HWp + p) * C + c];
+  s /= (float)HWp;
+  float ds = 0.f;
+  for (int hw = 0; hw < HW; ++hw) {
+    const long m = (long)b * HW + hw;
+    const float g = dout[m * lddo + c];
+    ds += g * F[m * ldf + c];
+    dF[m * lddf + c] += s * g;
+  }
+  for (int p = 0; p < HWp; ++p) dpooled[((long)b * HWp + p) * C + c] = ds / (float)HWp;
+}
+
 }  // namespace
+
+VC_API int vc_col2im3x3_pad(int B, int H, int W, int C, int pad, const float* dcol, float* dx, long lddx,
+                            int accumulate, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && C > 0 && (pad == 0 || pad == 1) && lddx >= C && H + 2 * pad - 2 > 0 && W + 2 * pad - 2 > 0);
+  const long total = (long)B * H * W * C;
+  VC_REQUIRE_I32(total);
+  hipLaunchKernelGGL(col2im3x3_pad, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
+                     make_fastdiv(W), make_fastdiv(H), pad, dcol, dx, lddx, accumulate);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_pool_scale_bwd(int B, int HW, int HWp, int C, const float* pooled, const float* F, long ldf,
+                             const float* dout, long lddo, float* dF, long lddf, float* dpooled, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && HW > 0 && HWp > 0 && C > 0);
+  hipLaunchKernelGGL(pool_scale_bwd, dim3(vc_cdiv((long)B * C, 256)), dim3(256), 0, stream, B, HW, HWp, C, pooled, F,
+                     ldf, dout, lddo, dF, lddf, dpooled);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
 
 VC_API int vc_im2col3x3_pad(int B, int H, int W, int C, int pad, const float* x, long ldx, float* col,
                             hipStream_t stream) {

@@ -1,4 +1,4 @@
-"""FusAtNet comparison model (config 5): forward on the MI355X path.
+"""FusAtNet comparison model (config 5) on the MI355X path.
 
 Reference: `model/compare_method/FusAtNet.py` (`FusAtNet` :168-186), built by `model_utils.py:109-118`
 (patch 11, Adam lr 1e-3).  The module keeps the reference's parameter tree and state_dict names.
@@ -7,10 +7,11 @@ over channels-last [B, H, W, C] rows: every 3x3 conv is `vc_im2col3x3_pad` + `vc
 BatchNorm `vc_bn_stats` + `vc_bn_apply` (ReLU fused), residual adds `vc_add2_2d`, pools
 `vc_maxpool2_fwd` / `vc_pool_scale`, products `vc_mul2_2d`, the concatenation is written in place.
 
-Backward: not provided.  The reference's own backward raises (the in-place `x += identity` on a
-saved ReLU output, :44, :61), so the pinned behaviour is the forward; the
-logits returned here carry no autograd graph, and `loss.backward()` raises RuntimeError as the
-reference's does.
+Backward: the reference's own autograd raises (the in-place `x += identity` on a saved ReLU output,
+:44, :61).  This path defines the out-of-place semantics (`b = relu(bn2(conv2(a)))
++ a`) and runs a hand-written backward over a tape of the forward's ops (conv: wgrad GEMM with the
+bias gradient fused, dgrad GEMM + `vc_col2im3x3_pad`; `vc_bn_bwd` with the ReLU mask; maxpool,
+pooled-scale and product backwards); parameter gradients land in `.grad` for the reference's Adam.
 """
 from __future__ import annotations
 
@@ -144,29 +145,80 @@ class FusAtNet(nn.Module):
             raise RuntimeError(f"expected x2 [B, {self.c2}, P, P] matching x1, got {list(x2.shape)}")
         if x1.shape[2] < 11:
             raise RuntimeError("FusAtNet needs patch >= 11 (five valid 3x3 convs + two 2x2 pools)")
+        x1 = x1.detach().float().contiguous()
+        x2 = x2.detach().float().contiguous()
+        params = [p for _, p in self.named_parameters()]
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _FusAtNetFunction.apply(self, x1, x2, *params)
         with torch.no_grad():
-            return _Program(self, x1.detach().float().contiguous(), x2.detach().float().contiguous()).run()
+            return _Program(self, x1, x2, False).run()
+
+
+class _FusAtNetFunction(torch.autograd.Function):
+    """Backward with out-of-place residual semantics (`b = relu(bn2(conv2(a))) + a`): the gradient the
+    reference's code would have if its in-place `x += identity` (FusAtNet.py:44, :61) were written
+    out of place -- the reference's own autograd raises there."""
+
+    @staticmethod
+    def forward(ctx, model, x1, x2, *params):
+        prog = _Program(model, x1, x2, True)
+        logits = prog.run()
+        ctx.prog = prog
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        grads = ctx.prog.backward(dlogits.detach().float().contiguous())
+        ctx.prog = None
+        return (None, None, None, *grads)
 
 
 class _Program:
     SCRATCH = 1 << 22
 
-    def __init__(self, m: FusAtNet, x1, x2):
+    def __init__(self, m: FusAtNet, x1, x2, grad: bool):
         self.m, self.L, self.dev = m, lib(), x1.device
         self.s = torch.cuda.current_stream(self.dev).cuda_stream
         self.B, self.P = x1.shape[0], x1.shape[2]
         self.x1, self.x2 = x1, x2
         self.scr = torch.empty(self.SCRATCH, dtype=torch.float32, device=self.dev)
         self.train = m.training
+        self.grad = grad
+        self.tape = []        # backward closures, run in reverse
+        self.g = {}           # id(activation) -> gradient buffer (zero-initialised on first use)
+        self.keep = {}        # id -> activation (keeps ids unique while the tape lives)
+        self.no_grad_ids = set()
 
     def new(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)
+
+    def grad_of(self, t):
+        k = id(t)
+        if k not in self.g:
+            buf = self.new(t.numel())
+            self.L.vc_fill(t.numel(), buf.data_ptr(), 0.0, self.s)
+            self.g[k] = buf
+        return self.g[k]
+
+    def record(self, fn, *acts):
+        if self.grad:
+            for a in acts:
+                self.keep[id(a)] = a
+            self.tape.append(fn)
+
+    def add_into(self, dst, src, M, C, ld_dst=None):
+        self.L.vc_add2_2d(M, C, src.data_ptr(), C, None, 0, dst.data_ptr(), ld_dst or C, 1.0, self.s)
 
     def nhwc(self, x):
         B, C, H, W = x.shape
         y = self.new(B, H, W, C)
         self.L.vc_nchw_to_nhwc(B, C, H * W, x.data_ptr(), y.data_ptr(), self.s)
+        self.no_grad_ids.add(id(y))
         return y
+
+    def gemm(self, tA, tB, M, N, K, A, lda, Bm, ldb, beta, C, ldc, bias=None, bias_grad=None):
+        self.L.vc_gemm(tA, tB, M, N, K, 1.0, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, bias, None, 0, 0, 0, bias_grad,
+                       self.scr.data_ptr(), self.SCRATCH, self.s)
 
     def conv3(self, x, ldx, H, C, conv, pad):
         """x [B,H,H,C] rows (ld ldx) -> conv3x3 + bias, [B,OH,OH,O] contiguous"""
@@ -176,9 +228,23 @@ class _Program:
         col = self.new(M, K)
         self.L.vc_im2col3x3_pad(B, H, H, C, pad, x.data_ptr(), ldx, col.data_ptr(), self.s)
         y = self.new(B, OH, OH, O)
-        self.L.vc_gemm(0, 1, M, O, K, 1.0, col.data_ptr(), K, 0, conv.weight.data_ptr(), K, 0, 0.0, y.data_ptr(), O, 0,
-                       1, conv.bias.data_ptr(), None, 0, 0, 0, None, self.scr.data_ptr(), self.SCRATCH, self.s)
+        self.gemm(0, 1, M, O, K, col.data_ptr(), K, conv.weight.data_ptr(), K, 0.0, y.data_ptr(), O,
+                  bias=conv.bias.data_ptr())
         del col
+
+        def bwd():
+            dy = self.grad_of(y)
+            colr = self.new(M, K)   # recomputed: cheaper than keeping every im2col matrix
+            self.L.vc_im2col3x3_pad(B, H, H, C, pad, x.data_ptr(), ldx, colr.data_ptr(), self.s)
+            self.gemm(1, 0, O, K, M, dy.data_ptr(), O, colr.data_ptr(), K, 0.0, self.pgrad(conv.weight), K,
+                      bias_grad=self.pgrad(conv.bias))
+            if id(x) in self.no_grad_ids:
+                return
+            dcol = colr
+            self.gemm(0, 0, M, K, O, dy.data_ptr(), O, conv.weight.data_ptr(), K, 0.0, dcol.data_ptr(), K)
+            self.L.vc_col2im3x3_pad(B, H, H, C, pad, dcol.data_ptr(), self.grad_of(x).data_ptr(), ldx, 1, self.s)
+
+        self.record(bwd, x, y)
         return y, OH
 
     def bn_relu(self, y, M, C, bn, relu=1):
@@ -188,9 +254,24 @@ class _Program:
                            bn.running_var.data_ptr(), self.scr.data_ptr(), self.SCRATCH, self.s)
         if self.train:
             bn.num_batches_tracked.add_(1)
+        z = self.new(*y.shape) if self.grad else y
         self.L.vc_bn_apply(M, C, y.data_ptr(), C, mean.data_ptr(), invstd.data_ptr(), bn.weight.data_ptr(),
-                           bn.bias.data_ptr(), relu, y.data_ptr(), C, self.s)
-        return y
+                           bn.bias.data_ptr(), relu, z.data_ptr(), C, self.s)
+
+        def bwd():
+            self.L.vc_bn_bwd(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
+                             z.data_ptr() if relu else None, C, mean.data_ptr(), invstd.data_ptr(),
+                             bn.weight.data_ptr(), self.grad_of(y).data_ptr(), C, 1.0, self.pgrad(bn.weight),
+                             self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.s)
+
+        self.record(bwd, y, z)
+        return z
+
+    def pgrad(self, p):
+        g = self.pg.get(id(p))
+        if g is None:
+            g = self.pg[id(p)] = torch.empty_like(p)
+        return g.data_ptr()
 
     def unit(self, x, ldx, H, C, u, pad=1):
         y, OH = self.conv3(x, ldx, H, C, u.conv, pad)
@@ -200,19 +281,49 @@ class _Program:
         a, _ = self.conv3(x, ldx, H, C, r.conv1, 1)
         O = r.conv1.out_channels
         M = self.B * H * H
-        self.bn_relu(a, M, O, r.bn1)
+        a = self.bn_relu(a, M, O, r.bn1)
         b, _ = self.conv3(a, O, H, O, r.conv2, 1)
-        self.bn_relu(b, M, O, r.bn2)
-        self.L.vc_add2_2d(M, O, b.data_ptr(), O, a.data_ptr(), O, b.data_ptr(), O, 0.0, self.s)  # x += identity
+        b = self.bn_relu(b, M, O, r.bn2)
+        out = self.new(*b.shape) if self.grad else b
+        self.L.vc_add2_2d(M, O, b.data_ptr(), O, a.data_ptr(), O, out.data_ptr(), O, 0.0, self.s)  # x += identity
+
+        def bwd():
+            d = self.grad_of(out)
+            self.add_into(self.grad_of(b), d, M, O)
+            self.add_into(self.grad_of(a), d, M, O)
+
+        self.record(bwd, a, b, out)
         if not pool:
-            return b, H
-        return self.maxpool(b, H, O), H // 2
+            return out, H
+        return self.maxpool(out, H, O), H // 2
 
     def maxpool(self, x, H, C):
         y = self.new(self.B, H // 2, H // 2, C)
         arg = torch.empty(y.numel(), dtype=torch.uint8, device=self.dev)
         self.L.vc_maxpool2_fwd(self.B, H, H, C, x.data_ptr(), C, y.data_ptr(), arg.data_ptr(), self.s)
+
+        def bwd():
+            tmp = self.new(x.numel())
+            self.L.vc_maxpool2_bwd(self.B, H, H, C, self.grad_of(y).data_ptr(), arg.data_ptr(), tmp.data_ptr(), C,
+                                   self.s)
+            self.add_into(self.grad_of(x), tmp, self.B * H * H, C)
+
+        self.record(bwd, x, y, arg)
         return y
+
+    def mul(self, a, b, M, C, out, ldo, dout_of):
+        """out (ld ldo) = a * b; dout_of() gives (gradient pointer, ld) of out at backward time"""
+        self.L.vc_mul2_2d(M, C, a.data_ptr(), C, b.data_ptr(), C, out, ldo, self.s)
+
+        def bwd():
+            dptr, ld = dout_of()
+            tmp = self.new(M * C)
+            self.L.vc_mul2_2d(M, C, dptr, ld, b.data_ptr(), C, tmp.data_ptr(), C, self.s)
+            self.add_into(self.grad_of(a), tmp, M, C)
+            self.L.vc_mul2_2d(M, C, dptr, ld, a.data_ptr(), C, tmp.data_ptr(), C, self.s)
+            self.add_into(self.grad_of(b), tmp, M, C)
+
+        self.record(bwd, a, b)
 
     def six(self, x, ldx, H, C, mod):
         for u in (mod.conv1, mod.conv2, mod.conv3, mod.conv4, mod.conv5, mod.conv6):
@@ -229,6 +340,7 @@ class _Program:
 
     def run(self):
         m, L, B, P = self.m, self.L, self.B, self.P
+        self.pg = {}
         c1, c2 = m.c1, m.c2
         x1, x2 = self.nhwc(self.x1), self.nhwc(self.x2)
         HW = P * P
@@ -244,27 +356,58 @@ class _Program:
         Hp = H // 2
         Ct = c1 + c2 + 2048
         cat = self.new(B, P, P, Ct)                                           # cat([x1, x2, Ms, Mt], 1)
+        self.cat = cat
         L.vc_add2_2d(M, c1, x1.data_ptr(), c1, None, 0, cat.data_ptr(), Ct, 0.0, self.s)
         L.vc_add2_2d(M, c2, x2.data_ptr(), c2, None, 0, cat.data_ptr() + F32 * c1, Ct, 0.0, self.s)
-        L.vc_pool_scale(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024, cat.data_ptr() + F32 * (c1 + c2), Ct,
+        offs = F32 * (c1 + c2)
+        L.vc_pool_scale(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024, cat.data_ptr() + offs, Ct,
                         self.s)                                               # Ms
+
+        def ms_bwd():
+            dpooled = self.grad_of(t)
+            L.vc_pool_scale_bwd(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024,
+                                self.grad_of(cat).data_ptr() + offs, Ct, self.grad_of(Fhs).data_ptr(), 1024,
+                                dpooled.data_ptr(), self.s)
+
+        self.record(ms_bwd, t, Fhs, cat)
         Sp = self.res_attention(x2, c2, P, c2, m.spatial_am)
-        L.vc_mul2_2d(M, 1024, Sp.data_ptr(), 1024, Fhs.data_ptr(), 1024, cat.data_ptr() + F32 * (c1 + c2 + 1024), Ct,
-                     self.s)                                                  # Mt
-        del Sp, Fhs, t
+        offt = F32 * (c1 + c2 + 1024)
+        self.mul(Sp, Fhs, M, 1024, cat.data_ptr() + offt, Ct,
+                 lambda: (self.grad_of(cat).data_ptr() + offt, Ct))           # Mt
         Fm = self.six(cat, Ct, P, Ct, m.mfe)
         Am = self.res_attention(cat, Ct, P, Ct, m.mam)
-        del cat
-        L.vc_mul2_2d(M, 1024, Fm.data_ptr(), 1024, Am.data_ptr(), 1024, Fm.data_ptr(), 1024, self.s)  # Fss
-        x, H, C = Fm, P, 1024
+        Fss = self.new(B, P, P, 1024) if self.grad else Fm
+        self.mul(Fm, Am, M, 1024, Fss.data_ptr(), 1024, lambda: (self.grad_of(Fss).data_ptr(), 1024))
+        self.keep[id(Fss)] = Fss
+        x, H, C = Fss, P, 1024
         for u in (m.cm.conv1, m.cm.conv2, m.cm.conv3, m.cm.conv4, m.cm.conv5):
             x, H = self.unit(x, C, H, C, u, pad=0)
             C = u.conv.out_channels
         Mo = B * H * H
         logits = self.new(Mo, m.ncls)
-        L.vc_gemm(0, 1, Mo, m.ncls, C, 1.0, x.data_ptr(), C, 0, m.cm.conv6.weight.data_ptr(), C, 0, 0.0,
-                  logits.data_ptr(), m.ncls, 0, 1, m.cm.conv6.bias.data_ptr(), None, 0, 0, 0, None,
-                  self.scr.data_ptr(), self.SCRATCH, self.s)
+        conv6 = m.cm.conv6
+        self.gemm(0, 1, Mo, m.ncls, C, x.data_ptr(), C, conv6.weight.data_ptr(), C, 0.0, logits.data_ptr(), m.ncls,
+                  bias=conv6.bias.data_ptr())
+        self.head = (x, Mo, C)
         if H == 1:
             return logits.view(B, m.ncls).squeeze()                          # torch.squeeze (:165)
         return logits.view(B, H, H, m.ncls).permute(0, 3, 1, 2).squeeze()
+
+    def backward(self, dlogits):
+        m = self.m
+        x, Mo, C = self.head
+        if dlogits.numel() != Mo * m.ncls or Mo != self.B:
+            raise RuntimeError("FusAtNet backward: the classifier output must be 1x1 (patch 11)")
+        conv6 = m.cm.conv6
+        self.gemm(1, 0, m.ncls, C, Mo, dlogits.data_ptr(), m.ncls, x.data_ptr(), C, 0.0, self.pgrad(conv6.weight), C,
+                  bias_grad=self.pgrad(conv6.bias))
+        self.gemm(0, 0, Mo, C, m.ncls, dlogits.data_ptr(), m.ncls, conv6.weight.data_ptr(), C, 1.0,
+                  self.grad_of(x).data_ptr(), C)
+        for fn in reversed(self.tape):
+            fn()
+        out = []
+        for _, p in m.named_parameters():
+            g = self.pg.get(id(p))
+            out.append(g if g is not None else torch.zeros_like(p))
+        self.tape, self.g, self.keep = [], {}, {}
+        return out
