@@ -11,7 +11,7 @@ replaces, so `main.py`-style drivers switch by changing one import:
 * `val(net, data_loader, device, supervision) -> accuracy` — :1135-1158.
 
 Registered: "Multimodality_Mamba" (the README's "ViT-CNN (ours)"), "S2EFT" (config 5, :400-423) and
-"FusAtNet" (config 5, :109-118, forward only).
+"FusAtNet" (config 5, :109-118).
 The reference's other branches import modules absent from the reference tree (SURVEY.md section 2a
 row 22) and are out of scope for this path.
 
@@ -116,8 +116,8 @@ def _get_s2eft(n_bands, n_classes, device, kwargs):
 def _get_fusatnet(n_bands, n_bands2, n_classes, device, kwargs):
     """FusAtNet branch of model_utils.py:109-118: FusAtNet(n_bands, n_bands2, n_classes), patch 11,
     torch.optim.Adam(lr 1e-3) as in the reference, weighted CE, epoch 150, batch 64, applyPCA False.
-    Forward only on this path (the reference's backward raises), so no gradient
-    ever reaches the optimizer."""
+    The reference's backward raises (in-place residual add); this path trains with
+    out-of-place residual semantics (vitcnn_amd/fusatnet.py)."""
     from .fusatnet import FusAtNet
     kwargs.setdefault("patch_size", 11)
     model = FusAtNet(n_bands, n_bands2, n_classes).to(device)
