@@ -265,6 +265,12 @@ VC_API int vc_s2eft_skip_pack(int B, int T, int D, const float* x, const float* 
 VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx, int acc_x, float* dlast,
                                 hipStream_t stream);
 VC_API int vc_s2eft_skip_bias_grad(int B, int T, int D, const float* dY, float* db, hipStream_t stream);
+/* nn.Dropout(p) in training (S2EFT emb_dropout :120, to_out :43, FeedForward :26, :28):
+ * keep = hash(seed, i) >= p (counter-based), y = add + keep * x / (1 - p) (add may be null, y may
+ * alias x), mask[i] = keep; backward dx = mask * dy / (1 - p) (dx may alias dy). */
+VC_API int vc_dropout_fwd(long n, const float* x, const float* add, float* y, unsigned char* mask, float p,
+                          unsigned long long seed, hipStream_t stream);
+VC_API int vc_dropout_bwd(long n, const float* dy, const unsigned char* mask, float p, float* dx, hipStream_t stream);
 
 /* ---------------------------------------------------------------- FusAtNet forward (config 5)
  * model/compare_method/FusAtNet.py over channels-last [B,H,W,C] rows.

@@ -191,3 +191,50 @@ def test_s2eft_gpu_pca30_vit_mode():
         flat = m.flat_params.grad.cpu()
         gref = torch.cat([og[n].reshape(-1) for n in m._poff])
         assert float((flat - gref).norm()) <= 1e-3 * float(gref.norm())
+
+
+@pytest.mark.gpu
+def test_s2eft_gpu_dropout_train():
+    """dropout 0.1 at the reference's sites (get_model's configuration): keep fraction ~0.9, and
+    logits / every gradient equal the oracle's evaluated with the HIP path's own keep masks"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vitcnn_amd.s2eft import ViT, _S2EFTFunction
+    from vitcnn_amd.losses import CrossEntropyLoss
+    z, sd, _ = _golden()
+    kw = dict(KW, dropout=0.1, emb_dropout=0.1)
+    m = ViT(**kw)
+    m.load_state_dict(sd)
+    m = m.to("cuda").train()
+    x, t, w = torch.from_numpy(z["x"]), torch.from_numpy(z["target"]), torch.from_numpy(z["weight"])
+    captured = {}
+    orig = _S2EFTFunction.forward
+
+    def spy(ctx, model, xx, flat, needs_grad):
+        out = orig(ctx, model, xx, flat, needs_grad)
+        captured["masks"] = {k: v.float().cpu() for k, v in ctx.prog.masks.items()}
+        return out
+
+    _S2EFTFunction.forward = staticmethod(spy)
+    try:
+        logits = m(x.cuda())
+    finally:
+        _S2EFTFunction.forward = staticmethod(orig)
+    CrossEntropyLoss(weight=w.cuda())(logits, t.cuda()).backward()
+    masks = captured["masks"]
+    assert set(masks) == {"emb"} | {f"{i}.{s}" for i in range(5) for s in ("attn", "ff1", "ff2")}
+    keep = torch.cat([v for v in masks.values()]).mean().item()
+    assert 0.88 < keep < 0.92, keep
+    drop = {k: (v, 0.1) for k, v in masks.items()}
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ref = O.forward(params, x, drop=drop)
+    torch.nn.functional.cross_entropy(ref, t, weight=w).backward()
+    assert _rel(logits.detach().cpu(), ref.detach()) < 1e-3
+    flat = m.flat_params.grad.cpu()
+    gref = torch.cat([params[n].grad.reshape(-1) if params[n].grad is not None else torch.zeros(params[n].numel())
+                      for n in m._poff])
+    assert float((flat - gref).norm()) <= 1e-3 * float(gref.norm())
+    m.eval()
+    with torch.no_grad():
+        le = m(x.cuda()).cpu()
+    assert _rel(le, O.forward(sd, x)) < 1e-3   # eval: no dropout

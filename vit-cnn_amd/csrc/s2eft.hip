@@ -292,7 +292,55 @@ __global__ __launch_bounds__(256) void skip_bias_grad(int B, int T, int D, const
   if (threadIdx.x == 0) db[o] = sh[0] + sh[1] + sh[2] + sh[3];
 }
 
+// ------------------------------------------------------------------ dropout (nn.Dropout, train mode)
+// keep_i = u_i >= p with u_i = hash(seed, i) / 2^32 (counter-based: no RNG state on the device);
+// y = add + keep * x * (1 / (1 - p)); the keep mask is saved as bytes for the backward.
+__device__ __forceinline__ uint32_t mix32(uint64_t seed, uint32_t i) {
+  uint64_t z = seed ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+__global__ void dropout_fwd(int n, const float* __restrict__ x, const float* __restrict__ add, float* __restrict__ y,
+                            unsigned char* __restrict__ mask, float p, float scale, unsigned long long seed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float u = (float)(mix32(seed, (uint32_t)i) >> 8) * (1.0f / 16777216.0f);
+  const bool keep = u >= p;
+  const float v = keep ? x[i] * scale : 0.f;
+  y[i] = add ? add[i] + v : v;
+  mask[i] = keep ? 1 : 0;
+}
+
+__global__ void dropout_bwd(int n, const float* __restrict__ dy, const unsigned char* __restrict__ mask, float scale,
+                            float* __restrict__ dx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dx[i] = mask[i] ? dy[i] * scale : 0.f;
+}
+
 }  // namespace
+
+VC_API int vc_dropout_fwd(long n, const float* x, const float* add, float* y, unsigned char* mask, float p,
+                          unsigned long long seed, hipStream_t stream) {
+  VC_REQUIRE(n >= 0 && p >= 0.f && p < 1.f);
+  VC_REQUIRE_I32(n);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(dropout_fwd, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, (int)n, x, add, y, mask, p,
+                     1.0f / (1.0f - p), seed);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_dropout_bwd(long n, const float* dy, const unsigned char* mask, float p, float* dx, hipStream_t stream) {
+  VC_REQUIRE(n >= 0 && p >= 0.f && p < 1.f);
+  VC_REQUIRE_I32(n);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(dropout_bwd, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, (int)n, dy, mask, 1.0f / (1.0f - p), dx);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
 
 VC_API int vc_s2eft_gate_fwd(int B, int N, int C, const float* x, const float* w, const float* bias, float beta,
                              float* xg, float* mask, hipStream_t stream) {

@@ -18,6 +18,7 @@ _HEADER_CANDIDATES = [
 ]
 
 _TYPE_MAP = {
+    "unsigned long long": ctypes.c_ulonglong,
     "long long": ctypes.c_longlong,
     "int": ctypes.c_int,
     "long": ctypes.c_long,

@@ -11,15 +11,14 @@ and `.pth` files interchange.  Forward and backward are one hand-written program
 parameters live in one flat fp32 buffer whose `.grad` the backward fills (the fused optimizer of
 `optim.py` then updates it in one pass; Adam = `AdamW(weight_decay=0)`).
 
-Deviations, stated: dropout (p = 0.1 in `get_model`) is not applied — the path runs the p = 0
-network (the reference's eval-mode function) in both modes and warns once when p > 0 in training;
-the `mask` argument is unsupported (the reference's mask path references an un-imported `F`,
-:58, and raises too).
+Dropout (p = 0.1 in `get_model`) is applied in training at the reference's four sites (emb_dropout
+:151, to_out :43, FeedForward :26 and :28) by a counter-based hash mask (`vc_dropout_fwd`, seeded
+from torch's CPU generator each forward, so `torch.manual_seed` reproduces a run; a hipGraph replay
+repeats the captured masks).  The `mask` argument is unsupported (the reference's mask path
+references an un-imported `F`, :58, and raises too).
 """
 from __future__ import annotations
 
-import math
-import warnings
 import weakref
 
 import torch
@@ -100,8 +99,7 @@ class ViT(nn.Module):
         # Conv2d(num_patches + 2) channels and pos_embedding's num_patches + 2 rows (S2EFT.py:88, :117)
         self.N, self.C, self.D, self.depth, self.heads = num_patches + 1, patch_dim, dim, depth, heads
         self.hidden, self.ncls, self.mode = mlp_dim, num_classes, mode
-        self.p_drop = max(dropout, emb_dropout)
-        self._warned = False
+        self.p_drop, self.p_emb = float(dropout), float(emb_dropout)
         self._build_flat()
 
     # ------------------------------------------------------------ flat parameter buffer
@@ -175,9 +173,6 @@ class ViT(nn.Module):
             raise RuntimeError("S2EFT MI355X path: input must be on a ROCm (cuda) device; no CPU fallback")
         if x.dim() != 3 or x.shape[1] != self.N or x.shape[2] != self.C:
             raise RuntimeError(f"expected x [B, {self.N}, {self.C}], got {list(x.shape)}")
-        if self.training and self.p_drop > 0 and not self._warned:
-            warnings.warn("S2EFT MI355X path: dropout is not applied (p = 0 network)")
-            self._warned = True
         self._ensure_flat()
         if self._flat_store.device != x.device:
             raise RuntimeError("model and input are on different devices")
@@ -218,6 +213,17 @@ class _Program:
         self.P = {n: base + F32 * o for n, o in m._poff.items()}
         self.scr = self.new(self.SCRATCH)
         self.keep = []
+        self.pd = m.p_drop if m.training else 0.0
+        self.pe = m.p_emb if m.training else 0.0
+        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (self.pd > 0 or self.pe > 0) else 0
+        self.masks = {}
+
+    def drop(self, site, x, add, y, n, p):
+        """y = add + dropout_p(x) (add may be None); the keep mask is saved under `site`"""
+        mk = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        self.L.vc_dropout_fwd(n, x.data_ptr(), add.data_ptr() if add is not None else None, y.data_ptr(),
+                              mk.data_ptr(), p, (self.seed + 1000003 * len(self.masks)) % (1 << 63), self.s)
+        self.masks[site] = mk
 
     def new(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)
@@ -247,6 +253,8 @@ class _Program:
         self.gemm(0, 1, N, D, C, xg.data_ptr(), C, N * C, P["patch_to_embedding.weight"], C, 0, 0.0,
                   X.data_ptr() + F32 * D, D, T * D, batch=B, bias=P["patch_to_embedding.bias"],
                   add=P["pos_embedding"] + F32 * D, add_ld=D, add_mod=N)
+        if self.pe > 0:
+            self.drop("emb", X, None, X, R * D, self.pe)
         self.xg = xg
         self.saved = []
         xin = []
@@ -272,8 +280,15 @@ class _Program:
             O, lse = self.new(R, Hh * 16), self.new(B, Hh, T)
             L.vc_s2eft_attn_fwd(B, T, Hh, qkv.data_ptr(), 16 ** -0.5, O.data_ptr(), lse.data_ptr(), self.s)
             X2 = self.new(B, T, D)
-            self.gemm(0, 1, R, D, Hh * 16, O.data_ptr(), Hh * 16, 0, P[pre + ".0.fn.fn.to_out.0.weight"], Hh * 16, 0,
-                      0.0, X2.data_ptr(), D, 0, bias=P[pre + ".0.fn.fn.to_out.0.bias"], add=X.data_ptr(), add_ld=D)
+            if self.pd > 0:
+                A2 = self.new(R, D)
+                self.gemm(0, 1, R, D, Hh * 16, O.data_ptr(), Hh * 16, 0, P[pre + ".0.fn.fn.to_out.0.weight"], Hh * 16,
+                          0, 0.0, A2.data_ptr(), D, 0, bias=P[pre + ".0.fn.fn.to_out.0.bias"])
+                self.drop(f"{li}.attn", A2, X, X2, R * D, self.pd)
+            else:
+                self.gemm(0, 1, R, D, Hh * 16, O.data_ptr(), Hh * 16, 0, P[pre + ".0.fn.fn.to_out.0.weight"], Hh * 16,
+                          0, 0.0, X2.data_ptr(), D, 0, bias=P[pre + ".0.fn.fn.to_out.0.bias"], add=X.data_ptr(),
+                          add_ld=D)
             # feed-forward sub-block
             Y2, mu2, rs2 = self.ln(pre + ".1.fn.norm", X2.data_ptr(), R, D)
             Hd = self.new(R, m.hidden)
@@ -281,9 +296,18 @@ class _Program:
                       Hd.data_ptr(), m.hidden, 0, bias=P[pre + ".1.fn.fn.net.0.bias"])
             G = self.new(R, m.hidden)
             L.vc_gelu_fwd(R * m.hidden, Hd.data_ptr(), G.data_ptr(), self.s)
+            if self.pd > 0:
+                self.drop(f"{li}.ff1", G, None, G, R * m.hidden, self.pd)
             X3 = self.new(B, T, D)
-            self.gemm(0, 1, R, D, m.hidden, G.data_ptr(), m.hidden, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0,
-                      0.0, X3.data_ptr(), D, 0, bias=P[pre + ".1.fn.fn.net.3.bias"], add=X2.data_ptr(), add_ld=D)
+            if self.pd > 0:
+                F2 = self.new(R, D)
+                self.gemm(0, 1, R, D, m.hidden, G.data_ptr(), m.hidden, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden,
+                          0, 0.0, F2.data_ptr(), D, 0, bias=P[pre + ".1.fn.fn.net.3.bias"])
+                self.drop(f"{li}.ff2", F2, X2, X3, R * D, self.pd)
+            else:
+                self.gemm(0, 1, R, D, m.hidden, G.data_ptr(), m.hidden, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden,
+                          0, 0.0, X3.data_ptr(), D, 0, bias=P[pre + ".1.fn.fn.net.3.bias"], add=X2.data_ptr(),
+                          add_ld=D)
             st.update(Y=Y, mu=mu, rs=rs, qkv=qkv, O=O, lse=lse, X2=X2, Y2=Y2, mu2=mu2, rs2=rs2, Hd=Hd, G=G)
             self.saved.append(st)
             X = X3
@@ -323,10 +347,18 @@ class _Program:
             st = self.saved[li]
             # feed-forward: X3 = X2 + W2 gelu(W1 LN(X2) + b1) + b2 ; dX holds dX3, becomes dX2 in place
             dG = self.new(R, m.hidden)
-            self.gemm(1, 0, D, m.hidden, R, dX.data_ptr(), D, 0, st["G"].data_ptr(), m.hidden, 0, 0.0,
+            dF2 = dX
+            if self.pd > 0:
+                dF2 = self.new(R, D)
+                L.vc_dropout_bwd(R * D, dX.data_ptr(), self.masks[f"{li}.ff2"].data_ptr(), self.pd, dF2.data_ptr(),
+                                 self.s)
+            self.gemm(1, 0, D, m.hidden, R, dF2.data_ptr(), D, 0, st["G"].data_ptr(), m.hidden, 0, 0.0,
                       G[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0, bias_grad=G[pre + ".1.fn.fn.net.3.bias"])
-            self.gemm(0, 0, R, m.hidden, D, dX.data_ptr(), D, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0, 0.0,
+            self.gemm(0, 0, R, m.hidden, D, dF2.data_ptr(), D, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0, 0.0,
                       dG.data_ptr(), m.hidden, 0)
+            if self.pd > 0:
+                L.vc_dropout_bwd(R * m.hidden, dG.data_ptr(), self.masks[f"{li}.ff1"].data_ptr(), self.pd,
+                                 dG.data_ptr(), self.s)
             dH = self.new(R, m.hidden)
             L.vc_gelu_bwd(R * m.hidden, dG.data_ptr(), st["Hd"].data_ptr(), dH.data_ptr(), self.s)
             self.gemm(1, 0, m.hidden, D, R, dH.data_ptr(), m.hidden, 0, st["Y2"].data_ptr(), D, 0, 0.0,
@@ -339,10 +371,15 @@ class _Program:
                                G[pre + ".1.fn.norm.weight"], G[pre + ".1.fn.norm.bias"], 0.0, scr, ns, self.s)
             # attention: X2 = Xs + Wo attn(Wqkv LN(Xs)) + bo ; dX becomes dXs in place
             E = Hh * 16
-            self.gemm(1, 0, D, E, R, dX.data_ptr(), D, 0, st["O"].data_ptr(), E, 0, 0.0,
+            dA2 = dX
+            if self.pd > 0:
+                dA2 = self.new(R, D)
+                L.vc_dropout_bwd(R * D, dX.data_ptr(), self.masks[f"{li}.attn"].data_ptr(), self.pd, dA2.data_ptr(),
+                                 self.s)
+            self.gemm(1, 0, D, E, R, dA2.data_ptr(), D, 0, st["O"].data_ptr(), E, 0, 0.0,
                       G[pre + ".0.fn.fn.to_out.0.weight"], E, 0, bias_grad=G[pre + ".0.fn.fn.to_out.0.bias"])
             dO = self.new(R, E)
-            self.gemm(0, 0, R, E, D, dX.data_ptr(), D, 0, P[pre + ".0.fn.fn.to_out.0.weight"], E, 0, 0.0,
+            self.gemm(0, 0, R, E, D, dA2.data_ptr(), D, 0, P[pre + ".0.fn.fn.to_out.0.weight"], E, 0, 0.0,
                       dO.data_ptr(), E, 0)
             dqkv = self.new(R, 3 * E)
             L.vc_s2eft_attn_bwd(B, T, Hh, st["qkv"].data_ptr(), st["O"].data_ptr(), dO.data_ptr(), st["lse"].data_ptr(),
@@ -375,7 +412,9 @@ class _Program:
                 dX = dXin
             if li in dlast:  # this layer's input is also last_output[li] of layer li + 2
                 L.vc_add2_2d(R, D, dX.data_ptr(), D, dlast[li].data_ptr(), D, dX.data_ptr(), D, 0.0, self.s)
-        # embedding: X0 = cat(cls, xg W^T + b) + pos
+        # embedding: X0 = dropout(cat(cls, xg W^T + b) + pos)
+        if self.pe > 0:
+            L.vc_dropout_bwd(R * D, dX.data_ptr(), self.masks["emb"].data_ptr(), self.pe, dX.data_ptr(), self.s)
         L.vc_colsum(B, T * D, dX.data_ptr(), T * D, G["pos_embedding"], 0.0, scr, ns, self.s)
         L.vc_colsum(B, D, dX.data_ptr(), T * D, G["cls_token"], 0.0, scr, ns, self.s)
         dE = self.new(B * N, D)
