@@ -278,6 +278,46 @@ def s2eft_leg(dev, steps, cpu_steps):
     return out
 
 
+def muufl_leg(dev, steps):
+    """Config 4 (SURVEY.md section 8 row A-MUUFL): the ViT-CNN train step on the MUUFL shape
+    (64 + 2 bands, 11x11 patches, 12 classes) at B = 64 per GPU, whole step as one hipGraph."""
+    from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba, fused_train_step
+    torch.manual_seed(0)
+    m = Multimodality_Mamba(11, 1, 1, 64, 2, 32, 12, "multi_clock_gate").to(dev).train()
+    opt = AdamW(m.parameters(), lr=8e-4)
+    w = torch.ones(12)
+    w[0] = 0.0
+    crit = CrossEntropyLoss(weight=w.to(dev))
+    g = torch.Generator().manual_seed(4)
+    hsi = torch.rand(64, 64, 11, 11, generator=g).to(dev)
+    lidar = torch.rand(64, 2, 11, 11, generator=g).to(dev)
+    tgt = torch.randint(1, 12, (64,), generator=g).to(dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            fused_train_step(m, crit, hsi, lidar, tgt)
+            opt.step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    opt.zero_grad(set_to_none=True)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        fused_train_step(m, crit, hsi, lidar, tgt)
+        opt.step()
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        graph.replay()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"workload": "ViT-CNN train step, MUUFL shape 64+2 bands, 11x11, 12 classes", "value": round(64 / ms * 1e3, 1),
+            "unit": "patches/s", "ms_per_step": round(ms, 4), "dtype": "fp32", "launch": "hipGraph"}
+
+
 FUSAT_GFLOP_PER_PATCH = 6.92  # SURVEY.md section 8(d), FusAtNet forward
 
 
@@ -476,6 +516,7 @@ def main():
     if world == 1 and not args.no_s2eft:
         out["config5_s2eft"] = s2eft_leg(dev, min(args.steps, 50), 0 if args.no_cpu_baseline else 5)
         out["config5_fusatnet"] = fusat_leg(dev, 5, not args.no_cpu_baseline)
+        out["config4_muufl"] = muufl_leg(dev, min(args.steps, 50))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
