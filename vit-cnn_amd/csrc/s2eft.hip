@@ -91,11 +91,18 @@ __device__ __forceinline__ float part_sum(float v) {
   return v;
 }
 
+// Forward on the matrix cores (v_mfma_f32_16x16x4_f32).  A wave owns 16 queries of one (b, h) and walks
+// the keys in 16-key tiles, computing S^T = K Q^T (so the scores of one query sit in the four
+// registers of the four lanes l, l^16, l^32, l^48 that share l & 15) and O^T += V^T P^T, whose B
+// operand is P^T straight from the S^T accumulator: the k order inside each MFMA is permuted so that
+// step s of lane group g = l >> 4 pairs key (or head-dim) 4g + s on both operands.  Online softmax
+// (running max / sum per query, rescaling the O^T accumulator) between tiles.
 __global__ __launch_bounds__(256) void attn_fwd(int T, int H, const float* __restrict__ qkv, float scale,
                                                 float* __restrict__ out, float* __restrict__ lse) {
   extern __shared__ f32x4 lds4[];  // 2 * T * 64 B
   f32x4* Ks = lds4;
   f32x4* Vs = lds4 + T * 4;
+  const float* Vf = (const float*)Vs;
   const int nq = (T + 63) >> 6;
   const int bh = blockIdx.x / nq, chunk = blockIdx.x % nq;
   const int b = bh / H, h = bh % H;
@@ -107,38 +114,55 @@ __global__ __launch_bounds__(256) void attn_fwd(int T, int H, const float* __res
     Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
   }
   __syncthreads();
-  const int part = threadIdx.x & (kParts - 1);
-  const int i = chunk * 64 + (threadIdx.x >> 2);
-  const bool valid = i < T;
-  const int ii = valid ? i : T - 1;  // idle lanes shadow the last row so the shuffles stay uniform
-  f32x4 q[4];
-  for (int k = 0; k < 4; ++k) q[k] = *(const f32x4*)(base + (long)ii * ld + h * 16 + k * 4);
-  float m = -INFINITY;
-  for (int j = part; j < T; j += kParts) m = fmaxf(m, dot16(q, Ks + j * 4) * scale);
-  float l = 0.f;
-  f32x4 acc[4] = {};
-  for (int j = part; j < T; j += kParts) {
-    const float p = expf(dot16(q, Ks + j * 4) * scale - m);
-    l += p;
-    for (int k = 0; k < 4; ++k) acc[k] += p * Vs[j * 4 + k];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q0 = chunk * 64 + wave * 16;
+  if (q0 >= T) return;                     // whole wave idle (no LDS barrier follows)
+  const int c = lane & 15, g = lane >> 4;
+  const int qi = min(q0 + c, T - 1);
+  // B operand of S^T: Q^T[d = 4g + s][q = c]
+  const f32x4 qv = *(const f32x4*)(base + (long)qi * ld + h * 16 + g * 4);
+  float m = -INFINITY, l = 0.f;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};          // O^T[d = 4g + r][q = c]
+  for (int k0 = 0; k0 < T; k0 += 16) {
+    const int key = min(k0 + c, T - 1);
+    const f32x4 kv = Ks[key * 4 + g];      // A operand: K[key = k0 + c][d = 4g + s]
+    f32x4 st = {0.f, 0.f, 0.f, 0.f};       // S^T[key = k0 + 4g + r][q = c]
+    st = __builtin_amdgcn_mfma_f32_16x16x4f32(kv.x, qv.x, st, 0, 0, 0);
+    st = __builtin_amdgcn_mfma_f32_16x16x4f32(kv.y, qv.y, st, 0, 0, 0);
+    st = __builtin_amdgcn_mfma_f32_16x16x4f32(kv.z, qv.z, st, 0, 0, 0);
+    st = __builtin_amdgcn_mfma_f32_16x16x4f32(kv.w, qv.w, st, 0, 0, 0);
+    float sv[4];
+    float tm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sv[r] = (k0 + 4 * g + r < T) ? st[r] * scale : -INFINITY;
+      tm = fmaxf(tm, sv[r]);
+    }
+    tm = fmaxf(tm, __shfl_xor(tm, 16, 64));
+    tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+    const float mn = fmaxf(m, tm);
+    const float corr = (m == -INFINITY) ? 0.f : expf(m - mn);
+    m = mn;
+    float pv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pv[r] = (sv[r] == -INFINITY) ? 0.f : expf(sv[r] - mn);
+      l = l * (r == 0 ? corr : 1.f) + pv[r];
+    }
+    o *= corr;
+    // O^T += V^T P^T: step s, group g pairs key k0 + 4g + s; A = V[key][d = c], B = P^T (register s)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int kk = min(k0 + 4 * g + s2, T - 1);
+      o = __builtin_amdgcn_mfma_f32_16x16x4f32(Vf[kk * 16 + c], pv[s2], o, 0, 0, 0);
+    }
   }
-  // merge the four partial states of the row
-  float M = fmaxf(m, __shfl_xor(m, 1, 64));
-  M = fmaxf(M, __shfl_xor(M, 2, 64));
-  const float f = (m == -INFINITY) ? 0.f : expf(m - M);
-  l = part_sum(l * f);
-  for (int k = 0; k < 4; ++k) {
-    acc[k] *= f;
-    acc[k].x = part_sum(acc[k].x);
-    acc[k].y = part_sum(acc[k].y);
-    acc[k].z = part_sum(acc[k].z);
-    acc[k].w = part_sum(acc[k].w);
-  }
-  if (!valid) return;
-  const float r = 1.0f / l;
-  float* o = out + ((long)b * T + i) * ldo + h * 16;
-  *(f32x4*)(o + part * 4) = acc[part] * r;
-  if (part == 0) lse[((long)b * H + h) * T + i] = M + logf(l);
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (q0 + c >= T) return;
+  const float rl = 1.0f / l;
+  *(f32x4*)(out + ((long)b * T + q0 + c) * ldo + h * 16 + g * 4) = o * rl;
+  if (g == 0) lse[((long)b * H + h) * T + q0 + c] = m + logf(l);
 }
 
 // dS = P * (dP - rowsum(dO * O)); pass 1 (lane group per query row) -> dq, pass 2 (per key row) -> dk, dv.
