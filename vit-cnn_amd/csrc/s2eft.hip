@@ -74,23 +74,8 @@ __global__ void strip_cls(int B, int N, int D, const float* __restrict__ dX, flo
 }
 
 // ------------------------------------------------------------------ attention core (dim_head 16)
-// Block = 256 lanes = 64 rows x 4 key-quarters: lane (row, part) walks keys j = part, part+4, ...; the four
-// partial softmax states / gradient sums of a row meet by lane shuffles.  Grid B*H*ceil(T/64) (768
-// blocks, 3072 waves at config 5).  The head's K/V (and for the backward Q, dO, lse, rowsum(dO*O)) sit in
-// LDS sized to T and are read as 4-way broadcasts.  P is never stored: the forward saves lse per row.
-constexpr int kParts = 4;
-
-__device__ __forceinline__ float dot16(const f32x4* q, const f32x4* k) {
-  f32x4 a = q[0] * k[0] + q[1] * k[1] + q[2] * k[2] + q[3] * k[3];
-  return (a.x + a.y + a.z + a.w);
-}
-
-__device__ __forceinline__ float part_sum(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  return v;
-}
-
+// Grid B*H*ceil(T/64) blocks of 4 waves (768 blocks at config 5); the head's K/V (and for the backward
+// Q, dO, lse, rowsum(dO*O)) sit in LDS sized to T.  P is never stored: the forward saves lse per row.
 // Forward on the matrix cores (v_mfma_f32_16x16x4_f32).  A wave owns 16 queries of one (b, h) and walks
 // the keys in 16-key tiles, computing S^T = K Q^T (so the scores of one query sit in the four
 // registers of the four lanes l, l^16, l^32, l^48 that share l & 15) and O^T += V^T P^T, whose B
@@ -165,7 +150,18 @@ __global__ __launch_bounds__(256) void attn_fwd(int T, int H, const float* __res
   if (g == 0) lse[((long)b * H + h) * T + q0 + c] = m + logf(l);
 }
 
-// dS = P * (dP - rowsum(dO * O)); pass 1 (lane group per query row) -> dq, pass 2 (per key row) -> dk, dv.
+// Backward on MFMA, same tile scheme as the forward.  dS = P * (dP - rowsum(dO*O)), P recomputed
+// from lse.  Pass 1: a wave owns 16 queries and walks 16-key tiles: S^T = K Q^T, dP^T = V dO^T,
+// dQ^T += K^T dS^T.  Pass 2: the wave owns 16 keys and walks 16-query tiles: S = Q K^T, dP = dO V^T,
+// dV^T += dO^T P, dK^T += Q^T dS (P / dS taken from the accumulators as B operands).
+__device__ __forceinline__ f32x4 mfma4(f32x4 a, f32x4 b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+  return c;
+}
+
 __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __restrict__ qkv,
                                                 const float* __restrict__ out, const float* __restrict__ dout,
                                                 const float* __restrict__ lse, float scale,
@@ -177,6 +173,9 @@ __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __res
   f32x4* dOs = lds4 + 3 * T * 4;
   float* Ls = (float*)(lds4 + 4 * T * 4);
   float* Ds = Ls + T;
+  const float* Qf = (const float*)Qs;
+  const float* Kf = (const float*)Ks;
+  const float* dOf = (const float*)dOs;
   const int nq = (T + 63) >> 6;
   const int bh = blockIdx.x / nq, chunk = blockIdx.x % nq;
   const int b = bh / H, h = bh % H;
@@ -202,58 +201,64 @@ __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __res
     }
   }
   __syncthreads();
-  const int part = threadIdx.x & (kParts - 1);
-  const int i = chunk * 64 + (threadIdx.x >> 2);
-  const bool valid = i < T;
-  const int ii = valid ? i : T - 1;
-  {  // dq of row ii
-    f32x4 q[4], go[4], dq[4] = {};
-    for (int k = 0; k < 4; ++k) {
-      q[k] = Qs[ii * 4 + k];
-      go[k] = dOs[ii * 4 + k];
-    }
-    const float li = Ls[ii], di = Ds[ii];
-    for (int j = part; j < T; j += kParts) {
-      const float p = expf(dot16(q, Ks + j * 4) * scale - li);
-      const float ds = p * (dot16(go, Vs + j * 4) - di);
-      for (int k = 0; k < 4; ++k) dq[k] += ds * Ks[j * 4 + k];
-    }
-    for (int k = 0; k < 4; ++k) {
-      dq[k].x = part_sum(dq[k].x);
-      dq[k].y = part_sum(dq[k].y);
-      dq[k].z = part_sum(dq[k].z);
-      dq[k].w = part_sum(dq[k].w);
-    }
-    if (valid) *(f32x4*)(dqkv + ((long)b * T + i) * ld + h * 16 + part * 4) = dq[part] * scale;
-  }
-  {  // dk, dv of key row ii
-    f32x4 kk[4], vv[4], dk[4] = {}, dv[4] = {};
-    for (int k = 0; k < 4; ++k) {
-      kk[k] = Ks[ii * 4 + k];
-      vv[k] = Vs[ii * 4 + k];
-    }
-    for (int r = part; r < T; r += kParts) {
-      const float p = expf(dot16(kk, Qs + r * 4) * scale - Ls[r]);
-      const float ds = p * (dot16(vv, dOs + r * 4) - Ds[r]);
-      for (int k = 0; k < 4; ++k) {
-        dv[k] += p * dOs[r * 4 + k];
-        dk[k] += ds * Qs[r * 4 + k];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r0 = chunk * 64 + wave * 16;
+  if (r0 >= T) return;
+  const int c = lane & 15, g = lane >> 4;
+  const int ri = min(r0 + c, T - 1);
+  {  // pass 1: dq of queries r0 .. r0 + 15 (query c of this lane)
+    const f32x4 qv = Qs[ri * 4 + g], gv = dOs[ri * 4 + g];
+    const float lq = Ls[ri], dq_ = Ds[ri];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};  // dQ^T[d = 4g + r][q = c]
+    for (int k0 = 0; k0 < T; k0 += 16) {
+      const int key = min(k0 + c, T - 1);
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 st = mfma4(Ks[key * 4 + g], qv, z);   // S^T[key = k0 + 4g + r][q = c]
+      const f32x4 dpt = mfma4(Vs[key * 4 + g], gv, z);  // dP^T
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool valid = k0 + 4 * g + r < T;
+        const float p = valid ? expf(st[r] * scale - lq) : 0.f;
+        ds[r] = p * (dpt[r] - dq_);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int kk = min(k0 + 4 * g + s2, T - 1);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Kf[kk * 16 + c], ds[s2], acc, 0, 0, 0);
       }
     }
-    for (int k = 0; k < 4; ++k) {
-      dk[k].x = part_sum(dk[k].x);
-      dk[k].y = part_sum(dk[k].y);
-      dk[k].z = part_sum(dk[k].z);
-      dk[k].w = part_sum(dk[k].w);
-      dv[k].x = part_sum(dv[k].x);
-      dv[k].y = part_sum(dv[k].y);
-      dv[k].z = part_sum(dv[k].z);
-      dv[k].w = part_sum(dv[k].w);
+    if (r0 + c < T) *(f32x4*)(dqkv + ((long)b * T + r0 + c) * ld + h * 16 + g * 4) = acc * scale;
+  }
+  {  // pass 2: dk, dv of keys r0 .. r0 + 15 (key c of this lane)
+    const f32x4 kv = Ks[ri * 4 + g], vv = Vs[ri * 4 + g];
+    f32x4 adk = {0.f, 0.f, 0.f, 0.f}, adv = {0.f, 0.f, 0.f, 0.f};  // dK^T / dV^T [d = 4g + r][key = c]
+    for (int q0 = 0; q0 < T; q0 += 16) {
+      const int qq = min(q0 + c, T - 1);
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 sm = mfma4(Qs[qq * 4 + g], kv, z);    // S[q = q0 + 4g + r][key = c]
+      const f32x4 dp = mfma4(dOs[qq * 4 + g], vv, z);   // dP
+      float pr[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = q0 + 4 * g + r;
+        const bool valid = q < T;
+        const int qc = valid ? q : T - 1;
+        const float p = valid ? expf(sm[r] * scale - Ls[qc]) : 0.f;
+        pr[r] = p;
+        ds[r] = p * (dp[r] - Ds[qc]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int qk = min(q0 + 4 * g + s2, T - 1);
+        adv = __builtin_amdgcn_mfma_f32_16x16x4f32(dOf[qk * 16 + c], pr[s2], adv, 0, 0, 0);
+        adk = __builtin_amdgcn_mfma_f32_16x16x4f32(Qf[qk * 16 + c], ds[s2], adk, 0, 0, 0);
+      }
     }
-    if (valid) {
-      float* w = dqkv + ((long)b * T + i) * ld + h * 16;
-      *(f32x4*)(w + H * 16 + part * 4) = dk[part] * scale;
-      *(f32x4*)(w + 2 * H * 16 + part * 4) = dv[part];
+    if (r0 + c < T) {
+      float* w = dqkv + ((long)b * T + r0 + c) * ld + h * 16 + g * 4;
+      *(f32x4*)(w + H * 16) = adk * scale;
+      *(f32x4*)(w + 2 * H * 16) = adv;
     }
   }
 }
