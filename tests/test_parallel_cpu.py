@@ -106,3 +106,51 @@ def test_allreduce_equals_mean_of_shard_gradients():
         torch.set_num_threads(nt)
     err = float((g - ref).abs().max() / ref.abs().max())
     assert err < 1e-6, err
+
+
+def _s2eft_worker(rank, world, port, out):
+    """config 5 data parallelism: each rank's S2EFT shard gradient (oracle, B = 2 of the golden
+    batch) in the model's flat layout, all-reduced through the same helpers as ViT-CNN"""
+    import numpy as np
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from oracle import s2eft_oracle as O
+    from vitcnn_amd import parallel
+    from vitcnn_amd.optim import AdamW
+    from vitcnn_amd.s2eft import ViT
+    parallel.init_from_env(backend="gloo")
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "s2eft_b4.npz"))
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p:")}
+    m = ViT(image_size=7, near_band=3, num_patches=144, num_classes=16, dim=64, depth=5, heads=4, mlp_dim=8)
+    m.load_state_dict(sd)
+    opt = AdamW(m.parameters(), lr=5e-4, weight_decay=0.0)
+    sl = slice(rank * 2, rank * 2 + 2)
+    x, t, w = torch.from_numpy(z["x"])[sl], torch.from_numpy(z["target"])[sl], torch.from_numpy(z["weight"])
+    _, _, g = O.train_step(sd, x, t, w)
+    m.flat_params.grad = torch.cat([g[n].reshape(-1) for n in m._poff])
+    parallel.allreduce_gradients(m, opt)
+    out[rank] = (m.flat_params.grad.clone() * opt.grad_scale, opt.grad_scale)
+    dist.destroy_process_group()
+
+
+def test_s2eft_gradient_allreduce_world2():
+    import numpy as np
+    from oracle import s2eft_oracle as O
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_s2eft_worker, args=(2, port, out), nprocs=2, join=True)
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "s2eft_b4.npz"))
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p:")}
+    x, t, w = torch.from_numpy(z["x"]), torch.from_numpy(z["target"]), torch.from_numpy(z["weight"])
+    names = list(sd.keys())
+    mean = None
+    for r in range(2):
+        _, _, g = O.train_step(sd, x[r * 2:r * 2 + 2], t[r * 2:r * 2 + 2], w)
+        flat = torch.cat([g[n].reshape(-1) for n in names])
+        mean = flat / 2 if mean is None else mean + flat / 2
+    for r in range(2):
+        got, scale = out[r]
+        assert scale == 0.5
+        assert torch.allclose(got, mean, rtol=1e-5, atol=1e-7)
