@@ -154,3 +154,28 @@ def test_s2eft_gradient_allreduce_world2():
         got, scale = out[r]
         assert scale == 0.5
         assert torch.allclose(got, mean, rtol=1e-5, atol=1e-7)
+
+
+def _perparam_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from vitcnn_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    m = torch.nn.Sequential(torch.nn.Linear(3, 4), torch.nn.Linear(4, 2))
+    for i, p in enumerate(m.parameters()):
+        p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
+    opt = torch.optim.Adam(m.parameters())
+    parallel.allreduce_gradients(m, opt)
+    out[rank] = [p.grad.clone() for p in m.parameters()]
+    dist.destroy_process_group()
+
+
+def test_perparam_gradient_allreduce_world2():
+    """models without the flat buffer (FusAtNet with torch Adam): per-parameter gradients averaged"""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_perparam_worker, args=(2, port, out), nprocs=2, join=True)
+    for r in range(2):
+        for i, g in enumerate(out[r]):
+            assert torch.allclose(g, torch.full_like(g, 1.5 * (i + 1)))

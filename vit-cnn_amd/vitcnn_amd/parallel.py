@@ -69,11 +69,24 @@ def allreduce_gradients(model, optimizer=None, group=None):
         if optimizer is not None and hasattr(optimizer, "grad_scale"):
             optimizer.grad_scale = 1.0
         return
+    n = dist.get_world_size(group)
+    if not hasattr(model, "flat_params"):
+        # per-parameter gradients (FusAtNet: torch.optim.Adam over .grad): one flattened bucket
+        grads = [p.grad for p in model.parameters() if p.grad is not None]
+        if not grads:
+            raise RuntimeError("allreduce_gradients: backward has not produced a gradient")
+        bucket = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
+        bucket.mul_(1.0 / n)
+        o = 0
+        for g in grads:
+            g.copy_(bucket[o:o + g.numel()].view_as(g))
+            o += g.numel()
+        return
     g = active_grad(model)
     if g is None:
         raise RuntimeError("allreduce_gradients: backward has not produced a gradient")
     dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
-    n = dist.get_world_size(group)
     if optimizer is not None and hasattr(optimizer, "grad_scale"):
         optimizer.grad_scale = 1.0 / n
     else:
