@@ -74,33 +74,31 @@ __global__ void strip_cls(int B, int N, int D, const float* __restrict__ dX, flo
 }
 
 // ------------------------------------------------------------------ attention core (dim_head 16)
-// Grid B*H*ceil(T/64) blocks of 4 waves (768 blocks at config 5); the head's K/V (and for the backward
-// Q, dO, lse, rowsum(dO*O)) sit in LDS sized to T.  P is never stored: the forward saves lse per row.
+// One block per (b, h) with ceil(T/16) waves (256 blocks x 10 waves at config 5), so the head's K/V (and
+// for the backward Q, dO, lse, rowsum(dO*O)) are staged into LDS (sized to T) once per head.  P is never stored: the forward saves lse per row.
 // Forward on the matrix cores (v_mfma_f32_16x16x4_f32).  A wave owns 16 queries of one (b, h) and walks
 // the keys in 16-key tiles, computing S^T = K Q^T (so the scores of one query sit in the four
 // registers of the four lanes l, l^16, l^32, l^48 that share l & 15) and O^T += V^T P^T, whose B
 // operand is P^T straight from the S^T accumulator: the k order inside each MFMA is permuted so that
 // step s of lane group g = l >> 4 pairs key (or head-dim) 4g + s on both operands.  Online softmax
 // (running max / sum per query, rescaling the O^T accumulator) between tiles.
-__global__ __launch_bounds__(256) void attn_fwd(int T, int H, const float* __restrict__ qkv, float scale,
+__global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __restrict__ qkv, float scale,
                                                 float* __restrict__ out, float* __restrict__ lse) {
   extern __shared__ f32x4 lds4[];  // 2 * T * 64 B
   f32x4* Ks = lds4;
   f32x4* Vs = lds4 + T * 4;
   const float* Vf = (const float*)Vs;
-  const int nq = (T + 63) >> 6;
-  const int bh = blockIdx.x / nq, chunk = blockIdx.x % nq;
-  const int b = bh / H, h = bh % H;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int ld = 3 * H * 16, ldo = H * 16;
   const float* base = qkv + (long)b * T * ld;
-  for (int i = threadIdx.x; i < T * 4; i += 256) {
+  for (int i = threadIdx.x; i < T * 4; i += blockDim.x) {
     const int t = i >> 2, q4 = i & 3;
     Ks[i] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
     Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q0 = chunk * 64 + wave * 16;
+  const int q0 = wave * 16;
   if (q0 >= T) return;                     // whole wave idle (no LDS barrier follows)
   const int c = lane & 15, g = lane >> 4;
   const int qi = min(q0 + c, T - 1);
@@ -162,7 +160,7 @@ __device__ __forceinline__ f32x4 mfma4(f32x4 a, f32x4 b, f32x4 c) {
   return c;
 }
 
-__global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __restrict__ qkv,
+__global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __restrict__ qkv,
                                                 const float* __restrict__ out, const float* __restrict__ dout,
                                                 const float* __restrict__ lse, float scale,
                                                 float* __restrict__ dqkv) {
@@ -176,12 +174,10 @@ __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __res
   const float* Qf = (const float*)Qs;
   const float* Kf = (const float*)Ks;
   const float* dOf = (const float*)dOs;
-  const int nq = (T + 63) >> 6;
-  const int bh = blockIdx.x / nq, chunk = blockIdx.x % nq;
-  const int b = bh / H, h = bh % H;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int ld = 3 * H * 16, ldo = H * 16;
   const float* base = qkv + (long)b * T * ld;
-  for (int i = threadIdx.x; i < T * 4; i += 256) {
+  for (int i = threadIdx.x; i < T * 4; i += blockDim.x) {
     const int t = i >> 2, q4 = i & 3;
     Qs[i] = *(const f32x4*)(base + (long)t * ld + h * 16 + q4 * 4);
     Ks[i] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
@@ -189,7 +185,7 @@ __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __res
     dOs[i] = *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4);
   }
   // rowsum(dO * O): 16 lanes per row, coalesced
-  for (int i0 = 0; i0 < T * 16; i0 += 256) {
+  for (int i0 = 0; i0 < T * 16; i0 += blockDim.x) {
     const int idx = i0 + threadIdx.x;
     const int r = idx >> 4, d = idx & 15;
     float v = 0.f;
@@ -202,7 +198,7 @@ __global__ __launch_bounds__(256) void attn_bwd(int T, int H, const float* __res
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r0 = chunk * 64 + wave * 16;
+  const int r0 = wave * 16;
   if (r0 >= T) return;
   const int c = lane & 15, g = lane >> 4;
   const int ri = min(r0 + c, T - 1);
@@ -397,7 +393,7 @@ VC_API int vc_s2eft_strip_cls(int B, int N, int D, const float* dX, float* dE, h
 VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale, float* out, float* lse,
                              hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_fwd, dim3(B * H * ((T + 63) / 64)), dim3(256), 2 * T * 64, stream, T, H, qkv, scale, out,
+  hipLaunchKernelGGL(attn_fwd, dim3(B * H), dim3(64 * ((T + 15) / 16)), 2 * T * 64, stream, T, H, qkv, scale, out,
                      lse);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -406,7 +402,7 @@ VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale,
 VC_API int vc_s2eft_attn_bwd(int B, int T, int H, const float* qkv, const float* out, const float* dout,
                              const float* lse, float scale, float* dqkv, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_bwd, dim3(B * H * ((T + 63) / 64)), dim3(256), 4 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
+  hipLaunchKernelGGL(attn_bwd, dim3(B * H), dim3(64 * ((T + 15) / 16)), 4 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
                      dout, lse, scale, dqkv);
   VC_CHECK_LAUNCH();
   return VC_OK;
