@@ -36,8 +36,10 @@
 /* ---------------------------------------------------------------- dense contractions
  * C[b] = alpha * op(A[b]) op(B[b]) + beta*C[b] (+ bias[n]) (+ addend[(m % add_mod)*add_ld + n]) (ReLU if flags&1)
  * op(A)(m,k) = transA ? A[k*lda+m] : A[m*lda+k];  op(B)(k,n) = transB ? B[n*ldb+k] : B[k*ldb+n].
- * fp32 in / fp32 accumulate on v_mfma_f32_16x16x4_f32; split-K (fixed-order) when the output
- * grid is small and ws is given.  bias_grad (batch 1 only, may be null) additionally receives
+ * fp32 in / fp32 accumulate on v_mfma_f32_16x16x4_f32, or, with flags&2, bf16 operands (rounded
+ * RNE as they are staged) with fp32 accumulation on v_mfma_f32_16x16x32_bf16 (the config-2 mode);
+ * flags&4 / flags&8 force the k-major / K-contiguous fp32 kernel (default: chosen by shape).
+ * Split-K (fixed-order, deterministic) when the output grid is small and ws is given.  bias_grad (batch 1 only, may be null) additionally receives
  * alpha * sum_k op(A)(m,k) (+ beta * bias_grad[m]) through an implicit ones column of op(B): the
  * bias gradient of a layer rides along its weight-gradient GEMM.  Replaces nn.Conv2d 1x1 /
  * 3x3-after-im2col / nn.Linear / torch.matmul forward and backward (Mutimodality_Mamba7.py:258,
@@ -58,6 +60,12 @@ VC_API int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha, 
                       long strideC, int batch, const float* bias, const float* addend, long add_ld, int add_mod,
                       int flags, float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
                       int n_counters, hipStream_t stream);
+
+/* Measurement hook: force the tile (bm, bn in {64, 128}), split-K slice count, prefetch depth
+ * (pf in {1, 2}) and combine path (combine: 1 in-launch, 0 separate reduce kernel) of the following
+ * vc_gemm / vc_gemm_ex calls; 0 (-1 for combine) restores the automatic choice.  Process-global
+ * state for tuning tools (tools/gemm_sweep.py), not for concurrent use. */
+VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
 
 /* out[c] = beta*out[c] + sum_r X[r*ldx + c]  (bias gradients; fixed-order two-stage) */
 VC_API int vc_colsum(int R, int C, const float* X, long ldx, float* out, float beta,

@@ -113,14 +113,23 @@ def test_fusat_gpu_backward_b4():
     params = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
     ref = O.forward(params, x1, x2, train=True)
     torch.nn.functional.cross_entropy(ref, t, weight=w).backward()
+    # float64 evaluation: the yardstick for "as accurate as the fp32 reference" (six train-mode
+    # BatchNorms deep, the first convolution's weight gradient carries ~1e-3 relative fp32 noise)
+    p64 = {k: (v.double() if v.is_floating_point() else v).clone().requires_grad_(v.is_floating_point() and
+                                                                                   "running" not in k)
+           for k, v in sd.items()}
+    ref64 = O.forward(p64, x1.double(), x2.double(), train=True)
+    torch.nn.functional.cross_entropy(ref64, t, weight=w.double()).backward()
     m = m.to("cuda").train()
     logits = m(x1.cuda(), x2.cuda())
     loss = CrossEntropyLoss(weight=w.cuda())(logits, t.cuda())
     loss.backward()
     assert _rel(logits.detach().cpu(), ref.detach()) < 1e-3
     named = dict(m.named_parameters())
-    gmax = max(float(params[k].grad.norm()) for k in named)
+    gmax = max(float(p64[k].grad.norm()) for k in named)
     for k, p in named.items():
-        g = params[k].grad
-        err = float((p.grad.cpu() - g).norm())
-        assert err <= 1e-3 * float(g.norm()) + 1e-5 * gmax, (k, err, float(g.norm()))
+        g64 = p64[k].grad
+        err = float((p.grad.cpu().double() - g64).norm())
+        err32 = float((params[k].grad.double() - g64).norm())
+        assert err <= 1e-3 * float(g64.norm()) + 1e-5 * gmax or err <= 3.0 * err32 + 1e-5 * gmax, \
+            (k, err, err32, float(g64.norm()))

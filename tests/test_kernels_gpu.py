@@ -39,39 +39,56 @@ def rnd(*shape, seed=0, scale=1.0):
     return (torch.rand(*shape, generator=g) * 2 - 1) * scale
 
 
+# vc_gemm flags: bit 0 ReLU, bit 1 bf16 operands (fp32 accumulate), bit 2 / bit 3 force the k-major /
+# the K-contiguous fp32 kernel (default: chosen by shape)
+F_BF16, F_LEGACY, F_V2 = 2, 4, 8
+KERNELS = [0, F_LEGACY, F_V2, F_BF16]
+
+
+def bf16_round(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+@pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("M,N,K", [(5184, 144, 144), (37, 41, 9), (1, 16, 128), (130, 70, 1296), (68, 132, 100), (260, 36, 44)])
-def test_gemm_layouts(L, ws, ta, tb, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(5184, 144, 144), (37, 41, 9), (1, 16, 128), (130, 70, 1296), (68, 132, 100),
+                                   (260, 36, 44), (3136, 256, 1296)])
+def test_gemm_layouts(L, ws, kern, ta, tb, M, N, K):
+    """fp32 kernels vs the fp32 product; the bf16 kernel vs the fp32 product of the bf16-rounded
+    operands (RNE, as torch) - the same products, so only the summation order differs."""
     A = rnd(K, M, seed=1) if ta else rnd(M, K, seed=1)
     B = rnd(N, K, seed=2) if tb else rnd(K, N, seed=2)
     bias = rnd(N, seed=3)
-    ref = (A.t() if ta else A) @ (B.t() if tb else B) + bias
+    Ar, Br = (bf16_round(A), bf16_round(B)) if kern & F_BF16 else (A, B)
+    ref = (Ar.t() if ta else Ar).double() @ (Br.t() if tb else Br).double() + bias.double()
     Ad, Bd, bd = A.to(DEV), B.to(DEV), bias.to(DEV)
     C = torch.full((M, N), float("nan"), device=DEV)
     lda = M if ta else K
     ldb = K if tb else N
-    L.vc_gemm(ta, tb, M, N, K, 1.0, P(Ad), lda, 0, P(Bd), ldb, 0, 0.0, P(C), N, 0, 1, P(bd), None, 0, 0, 0,
+    L.vc_gemm(ta, tb, M, N, K, 1.0, P(Ad), lda, 0, P(Bd), ldb, 0, 0.0, P(C), N, 0, 1, P(bd), None, 0, 0, kern,
               None, P(ws), ws.numel(), S())
     torch.cuda.synchronize()
-    assert rel_err(C.cpu().numpy(), ref.numpy()) < 1e-5
+    assert rel_err(C.cpu().numpy(), ref.float().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("M,N,K", [(144, 144, 5184), (41, 72, 51840), (256, 1296, 3136)])
-def test_gemm_splitk_weight_grad(L, ws, M, N, K):
+def test_gemm_splitk_weight_grad(L, ws, kern, M, N, K):
     # dW[M,N] = dY[K,M]^T X[K,N] accumulated into existing (beta=1)
     dY, X = rnd(K, M, seed=4), rnd(K, N, seed=5)
     C0 = rnd(M, N, seed=6)
-    ref = dY.t() @ X * 0.5 + C0
+    dYr, Xr = (bf16_round(dY), bf16_round(X)) if kern & F_BF16 else (dY, X)
+    ref = (dYr.t().double() @ Xr.double() * 0.5 + C0.double()).float()
     C = C0.to(DEV)
     dYd, Xd = dY.to(DEV), X.to(DEV)  # keep device copies alive until the kernel has run
     bg0 = rnd(M, seed=7)
     bg = bg0.to(DEV)
-    L.vc_gemm(1, 0, M, N, K, 0.5, P(dYd), M, 0, P(Xd), N, 0, 1.0, P(C), N, 0, 1, None, None, 0, 0, 0,
+    L.vc_gemm(1, 0, M, N, K, 0.5, P(dYd), M, 0, P(Xd), N, 0, 1.0, P(C), N, 0, 1, None, None, 0, 0, kern,
               P(bg), P(ws), ws.numel(), S())
     torch.cuda.synchronize()
     assert rel_err(C.cpu().numpy(), ref.numpy()) < 1e-5
     # fused bias gradient: column sums of op(A) through the implicit ones column of op(B)
-    assert rel_err(bg.cpu().numpy(), (dY.sum(0) * 0.5 + bg0).numpy()) < 1e-5
+    assert rel_err(bg.cpu().numpy(), (dYr.double().sum(0) * 0.5 + bg0.double()).float().numpy()) < 1e-5
 
 
 @pytest.mark.parametrize("M,N,K", [(72, 9, 51840), (16, 9, 64), (256, 1296, 200)])
@@ -87,24 +104,26 @@ def test_gemm_bias_grad_overwrite(L, ws, M, N, K):
     assert rel_err(bg.cpu().numpy(), dY.sum(0).numpy()) < 1e-5
 
 
-def test_gemm_batched_relu_addend(L, ws):
+@pytest.mark.parametrize("kern", KERNELS)
+def test_gemm_batched_relu_addend(L, ws, kern):
     Bt, M, N, K = 64, 49, 256, 81
     A, X = rnd(Bt, M, K, seed=7), rnd(Bt, K, N, seed=8)
     add = rnd(M, N, seed=9)
-    ref = torch.relu(torch.bmm(A, X) / 81.0)
+    rd = bf16_round if kern & F_BF16 else (lambda t: t)
+    ref = torch.relu(torch.bmm(rd(A).double(), rd(X).double()) / 81.0).float()
     C = torch.empty(Bt, M, N, device=DEV)
     Ad, Xd = A.to(DEV), X.to(DEV)
     L.vc_gemm(0, 0, M, N, K, 1.0 / 81, P(Ad), K, M * K, P(Xd), N, K * N, 0.0, P(C), N, M * N, Bt,
-              None, None, 0, 0, 1, None, P(ws), ws.numel(), S())
+              None, None, 0, 0, 1 | kern, None, P(ws), ws.numel(), S())
     torch.cuda.synchronize()
     assert rel_err(C.cpu().numpy(), ref.numpy()) < 1e-5
     # addend with row modulo (positional embedding broadcast over the batch)
     A2, W = rnd(4 * M, K, seed=10), rnd(N, K, seed=11)
-    ref2 = A2 @ W.t() + add.repeat(4, 1)
+    ref2 = (rd(A2).double() @ rd(W).double().t() + add.repeat(4, 1).double()).float()
     C2 = torch.empty(4 * M, N, device=DEV)
     A2d, Wd, addd = A2.to(DEV), W.to(DEV), add.to(DEV)
     L.vc_gemm(0, 1, 4 * M, N, K, 1.0, P(A2d), K, 0, P(Wd), K, 0, 0.0, P(C2), N, 0, 1, None,
-              P(addd), N, M, 0, None, P(ws), ws.numel(), S())
+              P(addd), N, M, kern, None, P(ws), ws.numel(), S())
     torch.cuda.synchronize()
     assert rel_err(C2.cpu().numpy(), ref2.numpy()) < 1e-5
 
@@ -176,10 +195,11 @@ def test_batchnorm_train_fwd_bwd(L, ws, M, C, relu):
     assert rel_err(db.cpu().numpy(), br.grad.numpy()) < 1e-4
 
 
+@pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("ta,tb,M,N,K,bgrad", [(1, 0, 72, 9, 51840, True), (1, 0, 256, 1296, 3136, True),
                                                (0, 1, 3136, 256, 1296, False), (1, 0, 41, 72, 51840, False),
                                                (0, 0, 3136, 256, 512, False)])
-def test_gemm_ex_in_launch_splitk_is_bit_identical(L, ws, ta, tb, M, N, K, bgrad):
+def test_gemm_ex_in_launch_splitk_is_bit_identical(L, ws, kern, ta, tb, M, N, K, bgrad):
     """vc_gemm_ex (last-arriving slice combines) == vc_gemm (separate reduce kernel), bit for bit,
     and the tile counters are left zero for the next call."""
     A = (rnd(K, M, seed=31) if ta else rnd(M, K, seed=31)).to(DEV)
@@ -190,8 +210,8 @@ def test_gemm_ex_in_launch_splitk_is_bit_identical(L, ws, ta, tb, M, N, K, bgrad
     for ex in (False, True):
         C = torch.full((M, N), float("nan"), device=DEV)
         bg = torch.full((M,), float("nan"), device=DEV) if bgrad else None
-        args = (ta, tb, M, N, K, 1.0, P(A), lda, 0, P(B), ldb, 0, 0.0, P(C), N, 0, 1, None, None, 0, 0, 0, P(bg),
-                P(ws), ws.numel())
+        args = (ta, tb, M, N, K, 1.0, P(A), lda, 0, P(B), ldb, 0, 0.0, P(C), N, 0, 1, None, None, 0, 0, kern,
+                P(bg), P(ws), ws.numel())
         for _ in range(2):  # twice: the counters must be back at zero after the first call
             if ex:
                 L.vc_gemm_ex(*args, P(cnt), cnt.numel(), S())
@@ -203,7 +223,8 @@ def test_gemm_ex_in_launch_splitk_is_bit_identical(L, ws, ta, tb, M, N, K, bgrad
     if bgrad:
         assert torch.equal(outs[0][1], outs[1][1])
     assert int(cnt.abs().sum()) == 0
-    ref = (A.t() if ta else A).cpu() @ (B.t() if tb else B).cpu()
+    rd = bf16_round if kern & F_BF16 else (lambda t: t)
+    ref = ((rd(A.t() if ta else A).cpu().double() @ rd(B.t() if tb else B).cpu().double())).float()
     assert rel_err(outs[1][0].numpy(), ref.numpy()) < 1e-5
 
 

@@ -1,5 +1,6 @@
 """GPU tool: every vc_gemm_ex call of one training step (B=64), re-timed in isolation with HIP events.
-Prints shape, layout, split, time and TFLOP/s per call, sorted by time.
+Prints shape, layout and time per call for the first-round fp32 kernel (legacy), the current fp32
+kernel and the bf16-operand kernel, sorted by the current fp32 time.
 usage: python tools/gemm_census.py [reps]"""
 import os
 import sys
@@ -35,11 +36,9 @@ def main():
     L.vc_gemm_ex = orig
     raw = L.raw["vc_gemm_ex"]
     st = torch.cuda.Stream(dev)
-    rows = []
-    for a in calls:
-        ta, tb, M, N, K = a[0], a[1], a[2], a[3], a[4]
-        batch = a[16]
+    def time_call(a, extra_flags):
         args = list(a[:-1]) + [st.cuda_stream]
+        args[21] = a[21] | extra_flags
         for _ in range(3):
             raw(*args)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -48,15 +47,24 @@ def main():
             raw(*args)
         e1.record(st)
         e1.synchronize()
-        us = e0.elapsed_time(e1) / reps * 1e3
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    rows = []
+    for a in calls:
+        ta, tb, M, N, K = a[0], a[1], a[2], a[3], a[4]
+        batch = a[16]
+        t_leg, t_new, t_bf = time_call(a, 4), time_call(a, 8), time_call(a, 2)
         fl = 2.0 * M * N * K * batch
-        rows.append((us, ta, tb, M, N, K, batch, a[22] is not None, fl / us * 1e-6))
+        rows.append((t_new, t_leg, t_bf, ta, tb, M, N, K, batch, a[22] is not None, fl / t_new * 1e-6,
+                     fl / t_bf * 1e-6))
     rows.sort(reverse=True)
-    tot = sum(r[0] for r in rows)
-    print(f"{len(rows)} GEMMs, isolated sum {tot:.1f} us, {sum(2.0*r[3]*r[4]*r[5]*r[6] for r in rows)/tot*1e-6:.1f} TFLOP/s")
-    print("   us   tA tB      M      N      K  batch bgrad  TFLOP/s")
+    tots = [sum(r[i] for r in rows) for i in range(3)]
+    fl = sum(2.0 * r[5] * r[6] * r[7] * r[8] for r in rows)
+    print(f"{len(rows)} GEMMs, isolated sums: fp32 {tots[0]:.1f} us ({fl/tots[0]*1e-6:.1f} TFLOP/s), "
+          f"legacy fp32 {tots[1]:.1f} us, bf16 {tots[2]:.1f} us ({fl/tots[2]*1e-6:.1f} TFLOP/s)")
+    print("  fp32  legacy   bf16  tA tB      M      N      K  batch bgrad  TF(fp32) TF(bf16)")
     for r in rows:
-        print("%7.1f  %d  %d %6d %6d %6d %5d %5s %8.1f" % r)
+        print("%6.1f %7.1f %6.1f  %d  %d %6d %6d %6d %5d %5s %8.1f %8.1f" % r)
 
 
 if __name__ == "__main__":

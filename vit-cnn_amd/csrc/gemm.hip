@@ -1,5 +1,6 @@
-// fp32 GEMM on CDNA4 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 fma chain),
-// plus split-K reduction and deterministic column sums.
+// GEMM on CDNA4 matrix cores: fp32 (v_mfma_f32_16x16x4_f32, an exact fp32 fma chain) or bf16
+// operands with fp32 accumulation (v_mfma_f32_16x16x32_bf16, the config-2 precision mode), plus
+// split-K reduction and deterministic column sums.
 //
 // Every dense contraction of the ViT-CNN step goes through vc_gemm: the 1x1 convolutions
 // (patch_embed, change_dim, channel_feature, NonLocal theta/phi/g/W, fusion layers;
@@ -16,7 +17,7 @@ namespace {
 constexpr int BM = 64, BN = 64;
 constexpr int LDS_STRIDE = 81;  // 64 + 17: conflict-free fragment reads, <=2-way stores
 
-enum { F_RELU = 1 };
+enum { F_RELU = 1, F_BF16 = 2, F_LEGACY = 4, F_V2 = 8 };
 
 struct Epi {
   float alpha, beta;
@@ -279,17 +280,469 @@ __global__ __launch_bounds__(256) void colsum_partial(int R, int Cn, const float
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------------
+// gemm_mfma: K-contiguous LDS images, fp32 (v_mfma_f32_16x16x4_f32) or bf16 operands
+// (v_mfma_f32_16x16x32_bf16, fp32 accumulation).
+//
+// Both operands are staged as K-contiguous LDS images: a tile row holds 128 B of k (32 fp32 or 64
+// bf16) as eight 16-B chunks, chunk c of row r at slot c ^ ((r >> 1) & 7).  The XOR makes the
+// fragment reads (ds_read_b128: rows lane&15, chunks lane>>4) and the staging writes
+// (ds_write_b128) bank-conflict-free.  A lane reads one 16-B chunk per operand, 16-row tile and
+// sub-step: in bf16 that is the 8-element k fragment of one 16x16x32 MFMA; in fp32 its 4 elements
+// feed four 16x16x4 MFMAs in which lane group g = lane>>4 supplies k = 4g + j (the k order inside
+// a 16-wide step is permuted identically for A and B: the same products, summed in another
+// order).  Two LDS stages and one barrier per k-tile: the next tile's global loads are in flight
+// while the current one is multiplied.  bf16 operands are rounded (RNE, v_cvt_pk_bf16_f32) as
+// they are staged, so activations stay fp32 in HBM and the mode only changes the contraction.
+namespace g2 {
+
+constexpr int ROWB = 128;  // bytes of k per LDS tile row and k-tile
+
+__device__ __forceinline__ int lds_off(int r, int c) { return (r << 7) + ((c ^ ((r >> 1) & 7)) << 4); }
+
+typedef float vf2 __attribute__((ext_vector_type(2)));
+typedef __bf16 vb2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((vf2){lo, hi}, vb2));
+}
+
+// One operand's share of a k-tile.  Element (r, k) of the operand is T ? p[k*ld + r] : p[r*ld + k]
+// for r < R and k < kend, else 0; with ONES, row R reads 1.0 (op(B)'s implicit ones column).
+// Both images of a tile take ROWS x 128 B of LDS, laid out after the source's contiguous axis:
+//  * K-contiguous sources (T = 0): [row][k] — eight 16-B k-chunks per row, chunk c of row r at
+//    slot c ^ ((r >> 1) & 7).  A thread owns chunks (row (tid>>3) + 32i, chunk tid&7) and reads
+//    each as float4s; a fragment is one ds_read_b128 (rows lane&15, chunk lane>>4).
+//  * row-contiguous sources (T = 1, the weight gradients' dY / X and the data gradients' W): [k][row]
+//    — a thread reads float4s along rows (16 lanes = 64 rows = 256 coalesced bytes at one k) and
+//    stores them as one 16-B (fp32) / 8-B (bf16) piece.  fp32 fragments are four ds_read_b32 (one
+//    k each); bf16 fragments two ds_read_b64_tr_b16 (4 k-rows x 16 columns each, delivered
+//    column-major: the hardware transpose).  16-column blocks are XOR-swizzled by k so the
+//    fragment reads and the stores are bank-conflict-free.
+// Fragment k order (both images, so A and B always pair the same k): bf16 lane group g = lane>>4 of
+// sub-step s holds k = 32s + 8g + j (j < 8); fp32 element j of group g holds k = 16s + 4g + j.
+// `vec`: the operand allows the vector loads (alignment, leading dimension), a uniform flag.
+template <bool BF, bool T, int ROWS, bool ONES>
+struct Stage {
+  static constexpr int KT = BF ? 64 : 32;      // k per tile
+  static constexpr int NR = KT * ROWS / 256;   // staged floats per thread
+  static constexpr int E = BF ? 8 : 4;         // KC: elements per 16-B chunk
+  float raw[NR];
+
+  __device__ __forceinline__ static float at(const float* p, long ld, int R, int kend, bool ones, int r, int k) {
+    if (k >= kend) return 0.f;
+    if (r < R) return T ? p[(long)k * ld + r] : p[(long)r * ld + k];
+    return (ONES && ones && r == R) ? 1.f : 0.f;
+  }
+
+  // RC image offsets
+  __device__ __forceinline__ static int rc_off(int k, int col) {
+    if (BF) {
+      const int x = ROWS == 64 ? (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) : ((k & 3) | (((k >> 3) & 1) << 2));
+      return k * (ROWS * 2) + ((((col >> 4) ^ x)) << 5) + ((col & 15) << 1);
+    }
+    return k * (ROWS * 4) + ((((col >> 4) ^ ((k >> 2) & 1))) << 6) + ((col & 15) << 2);
+  }
+
+  __device__ __forceinline__ void load(const float* p, long ld, int R, int row0, int k0, int kend, bool ones,
+                                       bool vec, int tid) {
+    if constexpr (!T) {
+#pragma unroll
+      for (int i = 0; i < NR / E; ++i) {
+        const int r = row0 + (tid >> 3) + 32 * i, k = k0 + (tid & 7) * E;
+        if (vec && r < R && k + E <= kend) {
+          const float* s = p + (long)r * ld + k;
+#pragma unroll
+          for (int v = 0; v < E / 4; ++v) {
+            const float4 x = *reinterpret_cast<const float4*>(s + 4 * v);
+            raw[i * E + 4 * v] = x.x;
+            raw[i * E + 4 * v + 1] = x.y;
+            raw[i * E + 4 * v + 2] = x.z;
+            raw[i * E + 4 * v + 3] = x.w;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < E; ++j) raw[i * E + j] = at(p, ld, R, kend, ones, r, k + j);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NR / 4; ++i) {
+        const int idx = tid + 256 * i;
+        const int k = k0 + idx / (ROWS / 4), r = row0 + 4 * (idx % (ROWS / 4));
+        if (vec && r + 3 < R && k < kend) {
+          const float4 x = *reinterpret_cast<const float4*>(p + (long)k * ld + r);
+          raw[4 * i] = x.x;
+          raw[4 * i + 1] = x.y;
+          raw[4 * i + 2] = x.z;
+          raw[4 * i + 3] = x.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) raw[4 * i + j] = at(p, ld, R, kend, ones, r + j, k);
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+    if constexpr (!T) {
+#pragma unroll
+      for (int i = 0; i < NR / E; ++i) {
+        const int r = (tid >> 3) + 32 * i, c = tid & 7;
+        uint4 w;
+        if (BF) {
+          w.x = pk_bf16(raw[i * E], raw[i * E + 1]);
+          w.y = pk_bf16(raw[i * E + 2], raw[i * E + 3]);
+          w.z = pk_bf16(raw[i * E + 4 % E], raw[i * E + 5 % E]);
+          w.w = pk_bf16(raw[i * E + 6 % E], raw[i * E + 7 % E]);
+        } else {
+          w.x = __float_as_uint(raw[i * E]);
+          w.y = __float_as_uint(raw[i * E + 1]);
+          w.z = __float_as_uint(raw[i * E + 2 % E]);
+          w.w = __float_as_uint(raw[i * E + 3 % E]);
+        }
+        *reinterpret_cast<uint4*>(lds + lds_off(r, c)) = w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NR / 4; ++i) {
+        const int idx = tid + 256 * i;
+        const int k = idx / (ROWS / 4), col = 4 * (idx % (ROWS / 4));
+        if (BF) {
+          uint2 w;
+          w.x = pk_bf16(raw[4 * i], raw[4 * i + 1]);
+          w.y = pk_bf16(raw[4 * i + 2], raw[4 * i + 3]);
+          *reinterpret_cast<uint2*>(lds + rc_off(k, col)) = w;
+        } else {
+          *reinterpret_cast<float4*>(lds + rc_off(k, col)) =
+              make_float4(raw[4 * i], raw[4 * i + 1], raw[4 * i + 2], raw[4 * i + 3]);
+        }
+      }
+    }
+  }
+
+  // the lane's fragment of the 16-row block starting at `rowbase`, sub-step s (bit pattern: 4 fp32
+  // or 8 bf16 in the k order above)
+  __device__ __forceinline__ static uint4 frag(const char* lds, int rowbase, int s, int lane) {
+    const int g = lane >> 4, l16 = lane & 15;
+    if constexpr (!T) {
+      return *reinterpret_cast<const uint4*>(lds + lds_off(rowbase + l16, 4 * s + g));
+    } else if constexpr (BF) {
+      typedef short s4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) s4 lds_s4;
+      const int q = l16 >> 2, pcol = l16 & 3;
+      uint4 out;
+      const s4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s4*)(lds + rc_off(32 * s + 8 * g + q, rowbase + 4 * pcol)));
+      const s4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s4*)(lds + rc_off(32 * s + 8 * g + 4 + q, rowbase + 4 * pcol)));
+      out.x = (uint32_t)(uint16_t)v0[0] | ((uint32_t)(uint16_t)v0[1] << 16);
+      out.y = (uint32_t)(uint16_t)v0[2] | ((uint32_t)(uint16_t)v0[3] << 16);
+      out.z = (uint32_t)(uint16_t)v1[0] | ((uint32_t)(uint16_t)v1[1] << 16);
+      out.w = (uint32_t)(uint16_t)v1[2] | ((uint32_t)(uint16_t)v1[3] << 16);
+      return out;
+    } else {
+      uint4 out;
+      const int k = 16 * s + 4 * g, col = rowbase + l16;
+      out.x = *reinterpret_cast<const uint32_t*>(lds + rc_off(k, col));
+      out.y = *reinterpret_cast<const uint32_t*>(lds + rc_off(k + 1, col));
+      out.z = *reinterpret_cast<const uint32_t*>(lds + rc_off(k + 2, col));
+      out.w = *reinterpret_cast<const uint32_t*>(lds + rc_off(k + 3, col));
+      return out;
+    }
+  }
+};
+
+// the wave's MT x NT tiles of 16x16 over one k-tile (two sub-steps).  fp32 keeps NC = 2 partial
+// accumulators per tile, one per sub-step s: two fma chains of half the length (long-K accuracy,
+// tools/gemm_err.py; with slices capped at 2048 of K the chains stay <= 1024 deep), and the MFMAs of
+// one fragment element go round all MT*NT accumulators before the next element (dependent issues
+// MT*NT >= 4 apart; 16x16x4 f32: 32-cycle issue, 40-cycle dependent latency).
+template <bool BF, int MT, int NT, class SA, class SB, int NC>
+__device__ __forceinline__ void mma_ktile(const char* As, const char* Bs, int arow, int brow, int lane,
+                                          f32x4 (&acc)[NC][MT][NT]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    uint4 a[MT], b[NT];
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) a[mi] = SA::frag(As, arow + 16 * mi, s, lane);
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni) b[ni] = SB::frag(Bs, brow + 16 * ni, s, lane);
+    if (BF) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+          acc[0][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[mi]),
+                                                                   __builtin_bit_cast(bf16x8, b[ni]), acc[0][mi][ni], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NT; ++ni)
+            acc[s % NC][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                __uint_as_float(a[mi][j]), __uint_as_float(b[ni][j]), acc[s % NC][mi][ni], 0, 0, 0);
+    }
+  }
+}
+
+// The fixed summation order of split-K slices (both combine paths): G interleaved partial sums
+// s_g = sum over z = g, g+G, ... (ascending), then s_0 + s_1 + ... + s_{G-1} left to right.  G (a
+// power of two <= 16) depends on nsplit only (slab_groups), so the in-launch and the separate
+// combine give bit-identical results.
+static inline int slab_groups(int nsplit) {
+  int g = 1;
+  while (g < 16 && 4 * (2 * g) <= nsplit) g *= 2;
+  return g;
+}
+
+__device__ __forceinline__ float slab_sum(const float* p, long slab, int nsplit, int G) {
+  float s[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) s[g] = 0.f;
+  for (int z0 = 0; z0 < nsplit; z0 += G) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+      if (g < G && z0 + g < nsplit) s[g] += p[(z0 + g) * slab];
+  }
+  float t = s[0];
+#pragma unroll
+  for (int g = 1; g < 16; ++g)
+    if (g < G) t += s[g];
+  return t;
+}
+
+// Block = 4 waves (2 x 2) over a BM x BN output tile, each wave (BM/2) x (BN/2).  1-D grid of
+// nsplit * tn * tm * batch blocks in XCD-aware order: the hardware deals block i to XCD i % 8, and
+// each XCD gets a contiguous run of logical blocks (split slice fastest, then n, m, batch): the K
+// slices of one tile run together on one XCD, so the in-launch combine reads their slabs from that
+// XCD's L2, and tiles sharing an A row panel meet in the same L2.
+template <bool BF, int BM, int BN, bool TA, bool TB, int PF>
+__global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g, int tn, int tm, unsigned total, int va, int vb,
+                                                  int G, int zfast) {
+  constexpr int KT = BF ? 64 : 32;
+  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int STAGE = (BM + BN) * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const unsigned bid = blockIdx.x, q8 = total >> 3, r8 = total & 7, x8 = bid & 7;
+  const unsigned lin = x8 * q8 + min(x8, r8) + (bid >> 3);
+  // zfast: split slice fastest (the slices of a tile share an XCD: L2-local in-launch combine);
+  // else tiles fastest (the tiles of one K slice share an XCD: its A / B rows are fetched once)
+  int zs, xn, ym, zb;
+  if (zfast) {
+    zs = (int)(lin % (unsigned)g.nsplit);
+    const unsigned t1 = lin / (unsigned)g.nsplit;
+    xn = (int)(t1 % (unsigned)tn);
+    const unsigned t2 = t1 / (unsigned)tn;
+    ym = (int)(t2 % (unsigned)tm);
+    zb = (int)(t2 / (unsigned)tm);
+  } else {
+    xn = (int)(lin % (unsigned)tn);
+    const unsigned t1 = lin / (unsigned)tn;
+    ym = (int)(t1 % (unsigned)tm);
+    const unsigned t2 = t1 / (unsigned)tm;
+    zs = (int)(t2 % (unsigned)g.nsplit);
+    zb = (int)(t2 / (unsigned)g.nsplit);
+  }
+  const int z = zb * g.nsplit + zs;
+  const int m0 = ym * BM, n0 = xn * BN;
+  const int kbeg = zs * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const float* A = g.A + (long)zb * g.sA;
+  const float* Bp = g.B + (long)zb * g.sB;
+  const bool ones = g.Ne > g.N;
+
+  typedef Stage<BF, TA, BM, false> SA;
+  typedef Stage<BF, !TB, BN, true> SB;
+  SA sa[PF];
+  SB sb[PF];
+  constexpr int NC = BF ? 1 : 2;
+  f32x4 acc[NC][MT][NT];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // PF = register sets of staged tiles: PF = 2 keeps two k-tiles of global loads in flight behind
+  // the MFMAs of the current one (for the bandwidth-bound shapes), PF = 1 one.
+  const int nk = kend > kbeg ? (kend - kbeg + KT - 1) / KT : 0;
+  if (nk > 0) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+      if (p < nk) {
+        sa[p].load(A, g.lda, g.M, m0, kbeg + p * KT, kend, false, va, tid);
+        sb[p].load(Bp, g.ldb, g.N, n0, kbeg + p * KT, kend, ones, vb, tid);
+      }
+    sa[0].store(smem, tid);
+    sb[0].store(smem + BM * ROWB, tid);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      char* cur = smem + (t & 1) * STAGE;
+      char* nxt = smem + ((t & 1) ^ 1) * STAGE;
+      if (PF == 1) {
+        if (t + 1 < nk) {
+          sa[0].load(A, g.lda, g.M, m0, kbeg + (t + 1) * KT, kend, false, va, tid);
+          sb[0].load(Bp, g.ldb, g.N, n0, kbeg + (t + 1) * KT, kend, ones, vb, tid);
+        }
+        mma_ktile<BF, MT, NT, SA, SB, NC>(cur, cur + BM * ROWB, wm * (BM / 2), wn * (BN / 2), lane, acc);
+        if (t + 1 < nk) {
+          sa[0].store(nxt, tid);
+          sb[0].store(nxt + BM * ROWB, tid);
+        }
+      } else {
+        // tile t+1 sits in set (t+1)&1 (issued one iteration ago), tile t+2 goes into set t&1,
+        // whose tile t reached LDS in the previous iteration
+        if (t + 2 < nk) {
+          const int k2 = kbeg + (t + 2) * KT;
+          if (t & 1) {
+            sa[1 % PF].load(A, g.lda, g.M, m0, k2, kend, false, va, tid);
+            sb[1 % PF].load(Bp, g.ldb, g.N, n0, k2, kend, ones, vb, tid);
+          } else {
+            sa[0].load(A, g.lda, g.M, m0, k2, kend, false, va, tid);
+            sb[0].load(Bp, g.ldb, g.N, n0, k2, kend, ones, vb, tid);
+          }
+        }
+        mma_ktile<BF, MT, NT, SA, SB, NC>(cur, cur + BM * ROWB, wm * (BM / 2), wn * (BN / 2), lane, acc);
+        if (t + 1 < nk) {
+          if (t & 1) {
+            sa[0].store(nxt, tid);
+            sb[0].store(nxt + BM * ROWB, tid);
+          } else {
+            sa[1 % PF].store(nxt, tid);
+            sb[1 % PF].store(nxt + BM * ROWB, tid);
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // C/D map of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (BM / 2) + mi * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * (BN / 2) + ni * 16 + (lane & 15);
+        float v = acc[0][mi][ni][r];
+#pragma unroll
+        for (int c = 1; c < NC; ++c) v += acc[c][mi][ni][r];
+        if (m < g.M && n < g.Ne) {
+          if (g.nsplit > 1) g.part[((long)z * g.M + m) * g.Ne + n] = v;
+          else store_out(g, zb, m, n, v);
+        }
+      }
+  if (g.nsplit == 1 || !g.cnt) return;
+
+  // In-launch split-K combine (cdna_hip_programming.md, "In-launch split-K reduction"), as in the
+  // fp32 kernel above; the "last arriver" flag travels through the (now idle) staging LDS.
+  int* last = reinterpret_cast<int*>(smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int tile = (zb * tm + ym) * tn + xn;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = __hip_atomic_fetch_add(&g.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = (tk == (unsigned)(g.nsplit - 1));
+  }
+  __syncthreads();
+  if (!*last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const long slab = (long)g.M * g.Ne;
+  const float* pz = g.part + (long)zb * g.nsplit * slab;
+  for (int e = tid; e < BM * BN; e += 256) {
+    const int m = m0 + e / BN, n = n0 + e % BN;
+    if (m >= g.M || n >= g.Ne) continue;
+    store_out(g, zb, m, n, slab_sum(pz + (long)m * g.Ne + n, slab, g.nsplit, G));
+  }
+  if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Separate split-K combine for large slab volumes: a block covers 256/G lanes x 4 consecutive output
+// elements (row-major over [batch][M][Ne], so rows wrap) x G z-groups (z = g, g+G, ...); the G
+// partial sums meet in LDS and are added in slab_sum's order (bit-identical to the in-launch path).
+__global__ __launch_bounds__(256) void splitk_reduce4(GemmArgs g, long nelem, int G) {
+  __shared__ float sh[1024];
+  const int lanes = 256 / G;
+  const int lane = threadIdx.x % lanes, zg = threadIdx.x / lanes;
+  const int per_block = 4 * lanes;
+  const long e0 = (long)blockIdx.x * per_block + 4 * lane;
+  const long slab = (long)g.M * g.Ne;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long e = e0 + i;
+    if (e < nelem) {
+      const long b = e / slab, w = e - b * slab;
+      const float* p = g.part + b * g.nsplit * slab + w;
+      float a = 0.f;
+      for (int z = zg; z < g.nsplit; z += G) a += p[z * slab];
+      s[i] = a;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sh[zg * per_block + 4 * lane + i] = s[i];
+  __syncthreads();
+  for (int t = threadIdx.x; t < per_block; t += 256) {
+    const long e = (long)blockIdx.x * per_block + t;
+    if (e >= nelem) break;
+    float v = sh[t];
+    for (int q = 1; q < G; ++q) v += sh[q * per_block + t];
+    const long b = e / slab, w = e - b * slab;
+    store_out(g, (int)b, (int)(w / g.Ne), (int)(w % g.Ne), v);
+  }
+}
+
+}  // namespace g2
+
+
 // C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b] (+ bias[n]) (+ addend[(m % add_mod), n]) (relu);
 // bias_grad (optional): bias_grad[m] = alpha * sum_k op(A)(m,k) + beta * bias_grad[m]
-VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha,
+// tuning override (vc_gemm_tune): 0 / -1 fields = automatic choice
+struct G2Tune {
+  int bm, bn, nsplit, pf, combine;
+};
+static G2Tune g_tune = {0, 0, 0, 0, -1};
+
+VC_EXPORT int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine) {
+  VC_REQUIRE((bm == 0 || bm == 64 || bm == 128) && (bn == 0 || bn == 64 || bn == 128));
+  VC_REQUIRE(nsplit >= 0 && nsplit <= 4096 && pf >= 0 && pf <= 2 && combine >= -1 && combine <= 1);
+  g_tune = G2Tune{bm, bn, nsplit, pf, combine};
+  return VC_OK;
+}
+
+// largest per-tile slab volume (bytes) combined in-launch by the last-arriving slice (else a separate
+// reduce kernel); VITCNN_SPLITK_COMBINE overrides it for measurements
+static long g2_combine_limit() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("VITCNN_SPLITK_COMBINE");
+    v = e ? atol(e) : 4096;
+  }
+  return v;
+}
+
+// the k-major fp32 kernel (LDS [k][row], 16x16x4 f32)
+static int launch_legacy(int transA, int transB, int M, int N, int K, float alpha,
                          const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
                          float beta, float* C, long ldc, long strideC, int batch,
                          const float* bias, const float* addend, long add_ld, int add_mod, int flags,
                          float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
                          int n_counters, hipStream_t stream) {
-  VC_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1);
-  VC_REQUIRE(!bias_grad || batch == 1);
-  if (M == 0 || N == 0) return VC_OK;
   Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, flags};
   const int Ne = N + (bias_grad ? 1 : 0);
   const int tn = vc_cdiv(Ne, BN), tm = vc_cdiv(M, BM);
@@ -336,6 +789,111 @@ VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alph
   VC_CHECK_LAUNCH();
   if (nsplit > 1 && !cnt) {
     hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(Ne, 64), M, batch), dim3(64), 0, stream, g);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
+VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha,
+                         const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                         float beta, float* C, long ldc, long strideC, int batch,
+                         const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                         float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                         int n_counters, hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1);
+  VC_REQUIRE(!bias_grad || batch == 1);
+  if (M == 0 || N == 0) return VC_OK;
+  const bool bf = (flags & F_BF16) != 0;
+  // fp32: the k-major kernel (faster on every shape of the ViT-CNN step, tools/gemm_census.py) except
+  // long contractions (K >= 4096, e.g. FusAtNet's 3x3 convs over 1024-2193 channels), where the
+  // K-contiguous kernel's two accumulator chains and <= 2048-long slices keep the fp32 rounding at
+  // the CPU reference's level (tools/gemm_err.py).  F_LEGACY / F_V2 force either (tests, census).
+  const bool legacy = !bf && !(flags & F_V2) && ((flags & F_LEGACY) || K < 4096 || transA);
+  if (legacy)
+    return launch_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
+                         batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
+                         n_counters, stream);
+  Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, flags};
+  const int Ne = N + (bias_grad ? 1 : 0);
+  const int KT = bf ? 64 : 32;
+  // Configuration from the sweep of the step's shapes (tools/gemm_sweep.py):
+  //  * 64 x 64 tiles; bf16 takes 128-row tiles for grids of >= 1024 tiles (fewer B re-reads);
+  //  * split K when the grid is small (< 192 tiles) or K is long (>= 1024): slices of >= 2 k-tiles,
+  //    up to ~4 blocks per CU (1024 blocks), at most 256 slices; the weight gradients (K = rows,
+  //    tiny grids) end at 64-256 slices of 2-3 k-tiles each;
+  //  * two k-tiles of loads in flight (pf 2) for bf16 weight gradients, else one.
+  const int tiles64 = vc_cdiv(Ne, 64) * vc_cdiv(M, 64) * batch;
+  int BM = (bf && tiles64 >= 1024) ? 128 : 64;
+  int BN = 64;
+  if (g_tune.bm) BM = g_tune.bm;
+  if (g_tune.bn) BN = g_tune.bn;
+  const int tn = vc_cdiv(Ne, BN), tm = vc_cdiv(M, BM);
+  const long tiles = (long)tn * tm * batch;
+  int nsplit = 1;
+  if (K >= 4 * KT && (tiles < 192 || K >= 1024)) {
+    const long by_k = K / (2 * KT);
+    const long by_blocks = std::max<long>(1, 1024 / tiles);
+    nsplit = (int)std::min<long>(std::min<long>(by_k, by_blocks), 256);
+  }
+  if (!bf) nsplit = std::max(nsplit, vc_cdiv(K, 2048));  // fp32: slices of <= 2048 (accuracy)
+  if (g_tune.nsplit) nsplit = std::min(g_tune.nsplit, std::max(1, K / KT));
+  if (!ws) nsplit = 1;
+  while (nsplit > 1 && (long)nsplit * batch * M * Ne > ws_floats) --nsplit;
+  int k_chunk = vc_cdiv(K, KT) * KT;
+  if (nsplit > 1) {
+    k_chunk = vc_cdiv(vc_cdiv(K, nsplit), KT) * KT;
+    nsplit = vc_cdiv(K, k_chunk);
+  }
+  const int pf = g_tune.pf ? g_tune.pf : ((bf && transA) ? 2 : 1);
+  // the slices of a tile run side by side on one XCD (split index fastest in the block order), so
+  // the last arriver's slab reads are L2 hits: combine in-launch unless the tile's slabs are large
+  const long slab_bytes = (long)nsplit * std::min(BM, M) * std::min(BN, Ne) * 4;
+  bool inl = slab_bytes <= g2_combine_limit();
+  if (g_tune.combine >= 0) inl = g_tune.combine == 1;
+  unsigned int* cnt = (nsplit > 1 && tile_counters && tiles <= n_counters && inl) ? tile_counters : nullptr;
+  GemmArgs g{M, N, K, Ne, k_chunk, nsplit, A, lda, strideA, B, ldb, strideB, C, ldc, strideC, bias_grad, ws, cnt, epi};
+  const long total = tiles * nsplit;
+  VC_REQUIRE(total < (1L << 31));
+  // vector staging (float4 along the contiguous axis): 16-B aligned base, ld % 4, batch stride % 4
+  auto vec_ok = [&](const float* p, long ld, long stride) {
+    return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0) && (batch == 1 || stride % 4 == 0);
+  };
+  const int va = vec_ok(A, lda, strideA);
+  const int vb = vec_ok(B, ldb, strideB);
+  const int G = g2::slab_groups(nsplit);
+  const int zfast = cnt ? 1 : 0;
+  dim3 grid((unsigned)total), block(256);
+#define VC_G2(BF_, BM_, BN_, PF_)                                                                                 \
+  do {                                                                                                            \
+    if (transA && transB)                                                                                         \
+      hipLaunchKernelGGL((g2::gemm_mfma<BF_, BM_, BN_, true, true, PF_>), grid, block, 0, stream, g, tn, tm, (unsigned)total, va, vb, G, zfast);   \
+    else if (transA)                                                                                              \
+      hipLaunchKernelGGL((g2::gemm_mfma<BF_, BM_, BN_, true, false, PF_>), grid, block, 0, stream, g, tn, tm, (unsigned)total, va, vb, G, zfast);  \
+    else if (transB)                                                                                              \
+      hipLaunchKernelGGL((g2::gemm_mfma<BF_, BM_, BN_, false, true, PF_>), grid, block, 0, stream, g, tn, tm, (unsigned)total, va, vb, G, zfast);  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((g2::gemm_mfma<BF_, BM_, BN_, false, false, PF_>), grid, block, 0, stream, g, tn, tm, (unsigned)total, va, vb, G, zfast); \
+  } while (0)
+#define VC_G2_T(BF_, PF_)                                  \
+  do {                                                     \
+    if (BM == 128 && BN == 128) VC_G2(BF_, 128, 128, PF_); \
+    else if (BM == 128) VC_G2(BF_, 128, 64, PF_);          \
+    else if (BN == 128) VC_G2(BF_, 64, 128, PF_);          \
+    else VC_G2(BF_, 64, 64, PF_);                          \
+  } while (0)
+  if (bf) {
+    if (pf == 2) VC_G2_T(true, 2);
+    else VC_G2_T(true, 1);
+  } else {
+    if (pf == 2) VC_G2_T(false, 2);
+    else VC_G2_T(false, 1);
+  }
+#undef VC_G2_T
+#undef VC_G2
+  VC_CHECK_LAUNCH();
+  if (nsplit > 1 && !cnt) {
+    const long nelem = (long)batch * M * Ne;
+    hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, g, nelem, G);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;

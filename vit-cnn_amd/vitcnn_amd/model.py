@@ -46,6 +46,16 @@ UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
                    "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
 
 
+PRECISIONS = ("fp32", "bf16")
+GEMM_BF16 = 2              # vc_gemm flags bit: bf16 operands, fp32 accumulation
+
+
+def _check_precision(p):
+    if p not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {p!r}")
+    return p
+
+
 class _Workspace:
     """Named, persistent device buffers for one (device, batch, mode) — stable addresses."""
 
@@ -75,8 +85,9 @@ class Multimodality_Mamba(nn.Module):
     SURVEY.md section 8 row A-MUUFL)."""
 
     def __init__(self, img_size=9, patch_size=1, stride=1, in_channels1=144, in_channels2=1, dim_embedding=32,
-                 num_class=16, path_type="multi_clock_gate"):
+                 num_class=16, path_type="multi_clock_gate", *, precision="fp32"):
         super().__init__()
+        self.precision = _check_precision(precision)
         P = int(img_size)
         if P < 7:
             raise ValueError("ViT-CNN needs patches of at least 7x7 (two valid 3x3 stages + 2x2 pooling)")
@@ -196,6 +207,14 @@ class Multimodality_Mamba(nn.Module):
         if flat.dtype != torch.float32:
             raise RuntimeError("ViT-CNN MI355X path computes in fp32 master weights; dtype casts are not supported")
         self._rebind(flat, fn(self._bflat), fn(self._iflat))
+        return self
+
+    def set_precision(self, precision: str):
+        """Arithmetic of the dense contractions (BASELINE config 2): "fp32" (the parity mode, exact fp32
+        MFMA) or "bf16" (every GEMM's operands rounded to bf16 as they are staged, fp32 accumulation;
+        master weights, AdamW, the scan state, LayerNorm / BatchNorm / TokenLearner statistics and
+        all elementwise work stay fp32)."""
+        self.precision = _check_precision(precision)
         return self
 
     @property
@@ -356,6 +375,7 @@ class _Program:
         self._raw = [st.cuda_stream for st in self.streams]
         self._scr = [(scr.data_ptr(), scr.numel())] + [(t.data_ptr(), t.numel()) for _, t in lanes]
         self._cnt = [t.data_ptr() for t in model._tile_counters(device)]
+        self.gemm_flags = GEMM_BF16 if model.precision == "bf16" else 0
         self.cur = 0
         self._ev_i = 0
         self._ev_lane = {}
@@ -389,9 +409,11 @@ class _Program:
         self._ev_i += 1
         return e
 
-    def gemm(self, *args):
+    def gemm(self, *args, exact=False):
         """vc_gemm_ex on the current lane with its scratch and split-K tile counters; args are
-        vc_gemm's up to bias_grad"""
+        vc_gemm's up to bias_grad (flags at index 21 get the model's precision bit unless `exact`)"""
+        if self.gemm_flags and not exact:
+            args = args[:21] + (args[21] | self.gemm_flags,) + args[22:]
         self.L.vc_gemm_ex(*args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
 
     def mark(self):
@@ -430,10 +452,10 @@ class _Program:
 
     # ---------------------------------------------------------------- gemm wrappers
     def mm_nt(self, M, N, K, A, lda, W, ldw, C, ldc, bias=0, alpha=1.0, beta=0.0, add=0, add_ld=0, add_mod=0,
-              relu=0):
+              relu=0, exact=False):
         """C[M,N] = alpha * A[M,K] W[N,K]^T + beta*C + bias + addend"""
         self.gemm(0, 1, M, N, K, alpha, A, lda, 0, W, ldw, 0, beta, C, ldc, 0, 1, bias or None, add or None,
-                       add_ld, add_mod, relu, None)
+                  add_ld, add_mod, relu, None, exact=exact)
 
     def mm_nn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0):
         """C[M,N] = alpha * A[M,K] B[K,N] + beta*C"""
