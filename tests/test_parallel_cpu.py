@@ -179,3 +179,132 @@ def test_perparam_gradient_allreduce_world2():
     for r in range(2):
         for i, g in enumerate(out[r]):
             assert torch.allclose(g, torch.full_like(g, 1.5 * (i + 1)))
+
+
+def _bucket_worker(rank, world, port, out):
+    """GradExchange (the bench / fused-step exchange): each rank's oracle shard gradient is
+    all-reduced bucket by bucket in the backward's completion order; world 4."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from vitcnn_amd import Multimodality_Mamba, parallel
+    parallel.init_from_env(backend="gloo")
+    sd = hash_state_dict()
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
+    m.load_state_dict(sd)
+    ex = parallel.GradExchange(m)
+    grad = ex.begin(m, "cpu")
+    grad.copy_(_shard_grad8(m, sd, rank, world))
+
+    class _Opt:
+        grad_scale = 1.0
+
+    opt = _Opt()
+    for name in ex.order:
+        ex.bucket_ready(name, ())
+    ex.finish(opt)
+    out[rank] = (grad[: m.n_active_params].clone() * opt.grad_scale, opt.grad_scale, dict(ex.ranges))
+    dist.destroy_process_group()
+
+
+def _shard_grad8(model, sd, r, world):
+    """oracle gradient of shard r of an 8-patch batch split over `world` ranks, flat layout"""
+    from oracle import vitcnn_oracle as O
+    hsi, lidar, target = golden_batch("golden.dp8", 8)
+    b = 8 // world
+    sl = slice(r * b, (r + 1) * b)
+    st = O.make_state(sd)
+    O.train_step(st, hsi[sl], lidar[sl], target[sl], O.ce_class_weights(16))
+    flat = torch.zeros(model.flat_params.numel())
+    for n, off in model._poff.items():
+        g = st[n].grad
+        if g is not None:
+            flat[off:off + g.numel()] = g.reshape(-1)
+    return flat
+
+
+def test_bucketed_exchange_world4_equals_mean_of_shards():
+    """SURVEY.md 8(e) / VERDICT item 4: three head-first buckets (LiDAR+fusion+classifier, hsi2,
+    hsi1) tile the active gradient; their all-reduce over 4 ranks = the mean of the 4 shards'
+    oracle gradients, with 1/world folded into the optimizer's grad_scale."""
+    world = 4
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(world, port, out), nprocs=world, join=True)
+    sd = hash_state_dict()
+    m = _load(sd)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        ref = sum(_shard_grad8(m, sd, r, world) for r in range(world))[: m.n_active_params] / world
+    finally:
+        torch.set_num_threads(nt)
+    ranges = out[0][2]
+    assert ranges == {"tail": (1595080, 1660090), "hsi2": (873324, 1595080), "hsi1": (0, 873324)}
+    for r in range(world):
+        g, scale, _ = out[r]
+        assert scale == 1.0 / world
+        err = float((g - ref).abs().max() / ref.abs().max())
+        assert err < 1e-6, (r, err)
+
+
+def test_bucket_order_is_checked():
+    from vitcnn_amd import Multimodality_Mamba, parallel
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
+    ex = parallel.GradExchange(m)
+    ex.begin(m, "cpu")
+    ex.bucket_ready("hsi2")
+    ex.bucket_ready("tail")
+    ex.bucket_ready("hsi1")
+    with pytest.raises(RuntimeError):
+        ex.finish()
+
+
+def _bn_model_worker(rank, world, port, out):
+    """models without flat buffers (FusAtNet-like: Conv + BatchNorm, torch optimizer): parameter and
+    buffer broadcasts, and a gradient bucket when one rank's graph left a parameter without .grad"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from vitcnn_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    torch.manual_seed(rank)
+    m = torch.nn.Sequential(torch.nn.Conv2d(2, 3, 3), torch.nn.BatchNorm2d(3), torch.nn.Linear(3, 2))
+    m.train()
+    m(torch.rand(4, 2, 5, 5))   # rank-dependent running statistics
+    parallel.broadcast_parameters(m)
+    parallel.broadcast_buffers(m)
+    params = [p.detach().clone() for p in m.parameters()]
+    bufs = [b.clone() for b in m.buffers()]
+    for i, p in enumerate(m.parameters()):
+        p.grad = None if (rank == 1 and i == 0) else torch.full_like(p, float(rank + 1))
+    parallel.allreduce_gradients(m, torch.optim.Adam(m.parameters()))
+    out[rank] = (params, bufs, [p.grad.clone() for p in m.parameters()])
+    dist.destroy_process_group()
+
+
+def test_broadcasts_and_sparse_grads_without_flat_buffers():
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bn_model_worker, args=(2, port, out), nprocs=2, join=True)
+    p0, b0, g0 = out[0]
+    p1, b1, g1 = out[1]
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+    assert all(torch.equal(a, b) for a, b in zip(b0, b1))
+    for i, (a, b) in enumerate(zip(g0, g1)):
+        expect = 0.5 if i == 0 else 1.5     # rank 1 had no gradient for parameter 0: it counts as zeros
+        assert torch.allclose(a, torch.full_like(a, expect)) and torch.equal(a, b)
+
+
+def test_sharded_loader_partitions_batches():
+    from vitcnn_amd import parallel
+    batches = list(range(11))
+
+    class _L(list):
+        dataset = None
+
+    loader = _L(batches)
+    parts = [list(parallel.ShardedLoader(loader, r, 4)) for r in range(4)]
+    assert sorted(sum(parts, [])) == batches
+    assert [len(parallel.ShardedLoader(loader, r, 4)) for r in range(4)] == [len(p) for p in parts]

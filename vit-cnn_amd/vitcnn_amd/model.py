@@ -824,10 +824,21 @@ class _Program:
             self.wait(e_ch)
             self.mm_nn(rows, Cin, E, dT, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
 
-    def backward(self, dlogits, lanes=True):
+    def bucket_ready(self, hook, name, *side_events):
+        """Gradient bucket `name` is complete once lane 0 reaches this point and the given side-lane
+        events have fired: hand `hook` (data parallelism, parallel.GradExchange) one lane-0 event plus
+        the side events to order its collective after."""
+        if hook is None:
+            return
+        assert self.cur == 0
+        hook(name, [self.mark()] + list(side_events))
+
+    def backward(self, dlogits, lanes=True, bucket_hook=None, out=None):
+        """bucket_hook(name, events): called as each gradient bucket of parallel.GradExchange.BUCKETS
+        ("tail": LiDAR + fusion + classifier, "hsi2", "hsi1" — head side first) is complete."""
         m, B, ws = self.m, self.B, self.ws
         self.lanes_on = lanes and _LANES and os.environ.get("VITCNN_LANES_BWD", "1") != "0"
-        grad = torch.empty(m._n_params, dtype=torch.float32, device=self.device)
+        grad = out if out is not None else torch.empty(m._n_params, dtype=torch.float32, device=self.device)
         if m._n_params > m._n_active:  # parameters the reference forward never uses get no gradient
             self.L.vc_fill(m._n_params - m._n_active, grad.data_ptr() + F32 * m._n_active, 0.0, self.s)
         gb = grad.data_ptr()
@@ -847,7 +858,12 @@ class _Program:
             e_f1 = self.mark()
             self.conv_bn_relu3_bwd("lidar2", self.L1, Pp - 2, 16, 32, dL2, dL1, 1.0)
             self.conv_bn_relu3_bwd("lidar1", self.LX, Pp, m.c2, 16, dL1, 0, 0.0)
+            e_l3 = self.mark()
+        # classifier + fusion2 (lane 0 so far) and fusion1 + LiDAR (lane 3): the "tail" bucket
+        self.bucket_ready(bucket_hook, "tail", e_l3)
         self.block_bwd(m.hsi2, "hsi2", self.H1, Pp - 2, dH2, dH1, e_f1)
+        self.bucket_ready(bucket_hook, "hsi2")   # block_bwd joined its lane-1 chain before dH1
         self.block_bwd(m.hsi1, "hsi1", self.X0, Pp, dH1, None, None)
         self.join_lanes()
+        self.bucket_ready(bucket_hook, "hsi1")
         return grad

@@ -16,9 +16,14 @@ The reference's other branches import modules absent from the reference tree (SU
 row 22) and are out of scope for this path.
 
 Data parallelism: when a torch.distributed process group with more than
-one rank is initialised, `train` all-reduces the flat gradient after every backward (one RCCL
-call) and folds the 1/world average into the fused AdamW update; each rank iterates its own
-shard of the patches (see `parallel.shard_indices`).
+one rank is initialised, `train` starts every replica from rank 0's parameters, all-reduces the
+gradient after every backward (RCCL) and folds the 1/world average into the fused AdamW update;
+each rank iterates its own shard of the batches (a loader that is not already sharded is wrapped in
+`parallel.ShardedLoader`).
+
+Precision (BASELINE.json config 2): `get_model(..., precision="bf16")` builds ViT-CNN with bf16
+GEMM operands and fp32 accumulation (`Multimodality_Mamba.set_precision`); the default "fp32" is
+the parity mode.
 """
 from __future__ import annotations
 
@@ -73,9 +78,10 @@ def get_model(name, **kwargs):
     if kwargs["applyPCA"]:
         n_bands = 30
     path_type = "multi_clock_gate"
+    precision = kwargs.setdefault("precision", "fp32")
     model = Multimodality_Mamba(img_size=patch_size, patch_size=1, stride=1, in_channels1=n_bands,
                                 in_channels2=n_bands2, dim_embedding=embed_dim, num_class=n_classes,
-                                path_type=path_type)
+                                path_type=path_type, precision=precision)
     lr = kwargs.setdefault("lr", 8e-4)
     model = model.to(device)
     optimizer = AdamW(model.parameters(), lr=lr)
@@ -158,6 +164,10 @@ def train(savename, run, bands, net, optimizer, criterion, data_loader, epoch, s
     if supervision != "full":
         raise ValueError('supervision mode "{}" is unknown.'.format(supervision))
     net.to(device)
+    if parallel.is_distributed():
+        parallel.broadcast_parameters(net)       # replicas start identical (rank 0's values)
+        if not parallel.is_sharded(data_loader):
+            data_loader = parallel.ShardedLoader(data_loader, parallel.rank(), parallel.world())
     save_epoch = 16 if epoch == 128 else (epoch // 20 if epoch > 20 else 1)
     best_val_acc = 0.0
     best_model_wts = None
@@ -244,8 +254,18 @@ def test(run, net, img1, img2, hyperparams):
     the reference's `probs`."""
     net.eval()
     if hyperparams.get("applyPCA", False):
-        raise NotImplementedError("applyPCA is not on the ViT-CNN path")
+        img1 = apply_pca(img1, 3)   # model_utils.py:1076-1077 (3 components, as the reference)
     runner = SlidingWindowInference(net, img1, img2, patch_size=hyperparams["patch_size"],
                                     step=hyperparams.get("test_stride", 1), n_classes=hyperparams["n_classes"],
                                     device=hyperparams["device"])
     return runner.run(batch_size=hyperparams["batch_size"])
+
+
+def apply_pca(X, num_components):
+    """utils.py:85-93 applyPCA: whitened PCA of the [W, H, C] cube's pixel spectra (host-side data
+    preparation, as in the reference; sklearn's PCA)."""
+    from sklearn.decomposition import PCA
+    X = np.asarray(X)
+    flat = np.reshape(X, (-1, X.shape[2]))
+    flat = PCA(n_components=num_components, whiten=True).fit_transform(flat)
+    return np.reshape(flat, (X.shape[0], X.shape[1], num_components))

@@ -1,16 +1,27 @@
 """Data parallelism for the ViT-CNN training step: one process per GPU, RCCL over xGMI.
 
-The reference is single-process; patches are independent, so the
-minibatch shards across ranks and the only exchange per step is the gradient all-reduce.
+The reference is single-process (`Mutimodality_Mamba7.py:60` pins
+`cuda:0`); patches are independent, so the minibatch shards across ranks and the only exchange per
+step is the gradient all-reduce.
 
-* The model's gradients are ONE flat fp32 tensor (`model.flat_params.grad`), so the exchange is a
-  single `all_reduce(SUM)` of 1,660,090 floats (the 1,170 never-used parameters sit at the tail
-  of the buffer and are excluded).  The 1/world average is folded into the fused AdamW kernel
-  (`AdamW.grad_scale`) instead of a separate scaling pass.
+* The model's gradients are ONE flat fp32 tensor (`model.flat_params.grad`).  `GradExchange` splits
+  its active part (1,660,090 floats; the 1,170 never-used parameters sit at the tail and are
+  excluded) into three contiguous buckets in the order the backward completes them, head side
+  first: "tail" (LiDAR convs, fusion1/2, classifier: 65k floats), "hsi2" (722k), "hsi1" (873k).
+  Each bucket's RCCL all-reduce is issued on a side stream as soon as the backward program has
+  written it (`_Program.backward(bucket_hook=...)`), so the first two overlap the remaining
+  backward; the optimizer step waits for the side stream.  The 1/world average is folded into the
+  fused AdamW kernel (`AdamW.grad_scale`) instead of a separate scaling pass.  The buffers are
+  persistent, so the whole step — forward, backward, the bucket all-reduces and AdamW — can be
+  captured into one hipGraph (bench.py).
+* `allreduce_gradients` is the single-bucket form used by `train()` and by models without the
+  bucket layout (S2EFT's flat buffer; FusAtNet / plain torch modules: one flattened bucket over
+  every parameter that requires grad, zeros for parameters that got none, so every rank's bucket
+  has the same size and layout).
 * BatchNorm stays local (not SyncBN): each rank's B=64 forward equals the reference's B=64
   forward.  Running statistics are rank-local during training; `broadcast_buffers` copies
   rank 0's before evaluation / checkpointing (DDP `broadcast_buffers` semantics).
-* Parameters are broadcast from rank 0 once at start so every replica starts identical.
+* `broadcast_parameters` makes every replica start from rank 0's parameters (train() calls it).
 
 Everything here also works with the `gloo` backend on CPU tensors, which is how the N>1 path is
 tested without GPUs (tests/test_parallel_cpu.py).
@@ -62,8 +73,15 @@ def active_grad(model) -> torch.Tensor | None:
     return flat.grad[: model.n_active_params]
 
 
+def _set_scale(optimizer, grad, n):
+    if optimizer is not None and hasattr(optimizer, "grad_scale"):
+        optimizer.grad_scale = 1.0 / n
+    else:
+        grad.mul_(1.0 / n)
+
+
 def allreduce_gradients(model, optimizer=None, group=None):
-    """Sum the flat gradient over ranks; the 1/world average goes into the optimizer's fused
+    """Sum the gradient over ranks (one bucket); the 1/world average goes into the optimizer's fused
     update when it supports it (vitcnn_amd.AdamW.grad_scale), else the gradient is scaled."""
     if not is_distributed():
         if optimizer is not None and hasattr(optimizer, "grad_scale"):
@@ -71,41 +89,146 @@ def allreduce_gradients(model, optimizer=None, group=None):
         return
     n = dist.get_world_size(group)
     if not hasattr(model, "flat_params"):
-        # per-parameter gradients (FusAtNet: torch.optim.Adam over .grad): one flattened bucket
-        grads = [p.grad for p in model.parameters() if p.grad is not None]
-        if not grads:
-            raise RuntimeError("allreduce_gradients: backward has not produced a gradient")
-        bucket = torch.cat([g.reshape(-1) for g in grads])
+        # per-parameter gradients (FusAtNet / torch modules): one flattened bucket over EVERY
+        # parameter that requires grad (zeros where backward produced none), so the bucket size
+        # and offsets are the same on every rank whatever the local graph touched
+        params = [p for p in model.parameters() if p.requires_grad]
+        if not params:
+            raise RuntimeError("allreduce_gradients: the model has no trainable parameters")
+        bucket = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
         bucket.mul_(1.0 / n)
         o = 0
-        for g in grads:
-            g.copy_(bucket[o:o + g.numel()].view_as(g))
-            o += g.numel()
+        for p in params:
+            v = bucket[o:o + p.numel()].view_as(p)
+            if p.grad is None:
+                p.grad = v.clone()
+            else:
+                p.grad.copy_(v)
+            o += p.numel()
         return
     g = active_grad(model)
     if g is None:
         raise RuntimeError("allreduce_gradients: backward has not produced a gradient")
     dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
-    if optimizer is not None and hasattr(optimizer, "grad_scale"):
-        optimizer.grad_scale = 1.0 / n
-    else:
-        g.mul_(1.0 / n)
+    _set_scale(optimizer, g, n)
+
+
+# bucket name -> state_dict prefixes, in the order the backward program completes them
+BUCKETS = (("tail", ("lidar1.", "lidar2.", "fusion1.", "fusion2.", "classifier.")),
+           ("hsi2", ("hsi2.",)),
+           ("hsi1", ("hsi1.",)))
+
+
+def bucket_ranges(model):
+    """{bucket: (lo, hi)} over the model's flat parameter layout; the buckets are contiguous,
+    disjoint and together cover exactly the active parameters [0, n_active)."""
+    named = dict(model.named_parameters())
+    out = {}
+    for name, prefixes in BUCKETS:
+        offs = [(o, o + named[n].numel()) for n, o in model._poff.items()
+                if n.startswith(prefixes) and o < model.n_active_params]
+        lo, hi = min(a for a, _ in offs), max(b for _, b in offs)
+        if sum(b - a for a, b in offs) != hi - lo:
+            raise RuntimeError(f"gradient bucket {name} is not contiguous in the flat layout")
+        out[name] = (lo, hi)
+    spans = sorted(out.values())
+    if spans[0][0] != 0 or spans[-1][1] != model.n_active_params or \
+            any(a[1] != b[0] for a, b in zip(spans, spans[1:])):
+        raise RuntimeError("gradient buckets do not tile the active parameters")
+    return out
+
+
+class GradExchange:
+    """Bucketed gradient all-reduce overlapped with the backward.
+
+    Usage (vitcnn_amd.step.fused_train_step(..., exchange=ex)):
+        grad = ex.begin(model, device)            # persistent flat gradient buffer
+        prog.backward(dlog, bucket_hook=ex.bucket_ready, out=grad)
+        ex.finish(optimizer)                       # caller's stream waits for the last bucket
+    On GPU tensors each bucket's collective runs on the exchange's side stream after the events the
+    backward hands over; on CPU (gloo) it runs inline.  `force` exchanges even in a world of one
+    (exercises the collective path on a single device)."""
+
+    def __init__(self, model, group=None, force: bool = False):
+        self.ranges = bucket_ranges(model)
+        self.order = [n for n, _ in BUCKETS]
+        self.group = group
+        self.force = force
+        self.grad = None
+        self.stream = None
+        self.done = []
+
+    @property
+    def active(self) -> bool:
+        return is_distributed() or (self.force and dist.is_available() and dist.is_initialized())
+
+    def begin(self, model, device):
+        n = model.flat_params.numel()
+        if self.grad is None or self.grad.numel() != n or self.grad.device != torch.device(device):
+            self.grad = torch.empty(n, dtype=torch.float32, device=device)
+            if self.grad.is_cuda:
+                self.stream = torch.cuda.Stream(device)
+        self.done = []
+        return self.grad
+
+    def bucket_ready(self, name, events=()):
+        """all-reduce bucket `name` of the current gradient once `events` have fired"""
+        self.done.append(name)
+        if not self.active:
+            return
+        lo, hi = self.ranges[name]
+        t = self.grad[lo:hi]
+        if t.is_cuda:
+            for e in events:
+                self.stream.wait_event(e)
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def finish(self, optimizer=None):
+        if self.done != self.order:
+            raise RuntimeError(f"gradient buckets completed as {self.done}, expected {self.order}")
+        n = dist.get_world_size(self.group) if self.active else 1
+        if self.grad.is_cuda and self.active:
+            torch.cuda.current_stream(self.grad.device).wait_stream(self.stream)
+        if optimizer is not None and hasattr(optimizer, "grad_scale"):
+            optimizer.grad_scale = 1.0 / n
+        elif n > 1:
+            self.grad.mul_(1.0 / n)
 
 
 def broadcast_parameters(model, src: int = 0, group=None):
-    """Make every replica start from rank `src`'s parameters (one broadcast of the flat buffer)."""
+    """Make every replica start from rank `src`'s parameters: one broadcast of the flat buffer, or of
+    one flattened bucket for models without it."""
     if not is_distributed():
         return
     with torch.no_grad():
-        dist.broadcast(model.flat_params.data, src=src, group=group)
+        if hasattr(model, "flat_params"):
+            dist.broadcast(model.flat_params.data, src=src, group=group)
+            return
+        params = [p for p in model.parameters()]
+        if not params:
+            return
+        bucket = torch.cat([p.detach().reshape(-1) for p in params])
+        dist.broadcast(bucket, src=src, group=group)
+        o = 0
+        for p in params:
+            p.data.copy_(bucket[o:o + p.numel()].view_as(p))
+            o += p.numel()
 
 
 def broadcast_buffers(model, src: int = 0, group=None):
-    """BN running statistics and counters from rank `src` (before eval / checkpoint)."""
+    """BN running statistics and counters from rank `src` (before eval / checkpoint): the model's two
+    flat buffers, or every registered buffer for models without them."""
     if not is_distributed():
         return
-    for b in model.flat_buffers():
+    if hasattr(model, "flat_buffers"):
+        for b in model.flat_buffers():
+            dist.broadcast(b, src=src, group=group)
+        return
+    for b in model.buffers():
         dist.broadcast(b, src=src, group=group)
 
 
@@ -120,3 +243,33 @@ def shard_indices(n: int, rank_: int, world_: int, seed: int = 0, epoch: int = 0
     if total > n:
         idx = np.concatenate([idx, idx[: total - n]])
     return idx[rank_:total:world_]
+
+
+class ShardedLoader:
+    """Wrap a reference-style DataLoader (batches of (data, data2, target)) so each rank iterates a
+    disjoint shard of its batches (batch b goes to rank b % world).  Used by train() when a process
+    group is up and the loader is not already sharded (a loader whose sampler is a
+    DistributedSampler, or whose dataset carries `rank`/`world` attributes, is)."""
+
+    def __init__(self, loader, rank_: int, world_: int):
+        self.loader, self.rank, self.world = loader, rank_, world_
+        self.dataset = loader.dataset
+
+    def __len__(self):
+        n = len(self.loader)
+        return (n - self.rank + self.world - 1) // self.world
+
+    def __iter__(self):
+        for b, item in enumerate(self.loader):
+            if b % self.world == self.rank:
+                yield item
+
+
+def is_sharded(loader) -> bool:
+    sampler = getattr(loader, "sampler", None)
+    if isinstance(sampler, torch.utils.data.distributed.DistributedSampler):
+        return True
+    if isinstance(loader, ShardedLoader):
+        return True
+    ds = getattr(loader, "dataset", None)
+    return getattr(ds, "world", 1) > 1 or getattr(loader, "world", 1) > 1

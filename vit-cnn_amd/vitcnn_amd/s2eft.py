@@ -216,6 +216,11 @@ class _Program:
         self.pd = m.p_drop if m.training else 0.0
         self.pe = m.p_emb if m.training else 0.0
         self.seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (self.pd > 0 or self.pe > 0) else 0
+        if self.seed:
+            # data parallelism: every rank seeds torch alike (main.py), so mix the rank in — the
+            # replicas must not apply the same keep masks to their different shards
+            from .parallel import rank
+            self.seed = (self.seed + 0x9E3779B97F4A7C15 * rank()) % (1 << 62)
         self.masks = {}
 
     def drop(self, site, x, add, y, n, p):

@@ -17,10 +17,12 @@ from .model import Multimodality_Mamba, _Program
 
 
 def fused_train_step(model: Multimodality_Mamba, criterion: CrossEntropyLoss, hsi, lidar, target,
-                     optimizer=None, grad_hook=None):
+                     optimizer=None, grad_hook=None, exchange=None):
     """Returns the loss tensor (device scalar).  Gradients land in `model.flat_params.grad`
     (accumulated like autograd if a gradient is already present); `grad_hook(model)` runs between
-    backward and the optimizer step (e.g. the data-parallel all-reduce)."""
+    backward and the optimizer step.  `exchange` (parallel.GradExchange) all-reduces the gradient
+    bucket by bucket on its own stream while the backward is still running, and the optimizer step
+    is ordered after the last bucket."""
     if not model.training:
         raise RuntimeError("fused_train_step needs the model in train mode")
     if hsi.device.type != "cuda":
@@ -35,12 +37,20 @@ def fused_train_step(model: Multimodality_Mamba, criterion: CrossEntropyLoss, hs
     if w is not None and w.device != logits.device:
         w = w.to(logits.device)
     loss, dlog = ce_forward_backward(logits, target, w, criterion.ignore_index)
-    grad = prog.backward(dlog)
     flat = model.flat_params
-    if flat.grad is None:
+    if exchange is not None:
+        if flat.grad is not None:
+            raise RuntimeError("fused_train_step(exchange=...): zero the gradients first (set_to_none)")
+        grad = exchange.begin(model, hsi.device)
+        prog.backward(dlog, bucket_hook=exchange.bucket_ready, out=grad)
+        exchange.finish(optimizer)
         flat.grad = grad
     else:
-        flat.grad.add_(grad)
+        grad = prog.backward(dlog)
+        if flat.grad is None:
+            flat.grad = grad
+        else:
+            flat.grad.add_(grad)
     if grad_hook is not None:
         grad_hook(model)
     if optimizer is not None:
