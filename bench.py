@@ -2,10 +2,16 @@
 
 One step = forward + weighted CE + backward (+ RCCL gradient all-reduce when N > 1) + fused AdamW
 over one resident synthetic batch (hsi U[0,1) [64,144,9,9], lidar U[0,1) [64,1,9,9], labels in
-[1,15]; random-init weights of the reference architecture).  N = 1 captures the whole step in a
-hipGraph; N > 1 captures forward+backward and runs the all-reduce and AdamW eagerly.
+[1,15]; random-init weights of the reference architecture).  The whole step is ONE hipGraph at every
+N: for N > 1 the gradient leaves the backward in three head-first buckets whose RCCL all-reduces run
+on a side stream while the backward continues (parallel.GradExchange), and AdamW waits for the last.
 
-  python bench.py [--gpus N --steps K --warmup W]            (torch.distributed.run for N > 1)
+  python bench.py [--gpus N --steps K --warmup W] [--precision fp32|bf16]   (torch.distributed.run for N > 1)
+
+`--precision` picks the headline step's GEMM operand precision (fp32 = the parity mode, default;
+bf16 = BASELINE config 2: bf16 operands, fp32 accumulation, fp32 master weights / scan state /
+norm statistics).  At N = 1 the line also carries the other precision's step (`config2_bf16`), the
+whole-image inference leg (`f1_test`), and the config-4/5 legs.
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with `roofline` for the dominant
 kernel (HIP-event timed inside this process) and `cpu_baseline` (the CPU oracle, rank 0, N=1).
@@ -40,7 +46,12 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-s2eft", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (median reported)")
+    ap.add_argument("--cpu-warmup", type=int, default=3)
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="run the bucketed RCCL exchange even at N = 1 (world-1 process group)")
+    ap.add_argument("--no-f1", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
 
@@ -186,26 +197,66 @@ def gemm_roofline(model, batch, reps):
             "flop_per_launch": flops}
 
 
-def cpu_baseline(steps):
-    """The CPU oracle (reference op order, naive sequential scan) timed on this host: one warm-up
-    step, then `steps` timed B=64 training steps (forward, CE, backward, AdamW, loss.item())."""
+def host_info():
+    """The GPU box's host CPU as the SURVEY.md section 8(d) protocol asks: nproc, the cores this
+    process may run on (its affinity mask: the box's CPU share), and the lscpu model name."""
+    import subprocess
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    if model is None and os.path.exists("/proc/cpuinfo"):
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "model": model}
+
+
+def cpu_threads():
+    """torch CPU threads for the baselines: every core this process may run on (os.cpu_count() on an
+    unrestricted host; on the GPU box the affinity mask is the box's CPU share, and threads beyond
+    it would only time-slice)."""
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
+def timed_median(fn, warmup, steps):
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def cpu_baseline(warmup, steps):
+    """The CPU oracle (reference op order, naive sequential scan; oracle/vitcnn_oracle.py) timed on
+    this host by the SURVEY.md section 8(d) protocol: all available cores, `warmup` untimed then the
+    median of `steps` timed B=64 training steps (forward, CE, backward, AdamW, loss.item())."""
     from oracle import vitcnn_oracle as O
     from vitcnn_amd import Multimodality_Mamba
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
     state = O.make_state(m.state_dict())
     opt = O.make_adamw(state)
     hsi, lidar, target = synthetic(64, 1234, "cpu")
     w = O.ce_class_weights(16)
-    O.train_step(state, hsi, lidar, target, w, opt)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        O.train_step(state, hsi, lidar, target, w, opt)
-    dt = time.perf_counter() - t0
-    return {"value": round(64 * steps / dt, 3), "unit": "patches/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} timed B=64 training steps (after 1 warm-up) of oracle/vitcnn_oracle.py, fp32, "
-                      f"torch CPU with {threads} threads; {dt / steps:.2f} s/step"}
+    med, ts = timed_median(lambda: O.train_step(state, hsi, lidar, target, w, opt), warmup, steps)
+    return {"value": round(64 / med, 3), "unit": "patches/s", "cores": threads, "kind": "port",
+            "host": host_info(),
+            "sample": f"median of {steps} timed B=64 training steps after {warmup} warm-up steps of "
+                      f"oracle/vitcnn_oracle.py (fp32, torch CPU, {threads} threads); s/step: "
+                      + ", ".join(f"{t:.2f}" for t in ts)}
 
 
 def s2eft_leg(dev, steps, cpu_steps):
@@ -265,7 +316,7 @@ def s2eft_leg(dev, steps, cpu_steps):
            "launch": launch}
     if cpu_steps > 0:
         from oracle import s2eft_oracle as O
-        threads = min(16, os.cpu_count() or 1)
+        threads = cpu_threads()
         torch.set_num_threads(threads)
         sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         O.train_step(sd, x, t, w)
@@ -373,7 +424,7 @@ def fusat_leg(dev, steps, cpu):
                           "achieved_tflops": round(64 / ms_train * 1e3 * 3 * FUSAT_GFLOP_PER_PATCH * 1e-3, 2)}}
     if cpu:
         from oracle import fusat_oracle as O
-        threads = min(16, os.cpu_count() or 1)
+        threads = cpu_threads()
         torch.set_num_threads(threads)
         sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         with torch.no_grad():
@@ -386,19 +437,21 @@ def fusat_leg(dev, steps, cpu):
     return out
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (not the 2:1-sparsity figure)
 
-    from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba, fused_train_step
+
+def build_step(dev, precision, world, rank, batch, exchange, warmup, use_graph):
+    """The benchmarked training step.  Returns (step, model, inputs, holder, launch).
+
+    exchange: False (no collective) or True: a parallel.GradExchange, with which the backward hands its three
+    head-first gradient buckets to RCCL on a side stream as it completes them, and AdamW is ordered
+    after the last one (fused_train_step(exchange=...)).  The whole step — forward, CE, backward, the
+    bucket all-reduces, AdamW — is captured as ONE hipGraph; if the capture fails the step runs eagerly
+    and the line says so (`launch`)."""
+    from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba, fused_train_step, parallel
     torch.manual_seed(0)
-    model = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16, "multi_clock_gate").to(dev).train()
+    model = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16, "multi_clock_gate", precision=precision).to(dev).train()
+    exchange = parallel.GradExchange(model, force=True) if exchange else None
     if world > 1:
         dist.broadcast(model.flat_params.data, 0)
     opt = AdamW(model.parameters(), lr=8e-4)
@@ -406,53 +459,44 @@ def main():
     w = torch.ones(16)
     w[0] = 0.0
     crit = CrossEntropyLoss(weight=w.to(dev))
-    hsi, lidar, target = synthetic(args.batch, 1000 + rank, dev)
+    hsi, lidar, target = synthetic(batch, 1000 + rank, dev)
     holder = {}
 
-    def fwd_bwd():
-        # forward + weighted CE + backward issued from this thread (vitcnn_amd/step.py), so the
-        # step's side streams are captured with it
-        holder["loss"] = fused_train_step(model, crit, hsi, lidar, target)
-
-    from vitcnn_amd import parallel
-
-    def allreduce():
-        # one RCCL all-reduce of the flat gradient (active parameters); 1/world folded into AdamW
-        parallel.allreduce_gradients(model, opt)
+    def body():
+        holder["loss"] = fused_train_step(model, crit, hsi, lidar, target, optimizer=opt, exchange=exchange)
 
     def eager_step():
         opt.zero_grad(set_to_none=True)
-        fwd_bwd()
-        allreduce()
-        opt.step()
+        body()
 
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
-        for _ in range(max(3, args.warmup)):
+        for _ in range(max(3, warmup)):
             eager_step()
     torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize(dev)
-
-    use_graph = not args.no_graph
-    graph = None
+    if world > 1:
+        dist.barrier()
+    launch = "eager"
+    step = eager_step
     if use_graph:
-        opt.zero_grad(set_to_none=True)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            fwd_bwd()
-            if world == 1:
-                opt.step()
+        try:
+            opt.zero_grad(set_to_none=True)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                body()
+            step = graph.replay
+            launch = "hipGraph (whole step" + (", bucketed RCCL all-reduce inside)" if exchange is not None else ")")
+            holder["graph"] = graph
+        except RuntimeError as e:  # reported in the line, never silent
+            launch = f"eager (graph capture failed: {str(e)[:100]})"
+            torch.cuda.synchronize(dev)
+    return step, model, (hsi, lidar, target), holder, launch
 
-    def step():
-        if graph is not None:
-            graph.replay()
-            if world > 1:
-                allreduce()
-                opt.step()
-        else:
-            eager_step()
 
+def time_steps(step, dev, steps, world):
+    """K steps bracketed by barrier + synchronize on both sides; max over ranks."""
     for _ in range(3):
         step()
     torch.cuda.synchronize(dev)
@@ -460,18 +504,126 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    loss_val = float(holder["loss"].item())
     t = torch.tensor([elapsed], device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    return float(t.item())
+
+
+def bf16_gemm_roofline(model, batch, reps):
+    """The largest contraction of the step in bf16-operand mode (hsi1.local_feature 3x3 conv, M = B*49,
+    N = 256, K = 1296 on v_mfma_f32_16x16x32_bf16, fp32 accumulation) against the dense bf16 peak."""
+    from vitcnn_amd._lib import lib
+    from vitcnn_amd.model import _Program
+    dev = model.flat_params.device
+    prog = _Program(model, dev, batch, True, "grad")
+    L = lib()
+    M, N, K = batch * 49, 256, 9 * 144
+    col = prog.ws.f("hsi1.local_feature.col", M * K)
+    out = prog.ws.f("hsi1.local_feature.out", M * N)
+    W, b = prog.P["hsi1.local_feature.conv.weight"], prog.P["hsi1.local_feature.conv.bias"]
+    stream = torch.cuda.current_stream(dev)
+
+    def fn():
+        L.vc_gemm(0, 1, M, N, K, 1.0, col, K, 0, W, K, 0, 0.0, out, N, 0, 1, b, None, 0, 0, 1 | 2, None, prog.scr_p,
+                  prog.scr_n, stream.cuda_stream)
+
+    t = time_kernel(fn, reps, stream)
+    flops = 2.0 * M * N * K
+    achieved = flops / t / 1e12
+    return {"kernel": "gemm_mfma<bf16> (hsi1.local_feature conv3x3, M=%d N=%d K=%d)" % (M, N, K),
+            "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_BF16_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_MFMA_TFLOPS, 5), "avg_launch_us": round(t * 1e6, 2),
+            "flop_per_launch": flops}
+
+
+def mfu(value_per_gpu, peak):
+    tf = value_per_gpu * GFLOP_PER_PATCH * 1e-3
+    return {"gflop_per_patch": GFLOP_PER_PATCH, "achieved_tflops": round(tf, 3), "peak_tflops": peak,
+            "frac": round(tf / peak, 5)}
+
+
+def precision_leg(dev, precision, steps, warmup, reps):
+    """The same N = 1 training step in the other GEMM-operand precision (config 2 = bf16)."""
+    step, model, _, holder, launch = build_step(dev, precision, 1, 0, 64, False, warmup, True)
+    el = time_steps(step, dev, steps, 1)
+    v = 64 * steps / el
+    out = {"workload": "ViT-CNN train step, Houston2013 shape, B=64, GEMM operands " + precision,
+           "value": round(v, 1), "unit": "patches/s", "ms_per_step": round(el / steps * 1e3, 4), "dtype": precision,
+           "launch": launch, "final_loss": round(float(holder["loss"].item()), 6)}
+    if precision == "bf16":
+        out["model_flops_util"] = mfu(v, PEAK_BF16_MFMA_TFLOPS)
+        out["roofline_gemm"] = bf16_gemm_roofline(model, 64, reps)
+    else:
+        out["model_flops_util"] = mfu(v, PEAK_FP32_MFMA_TFLOPS)
+    return out
+
+
+def f1_leg(dev, cpu):
+    """Row F1: whole-image inference, model_utils.test (model_utils.py:1067-1132)
+    over a Houston2013-size synthetic scene (349 x 1905, 144 + 1 bands, 9x9 windows, stride 1:
+    646,877 windows), eval-mode BatchNorm (running statistics), device-side window gather and fp64
+    centre-pixel accumulation (vitcnn_amd.window.SlidingWindowInference).  CPU baseline: the oracle's
+    eval-mode forward (the reference per-window path's arithmetic) on B=64 windows."""
+    from vitcnn_amd import Multimodality_Mamba
+    from vitcnn_amd.window import SlidingWindowInference
+    torch.manual_seed(0)
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16).to(dev)
+    rng = np.random.default_rng(5)
+    img1 = rng.random((349, 1905, 144), dtype=np.float32)
+    img2 = rng.random((349, 1905, 1), dtype=np.float32)
+    # warm-up on a small crop builds the eval workspaces of the batch sizes the full run uses
+    SlidingWindowInference(m, img1[:80, :80], img2[:80, :80], 9, 1, 16, dev).run(batch_size=64)
+    runner = SlidingWindowInference(m, img1, img2, 9, 1, 16, dev)
+    del img1, img2
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    probs = runner.run(batch_size=64)
+    el = time.perf_counter() - t0
+    out = {"workload": "test(): 349x1905 scene, 144+1 bands, 9x9 windows, stride 1, eval mode, 4096 windows per "
+                       "forward, fp64 centre accumulation (incl. the probability map's copy to the host)",
+           "windows": runner.n, "value": round(runner.n / el, 1), "unit": "windows/s", "seconds": round(el, 3),
+           "dtype": "fp32", "probs_finite": bool(np.isfinite(probs).all())}
+    if cpu:
+        from oracle import vitcnn_oracle as O
+        threads = cpu_threads()
+        torch.set_num_threads(threads)
+        st = O.make_state(m.cpu().state_dict(), requires_grad=False)
+        x1, x2, _ = synthetic(64, 77, "cpu")
+        P = O.Params(st, training=False)
+        with torch.no_grad():
+            med, _ = timed_median(lambda: O.forward(P, x1, x2), 2, 3)
+        out["cpu_baseline"] = {"value": round(64 / med, 2), "unit": "windows/s", "cores": threads, "kind": "port",
+                               "sample": "median of 3 eval-mode B=64 forwards of oracle/vitcnn_oracle.py after 2 warm-up"}
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif args.force_exchange:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    exchange = world > 1 or args.force_exchange
+    step, model, (hsi, lidar, target), holder, launch = build_step(
+        dev, args.precision, world, rank, args.batch, exchange, args.warmup, not args.no_graph)
+    elapsed = time_steps(step, dev, args.steps, world)
+    loss_val = float(holder["loss"].item())
 
     # reference-loop variant: loss.item() host sync every step (model_utils.py:936)
     t1 = time.perf_counter()
@@ -488,38 +640,45 @@ def main():
     ms_asm = batch_assembly_ms(step, hsi, lidar, target, dev, min(args.steps, 50), 1000 + rank)
 
     roof = dominant_kernel_roofline(model, args.batch, args.kernel_reps)
-    roof_gemm = gemm_roofline(model, args.batch, args.kernel_reps)
+    roof_gemm = (gemm_roofline if args.precision == "fp32" else bf16_gemm_roofline)(model, args.batch,
+                                                                                     args.kernel_reps)
     patches = world * args.batch * args.steps
     value = patches / elapsed
+    peak = PEAK_FP32_MFMA_TFLOPS if args.precision == "fp32" else PEAK_BF16_MFMA_TFLOPS
     out = {
         "metric": "training patches/sec, 9×9 HSI(144)+LiDAR patch, batch 64, 1/2/4/8 GPU",
         "value": round(value, 1), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
         "data": "synthetic (U[0,1) HSI/LiDAR patches, random-init weights, resident in HBM)",
         "config": {"workload": "ViT-CNN (Multimodality_Mamba) train step, Houston2013 shape 144+1 bands, 9x9, "
                                "16 classes", "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                   "parallelism": f"dp{world}", "hipgraph": use_graph},
+                   "parallelism": f"dp{world}", "launch": launch,
+                   "gradient_exchange": (None if not exchange else
+                                         "RCCL all-reduce of 3 head-first buckets on a side stream, overlapped "
+                                         "with the backward; 1/world folded into AdamW")},
         "ms_per_step_with_loss_item": round(ms_sync, 4),
         "ms_per_step_with_batch_assembly": round(ms_asm, 4),
         "value_with_batch_assembly": round(world * args.batch / ms_asm * 1e3, 1),
         "final_loss": round(loss_val, 6),
-        "model_flops_util": {"gflop_per_patch": GFLOP_PER_PATCH,
-                             "achieved_tflops": round(value / world * GFLOP_PER_PATCH * 1e-3, 3),
-                             "peak_tflops_fp32_mfma": PEAK_FP32_MFMA_TFLOPS,
-                             "frac": round(value / world * GFLOP_PER_PATCH * 1e-3 / PEAK_FP32_MFMA_TFLOPS, 5)},
+        "model_flops_util": mfu(value / world, peak),
         "roofline": roof,
         "roofline_gemm": roof_gemm,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_warmup, args.cpu_steps)
     if world == 1 and not args.no_s2eft:
+        other = "bf16" if args.precision == "fp32" else "fp32"
+        out["config2_bf16" if other == "bf16" else "parity_fp32"] = precision_leg(
+            dev, other, min(args.steps, 50), args.warmup, args.kernel_reps)
         out["config5_s2eft"] = s2eft_leg(dev, min(args.steps, 50), 0 if args.no_cpu_baseline else 5)
         out["config5_fusatnet"] = fusat_leg(dev, 5, not args.no_cpu_baseline)
         out["config4_muufl"] = muufl_leg(dev, min(args.steps, 50))
+    if world == 1 and not args.no_f1:
+        out["f1_test"] = f1_leg(dev, not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 
