@@ -53,18 +53,19 @@ def main():
     for a in calls:
         ta, tb, M, N, K = a[0], a[1], a[2], a[3], a[4]
         batch = a[16]
-        t_leg, t_new, t_bf = time_call(a, 4), time_call(a, 8), time_call(a, 2)
+        base = a[21] & ~(2 | 4 | 8 | 16 | 32)
+        a = a[:21] + (base,) + a[22:]
+        t_auto, t_leg, t_v2, t_bf = time_call(a, 0), time_call(a, 4), time_call(a, 8), time_call(a, 2)
         fl = 2.0 * M * N * K * batch
-        rows.append((t_new, t_leg, t_bf, ta, tb, M, N, K, batch, a[22] is not None, fl / t_new * 1e-6,
-                     fl / t_bf * 1e-6))
+        rows.append((t_auto, t_leg, t_v2, t_bf, ta, tb, M, N, K, batch, a[22] is not None,
+                     fl / min(t_leg, t_v2) * 1e-6, fl / t_bf * 1e-6))
     rows.sort(reverse=True)
-    tots = [sum(r[i] for r in rows) for i in range(3)]
-    fl = sum(2.0 * r[5] * r[6] * r[7] * r[8] for r in rows)
-    print(f"{len(rows)} GEMMs, isolated sums: fp32 {tots[0]:.1f} us ({fl/tots[0]*1e-6:.1f} TFLOP/s), "
-          f"legacy fp32 {tots[1]:.1f} us, bf16 {tots[2]:.1f} us ({fl/tots[2]*1e-6:.1f} TFLOP/s)")
-    print("  fp32  legacy   bf16  tA tB      M      N      K  batch bgrad  TF(fp32) TF(bf16)")
+    tots = [sum(r[i] for r in rows) for i in range(4)]
+    print(f"{len(rows)} GEMMs, isolated sums (us): auto {tots[0]:.1f}  legacy {tots[1]:.1f}  v2 {tots[2]:.1f}  "
+          f"bf16 {tots[3]:.1f}")
+    print("  auto legacy     v2   bf16  tA tB      M      N      K  batch bgrad TF(fp32) TF(bf16)")
     for r in rows:
-        print("%6.1f %7.1f %6.1f  %d  %d %6d %6d %6d %5d %5s %8.1f %8.1f" % r)
+        print("%6.1f %6.1f %6.1f %6.1f  %d  %d %6d %6d %6d %5d %5s %8.1f %8.1f" % r)
 
 
 if __name__ == "__main__":

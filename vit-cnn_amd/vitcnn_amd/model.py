@@ -37,6 +37,8 @@ BN_EPS = 1e-5
 BN_MOM = 0.1
 NDIR = 10
 N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
+WGRAD_LANE = 2             # backward: lane 0's deferred weight gradients (lane 2 is idle after the forward)
+_DEFER_WGRAD = os.environ.get("VITCNN_DEFER_WGRAD", "0") == "1"   # measured slower (2.39 -> 2.63 ms): each cross-lane graph edge costs more than the overlap gains
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
@@ -380,6 +382,7 @@ class _Program:
         self._ev_i = 0
         self._ev_lane = {}
         self.lanes_on = _LANES
+        self.wgrad_tail = None
         _, self.P, self.BUF, self.I64 = model._ptrs()
         self.device = device
 
@@ -670,25 +673,43 @@ class _Program:
                                 dX, C, beta_dx, self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p,
                                 self.scr_n, self.s)
 
-    def linear_bwd(self, wname, bname, dY, M, N, K, X, ldx, dX, beta_dx, lddy=None):
-        """Y[M,N] = X[M,K] W[N,K]^T + b:  dW = dY^T X, db = colsum(dY), dX (+)= dY W."""
+    def linear_bwd(self, wname, bname, dY, M, N, K, X, ldx, dX, beta_dx, lddy=None, defer=False):
+        """Y[M,N] = X[M,K] W[N,K]^T + b:  dW = dY^T X, db = colsum(dY), dX (+)= dY W.
+
+        defer (lane 0 only): the weight gradient (and its split-K combine) runs on the weight-gradient
+        lane, forked from here, so the data gradient — the only part the rest of the backward waits
+        for — follows at once on lane 0.  Returns the wgrad lane's event after it (or None); the
+        caller must wait on it before anything overwrites dY or X."""
         lddy = lddy or N
-        self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K, bias_grad=self.G[bname] if bname else 0)
+        ev = None
+        if defer and _DEFER_WGRAD and self.lanes_on and self.cur == 0:
+            e = self.mark()
+            with self.lane(WGRAD_LANE, e):
+                self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K, bias_grad=self.G[bname] if bname else 0)
+                ev = self.mark()
+            self.wgrad_tail = ev
+        else:
+            self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K, bias_grad=self.G[bname] if bname else 0)
         if dX:
             self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
+        return ev
 
-    def conv1x1_bn_relu_bwd(self, seq, X, M, Cin, Cout, dOut, dX, beta_dx):
+    def wgrad_events(self):
+        """the weight-gradient lane's latest event, as a list (empty if nothing was deferred)"""
+        return [self.wgrad_tail] if self.wgrad_tail is not None else []
+
+    def conv1x1_bn_relu_bwd(self, seq, X, M, Cin, Cout, dOut, dX, beta_dx, defer=False):
         ws = self.ws
         pre, out = ws.f(seq + ".pre", M * Cout), ws.f(seq + ".out", M * Cout)
         dpre = ws.f(seq + ".dpre", M * Cout)
         self.bn_bwd(seq + ".1", seq + ".1", dOut, Cout, pre, Cout, out, M, Cout, dpre, Cout, 0.0)
-        self.linear_bwd(seq + ".0.weight", seq + ".0.bias", dpre, M, Cout, Cin, X, Cin, dX, beta_dx)
+        self.linear_bwd(seq + ".0.weight", seq + ".0.bias", dpre, M, Cout, Cin, X, Cin, dX, beta_dx, defer=defer)
 
-    def fusion_bwd(self, pfx, X1, C1, X2, C2, M, Cout, dOut, dX1, beta1, dX2, beta2):
+    def fusion_bwd(self, pfx, X1, C1, X2, C2, M, Cout, dOut, dX1, beta1, dX2, beta2, defer=False):
         ws = self.ws
         cat = ws.f(pfx + ".cat", M * (C1 + C2))
         dcat = ws.f(pfx + ".dcat", M * (C1 + C2))
-        self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer", cat, M, C1 + C2, Cout, dOut, dcat, 0.0)
+        self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer", cat, M, C1 + C2, Cout, dOut, dcat, 0.0, defer=defer)
         self.L.vc_cat2_bwd(M, C1, C2, dcat, 1 if C1 == C2 else 0, dX1 or None, C1, beta1, dX2 or None, C2, beta2,
                            self.s)
 
@@ -742,7 +763,7 @@ class _Program:
         FMo = f(pfx + ".FusionLayer.FusionLayer.out", M * Cout)
         # fusionBlock(Fg, FM)
         dFg, dFM = f(pfx + ".dFg", M * Cout), f(pfx + ".dFM", M * Cout)
-        self.fusion_bwd(pfx + ".fusion", Fg, Cout, FMo, Cout, M, Cout, dOut, dFg, 0.0, dFM, 0.0)
+        self.fusion_bwd(pfx + ".fusion", Fg, Cout, FMo, Cout, M, Cout, dOut, dFg, 0.0, dFM, 0.0, defer=True)
         if dX and dx_ready is not None:
             self.wait(dx_ready)  # lane 1 accumulates into dX: order it after dX's producer
         e0 = self.mark()
@@ -788,12 +809,14 @@ class _Program:
         CD, dCD = f(pfx + ".CD", rows * Cout), f(pfx + ".dCD", rows * Cout)
         self.token_learner_bwd(pfx + ".global_feature", CD, L_, Cout, S, dZg, dCD)
         Gm, dG = f(pfx + ".G", rows * E), f(pfx + ".dG", rows * E)
-        self.linear_bwd(pfx + ".change_dim.weight", pfx + ".change_dim.bias", dCD, rows, Cout, E, Gm, E, dG, 0.0)
+        self.linear_bwd(pfx + ".change_dim.weight", pfx + ".change_dim.bias", dCD, rows, Cout, E, Gm, E, dG, 0.0,
+                        defer=True)
         # hsiMamba: ln1 -> out_proj -> scan/combine -> x_proj/dt_proj -> conv -> in_proj -> pre_norm -> patch_embed
         T2, dT = f(pfx + ".T2", rows * E), f(pfx + ".dT", rows * E)
         self.ln_bwd(gv + ".ln1", pfx + ".G", dG, T2, rows, E, dT, 0.0)
         YS, dYS = f(pfx + ".YS", rows * D), f(pfx + ".dYS", rows * D)
-        self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0)
+        # its weight gradient reads dT, which the pre_norm backward below accumulates into
+        e_outw = self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0, defer=True)
         U, XD, XZ = f(pfx + ".U", NDIR * rows * D), f(pfx + ".XD", NDIR * rows * XW), f(pfx + ".XZ", rows * 2 * D)
         Y, YP = f(pfx + ".Y", NDIR * rows * D), f(pfx + ".YP", rows * D)
         dU, dDTL = f(pfx + ".dU", NDIR * rows * D), f(pfx + ".dDTL", NDIR * rows * D)
@@ -807,22 +830,36 @@ class _Program:
                                  self.scr_n, self.s)
         nr = NDIR * rows
         # dt_proj: dt_lin = xdbl[:, :R] W_dt^T + b_dt
+        # (the weight gradient reads dDTL and XD's dt-rank columns; the data gradient writes dXD's)
+        if _DEFER_WGRAD and self.lanes_on and self.cur == 0:
+            e = self.mark()
+            with self.lane(WGRAD_LANE, e):
+                self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, bias_grad=G[mx + ".dt_proj.bias"])
+                self.wgrad_tail = self.mark()
+        else:
+            self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, bias_grad=G[mx + ".dt_proj.bias"])
         self.mm_nn(nr, R, D, dDTL, D, P[mx + ".dt_proj.weight"], R, dXD, XW)
-        self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, bias_grad=G[mx + ".dt_proj.bias"])
         # x_proj: xdbl = u W_x^T
-        self.linear_bwd(mx + ".x_proj.weight", None, dXD, nr, XW, D, U, D, dU, 1.0)
+        self.linear_bwd(mx + ".x_proj.weight", None, dXD, nr, XW, D, U, D, dU, 1.0, defer=True)
         self.L.vc_mamba_dirconv_bwd(B, L_, D, NDIR, order, inv, XZ, P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"],
                                     dU, dXZ, G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"], self.scr_p,
                                     self.scr_n, self.s)
         Xn, dXn = f(pfx + ".Xn", rows * E), f(pfx + ".dXn", rows * E)
-        self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0)
+        self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0, defer=True)
         T = f(pfx + ".T", rows * E)
+        if e_outw is not None:
+            self.wait(e_outw)
         self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dT, 1.0)   # dT = residual + LN grad
-        self.colsum(B, L_ * E, dT, L_ * E, G[gv + ".pos_embed"])
-        self.linear_bwd(gv + ".patch_embed.projection.weight", None, dT, rows, E, Cin, X, Cin, 0, 0.0)
         if dX:
             self.wait(e_ch)
             self.mm_nn(rows, Cin, E, dT, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
+        # pos_embed and patch_embed weight gradients: off the critical path
+        e = self.mark()
+        with self.lane(WGRAD_LANE if _DEFER_WGRAD else 0, e):
+            self.colsum(B, L_ * E, dT, L_ * E, G[gv + ".pos_embed"])
+            self.mm_tn(E, Cin, rows, dT, E, X, Cin, G[gv + ".patch_embed.projection.weight"], Cin)
+            if self.lanes_on and _DEFER_WGRAD:
+                self.wgrad_tail = self.mark()
 
     def bucket_ready(self, hook, name, *side_events):
         """Gradient bucket `name` is complete once lane 0 reaches this point and the given side-lane
@@ -851,7 +888,8 @@ class _Program:
                            dF2, self.G["classifier.weight"], self.G["classifier.bias"], self.s)
         dH1, dH2 = ws.f("dH1", B * S1 * C1o), ws.f("dH2", B * S2 * C2o)
         dL1, dL2 = ws.f("dL1", B * S1 * 16), ws.f("dL2", B * S2 * 32)
-        self.fusion_bwd("fusion2", self.H2, C2o, self.L2, 32, B * S2, 128, dF2, dH2, 0.0, dL2, 0.0)
+        self.wgrad_tail = None
+        self.fusion_bwd("fusion2", self.H2, C2o, self.L2, 32, B * S2, 128, dF2, dH2, 0.0, dL2, 0.0, defer=True)
         e_f2 = self.mark()
         with self.lane(3, e_f2):  # fusion1 + LiDAR branch on lane 3
             self.fusion_bwd("fusion1", self.H1, C1o, self.L1, 16, B * S1, 128, dF1, dH1, 0.0, dL1, 0.0)
@@ -860,9 +898,10 @@ class _Program:
             self.conv_bn_relu3_bwd("lidar1", self.LX, Pp, m.c2, 16, dL1, 0, 0.0)
             e_l3 = self.mark()
         # classifier + fusion2 (lane 0 so far) and fusion1 + LiDAR (lane 3): the "tail" bucket
-        self.bucket_ready(bucket_hook, "tail", e_l3)
+        self.bucket_ready(bucket_hook, "tail", e_l3, *self.wgrad_events())
         self.block_bwd(m.hsi2, "hsi2", self.H1, Pp - 2, dH2, dH1, e_f1)
-        self.bucket_ready(bucket_hook, "hsi2")   # block_bwd joined its lane-1 chain before dH1
+        # block_bwd joined its lane-1 chain before dH1; its deferred weight gradients end at wgrad_tail
+        self.bucket_ready(bucket_hook, "hsi2", *self.wgrad_events())
         self.block_bwd(m.hsi1, "hsi1", self.X0, Pp, dH1, None, None)
         self.join_lanes()
         self.bucket_ready(bucket_hook, "hsi1")
