@@ -1,4 +1,5 @@
-"""Run K eager training steps of the B=64 bench workload (profiling driver for rocprofv3 --pmc)."""
+"""Run K eager training steps of the B=64 bench workload (profiling driver for rocprofv3 --pmc).
+usage: python tools/run_steps.py [K] [fp32|bf16]"""
 import os
 import sys
 
@@ -11,9 +12,10 @@ from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba, fused_train
 
 def main():
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16).to(dev).train()
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16, precision=prec).to(dev).train()
     opt = AdamW(m.parameters(), lr=8e-4)
     crit = CrossEntropyLoss(weight=torch.ones(16, device=dev))
     hsi, lidar = torch.rand(64, 144, 9, 9, device=dev), torch.rand(64, 1, 9, 9, device=dev)

@@ -66,6 +66,16 @@ def main():
 
         print(f"{pfx}: scan_fwd {timed(fwd, reps, st):7.1f} us   scan_bwd(+reductions) {timed(bwd, reps, st):7.1f} us",
               flush=True)
+        # grid scaling of the backward kernel alone (sequences = 10 x b; buffers sized for B = 64):
+        # flat time over b = a per-block latency chain, linear = throughput-bound
+        for b in (64, 32, 16, 8, 4, 1):
+            def bwd_b(b=b):
+                L.vc_mamba_scan_bwd(b, Lt, D, R, NDIR, f(pfx + ".U", nr * D), f(pfx + ".XD", nr * XW), order,
+                                    P[mx + ".dt_proj.weight"], P[mx + ".dt_proj.bias"], P[mx + ".A_log"],
+                                    P[mx + ".D"], P[gv + ".weights"], f(pfx + ".Y", nr * D), f(pfx + ".dYP", rows * D),
+                                    ckp, f(pfx + ".dU", nr * D), f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW),
+                                    None, None, None, prog.scr_p, prog.scr_n, st.cuda_stream)
+            print(f"    scan_bwd kernel, {NDIR * b:4d} sequences: {timed(bwd_b, reps, st):7.1f} us", flush=True)
 
 
 if __name__ == "__main__":

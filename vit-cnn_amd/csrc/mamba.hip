@@ -174,11 +174,6 @@ __device__ __forceinline__ void stage_seq(const ScanArgs& a, int s, const SeqLds
   __syncthreads();
 }
 
-// sum over the 4 rows of a wave (cross_row_sum, common.h) of 4 in-lane terms
-__device__ __forceinline__ float state_sum(float a0, float a1, float a2, float a3) {
-  return cross_row_sum((a0 + a1) + (a2 + a3));
-}
-
 template <int RT>
 __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ y, float* __restrict__ ckpt) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -221,11 +216,13 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
       const float4 cv = *reinterpret_cast<const float4*>(m.Cs + t * NST + NQ * q);
       const float dt = m.dts[t * Dp + d];
       const float dtu = dt * uc[i];
-      h[0] = __builtin_amdgcn_exp2f(dt * A2[0]) * h[0] + dtu * bv.x;
-      h[1] = __builtin_amdgcn_exp2f(dt * A2[1]) * h[1] + dtu * bv.y;
-      h[2] = __builtin_amdgcn_exp2f(dt * A2[2]) * h[2] + dtu * bv.z;
-      h[3] = __builtin_amdgcn_exp2f(dt * A2[3]) * h[3] + dtu * bv.w;
-      const float yt = state_sum(h[0] * cv.x, h[1] * cv.y, h[2] * cv.z, h[3] * cv.w) + Dd * uc[i];
+      // h = dtu * B + exp(dt A) h (the product exp(dt A) h rounded first: the backward's recompute
+      // reuses it and so reproduces these states exactly)
+      h[0] = fmaf(dtu, bv.x, __builtin_amdgcn_exp2f(dt * A2[0]) * h[0]);
+      h[1] = fmaf(dtu, bv.y, __builtin_amdgcn_exp2f(dt * A2[1]) * h[1]);
+      h[2] = fmaf(dtu, bv.z, __builtin_amdgcn_exp2f(dt * A2[2]) * h[2]);
+      h[3] = fmaf(dtu, bv.w, __builtin_amdgcn_exp2f(dt * A2[3]) * h[3]);
+      const float yt = cross_row_sum(fmaf(h[3], cv.w, fmaf(h[2], cv.z, fmaf(h[1], cv.y, h[0] * cv.x)))) + Dd * uc[i];
       // the 4 rows hold the same value: an unconditional store of identical bytes
       if (y && valid && t < a.L) y[((long)s * a.L + t) * a.D + d] = yt;
     }
@@ -265,7 +262,7 @@ struct ScanBwdOut {
 };
 
 template <int RT>
-__global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
+__global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
                                                 const float* __restrict__ yp, const float* __restrict__ dyp,
                                                 const float* __restrict__ ckpt, ScanBwdOut o) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // SeqLds, red [2][nw][SCK][32], [nw]
@@ -326,7 +323,7 @@ __global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const floa
       dg_acc += dyr[i] * yn[i];
     }
     if (c > 0) load_seg(c - 1);
-    // recompute the segment's states (and keep exp(dt A) for the reverse sweep)
+    // recompute the segment's states as the forward did (keep exp(dt A) for the reverse sweep)
     float dAs[SCK][NQ];
 #pragma unroll
     for (int i = 0; i < SCK; ++i) {
@@ -338,7 +335,7 @@ __global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const floa
 #pragma unroll
       for (int j = 0; j < NQ; ++j) {
         dAs[i][j] = __builtin_amdgcn_exp2f(dt * A2[j]);
-        hs[i + 1][j] = dAs[i][j] * hs[i][j] + dtu * bb[j];
+        hs[i + 1][j] = fmaf(dtu, bb[j], dAs[i][j] * hs[i][j]);
       }
     }
     // reverse sweep
@@ -351,21 +348,20 @@ __global__ __launch_bounds__(512) void scan_bwd(ScanArgs a, int ndir, const floa
       const float bv[NQ] = {b4.x, b4.y, b4.z, b4.w}, cv[NQ] = {c4.x, c4.y, c4.z, c4.w};
       const float dt = m.dts[t * Dp + d], ut = uc[i], dy = g * dyr[i];
       const float dtu = dt * ut;
-      float Sp[NQ], qp[NQ], v[8];
+      float v[8];
+      float S = 0.f, qa = 0.f;   // this lane's 4 terms of sum_n dhn B and sum_n (dL/d(dA) dA) A
 #pragma unroll
       for (int j = 0; j < NQ; ++j) {
-        const float dhn = dh[j] + cv[j] * dy;                  // dL/dh_t
-        const float dA = dAs[i][j];
-        const float qq = dhn * hs[i][j] * dA;                  // dL/d(dA_t) * dA_t
-        dAacc[j] += qq * dt;
-        qp[j] = qq * A2[j];
-        Sp[j] = dhn * bv[j];
+        const float dhn = fmaf(cv[j], dy, dh[j]);              // dL/dh_t
+        const float qq = dhn * (dAs[i][j] * hs[i][j]);         // dL/d(dA_t) * dA_t
+        dAacc[j] = fmaf(qq, dt, dAacc[j]);
+        qa = j ? fmaf(qq, A2[j], qa) : qq * A2[j];
+        S = j ? fmaf(dhn, bv[j], S) : dhn * bv[j];
         v[j] = dhn * dtu;                                      // dL/dB_t[n], this channel
         v[4 + j] = dy * hs[i + 1][j];                          // dL/dC_t[n], this channel
-        dh[j] = dhn * dA;                                      // carried to t - 1
+        dh[j] = dhn * dAs[i][j];                               // carried to t - 1
       }
-      const float S = state_sum(Sp[0], Sp[1], Sp[2], Sp[3]);
-      const float qa = state_sum(qp[0], qp[1], qp[2], qp[3]);
+      cross_row_sum2(S, qa);   // sums over the 16 states (the wave's 4 rows)
       if (valid && t < a.L) {   // the 4 rows store identical values
         o.du[(base + t) * a.D + d] = dt * S + Dd * dy;
         // softplus'(dt_lin) = sigmoid(dt_lin) = 1 - exp(-softplus(dt_lin))
