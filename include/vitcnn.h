@@ -104,6 +104,24 @@ VC_API int vc_nchw_to_nhwc(int B, int C, int HW, const float* x, float* y, hipSt
  * (Mutimodality_Mamba7.py:1035-1048), column order matching the [Co, Ci, 3, 3] weight. */
 VC_API int vc_im2col3x3(int B, int H, int W, int C, const float* x, const float* bn_mean, const float* bn_invstd,
                         const float* bn_w, const float* bn_b, float* col, hipStream_t stream);
+/* Implicit-GEMM 3x3 convolution (no im2col matrix) over channels-last maps, k = c*9 + kh*3 + kw over
+ * the torch weight [O][C][3][3] = [O][9C] (ms_conv_bn_relu, Mutimodality_Mamba7.py:1035-1048; FusAtNet
+ * ConvUnit / ConvUnit_NP / Residual units, FusAtNet.py:9-60).  x [B,H,W,C] (row stride ldx); pad 0
+ * (valid) or 1; output map [B,OH,OW,O], OH = H + 2 pad - 2.  bn_* (all or none): the preceding
+ * BatchNorm's affine (x - mean) * invstd * w + b applied to in-range pixels as the operand is gathered.
+ *   fwd:   y (ld ldy) = conv(x) + bias (ReLU if relu)
+ *   wgrad: dweight [O][9C] = beta*dweight + dY^T im2col(x); dbias [O] (may be null) = beta*dbias + colsum(dY)
+ *   dgrad: dx (ld lddx) = beta*dx + the conv's input gradient for dY [B,OH,OW,O] (ld lddy)
+ * ws: split-K slabs (fixed-order sums); may be null (no split). */
+VC_API int vc_conv3x3_fwd(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* bn_mean,
+                          const float* bn_invstd, const float* bn_w, const float* bn_b, const float* weight,
+                          const float* bias, int relu, float* y, long ldy, float* ws, long ws_floats,
+                          hipStream_t stream);
+VC_API int vc_conv3x3_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* bn_mean,
+                            const float* bn_invstd, const float* bn_w, const float* bn_b, const float* dy, long lddy,
+                            float beta, float* dweight, float* dbias, float* ws, long ws_floats, hipStream_t stream);
+VC_API int vc_conv3x3_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy, const float* weight,
+                            float beta, float* dx, long lddx, float* ws, long ws_floats, hipStream_t stream);
 /* gradient of vc_im2col3x3 w.r.t. its (post-BN) input, gather form: dx [B,H,W,C] overwritten */
 VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx, hipStream_t stream);
 

@@ -4,7 +4,7 @@ CPU: the oracle (oracle/fusat_oracle.py) reproduces the reference module's train
 running-statistic updates and its eval-mode logits (tests/golden/fusat_b4.npz from
 tests/golden/gen_fusat_golden.py); the product module, seeded alike, has the reference's state_dict
 names and initial values (per-tensor sums).
-GPU: the HIP forward (im2col3x3_pad + vc_gemm, BN, pools, products) vs the oracle: logits within
+GPU: the HIP forward (implicit-GEMM convs, BN, pools, products) vs the oracle: logits within
 1e-3 relative (north_star fp32), argmax bit-exact, in train mode (B = 4 golden batch, B = 16) and
 in eval mode after the running statistics were updated; and the backward (out-of-place residual
 semantics, the reference's own autograd raises) against torch autograd over the oracle: every

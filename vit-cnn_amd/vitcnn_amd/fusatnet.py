@@ -3,14 +3,16 @@
 Reference: `model/compare_method/FusAtNet.py` (`FusAtNet` :168-186), built by `model_utils.py:109-118`
 (patch 11, Adam lr 1e-3).  The module keeps the reference's parameter tree and state_dict names.
 Forward (train-mode BatchNorm with running-stat updates, or eval-mode) is a program of HIP kernels
-over channels-last [B, H, W, C] rows: every 3x3 conv is `vc_im2col3x3_pad` + `vc_gemm` (bias fused),
+over channels-last [B, H, W, C] rows: every 3x3 conv is `vc_im2col3x3_pad` + `vc_gemm` (bias fused; or
+the implicit GEMM `vc_conv3x3_fwd` with VITCNN_IMPLICIT_CONV=1),
 BatchNorm `vc_bn_stats` + `vc_bn_apply` (ReLU fused), residual adds `vc_add2_2d`, pools
 `vc_maxpool2_fwd` / `vc_pool_scale`, products `vc_mul2_2d`, the concatenation is written in place.
 
 Backward: the reference's own autograd raises (the in-place `x += identity` on a saved ReLU output,
 :44, :61).  This path defines the out-of-place semantics (`b = relu(bn2(conv2(a)))
 + a`) and runs a hand-written backward over a tape of the forward's ops (conv: wgrad GEMM with the
-bias gradient fused, dgrad GEMM + `vc_col2im3x3_pad`; `vc_bn_bwd` with the ReLU mask; maxpool,
+bias gradient fused, dgrad GEMM + `vc_col2im3x3_pad` (or `vc_conv3x3_wgrad` / `_dgrad`); `vc_bn_bwd`
+with the ReLU mask; maxpool,
 pooled-scale and product backwards); parameter gradients land in `.grad` for the reference's Adam.
 """
 from __future__ import annotations
@@ -19,6 +21,7 @@ import torch
 import torch.nn as nn
 
 from ._lib import lib
+from .model import _IMPLICIT_CONV
 
 F32 = 4
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
@@ -221,28 +224,42 @@ class _Program:
                        self.scr.data_ptr(), self.SCRATCH, self.s)
 
     def conv3(self, x, ldx, H, C, conv, pad):
-        """x [B,H,H,C] rows (ld ldx) -> conv3x3 + bias, [B,OH,OH,O] contiguous"""
+        """x [B,H,W,C] rows (ld ldx) -> conv3x3 + bias, [B,OH,OH,O] contiguous: vc_im2col3x3_pad + vc_gemm
+        (the im2col matrix is recomputed in the backward rather than kept), or the implicit GEMM
+        vc_conv3x3_* with VITCNN_IMPLICIT_CONV=1 (no col matrix; measured slower at B = 64)."""
         B, O = self.B, conv.out_channels
         OH = H + 2 * pad - 2
         M, K = B * OH * OH, C * 9
-        col = self.new(M, K)
-        self.L.vc_im2col3x3_pad(B, H, H, C, pad, x.data_ptr(), ldx, col.data_ptr(), self.s)
+        L, scr = self.L, self.scr.data_ptr()
         y = self.new(B, OH, OH, O)
-        self.gemm(0, 1, M, O, K, col.data_ptr(), K, conv.weight.data_ptr(), K, 0.0, y.data_ptr(), O,
-                  bias=conv.bias.data_ptr())
-        del col
+        if _IMPLICIT_CONV:
+            L.vc_conv3x3_fwd(B, H, H, C, O, pad, x.data_ptr(), ldx, None, None, None, None, conv.weight.data_ptr(),
+                             conv.bias.data_ptr(), 0, y.data_ptr(), O, scr, self.SCRATCH, self.s)
+        else:
+            col = self.new(M, K)
+            L.vc_im2col3x3_pad(B, H, H, C, pad, x.data_ptr(), ldx, col.data_ptr(), self.s)
+            self.gemm(0, 1, M, O, K, col.data_ptr(), K, conv.weight.data_ptr(), K, 0.0, y.data_ptr(), O,
+                      bias=conv.bias.data_ptr())
+            del col
 
         def bwd():
             dy = self.grad_of(y)
+            if _IMPLICIT_CONV:
+                L.vc_conv3x3_wgrad(B, H, H, C, O, pad, x.data_ptr(), ldx, None, None, None, None, dy.data_ptr(), O,
+                                   0.0, self.pgrad(conv.weight), self.pgrad(conv.bias), scr, self.SCRATCH, self.s)
+                if id(x) not in self.no_grad_ids:
+                    L.vc_conv3x3_dgrad(B, H, H, C, O, pad, dy.data_ptr(), O, conv.weight.data_ptr(), 1.0,
+                                       self.grad_of(x).data_ptr(), ldx, scr, self.SCRATCH, self.s)
+                return
             colr = self.new(M, K)   # recomputed: cheaper than keeping every im2col matrix
-            self.L.vc_im2col3x3_pad(B, H, H, C, pad, x.data_ptr(), ldx, colr.data_ptr(), self.s)
+            L.vc_im2col3x3_pad(B, H, H, C, pad, x.data_ptr(), ldx, colr.data_ptr(), self.s)
             self.gemm(1, 0, O, K, M, dy.data_ptr(), O, colr.data_ptr(), K, 0.0, self.pgrad(conv.weight), K,
                       bias_grad=self.pgrad(conv.bias))
             if id(x) in self.no_grad_ids:
                 return
             dcol = colr
             self.gemm(0, 0, M, K, O, dy.data_ptr(), O, conv.weight.data_ptr(), K, 0.0, dcol.data_ptr(), K)
-            self.L.vc_col2im3x3_pad(B, H, H, C, pad, dcol.data_ptr(), self.grad_of(x).data_ptr(), ldx, 1, self.s)
+            L.vc_col2im3x3_pad(B, H, H, C, pad, dcol.data_ptr(), self.grad_of(x).data_ptr(), ldx, 1, self.s)
 
         self.record(bwd, x, y)
         return y, OH

@@ -38,6 +38,11 @@ BN_MOM = 0.1
 NDIR = 10
 N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
 WGRAD_LANE = 2             # backward: lane 0's deferred weight gradients (lane 2 is idle after the forward)
+# 3x3 convs of ViT-CNN: im2col + vc_gemm by default; VITCNN_IMPLICIT_CONV=1 selects the implicit GEMM
+# (vc_conv3x3_*), measured slower on this step (2.39 -> 2.55 ms: the per-element gather with the fused
+# BN affine costs more VALU than the small im2col matrices cost bandwidth); FusAtNet, whose col
+# matrices reach 611 MB, always uses the implicit GEMM
+_IMPLICIT_CONV = os.environ.get("VITCNN_IMPLICIT_CONV", "0") == "1"
 _DEFER_WGRAD = os.environ.get("VITCNN_DEFER_WGRAD", "0") == "1"   # measured slower (2.39 -> 2.63 ms): each cross-lane graph edge costs more than the overlap gains
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
@@ -378,6 +383,8 @@ class _Program:
         self._scr = [(scr.data_ptr(), scr.numel())] + [(t.data_ptr(), t.numel()) for _, t in lanes]
         self._cnt = [t.data_ptr() for t in model._tile_counters(device)]
         self.gemm_flags = GEMM_BF16 if model.precision == "bf16" else 0
+        # 3x3 convs as implicit GEMMs (fp32 only, opt-in); bf16 operands use im2col + the bf16 vc_gemm
+        self.implicit_conv = not self.gemm_flags and _IMPLICIT_CONV
         self.cur = 0
         self._ev_i = 0
         self._ev_lane = {}
@@ -490,9 +497,16 @@ class _Program:
         return Y
 
     def conv_bn_relu3(self, pfx, X, H, Cin, Cout):
-        """ms_conv_bn_relu: BN(X) -> conv3x3 valid (+bias) -> ReLU."""
+        """ms_conv_bn_relu: BN(X) -> conv3x3 valid (+bias) -> ReLU: vc_im2col3x3 (BN affine fused) +
+        vc_gemm, or the implicit GEMM vc_conv3x3_fwd (VITCNN_IMPLICIT_CONV=1, fp32)."""
         B, S = self.B, (H - 2) * (H - 2)
         mean, inv = self.bn_stats(pfx + ".bn", X, Cin, B * H * H, Cin, pfx + ".bn")
+        if self.implicit_conv:
+            out = self.ws.f(pfx + ".out", B * S * Cout)
+            self.L.vc_conv3x3_fwd(B, H, H, Cin, Cout, 0, X, Cin, mean, inv, self.P[pfx + ".bn.weight"],
+                                  self.P[pfx + ".bn.bias"], self.P[pfx + ".conv.weight"], self.P[pfx + ".conv.bias"], 1,
+                                  out, Cout, self.scr_p, self.scr_n, self.s)
+            return out
         col = self.ws.f(pfx + ".col", B * S * 9 * Cin)
         self.L.vc_im2col3x3(B, H, H, Cin, X, mean, inv, self.P[pfx + ".bn.weight"], self.P[pfx + ".bn.bias"], col,
                             self.s)
@@ -716,13 +730,24 @@ class _Program:
     def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx):
         B, ws = self.B, self.ws
         S = (H - 2) * (H - 2)
-        out, col = ws.f(pfx + ".out", B * S * Cout), ws.f(pfx + ".col", B * S * 9 * Cin)
+        out = ws.f(pfx + ".out", B * S * Cout)
         dpre = ws.f(pfx + ".dpre", B * S * Cout)
         self.L.vc_relu_bwd(B * S * Cout, dOut, out, dpre, self.s)
-        dcol = ws.f(pfx + ".dcol", B * S * 9 * Cin)
-        self.linear_bwd(pfx + ".conv.weight", pfx + ".conv.bias", dpre, B * S, Cout, 9 * Cin, col, 9 * Cin, dcol, 0.0)
         dxbn = ws.f(pfx + ".dxbn", B * H * H * Cin)
-        self.L.vc_col2im3x3(B, H, H, Cin, dcol, dxbn, self.s)
+        if self.implicit_conv:
+            tag = pfx + ".bn"
+            self.L.vc_conv3x3_wgrad(B, H, H, Cin, Cout, 0, X, Cin, ws.f(tag + ".bm", Cin), ws.f(tag + ".bi", Cin),
+                                    self.P[tag + ".weight"], self.P[tag + ".bias"], dpre, Cout, 0.0,
+                                    self.G[pfx + ".conv.weight"], self.G[pfx + ".conv.bias"], self.scr_p, self.scr_n,
+                                    self.s)
+            self.L.vc_conv3x3_dgrad(B, H, H, Cin, Cout, 0, dpre, Cout, self.P[pfx + ".conv.weight"], 0.0, dxbn, Cin,
+                                    self.scr_p, self.scr_n, self.s)
+        else:
+            col = ws.f(pfx + ".col", B * S * 9 * Cin)
+            dcol = ws.f(pfx + ".dcol", B * S * 9 * Cin)
+            self.linear_bwd(pfx + ".conv.weight", pfx + ".conv.bias", dpre, B * S, Cout, 9 * Cin, col, 9 * Cin, dcol,
+                            0.0)
+            self.L.vc_col2im3x3(B, H, H, Cin, dcol, dxbn, self.s)
         self.bn_bwd(pfx + ".bn", pfx + ".bn", dxbn, Cin, X, Cin, 0, B * H * H, Cin, dX, Cin, beta_dx)
 
     def token_learner_bwd(self, pfx, X, L_, C, S, dZ, dX):
