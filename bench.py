@@ -171,32 +171,27 @@ def dominant_kernel_roofline(model, batch, reps):
 
 
 def gemm_roofline(model, batch, reps):
-    """The largest contraction of the step: the hsi1.local_feature 3x3 conv (ms_conv_bn_relu,
-    M = B*49 output pixels, N = 256, K = 9*144), an implicit GEMM with the BatchNorm affine applied as
-    the operand is gathered (vc_conv3x3_fwd, fp32 MFMA), timed on its live workspace the same way;
-    MFMA-bound (fp32 peak).  Reported beside the dominant kernel."""
+    """The largest GEMM of the step (hsi1.local_feature im2col'ed 3x3 conv, M = B*49, N = 256,
+    K = 9*144) timed the same way; MFMA-bound (fp32 peak).  Reported beside the dominant kernel."""
     from vitcnn_amd._lib import lib
     from vitcnn_amd.model import _Program
     dev = model.flat_params.device
     prog = _Program(model, dev, batch, True, "grad")
     L = lib()
-    H, C, O = 9, 144, 256
-    M, N, K = batch * 49, O, 9 * C
-    P, f = prog.P, prog.ws.f
-    x = f("x0", batch * H * H * C)
-    mean, inv = f("hsi1.local_feature.bn.bm", C), f("hsi1.local_feature.bn.bi", C)
-    out = f("hsi1.local_feature.out", M * N)
+    M, N, K = batch * 49, 256, 9 * 144
+    col = prog.ws.f("hsi1.local_feature.col", M * K)
+    out = prog.ws.f("hsi1.local_feature.out", M * N)
+    W, b = prog.P["hsi1.local_feature.conv.weight"], prog.P["hsi1.local_feature.conv.bias"]
     stream = torch.cuda.current_stream(dev)
 
     def fn():
-        L.vc_conv3x3_fwd(batch, H, H, C, O, 0, x, C, mean, inv, P["hsi1.local_feature.bn.weight"],
-                         P["hsi1.local_feature.bn.bias"], P["hsi1.local_feature.conv.weight"],
-                         P["hsi1.local_feature.conv.bias"], 1, out, O, prog.scr_p, prog.scr_n, stream.cuda_stream)
+        L.vc_gemm(0, 1, M, N, K, 1.0, col, K, 0, W, K, 0, 0.0, out, N, 0, 1, b, None, 0, 0, 1, None, prog.scr_p,
+                  prog.scr_n, stream.cuda_stream)
 
     t = time_kernel(fn, reps, stream)
     flops = 2.0 * M * N * K
     achieved = flops / t / 1e12
-    return {"kernel": "conv_gemm<fwd> (hsi1.local_feature implicit-GEMM conv3x3, M=%d N=%d K=%d)" % (M, N, K),
+    return {"kernel": "gemm_f32_mfma<false,true> (hsi1.local_feature conv3x3, M=%d N=%d K=%d)" % (M, N, K),
             "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "avg_launch_us": round(t * 1e6, 2),
             "flop_per_launch": flops}
