@@ -197,9 +197,24 @@ def gemm_roofline(model, batch, reps):
             "flop_per_launch": flops}
 
 
+def log(msg):
+    """progress on stderr (the one JSON line goes to stdout)"""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _cgroup_cpus():
+    """the CPU quota of this process's cgroup (cgroup v2 cpu.max), or None when unlimited / absent"""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        return None
+
+
 def host_info():
     """The GPU box's host CPU as the SURVEY.md section 8(d) protocol asks: nproc, the cores this
-    process may run on (its affinity mask: the box's CPU share), and the lscpu model name."""
+    process may run on (affinity mask and cgroup quota: the box's CPU share), and the lscpu model name."""
     import subprocess
     model = None
     try:
@@ -217,14 +232,16 @@ def host_info():
                     model = line.split(":", 1)[1].strip()
                     break
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "model": model}
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpus": _cgroup_cpus(), "model": model}
 
 
 def cpu_threads():
-    """torch CPU threads for the baselines: every core this process may run on (os.cpu_count() on an
-    unrestricted host; on the GPU box the affinity mask is the box's CPU share, and threads beyond
-    it would only time-slice)."""
-    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    """torch CPU threads for the baselines: every core this process may use -- os.cpu_count() on an
+    unrestricted host; on the GPU box the affinity mask / cgroup quota is the box's CPU share, and
+    threads beyond it would only time-slice."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    q = _cgroup_cpus()
+    return min(n, q) if q else n
 
 
 def timed_median(fn, warmup, steps):
@@ -373,16 +390,21 @@ FUSAT_GFLOP_PER_PATCH = 6.92  # SURVEY.md section 8(d), FusAtNet forward
 
 
 def fusat_leg(dev, steps, cpu):
-    """Config 5: FusAtNet train-mode forward (batch-statistics BN with
-    running-stat updates) at B = 64 on [64,144,11,11] + [64,1,11,11], and the training step (the
-    reference's own backward raises; this path's uses out-of-place residual semantics).  CPU
-    baseline: oracle/fusat_oracle.py forward at B = 4."""
+    """Config 5: the FusAtNet TRAINING step at B = 64 on [64,144,11,11] +
+    [64,1,11,11] (train-mode forward with batch-statistics BN and running-stat updates, weighted CE,
+    hand-written backward with out-of-place residual semantics -- the reference's own backward raises --,
+    and the reference's Adam(lr 1e-3, model_utils.py:109-118) as the fused kernel over the flat parameter
+    buffer), captured as one hipGraph when the capture succeeds; the train-mode forward alone beside it.
+    CPU baseline: the oracle's B = 4 training step (forward + autograd backward, oracle/fusat_oracle.py)."""
+    from vitcnn_amd import CrossEntropyLoss
     from vitcnn_amd.fusatnet import FusAtNet
+    from vitcnn_amd.optim import AdamW
     torch.manual_seed(0)
     m = FusAtNet(144, 1, 16).to(dev).train()
     g = torch.Generator().manual_seed(3)
     x1, x2 = torch.rand(64, 144, 11, 11, generator=g), torch.rand(64, 1, 11, 11, generator=g)
     a, b = x1.to(dev), x2.to(dev)
+    tgt = torch.randint(1, 16, (64,), generator=g).to(dev)
     with torch.no_grad():
         for _ in range(2):
             m(a, b)
@@ -391,49 +413,69 @@ def fusat_leg(dev, steps, cpu):
         for _ in range(steps):
             m(a, b)
         torch.cuda.synchronize(dev)
-        ms = (time.perf_counter() - t0) / steps * 1e3
-    # training step: forward, weighted CE, hand-written backward (out-of-place residual semantics),
-    # the reference's torch.optim.Adam(lr 1e-3) (model_utils.py:109-118)
-    from vitcnn_amd import CrossEntropyLoss
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        ms_fwd = (time.perf_counter() - t0) / steps * 1e3
+    opt = AdamW(m.parameters(), lr=1e-3, weight_decay=0.0)
     w = torch.ones(16, device=dev)
     w[0] = 0.0
     crit = CrossEntropyLoss(weight=w)
-    tgt = torch.randint(1, 16, (64,), generator=g).to(dev)
 
-    def train_step():
+    def eager_step():
         opt.zero_grad(set_to_none=True)
         crit(m(a, b), tgt).backward()
         opt.step()
 
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            eager_step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    launch = "hipGraph"
+    try:
+        graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            crit(m(a, b), tgt).backward()
+            opt.step()
+        step = graph.replay
+    except RuntimeError as e:  # reported in the line, never silent
+        launch = f"eager (graph capture failed: {str(e)[:80]})"
+        torch.cuda.synchronize(dev)
+        step = eager_step
     for _ in range(2):
-        train_step()
+        step()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
-        train_step()
+        step()
     torch.cuda.synchronize(dev)
-    ms_train = (time.perf_counter() - t0) / steps * 1e3
-    tf = 64 / ms * 1e3 * FUSAT_GFLOP_PER_PATCH * 1e-3
-    out = {"workload": "FusAtNet train-mode forward, [64,144,11,11] + [64,1,11,11], 16 classes",
-           "value": round(64 / ms * 1e3, 1), "unit": "patches/s (forward)", "ms_per_batch": round(ms, 3),
-           "dtype": "fp32", "achieved_tflops": round(tf, 2),
-           "mfma_frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4),
-           "train_step": {"value": round(64 / ms_train * 1e3, 1), "unit": "patches/s", "ms_per_step": round(ms_train, 3),
-                          "note": "forward + CE + backward (out-of-place residual) + torch Adam; ~3x forward flops",
-                          "achieved_tflops": round(64 / ms_train * 1e3 * 3 * FUSAT_GFLOP_PER_PATCH * 1e-3, 2)}}
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    tf = 64 / ms * 1e3 * 3 * FUSAT_GFLOP_PER_PATCH * 1e-3
+    tf_fwd = 64 / ms_fwd * 1e3 * FUSAT_GFLOP_PER_PATCH * 1e-3
+    out = {"workload": "FusAtNet train step (fwd + CE + bwd + fused Adam), [64,144,11,11] + [64,1,11,11], 16 classes",
+           "value": round(64 / ms * 1e3, 1), "unit": "patches/s", "ms_per_step": round(ms, 3), "dtype": "fp32",
+           "launch": launch, "achieved_tflops": round(tf, 2), "mfma_frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4),
+           "forward": {"value": round(64 / ms_fwd * 1e3, 1), "unit": "patches/s (train-mode forward)",
+                       "ms_per_batch": round(ms_fwd, 3), "achieved_tflops": round(tf_fwd, 2),
+                       "mfma_frac": round(tf_fwd / PEAK_FP32_MFMA_TFLOPS, 4)}}
     if cpu:
         from oracle import fusat_oracle as O
         threads = cpu_threads()
         torch.set_num_threads(threads)
         sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-        with torch.no_grad():
-            O.forward(sd, x1[:4], x2[:4])
-            t0 = time.perf_counter()
-            O.forward(sd, x1[:4], x2[:4])
-            dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(4 / dt, 2), "unit": "patches/s (forward)", "cores": threads,
-                               "kind": "port", "sample": "1 B=4 train-mode forward of oracle/fusat_oracle.py"}
+        params = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+        tc, wc = tgt[:4].cpu(), w.cpu()
+
+        def cpu_step():
+            for v in params.values():
+                v.grad = None
+            torch.nn.functional.cross_entropy(O.forward(params, x1[:4], x2[:4], train=True), tc, weight=wc).backward()
+
+        med, _ = timed_median(cpu_step, 1, 3)
+        out["cpu_baseline"] = {"value": round(4 / med, 2), "unit": "patches/s", "cores": threads, "kind": "port",
+                               "sample": "median of 3 B=4 training steps (forward + autograd backward) of "
+                                         "oracle/fusat_oracle.py after 1 warm-up"}
     return out
 
 
@@ -620,8 +662,10 @@ def main():
     dev = torch.device("cuda", local)
 
     exchange = world > 1 or args.force_exchange
+    log(f"rank {rank}/{world}: building the {args.precision} step")
     step, model, (hsi, lidar, target), holder, launch = build_step(
         dev, args.precision, world, rank, args.batch, exchange, args.warmup, not args.no_graph)
+    log(f"timing {args.steps} steps ({launch})")
     elapsed = time_steps(step, dev, args.steps, world)
     loss_val = float(holder["loss"].item())
 
@@ -666,15 +710,21 @@ def main():
         "roofline_gemm": roof_gemm,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log(f"CPU baseline: {args.cpu_warmup} + {args.cpu_steps} oracle steps on {cpu_threads()} threads")
         out["cpu_baseline"] = cpu_baseline(args.cpu_warmup, args.cpu_steps)
     if world == 1 and not args.no_s2eft:
         other = "bf16" if args.precision == "fp32" else "fp32"
+        log(f"{other} leg")
         out["config2_bf16" if other == "bf16" else "parity_fp32"] = precision_leg(
             dev, other, min(args.steps, 50), args.warmup, args.kernel_reps)
+        log("config 5: S2EFT leg")
         out["config5_s2eft"] = s2eft_leg(dev, min(args.steps, 50), 0 if args.no_cpu_baseline else 5)
+        log("config 5: FusAtNet leg")
         out["config5_fusatnet"] = fusat_leg(dev, 5, not args.no_cpu_baseline)
+        log("config 4: MUUFL leg")
         out["config4_muufl"] = muufl_leg(dev, min(args.steps, 50))
     if world == 1 and not args.no_f1:
+        log("F1: whole-image test()")
         out["f1_test"] = f1_leg(dev, not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(out), flush=True)

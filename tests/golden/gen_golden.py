@@ -227,6 +227,46 @@ def train_step_fixture(mod, batch, tag, full_grad_max=2048, acts=True, opt_step=
     return out
 
 
+TRAIN_STEPS_EVAL = 8
+VAL_PASSES = 40
+
+
+def trained_eval_fixture(mod, steps=TRAIN_STEPS_EVAL):
+    """Eval-mode class indices that vary across samples: the reference module (hash init) takes `steps`
+    AdamW(lr 8e-4) training steps on the golden B=64 batch (model_utils.py:918-934) and VAL_PASSES
+    train-mode no-grad forwards of it (the reference's val()), then predicts the trained batch and a
+    second synthetic batch in eval mode (running-statistic BatchNorm, model_utils.py:1067-1132 test()).
+    The untrained network's eval argmax is degenerate (one class for every sample); after training it
+    is not.  Saved: the loss trajectory, eval logits and argmax."""
+    torch.manual_seed(0)
+    net = build_net(mod)
+    net.train()
+    hsi, lidar, target = synthetic_batch("golden.b64", 64, 144, 1, 9, N_CLASSES)
+    hsi_t, lidar_t, tgt_t = torch.from_numpy(hsi), torch.from_numpy(lidar), torch.from_numpy(target)
+    crit = nn.CrossEntropyLoss(weight=ce_weights(N_CLASSES))
+    opt = torch.optim.AdamW(net.parameters(), lr=8e-4)
+    losses = []
+    for _ in range(steps):
+        opt.zero_grad()
+        loss = crit(net(hsi_t, lidar_t), tgt_t)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    # val-style train-mode forwards (model_utils.py:1135-1158 runs val() without net.eval(), so every
+    # val batch updates the BatchNorm running statistics): they settle at the trained batch's statistics
+    with torch.no_grad():
+        for _ in range(VAL_PASSES):
+            net(hsi_t, lidar_t)
+    ehsi, elidar, _ = synthetic_batch("golden.eval64", 64, 144, 1, 9, N_CLASSES)
+    net.eval()
+    with torch.no_grad():
+        logits = net(hsi_t, lidar_t).numpy()                                   # the trained batch
+        logits2 = net(torch.from_numpy(ehsi), torch.from_numpy(elidar)).numpy()  # a fresh batch
+    return {"losses": np.array(losses, dtype=np.float64), "eval_logits": logits, "eval_argmax": logits.argmax(1),
+            "eval2_logits": logits2, "eval2_argmax": logits2.argmax(1), "target": target, "steps": np.array(steps),
+            "val_passes": np.array(VAL_PASSES)}
+
+
 def mixer_fixture(mod):
     from transformers.models.mamba.modeling_mamba import MambaMixer
     cfgs = {"e144": (144, 72, 81), "e256": (256, 128, 49)}
@@ -292,6 +332,13 @@ def capture_scan_orders(mod, net):
 def main():
     torch.set_num_threads(os.cpu_count())
     mod = load_reference()
+    if "--eval-only" in sys.argv:   # only the trained eval-mode fixture (the others unchanged)
+        z = trained_eval_fixture(mod)
+        np.savez_compressed(os.path.join(HERE, "vitcnn_eval64.npz"), **z)
+        am, am2 = z["eval_argmax"], z["eval2_argmax"]
+        print("eval64 fixture done: losses", np.round(z["losses"], 4), "distinct classes", len(set(am.tolist())),
+              "(fresh batch:", len(set(am2.tolist())), ") argmax == target", float((am == z["target"]).mean()))
+        return
     net = build_net(mod)
     with open(os.path.join(HERE, "scan_orders.json"), "w") as f:
         json.dump(capture_scan_orders(mod, net), f)

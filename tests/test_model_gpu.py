@@ -266,3 +266,88 @@ def test_fused_step_and_graph_capture_match_autograd():
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(m3.flat_params.grad, g_auto), use_fused
+
+
+def test_gradients_vs_reference_golden_b4(b4):
+    """Element-wise gradient parity with NO HIP-derived inputs: every small-parameter gradient the
+    reference module itself produced (vitcnn_b4.npz grad/*, the reference's fp32 autograd) against the
+    HIP gradient.  A tensor passes directly when max|hip - ref| <= 1e-3 max|ref| + floor.  Otherwise it
+    must pass the fp64 argument: max|hip - exact| <= 3 max|ref - exact| + floor, exact = the pure float64
+    oracle (no HIP ReLU decisions or pooled values fed in) -- i.e. the HIP value is no further from the
+    exact gradient than the reference's own fp32 value is (measured: 594 of 671 tensors pass directly;
+    the rest are the train-mode-BatchNorm-conditioned families -- TokenLearner BN(1) tokenizers, BN /
+    LN affine parameters downstream of them -- and sums over all 10 x B x L tokens such as the conv1d,
+    D and bias gradients, where the reference's fp32 value is up to 0.7 % off the exact one and the HIP
+    value within 1e-5 of it).  The per-tensor outcome (and whether the name is in a BN-conditioned
+    family) is written to gpurun_out/grad_parity_b4.json when that directory exists."""
+    import json
+    import os
+    m, exact = b4["m"], b4["ref64_own"]
+    g = load_npz("vitcnn_b4.npz")
+    flat = m.flat_params.grad.detach().cpu()
+    named = dict(m.named_parameters())
+    keys = [k[5:] for k in g.files if k.startswith("grad/")]
+    gmax = max(float(abs(g["grad/" + k]).max()) for k in keys)
+    floor = 1e-5 * gmax
+    direct, fp64, bad = [], [], []
+    conditioned = ("tokenizers", "cross_attention", ".ln", "norm", ".bn", "FusionLayer", "local_feature", "weights")
+    for k in keys:
+        ref = torch.from_numpy(g["grad/" + k]).double()
+        off = m._poff[k]
+        got = flat[off:off + named[k].numel()].view(named[k].shape).double()
+        scale = float(ref.abs().max())
+        err = float((got - ref).abs().max())
+        if err <= 1e-3 * scale + floor:
+            direct.append(k)
+            continue
+        ex = exact[k].double()
+        err_ex, ref_ex = float((got - ex).abs().max()), float((ref - ex).abs().max())
+        if err_ex <= 3.0 * ref_ex + floor:
+            fp64.append((k, err, scale, err_ex, ref_ex, any(c in k for c in conditioned)))
+        else:
+            bad.append((k, err, scale, err_ex, ref_ex))
+    if os.path.isdir("gpurun_out"):
+        with open("gpurun_out/grad_parity_b4.json", "w") as f:
+            json.dump({"tensors": len(keys), "direct": len(direct), "fp64_argument": fp64, "failed": bad}, f, indent=1)
+    assert not bad, bad[:5]
+    assert len(direct) >= 0.85 * len(keys), (len(direct), len(keys))
+
+
+def test_trained_eval_mode_class_indices():
+    """Eval-mode class indices that vary across samples (the untrained fixture's eval argmax
+    is one class everywhere): 8 AdamW(8e-4) steps on the golden B=64 batch, 40 val-style train-mode
+    forwards (running statistics settle, the reference's val() runs without net.eval()), then eval-mode
+    logits of the trained batch (15 distinct classes in the reference's run) and of a fresh batch,
+    against vitcnn_eval64.npz made by the reference module itself (tests/golden/gen_golden.py
+    --eval-only).  Eight Adam steps amplify fp32 rounding-order differences (measured between the CPU
+    oracle and the reference itself: losses 1e-3, eval logits 2e-2 relative, argmax identical,
+    tests/test_oracle_golden.py); the same bounds hold here: losses 3e-3, logits 6e-2, argmax identical
+    wherever the reference's top-2 margin exceeds 2e-2 of the logit scale."""
+    _need_gpu()
+    from vitcnn_amd import AdamW, CrossEntropyLoss, fused_train_step
+    z = load_npz("vitcnn_eval64.npz")
+    sd = hash_state_dict()
+    hsi, lidar, target = golden_batch("golden.b64", 64)
+    ehsi, elidar, _ = golden_batch("golden.eval64", 64)
+    m = _product(sd).train()
+    crit = CrossEntropyLoss(weight=O.ce_class_weights(16).to(DEV))
+    opt = AdamW(m.parameters(), lr=8e-4)
+    x1, x2, t = hsi.to(DEV), lidar.to(DEV), target.to(DEV)
+    losses = []
+    for _ in range(int(z["steps"])):
+        opt.zero_grad()
+        losses.append(float(fused_train_step(m, crit, x1, x2, t, optimizer=opt)))
+    assert np.allclose(losses, z["losses"], rtol=3e-3, atol=1e-5), (losses, z["losses"])
+    with torch.no_grad():
+        for _ in range(int(z["val_passes"])):
+            m(x1, x2)
+        m.eval()
+        for key, (a, b) in (("eval", (x1, x2)), ("eval2", (ehsi.to(DEV), elidar.to(DEV)))):
+            got = m(a, b).cpu().numpy()
+            ref = z[key + "_logits"]
+            assert rel_err(got, ref) < 6e-2, (key, rel_err(got, ref))
+            top2 = np.sort(ref, axis=1)[:, -2:]
+            sel = (top2[:, 1] - top2[:, 0]) > 2e-2 * np.abs(ref).max()
+            assert sel.sum() >= 56, (key, int(sel.sum()))
+            assert np.array_equal(got.argmax(1)[sel], ref.argmax(1)[sel]), key
+    assert len(set(z["eval_argmax"].tolist())) >= 10

@@ -1,0 +1,92 @@
+"""One flat fp32 parameter buffer behind an nn.Module's parameter tree (S2EFT, FusAtNet).
+
+Every registered nn.Parameter is re-pointed at a view of one contiguous fp32 buffer (`flat_params`),
+in `named_parameters()` order, so state_dict() / load_state_dict() / parameters() keep the reference's
+names and shapes while the hand-written backward writes ONE flat gradient (`flat_params.grad`): the
+fused optimizer (vitcnn_amd.optim.AdamW, one HBM pass) and the data-parallel exchange
+(parallel.allreduce_gradients, one collective) then each touch a single tensor instead of a
+per-parameter list.  Buffers (BatchNorm running statistics) stay ordinary registered buffers.
+"""
+from __future__ import annotations
+
+import weakref
+
+import torch
+import torch.nn as nn
+
+F32 = 4
+
+
+class FlatParams:
+    """Mixin for an nn.Module whose parameters live in one flat buffer; call `_build_flat()` at the end
+    of __init__.  Provides flat_params, n_active_params, _ensure_flat (re-pack after a parameter was
+    replaced, e.g. by load_state_dict with assign), device moves and zero_grad on the flat buffer."""
+
+    def _build_flat(self):
+        named = list(nn.Module.named_parameters(self))
+        self._poff, off = {}, 0
+        for n, p in named:
+            self._poff[n] = off
+            off += p.numel()
+        self._n_params = self._n_active = off
+        flat = torch.empty(off, dtype=torch.float32, device=named[0][1].device)
+        for n, p in named:
+            flat[self._poff[n]:self._poff[n] + p.numel()].copy_(p.detach().reshape(-1))
+        self._pmods = {}
+        for mn, m in nn.Module.named_modules(self):
+            for pn, p in m._parameters.items():
+                if p is None:
+                    continue
+                self._pmods[(mn + "." if mn else "") + pn] = (m, pn)
+        self._rebind(flat)
+        me = weakref.ref(self)
+        for _, p in named:
+            p._vc_owner = me
+
+    def _rebind(self, flat):
+        object.__setattr__(self, "_flat_store", flat.detach().requires_grad_(True))
+        base = self._flat_store.detach()
+        for n, (m, pn) in self._pmods.items():
+            p = m._parameters[pn]
+            o = self._poff[n]
+            p.data = base[o:o + p.numel()].view(p.shape)
+
+    def _repack(self, device):
+        flat = torch.empty(self._n_params, dtype=torch.float32, device=device)
+        for n, (m, pn) in self._pmods.items():
+            o = self._poff[n]
+            flat[o:o + m._parameters[pn].numel()].copy_(m._parameters[pn].detach().reshape(-1))
+        self._rebind(flat)
+
+    def _apply(self, fn, recurse=True):
+        # parameters and buffers through nn.Module (buffers: BN running statistics), then the
+        # parameters re-packed into one flat buffer on their new device
+        nn.Module._apply(self, fn, recurse)
+        first = next(iter(self._pmods.values()))
+        p0 = first[0]._parameters[first[1]]
+        if p0.dtype != torch.float32:
+            raise RuntimeError(f"{type(self).__name__} MI355X path computes in fp32; dtype casts are not supported")
+        self._repack(p0.device)
+        return self
+
+    def _ensure_flat(self):
+        base = self._flat_store.data_ptr()
+        for n, (m, pn) in self._pmods.items():
+            if m._parameters[pn].data_ptr() != base + F32 * self._poff[n]:
+                self._repack(self._flat_store.device)
+                return
+
+    @property
+    def flat_params(self) -> torch.Tensor:
+        return self._flat_store
+
+    @property
+    def n_active_params(self) -> int:
+        return self._n_active
+
+    def zero_grad(self, set_to_none: bool = True):
+        nn.Module.zero_grad(self, set_to_none=set_to_none)
+        if set_to_none:
+            self._flat_store.grad = None
+        elif self._flat_store.grad is not None:
+            self._flat_store.grad.zero_()

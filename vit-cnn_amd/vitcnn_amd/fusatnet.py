@@ -13,7 +13,8 @@ Backward: the reference's own autograd raises (the in-place `x += identity` on a
 + a`) and runs a hand-written backward over a tape of the forward's ops (conv: wgrad GEMM with the
 bias gradient fused, dgrad GEMM + `vc_col2im3x3_pad` (or `vc_conv3x3_wgrad` / `_dgrad`); `vc_bn_bwd`
 with the ReLU mask; maxpool,
-pooled-scale and product backwards); parameter gradients land in `.grad` for the reference's Adam.
+pooled-scale and product backwards); the parameter gradients land in one flat gradient
+(`flat_params.grad`) for the fused Adam (vitcnn_amd.optim.AdamW, weight_decay 0).
 """
 from __future__ import annotations
 
@@ -21,9 +22,9 @@ import torch
 import torch.nn as nn
 
 from ._lib import lib
+from .flat import F32, FlatParams
 from .model import _IMPLICIT_CONV
 
-F32 = 4
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
 
 
@@ -126,8 +127,11 @@ class Classification_Module(nn.Module):
         self.conv6 = nn.Conv2d(1024, num_classes, kernel_size=1, bias=True)
 
 
-class FusAtNet(nn.Module):
-    """Same constructor as the reference (FusAtNet.py:168-176); forward(x1 [B,C1,P,P], x2 [B,C2,P,P])."""
+class FusAtNet(FlatParams, nn.Module):
+    """Same constructor as the reference (FusAtNet.py:168-176); forward(x1 [B,C1,P,P], x2 [B,C2,P,P]).
+    Parameters live in one flat buffer (vitcnn_amd.flat): the backward writes one flat gradient, which
+    the fused optimizer (vitcnn_amd.optim.AdamW with weight_decay=0: the reference's Adam,
+    model_utils.py:109-118) updates in one pass."""
 
     def __init__(self, input_channels, input_channels2, num_classes):
         super().__init__()
@@ -138,6 +142,7 @@ class FusAtNet(nn.Module):
         self.mam = Modality_Attention_Module(1024 * 2 + input_channels + input_channels2, 1024)
         self.cm = Classification_Module(1024, num_classes)
         self.c1, self.c2, self.ncls = input_channels, input_channels2, num_classes
+        self._build_flat()
 
     def forward(self, x1: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
         if x1.device.type != "cuda":
@@ -150,9 +155,11 @@ class FusAtNet(nn.Module):
             raise RuntimeError("FusAtNet needs patch >= 11 (five valid 3x3 convs + two 2x2 pools)")
         x1 = x1.detach().float().contiguous()
         x2 = x2.detach().float().contiguous()
-        params = [p for _, p in self.named_parameters()]
-        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-            return _FusAtNetFunction.apply(self, x1, x2, *params)
+        self._ensure_flat()
+        if self._flat_store.device != x1.device:
+            raise RuntimeError("model and inputs are on different devices")
+        if torch.is_grad_enabled() and self._flat_store.requires_grad:
+            return _FusAtNetFunction.apply(self, x1, x2, self._flat_store)
         with torch.no_grad():
             return _Program(self, x1, x2, False).run()
 
@@ -163,7 +170,7 @@ class _FusAtNetFunction(torch.autograd.Function):
     out of place -- the reference's own autograd raises there."""
 
     @staticmethod
-    def forward(ctx, model, x1, x2, *params):
+    def forward(ctx, model, x1, x2, flat):
         prog = _Program(model, x1, x2, True)
         logits = prog.run()
         ctx.prog = prog
@@ -171,9 +178,9 @@ class _FusAtNetFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dlogits):
-        grads = ctx.prog.backward(dlogits.detach().float().contiguous())
+        grad = ctx.prog.backward(dlogits.detach().float().contiguous())
         ctx.prog = None
-        return (None, None, None, *grads)
+        return None, None, None, grad
 
 
 class _Program:
@@ -285,10 +292,8 @@ class _Program:
         return z
 
     def pgrad(self, p):
-        g = self.pg.get(id(p))
-        if g is None:
-            g = self.pg[id(p)] = torch.empty_like(p)
-        return g.data_ptr()
+        """address of p's slice of the flat gradient (every parameter is written once, beta 0)"""
+        return self.gflat.data_ptr() + F32 * self.poff[id(p)]
 
     def unit(self, x, ldx, H, C, u, pad=1):
         y, OH = self.conv3(x, ldx, H, C, u.conv, pad)
@@ -357,7 +362,6 @@ class _Program:
 
     def run(self):
         m, L, B, P = self.m, self.L, self.B, self.P
-        self.pg = {}
         c1, c2 = m.c1, m.c2
         x1, x2 = self.nhwc(self.x1), self.nhwc(self.x2)
         HW = P * P
@@ -411,10 +415,15 @@ class _Program:
         return logits.view(B, H, H, m.ncls).permute(0, 3, 1, 2).squeeze()
 
     def backward(self, dlogits):
+        """the flat gradient of every parameter (zero where the forward does not reach)"""
         m = self.m
         x, Mo, C = self.head
         if dlogits.numel() != Mo * m.ncls or Mo != self.B:
             raise RuntimeError("FusAtNet backward: the classifier output must be 1x1 (patch 11)")
+        named = dict(m.named_parameters())
+        self.poff = {id(named[n]): o for n, o in m._poff.items()}
+        self.gflat = self.new(m._n_params)
+        self.L.vc_fill(m._n_params, self.gflat.data_ptr(), 0.0, self.s)
         conv6 = m.cm.conv6
         self.gemm(1, 0, m.ncls, C, Mo, dlogits.data_ptr(), m.ncls, x.data_ptr(), C, 0.0, self.pgrad(conv6.weight), C,
                   bias_grad=self.pgrad(conv6.bias))
@@ -422,9 +431,5 @@ class _Program:
                   self.grad_of(x).data_ptr(), C)
         for fn in reversed(self.tape):
             fn()
-        out = []
-        for _, p in m.named_parameters():
-            g = self.pg.get(id(p))
-            out.append(g if g is not None else torch.zeros_like(p))
         self.tape, self.g, self.keep = [], {}, {}
-        return out
+        return self.gflat

@@ -121,14 +121,15 @@ def _get_s2eft(n_bands, n_classes, device, kwargs):
 
 def _get_fusatnet(n_bands, n_bands2, n_classes, device, kwargs):
     """FusAtNet branch of model_utils.py:109-118: FusAtNet(n_bands, n_bands2, n_classes), patch 11,
-    torch.optim.Adam(lr 1e-3) as in the reference, weighted CE, epoch 150, batch 64, applyPCA False.
+    Adam(lr 1e-3) as in the reference -- the fused AdamW kernel with weight_decay 0 over the model's flat
+    parameter buffer (torch.optim.Adam's update exactly) --, weighted CE, epoch 150, batch 64, applyPCA False.
     The reference's backward raises (in-place residual add); this path trains with
     out-of-place residual semantics (vitcnn_amd/fusatnet.py)."""
     from .fusatnet import FusAtNet
     kwargs.setdefault("patch_size", 11)
     model = FusAtNet(n_bands, n_bands2, n_classes).to(device)
     lr = kwargs.setdefault("lr", 0.001)
-    optimizer = torch.optim.Adam(model.parameters(), lr=lr)
+    optimizer = AdamW(model.parameters(), lr=lr, weight_decay=0.0)
     criterion = CrossEntropyLoss(weight=kwargs["weights"])
     kwargs.setdefault("epoch", 150)
     kwargs.setdefault("batch_size", 64)

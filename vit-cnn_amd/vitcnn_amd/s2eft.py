@@ -19,14 +19,12 @@ references an un-imported `F`, :58, and raises too).
 """
 from __future__ import annotations
 
-import weakref
-
 import torch
 import torch.nn as nn
 
 from ._lib import lib
+from .flat import F32, FlatParams
 
-F32 = 4
 LN_EPS = 1e-5  # nn.LayerNorm default (PreNorm :13-19, mlp_head :125-128)
 
 
@@ -75,7 +73,7 @@ class Transformer(nn.Module):
             self.skipcat.append(nn.Conv2d(num_channel + 1, num_channel + 1, [1, 2], 1, 0))
 
 
-class ViT(nn.Module):
+class ViT(FlatParams, nn.Module):
     """Same constructor as the reference `ViT` (S2EFT.py:110-131); forward(x [B, N, C]) -> logits."""
 
     def __init__(self, image_size, near_band, num_patches, num_classes, dim, depth, heads, mlp_dim, pool="cls",
@@ -101,69 +99,6 @@ class ViT(nn.Module):
         self.hidden, self.ncls, self.mode = mlp_dim, num_classes, mode
         self.p_drop, self.p_emb = float(dropout), float(emb_dropout)
         self._build_flat()
-
-    # ------------------------------------------------------------ flat parameter buffer
-    def _build_flat(self):
-        named = list(nn.Module.named_parameters(self))
-        self._poff, off = {}, 0
-        for n, p in named:
-            self._poff[n] = off
-            off += p.numel()
-        self._n_params = self._n_active = off
-        flat = torch.empty(off, dtype=torch.float32, device=named[0][1].device)
-        for n, p in named:
-            flat[self._poff[n]:self._poff[n] + p.numel()].copy_(p.detach().reshape(-1))
-        self._pmods = {}
-        for mn, m in nn.Module.named_modules(self):
-            for pn, p in m._parameters.items():
-                if p is None:
-                    continue
-                self._pmods[(mn + "." if mn else "") + pn] = (m, pn)
-        self._rebind(flat)
-        me = weakref.ref(self)
-        for _, p in named:
-            p._vc_owner = me
-
-    def _rebind(self, flat):
-        object.__setattr__(self, "_flat_store", flat.detach().requires_grad_(True))
-        base = self._flat_store.detach()
-        for n, (m, pn) in self._pmods.items():
-            p = m._parameters[pn]
-            o = self._poff[n]
-            p.data = base[o:o + p.numel()].view(p.shape)
-
-    def _apply(self, fn, recurse=True):
-        flat = fn(self._flat_store.detach())
-        if flat.dtype != torch.float32:
-            raise RuntimeError("S2EFT MI355X path computes in fp32; dtype casts are not supported")
-        self._rebind(flat)
-        return self
-
-    def _ensure_flat(self):
-        base = self._flat_store.data_ptr()
-        for n, (m, pn) in self._pmods.items():
-            if m._parameters[pn].data_ptr() != base + F32 * self._poff[n]:
-                flat = torch.empty(self._n_params, dtype=torch.float32, device=self._flat_store.device)
-                for n2, (m2, pn2) in self._pmods.items():
-                    o = self._poff[n2]
-                    flat[o:o + m2._parameters[pn2].numel()].copy_(m2._parameters[pn2].detach().reshape(-1))
-                self._rebind(flat)
-                return
-
-    @property
-    def flat_params(self) -> torch.Tensor:
-        return self._flat_store
-
-    @property
-    def n_active_params(self) -> int:
-        return self._n_active
-
-    def zero_grad(self, set_to_none: bool = True):
-        super().zero_grad(set_to_none=set_to_none)
-        if set_to_none:
-            self._flat_store.grad = None
-        elif self._flat_store.grad is not None:
-            self._flat_store.grad.zero_()
 
     # ------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, mask=None) -> torch.Tensor:
