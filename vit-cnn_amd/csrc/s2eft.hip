@@ -82,13 +82,6 @@ __global__ void strip_cls(int B, int N, int D, const float* __restrict__ dX, flo
 // operand is P^T straight from the S^T accumulator: the k order inside each MFMA is permuted so that
 // step s of lane group g = l >> 4 pairs key (or head-dim) 4g + s on both operands.  Online softmax
 // (running max / sum per query, rescaling the O^T accumulator) between tiles.
-// LDS image of a head's [T][16] rows as float4 quads with a rotating quad order: quad q4 of row t sits
-// at slot (q4 + t / 4) & 3.  The MFMA operand reads take the quad g of 16 consecutive rows (one per lane
-// of a 16-lane group) -- unswizzled, rows 4 apart hit the same bank quad (4-way conflicts); rotated,
-// the 16 rows' quads cover all 64 banks once.  Single floats (row t, column d) stay conflict-free.
-__device__ __forceinline__ int sw4(int t, int q4) { return t * 4 + ((q4 + (t >> 2)) & 3); }
-__device__ __forceinline__ int sw1(int t, int d) { return sw4(t, d >> 2) * 4 + (d & 3); }
-
 __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __restrict__ qkv, float scale,
                                                 float* __restrict__ out, float* __restrict__ lse) {
   extern __shared__ f32x4 lds4[];  // 2 * T * 64 B
@@ -100,8 +93,8 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
   const float* base = qkv + (long)b * T * ld;
   for (int i = threadIdx.x; i < T * 4; i += blockDim.x) {
     const int t = i >> 2, q4 = i & 3;
-    Ks[sw4(t, q4)] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
-    Vs[sw4(t, q4)] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
+    Ks[i] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
+    Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -115,7 +108,7 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
   f32x4 o = {0.f, 0.f, 0.f, 0.f};          // O^T[d = 4g + r][q = c]
   for (int k0 = 0; k0 < T; k0 += 16) {
     const int key = min(k0 + c, T - 1);
-    const f32x4 kv = Ks[sw4(key, g)];      // A operand: K[key = k0 + c][d = 4g + s]
+    const f32x4 kv = Ks[key * 4 + g];      // A operand: K[key = k0 + c][d = 4g + s]
     f32x4 st = {0.f, 0.f, 0.f, 0.f};       // S^T[key = k0 + 4g + r][q = c]
     st = __builtin_amdgcn_mfma_f32_16x16x4f32(kv.x, qv.x, st, 0, 0, 0);
     st = __builtin_amdgcn_mfma_f32_16x16x4f32(kv.y, qv.y, st, 0, 0, 0);
@@ -144,7 +137,7 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
       const int kk = min(k0 + 4 * g + s2, T - 1);
-      o = __builtin_amdgcn_mfma_f32_16x16x4f32(Vf[sw1(kk, c)], pv[s2], o, 0, 0, 0);
+      o = __builtin_amdgcn_mfma_f32_16x16x4f32(Vf[kk * 16 + c], pv[s2], o, 0, 0, 0);
     }
   }
   l += __shfl_xor(l, 16, 64);
@@ -185,11 +178,11 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   const int ld = 3 * H * 16, ldo = H * 16;
   const float* base = qkv + (long)b * T * ld;
   for (int i = threadIdx.x; i < T * 4; i += blockDim.x) {
-    const int t = i >> 2, q4 = i & 3, j = sw4(t, q4);
-    Qs[j] = *(const f32x4*)(base + (long)t * ld + h * 16 + q4 * 4);
-    Ks[j] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
-    Vs[j] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
-    dOs[j] = *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4);
+    const int t = i >> 2, q4 = i & 3;
+    Qs[i] = *(const f32x4*)(base + (long)t * ld + h * 16 + q4 * 4);
+    Ks[i] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
+    Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
+    dOs[i] = *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4);
   }
   // rowsum(dO * O): 16 lanes per row, coalesced
   for (int i0 = 0; i0 < T * 16; i0 += blockDim.x) {
@@ -210,14 +203,14 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   const int c = lane & 15, g = lane >> 4;
   const int ri = min(r0 + c, T - 1);
   {  // pass 1: dq of queries r0 .. r0 + 15 (query c of this lane)
-    const f32x4 qv = Qs[sw4(ri, g)], gv = dOs[sw4(ri, g)];
+    const f32x4 qv = Qs[ri * 4 + g], gv = dOs[ri * 4 + g];
     const float lq = Ls[ri], dq_ = Ds[ri];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};  // dQ^T[d = 4g + r][q = c]
     for (int k0 = 0; k0 < T; k0 += 16) {
       const int key = min(k0 + c, T - 1);
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 st = mfma4(Ks[sw4(key, g)], qv, z);   // S^T[key = k0 + 4g + r][q = c]
-      const f32x4 dpt = mfma4(Vs[sw4(key, g)], gv, z);  // dP^T
+      const f32x4 st = mfma4(Ks[key * 4 + g], qv, z);   // S^T[key = k0 + 4g + r][q = c]
+      const f32x4 dpt = mfma4(Vs[key * 4 + g], gv, z);  // dP^T
       float ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -228,19 +221,19 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
         const int kk = min(k0 + 4 * g + s2, T - 1);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Kf[sw1(kk, c)], ds[s2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Kf[kk * 16 + c], ds[s2], acc, 0, 0, 0);
       }
     }
     if (r0 + c < T) *(f32x4*)(dqkv + ((long)b * T + r0 + c) * ld + h * 16 + g * 4) = acc * scale;
   }
   {  // pass 2: dk, dv of keys r0 .. r0 + 15 (key c of this lane)
-    const f32x4 kv = Ks[sw4(ri, g)], vv = Vs[sw4(ri, g)];
+    const f32x4 kv = Ks[ri * 4 + g], vv = Vs[ri * 4 + g];
     f32x4 adk = {0.f, 0.f, 0.f, 0.f}, adv = {0.f, 0.f, 0.f, 0.f};  // dK^T / dV^T [d = 4g + r][key = c]
     for (int q0 = 0; q0 < T; q0 += 16) {
       const int qq = min(q0 + c, T - 1);
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 sm = mfma4(Qs[sw4(qq, g)], kv, z);    // S[q = q0 + 4g + r][key = c]
-      const f32x4 dp = mfma4(dOs[sw4(qq, g)], vv, z);   // dP
+      const f32x4 sm = mfma4(Qs[qq * 4 + g], kv, z);    // S[q = q0 + 4g + r][key = c]
+      const f32x4 dp = mfma4(dOs[qq * 4 + g], vv, z);   // dP
       float pr[4], ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -254,8 +247,8 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
         const int qk = min(q0 + 4 * g + s2, T - 1);
-        adv = __builtin_amdgcn_mfma_f32_16x16x4f32(dOf[sw1(qk, c)], pr[s2], adv, 0, 0, 0);
-        adk = __builtin_amdgcn_mfma_f32_16x16x4f32(Qf[sw1(qk, c)], ds[s2], adk, 0, 0, 0);
+        adv = __builtin_amdgcn_mfma_f32_16x16x4f32(dOf[qk * 16 + c], pr[s2], adv, 0, 0, 0);
+        adk = __builtin_amdgcn_mfma_f32_16x16x4f32(Qf[qk * 16 + c], ds[s2], adk, 0, 0, 0);
       }
     }
     if (r0 + c < T) {
