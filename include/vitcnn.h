@@ -94,6 +94,15 @@ VC_API int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, const
                      const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
                      float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w,
                      float* ws, long ws_floats, hipStream_t stream);
+/* The same with >= ceil(C/64) zeroed arrival counters (left zero; per stream, as vc_gemm_ex's):
+ * the per-channel reduction runs in the last-arriving partial block, one launch fewer. */
+VC_API int vc_bn_stats_ex(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                          float* save_mean, float* save_invstd, float* run_mean, float* run_var,
+                          float* ws, long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream);
+VC_API int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
+                        const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
+                        float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w,
+                        float* ws, long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream);
 
 /* ---------------------------------------------------------------- layout / spatial
  * NCHW input patches (the reference's batch layout, datasets.py:571-572) -> channels-last. */

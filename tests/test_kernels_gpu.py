@@ -195,6 +195,43 @@ def test_batchnorm_train_fwd_bwd(L, ws, M, C, relu):
     assert rel_err(db.cpu().numpy(), br.grad.numpy()) < 1e-4
 
 
+@pytest.mark.parametrize("M,C,relu", [(5184, 144, 0), (3136, 512, 1), (5184, 1, 0), (1600, 16, 1), (37, 200, 1)])
+def test_batchnorm_ticketed_reduction_is_bit_identical(L, ws, M, C, relu):
+    """vc_bn_stats_ex / vc_bn_bwd_ex (the last-arriving partial block of each channel group reduces)
+    == vc_bn_stats / vc_bn_bwd (separate reduction launch), bit for bit, twice in a row (the arrival
+    counters are left zero)"""
+    x = (rnd(M, C, seed=41, scale=3.0) + 5.0).to(DEV)
+    w, dy = (rnd(C, seed=42) + 1.0).to(DEV), rnd(M, C, seed=43).to(DEV)
+    relu_out = torch.relu(rnd(M, C, seed=44)).to(DEV) if relu else None
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    outs = []
+    for ex in (False, True):
+        for _ in range(2):
+            rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+            mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+            dx = torch.full((M, C), 0.5, device=DEV)
+            dw, db = torch.full((C,), 2.0, device=DEV), torch.full((C,), 3.0, device=DEV)
+            sargs = (1, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(ws), ws.numel())
+            bargs = (1, M, C, P(dy), C, P(x), C, P(relu_out), C, P(mean), P(inv), P(w), P(dx), C, 1.0, P(dw), P(db),
+                     0.5, P(ws), ws.numel())
+            if ex:
+                L.vc_bn_stats_ex(*sargs, P(cnt), cnt.numel(), S())
+                L.vc_bn_bwd_ex(*bargs, P(cnt), cnt.numel(), S())
+            else:
+                L.vc_bn_stats(*sargs, S())
+                L.vc_bn_bwd(*bargs, S())
+            torch.cuda.synchronize()
+            outs.append([t.cpu() for t in (mean, inv, rm, rv, dx, dw, db)])
+            assert int(cnt.abs().sum()) == 0
+    # the shifted fp64 sums keep a large channel offset (x ~ 5 +- 3) exact to fp32
+    xm = x.double().cpu()
+    assert torch.allclose(outs[0][0].double(), xm.mean(0), rtol=1e-6, atol=1e-6)
+    assert torch.allclose(outs[0][1].double(), 1 / torch.sqrt(xm.var(0, unbiased=False) + 1e-5), rtol=1e-6)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("ta,tb,M,N,K,bgrad", [(1, 0, 72, 9, 51840, True), (1, 0, 256, 1296, 3136, True),
                                                (0, 1, 3136, 256, 1296, False), (1, 0, 41, 72, 51840, False),

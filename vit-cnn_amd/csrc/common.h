@@ -125,6 +125,32 @@ __device__ __forceinline__ void cross_row_sum2(float& a, float& b) {
   b = __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
+// In-launch "last arriver" of a group of n blocks that each published a partial result (the split-K
+// combine's protocol, cdna_hip_programming.md "In-launch split-K reduction"): the block's global
+// stores are drained and released at agent scope, thread 0 takes a ticket from *cnt; the block that
+// draws the last ticket re-zeroes *cnt (all n have arrived, so the next launch on this stream finds it
+// zero), acquires the others' partials and returns true in every thread.  The partials are then
+// reduced in a fixed order by the caller, so the result does not depend on which block came last.
+// Call from all threads of the block (contains barriers).
+__device__ __forceinline__ bool block_last_arriver(unsigned int* cnt, unsigned n) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == n - 1);
+    if (last) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return last != 0;
+}
+
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
@@ -170,38 +196,4 @@ static inline int launch_sum_rows(int P, int C, const float* part, long stride, 
   if (C <= 0) return 0;
   hipLaunchKernelGGL(sum_rows_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, P, C, part, stride, off, out, beta);
   return (int)hipGetLastError();
-}
-
-// double-precision variant (BatchNorm statistics and gradient sums accumulate in fp64 like
-// torch's CPU kernels, acc_type<float> = double)
-static __global__ __launch_bounds__(256) void sum_rows_d_kernel(int P, int C, const double* __restrict__ part,
-                                                                long stride, long off, double* __restrict__ out) {
-  __shared__ double sh[16][17];
-  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  double s = 0.0;
-  if (c < C) {
-#pragma unroll 4
-    for (int p = pl; p < P; p += 16) s += part[(long)p * stride + off + c];
-  }
-  sh[pl][cl] = s;
-  __syncthreads();
-  if (pl == 0 && c < C) {
-    double v = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v += sh[i][cl];
-    out[c] = v;
-  }
-}
-
-// Chan's parallel combination of (count, mean, M2) triples.
-template <typename T>
-__device__ __forceinline__ void welford_merge(T& n, T& mean, T& m2, T nb, T meanb, T m2b) {
-  T nn = n + nb;
-  if (nn <= T(0)) return;
-  T d = meanb - mean;
-  T fb = nb / nn;
-  mean = mean + d * fb;
-  m2 = m2 + m2b + d * d * n * fb;
-  n = nn;
 }

@@ -113,65 +113,84 @@ __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, 
 }
 
 // ---------------------------------------------------------------- BatchNorm (channels-last)
-__global__ __launch_bounds__(256) void bn_stats_partial(int M, int C, const float* __restrict__ x, long ldx,
-                                                        int rows_per, double* __restrict__ part) {
-  __shared__ double sh[3][4][64];
+// Batch statistics as shifted sums in fp64 (torch's CPU kernels accumulate in double too): per
+// channel s1 = sum (x - k), s2 = sum (x - k)^2 with the shift k = x[0, c] (the first row: keeps
+// s2/M - (s1/M)^2 free of cancellation whatever the channel's offset), so mean = k + s1/M and the
+// biased variance = s2/M - (s1/M)^2.  A partial block (64 channels x 4 row lanes) sums rows_per
+// rows into part[p][2][C]; the reduction over the P partials runs in a fixed order (4 partial lanes
+// p = l, l+4, ..., then the 4 lanes in order), either in the last-arriving partial block of each
+// 64-channel group (tickets: no second launch) or in bn_stats_final (same code, same result).
+__device__ __forceinline__ void bn_stats_reduce(int P, int C, long M, const float* __restrict__ x,
+                                                const double* __restrict__ part, int cx, float eps, float momentum,
+                                                float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                float* __restrict__ run_mean, float* __restrict__ run_var) {
+  __shared__ double shr[2][4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = cx * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += 4) {
+      s1 += part[(long)p * 2 * C + c];
+      s2 += part[(long)p * 2 * C + C + c];
+    }
+  }
+  shr[0][pl][cl] = s1;
+  shr[1][pl][cl] = s2;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  s1 = shr[0][0][cl] + shr[0][1][cl] + shr[0][2][cl] + shr[0][3][cl];
+  s2 = shr[1][0][cl] + shr[1][1][cl] + shr[1][2][cl] + shr[1][3][cl];
+  const double d = s1 / (double)M;
+  const double var = fmax(s2 / (double)M - d * d, 0.0);
+  const double mean = (double)x[c] + d;
+  save_mean[c] = (float)mean;
+  save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    const double unb = M > 1 ? var * ((double)M / (double)(M - 1)) : var;
+    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
+    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+  }
+}
+
+// grid (ceil(C/64), P); cnt (optional) = one zeroed arrival counter per 64-channel group
+__global__ __launch_bounds__(256) void bn_stats_sums(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
+                                                     double* __restrict__ part, unsigned int* __restrict__ cnt,
+                                                     float eps, float momentum, float* __restrict__ save_mean,
+                                                     float* __restrict__ save_invstd, float* __restrict__ run_mean,
+                                                     float* __restrict__ run_var) {
+  __shared__ double sh[2][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per;
   const long r1 = min((long)M, r0 + rows_per);
-  double n = 0.0, mean = 0.0, m2 = 0.0;
+  double s1 = 0.0, s2 = 0.0;
   if (c < C) {
+    const double k = x[c];
+#pragma unroll 4
     for (long r = r0 + rl; r < r1; r += 4) {
-      const double v = x[r * ldx + c];
-      n += 1.0;
-      const double d = v - mean;
-      mean += d / n;
-      m2 += d * (v - mean);
+      const double d = (double)x[r * ldx + c] - k;
+      s1 += d;
+      s2 = fma(d, d, s2);
     }
   }
-  sh[0][rl][cl] = n;
-  sh[1][rl][cl] = mean;
-  sh[2][rl][cl] = m2;
+  sh[0][rl][cl] = s1;
+  sh[1][rl][cl] = s2;
   __syncthreads();
   if (rl == 0 && c < C) {
-    for (int k = 1; k < 4; ++k) welford_merge(n, mean, m2, sh[0][k][cl], sh[1][k][cl], sh[2][k][cl]);
-    double* p = part + (long)blockIdx.y * 3 * C + c;
-    p[0] = n;
-    p[C] = mean;
-    p[2 * C] = m2;
+    double* p = part + (long)blockIdx.y * 2 * C + c;
+    p[0] = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+    p[C] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
   }
+  if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
+  bn_stats_reduce(gridDim.y, C, M, x, part, blockIdx.x, eps, momentum, save_mean, save_invstd, run_mean, run_var);
 }
 
-// block = 16 channels x 16 partial lanes; each lane Chan-merges its partials, then a fixed-order
-// 16-way merge in LDS
-__global__ __launch_bounds__(256) void bn_stats_final(int P, int C, long M, const double* __restrict__ part, float eps,
-                                                      float momentum, float* __restrict__ save_mean,
-                                                      float* __restrict__ save_invstd, float* __restrict__ run_mean,
-                                                      float* __restrict__ run_var) {
-  __shared__ double sh[3][16][17];
-  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  if (c < C)
-    for (int p = pl; p < P; p += 16) {
-      const double* q = part + (long)p * 3 * C + c;
-      welford_merge(n, mean, m2, q[0], q[C], q[2 * C]);
-    }
-  sh[0][pl][cl] = n;
-  sh[1][pl][cl] = mean;
-  sh[2][pl][cl] = m2;
-  __syncthreads();
-  if (pl != 0 || c >= C) return;
-  for (int k = 1; k < 16; ++k) welford_merge(n, mean, m2, sh[0][k][cl], sh[1][k][cl], sh[2][k][cl]);
-  const double var = m2 / (double)M;
-  save_mean[c] = (float)mean;
-  save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (run_mean) {
-    const double unb = M > 1 ? m2 / (double)(M - 1) : var;
-    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
-    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
-  }
+__global__ __launch_bounds__(256) void bn_stats_final(int P, int C, long M, const float* __restrict__ x,
+                                                      const double* __restrict__ part, float eps, float momentum,
+                                                      float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                      float* __restrict__ run_mean, float* __restrict__ run_var) {
+  bn_stats_reduce(P, C, M, x, part, blockIdx.x, eps, momentum, save_mean, save_invstd, run_mean, run_var);
 }
 
 __global__ void bn_eval_prep(int C, const float* __restrict__ run_mean, const float* __restrict__ run_var, float eps,
@@ -194,12 +213,43 @@ __global__ void bn_apply(int total, FastDiv fC, const float* __restrict__ x, lon
   y[r * ldy + c] = v;
 }
 
-// partial sums of dyv and dyv*xhat,  dyv = dy * (relu_out > 0 if relu_out)
-__global__ __launch_bounds__(256) void bn_bwd_partial(int M, int C, const float* __restrict__ dy, long lddy,
-                                                      const float* __restrict__ x, long ldx,
-                                                      const float* __restrict__ relu_out, long ldo,
-                                                      const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                      int rows_per, double* __restrict__ part) {
+// BN backward sums: s1 = sum dyv, s2 = sum dyv*xhat (dyv = dy * (relu_out > 0) if relu_out) in fp64.
+// Partial blocks (64 channels x 4 row lanes) -> part[p][2][C]; the fixed-order reduction (as in
+// bn_stats_reduce) writes sums[0:C] = s1, sums[C:2C] = s2 and dw = beta_w*dw + s2, db = beta_w*db + s1,
+// in the last-arriving block of each 64-channel group (tickets) or in bn_bwd_final.
+__device__ __forceinline__ void bn_bwd_reduce(int P, int C, const double* __restrict__ part, int cx,
+                                              double* __restrict__ sums, float* __restrict__ dw,
+                                              float* __restrict__ db, float beta_w) {
+  __shared__ double shr[2][4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = cx * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += 4) {
+      s1 += part[(long)p * 2 * C + c];
+      s2 += part[(long)p * 2 * C + C + c];
+    }
+  }
+  shr[0][pl][cl] = s1;
+  shr[1][pl][cl] = s2;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  s1 = shr[0][0][cl] + shr[0][1][cl] + shr[0][2][cl] + shr[0][3][cl];
+  s2 = shr[1][0][cl] + shr[1][1][cl] + shr[1][2][cl] + shr[1][3][cl];
+  sums[c] = s1;
+  sums[C + c] = s2;
+  if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)s2;
+  if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_sums(int M, int C, const float* __restrict__ dy, long lddy,
+                                                   const float* __restrict__ x, long ldx,
+                                                   const float* __restrict__ relu_out, long ldo,
+                                                   const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                   int rows_per, double* __restrict__ part,
+                                                   unsigned int* __restrict__ cnt, double* __restrict__ sums,
+                                                   float* __restrict__ dw, float* __restrict__ db, float beta_w) {
   __shared__ double sh[2][4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -208,6 +258,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(int M, int C, const float*
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const float mu = mean[c], is = invstd[c];
+#pragma unroll 4
     for (long r = r0 + rl; r < r1; r += 4) {
       float d = dy[r * lddy + c];
       if (relu_out && !(relu_out[r * ldo + c] > 0.f)) d = 0.f;
@@ -223,30 +274,23 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(int M, int C, const float*
     p[0] = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
     p[C] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
   }
+  if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
+  bn_bwd_reduce(gridDim.y, C, part, blockIdx.x, sums, dw, db, beta_w);
 }
 
-// dw/db from the reduced sums (sums[0:C] = sum dyv, sums[C:2C] = sum dyv*xhat)
-__global__ void bn_bwd_finish(int C, const double* __restrict__ sums, float* __restrict__ dw, float* __restrict__ db,
-                              float beta_w) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)sums[C + c];
-  if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)sums[c];
+__global__ __launch_bounds__(256) void bn_bwd_final(int P, int C, const double* __restrict__ part,
+                                                    double* __restrict__ sums, float* __restrict__ dw,
+                                                    float* __restrict__ db, float beta_w) {
+  bn_bwd_reduce(P, C, part, blockIdx.x, sums, dw, db, beta_w);
 }
 
 // train: dx = w*invstd*(dyv - s1/M - xhat*s2/M);  eval (sums == null): dx = w*invstd*dyv
 __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, long lddy, const float* __restrict__ x,
                              long ldx, const float* __restrict__ relu_out, long ldo, const float* __restrict__ mean,
                              const float* __restrict__ invstd, const float* __restrict__ w,
-                             const double* __restrict__ sums, float* __restrict__ dx, long lddx, float beta_dx,
-                             const double* __restrict__ red, float* __restrict__ dw, float* __restrict__ db,
-                             float beta_w) {
+                             const double* __restrict__ sums, float* __restrict__ dx, long lddx, float beta_dx) {
   const int C = fC.div;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < C) {
-    if (dw) dw[idx] = (beta_w != 0.f ? beta_w * dw[idx] : 0.f) + (float)red[C + idx];
-    if (db) db[idx] = (beta_w != 0.f ? beta_w * db[idx] : 0.f) + (float)red[idx];
-  }
   if (idx >= M * C) return;
   int c;
   const long r = fdivmod(idx, fC, c);
@@ -265,9 +309,11 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
   *p = (beta_dx != 0.f ? beta_dx * *p : 0.f) + v;
 }
 
-int bn_rows_per(long M, int C, long ws_floats, int per_row_floats) {
-  int rows_per = std::max<long>(32, (M + 255) / 256);
-  while ((long)vc_cdiv(M, rows_per) * C * per_row_floats > ws_floats || vc_cdiv(M, rows_per) > 2048) rows_per *= 2;
+// rows per partial block: at most 64 partials per 64-channel group (the fixed-order reduction reads
+// P/4 of them per thread), at least 32 rows each, fewer partials if the fp64 workspace is short
+int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
+  int rows_per = std::max<long>(32, (M + 63) / 64);
+  while ((long)vc_cdiv(M, rows_per) * 2 * C + reserve_doubles > ws_doubles && rows_per < (1 << 29)) rows_per *= 2;
   return rows_per;
 }
 
@@ -307,10 +353,11 @@ VC_EXPORT int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const f
 }
 
 // Train: batch statistics -> save_mean / save_invstd, running stats updated (if run_mean).
-// Eval (train == 0): save_* filled from the running statistics.
-VC_EXPORT int vc_bn_stats(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
-                          float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* ws,
-                          long ws_floats, hipStream_t stream) {
+// Eval (train == 0): save_* filled from the running statistics.  counters (optional): >= ceil(C/64)
+// zeroed arrival counters (left zero) — the reduction then runs in the partial launch itself.
+VC_EXPORT int vc_bn_stats_ex(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                             float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* ws,
+                             long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream) {
   VC_REQUIRE(C > 0 && M >= 0);
   if (!train) {
     hipLaunchKernelGGL(bn_eval_prep, dim3(vc_cdiv(C, 256)), dim3(256), 0, stream, C, run_mean, run_var, eps,
@@ -318,20 +365,30 @@ VC_EXPORT int vc_bn_stats(int train, long M, int C, const float* x, long ldx, fl
     VC_CHECK_LAUNCH();
     return VC_OK;
   }
-  VC_REQUIRE(M > 0 && ((uintptr_t)ws & 7) == 0);
-  // partial (count, mean, M2) triples are fp64: the workspace holds ws_floats/2 doubles
+  VC_REQUIRE(M > 0 && M < (1L << 31) && ((uintptr_t)ws & 7) == 0);
+  // partial (s1, s2) pairs are fp64: the workspace holds ws_floats/2 doubles
   double* wsd = reinterpret_cast<double*>(ws);
   const long ws_doubles = ws_floats / 2;
-  const int rows_per = bn_rows_per(M, C, ws_doubles, 3);
+  const int rows_per = bn_rows_per(M, C, ws_doubles, 0);
   const int P = vc_cdiv(M, rows_per);
-  VC_REQUIRE((long)P * C * 3 <= ws_doubles);
-  hipLaunchKernelGGL(bn_stats_partial, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, x, ldx, rows_per,
-                     wsd);
+  VC_REQUIRE((long)P * C * 2 <= ws_doubles && P <= 65535);
+  unsigned int* cnt = (counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;
+  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
+                     cnt, eps, momentum, save_mean, save_invstd, run_mean, run_var);
   VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_final, dim3(vc_cdiv(C, 16)), dim3(256), 0, stream, P, C, M, wsd, eps, momentum,
-                     save_mean, save_invstd, run_mean, run_var);
-  VC_CHECK_LAUNCH();
+  if (!cnt) {
+    hipLaunchKernelGGL(bn_stats_final, dim3(vc_cdiv(C, 64)), dim3(256), 0, stream, P, C, M, x, wsd, eps, momentum,
+                       save_mean, save_invstd, run_mean, run_var);
+    VC_CHECK_LAUNCH();
+  }
   return VC_OK;
+}
+
+VC_EXPORT int vc_bn_stats(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                          float* save_mean, float* save_invstd, float* run_mean, float* run_var, float* ws,
+                          long ws_floats, hipStream_t stream) {
+  return vc_bn_stats_ex(train, M, C, x, ldx, eps, momentum, save_mean, save_invstd, run_mean, run_var, ws, ws_floats,
+                        nullptr, 0, stream);
 }
 
 VC_EXPORT int vc_bn_apply(long M, int C, const float* x, long ldx, const float* mean, const float* invstd,
@@ -347,36 +404,42 @@ VC_EXPORT int vc_bn_apply(long M, int C, const float* x, long ldx, const float* 
 }
 
 // BN backward (optionally through a following ReLU whose output is relu_out).
-// dx = beta_dx*dx + ...;  dw/db = beta_w*dw/db + ... (either may be null).
+// dx = beta_dx*dx + ...;  dw/db = beta_w*dw/db + ... (either may be null).  counters (optional):
+// >= ceil(C/64) zeroed arrival counters (left zero): the sums are reduced inside the partial launch.
+VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
+                           const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
+                           float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w, float* ws,
+                           long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream) {
+  VC_REQUIRE(C > 0 && M > 0 && M < (1L << 31) && ((uintptr_t)ws & 7) == 0);
+  // per-row-block partial sums [P][2][C] and the final [2][C] sums are fp64
+  double* wsd = reinterpret_cast<double*>(ws);
+  const long ws_doubles = ws_floats / 2;
+  const int rows_per = bn_rows_per(M, C, ws_doubles, 2L * C);
+  const int P = vc_cdiv(M, rows_per);
+  VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_doubles && P <= 65535);
+  double* sums = wsd + (long)P * C * 2;
+  unsigned int* cnt = (counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;
+  hipLaunchKernelGGL(bn_bwd_sums, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, dy, lddy, x, ldx,
+                     relu_out, ldo, mean, invstd, rows_per, wsd, cnt, sums, dw, db, beta_w);
+  VC_CHECK_LAUNCH();
+  if (!cnt) {
+    hipLaunchKernelGGL(bn_bwd_final, dim3(vc_cdiv(C, 64)), dim3(256), 0, stream, P, C, wsd, sums, dw, db, beta_w);
+    VC_CHECK_LAUNCH();
+  }
+  if (dx) {
+    VC_REQUIRE_I32(M * C);
+    hipLaunchKernelGGL(bn_bwd_apply, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)M, make_fastdiv(C), dy,
+                       lddy, x, ldx, relu_out, ldo, mean, invstd, w, train ? sums : (const double*)nullptr, dx, lddx,
+                       beta_dx);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
 VC_EXPORT int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
                         const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
                         float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w, float* ws,
                         long ws_floats, hipStream_t stream) {
-  VC_REQUIRE(C > 0 && M > 0 && ((uintptr_t)ws & 7) == 0);
-  // per-row-block partial sums [P][2][C] and the final [2][C] sums are fp64
-  double* wsd = reinterpret_cast<double*>(ws);
-  const long ws_doubles = ws_floats / 2;
-  const int rows_per = bn_rows_per(M, C, ws_doubles - 2L * C, 2);
-  const int P = vc_cdiv(M, rows_per);
-  VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_doubles);
-  double* sums = wsd + (long)P * C * 2;
-  hipLaunchKernelGGL(bn_bwd_partial, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, dy, lddy, x, ldx,
-                     relu_out, ldo, mean, invstd, rows_per, wsd);
-  VC_CHECK_LAUNCH();
-  // one pass over the [P][2C] partials gives both sums (sum dy, sum dy*xhat)
-  hipLaunchKernelGGL(sum_rows_d_kernel, dim3(vc_cdiv(2L * C, 16)), dim3(256), 0, stream, P, 2 * C, wsd, 2L * C, 0L,
-                     sums);
-  VC_CHECK_LAUNCH();
-  if (dx) {
-    VC_REQUIRE_I32(M * C);
-    hipLaunchKernelGGL(bn_bwd_apply, dim3(vc_cdiv(std::max<long>(M * C, C), 256)), dim3(256), 0, stream, (int)M,
-                       make_fastdiv(C), dy,
-                       lddy, x, ldx, relu_out, ldo, mean, invstd, w, train ? sums : (const double*)nullptr, dx, lddx,
-                       beta_dx, sums, dw, db, beta_w);
-    VC_CHECK_LAUNCH();
-  } else {
-    hipLaunchKernelGGL(bn_bwd_finish, dim3(vc_cdiv(C, 256)), dim3(256), 0, stream, C, sums, dw, db, beta_w);
-    VC_CHECK_LAUNCH();
-  }
-  return VC_OK;
+  return vc_bn_bwd_ex(train, M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, w, dx, lddx, beta_dx, dw, db,
+                      beta_w, ws, ws_floats, nullptr, 0, stream);
 }

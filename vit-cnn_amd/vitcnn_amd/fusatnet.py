@@ -23,9 +23,19 @@ import torch.nn as nn
 
 from ._lib import lib
 from .flat import F32, FlatParams
-from .model import _IMPLICIT_CONV
+from .model import _IMPLICIT_CONV, N_COUNTERS
 
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
+_COUNTER_BUFS = {}
+
+
+def _counters(dev, stream):
+    """one zeroed arrival-counter array per (device, stream) (split-K in-launch combine, BN
+    reductions): kernels of one stream run in order and each leaves its counters zero"""
+    key = (dev.type, dev.index, stream)
+    if key not in _COUNTER_BUFS:
+        _COUNTER_BUFS[key] = torch.zeros(N_COUNTERS, dtype=torch.int32, device=dev)
+    return _COUNTER_BUFS[key].data_ptr()
 
 
 class ConvUnit(nn.Module):
@@ -192,6 +202,7 @@ class _Program:
         self.B, self.P = x1.shape[0], x1.shape[2]
         self.x1, self.x2 = x1, x2
         self.scr = torch.empty(self.SCRATCH, dtype=torch.float32, device=self.dev)
+        self.cnt = _counters(self.dev, self.s)
         self.train = m.training
         self.grad = grad
         self.tape = []        # backward closures, run in reverse
@@ -227,8 +238,8 @@ class _Program:
         return y
 
     def gemm(self, tA, tB, M, N, K, A, lda, Bm, ldb, beta, C, ldc, bias=None, bias_grad=None):
-        self.L.vc_gemm(tA, tB, M, N, K, 1.0, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, bias, None, 0, 0, 0, bias_grad,
-                       self.scr.data_ptr(), self.SCRATCH, self.s)
+        self.L.vc_gemm_ex(tA, tB, M, N, K, 1.0, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, bias, None, 0, 0, 0,
+                          bias_grad, self.scr.data_ptr(), self.SCRATCH, self.cnt, N_COUNTERS, self.s)
 
     def conv3(self, x, ldx, H, C, conv, pad):
         """x [B,H,W,C] rows (ld ldx) -> conv3x3 + bias, [B,OH,OH,O] contiguous: vc_im2col3x3_pad + vc_gemm
@@ -273,9 +284,10 @@ class _Program:
 
     def bn_relu(self, y, M, C, bn, relu=1):
         mean, invstd = self.new(C), self.new(C)
-        self.L.vc_bn_stats(1 if self.train else 0, M, C, y.data_ptr(), C, bn.eps, bn.momentum if bn.momentum is not None
-                           else BN_MOMENTUM, mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(),
-                           bn.running_var.data_ptr(), self.scr.data_ptr(), self.SCRATCH, self.s)
+        self.L.vc_bn_stats_ex(1 if self.train else 0, M, C, y.data_ptr(), C, bn.eps,
+                              bn.momentum if bn.momentum is not None else BN_MOMENTUM, mean.data_ptr(),
+                              invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                              self.scr.data_ptr(), self.SCRATCH, self.cnt, N_COUNTERS, self.s)
         if self.train:
             bn.num_batches_tracked.add_(1)
         z = self.new(*y.shape) if self.grad else y
@@ -283,10 +295,11 @@ class _Program:
                            bn.bias.data_ptr(), relu, z.data_ptr(), C, self.s)
 
         def bwd():
-            self.L.vc_bn_bwd(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
-                             z.data_ptr() if relu else None, C, mean.data_ptr(), invstd.data_ptr(),
-                             bn.weight.data_ptr(), self.grad_of(y).data_ptr(), C, 1.0, self.pgrad(bn.weight),
-                             self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.s)
+            self.L.vc_bn_bwd_ex(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
+                                z.data_ptr() if relu else None, C, mean.data_ptr(), invstd.data_ptr(),
+                                bn.weight.data_ptr(), self.grad_of(y).data_ptr(), C, 1.0, self.pgrad(bn.weight),
+                                self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.cnt, N_COUNTERS,
+                                self.s)
 
         self.record(bwd, y, z)
         return z

@@ -485,8 +485,9 @@ class _Program:
     def bn_stats(self, pfx, X, ldx, M, C, tag):
         ws = self.ws
         mean, inv = ws.f(tag + ".bm", C), ws.f(tag + ".bi", C)
-        self.L.vc_bn_stats(self.train, M, C, X, ldx, BN_EPS, BN_MOM, mean, inv, self.BUF[pfx + ".running_mean"],
-                           self.BUF[pfx + ".running_var"], self.scr_p, self.scr_n, self.s)
+        self.L.vc_bn_stats_ex(self.train, M, C, X, ldx, BN_EPS, BN_MOM, mean, inv, self.BUF[pfx + ".running_mean"],
+                              self.BUF[pfx + ".running_var"], self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS,
+                              self.s)
         return mean, inv
 
     def layernorm(self, pfx, X, R, C, tag):
@@ -677,9 +678,10 @@ class _Program:
     # ---------------------------------------------------------------- backward
     def bn_bwd(self, pfx, tag, dY, lddy, X, ldx, relu_out, M, C, dX, lddx, beta_dx):
         ws = self.ws
-        self.L.vc_bn_bwd(self.train, M, C, dY, lddy, X, ldx, relu_out or None, C, ws.f(tag + ".bm", C),
-                         ws.f(tag + ".bi", C), self.P[pfx + ".weight"], dX or None, lddx, beta_dx,
-                         self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n, self.s)
+        self.L.vc_bn_bwd_ex(self.train, M, C, dY, lddy, X, ldx, relu_out or None, C, ws.f(tag + ".bm", C),
+                            ws.f(tag + ".bi", C), self.P[pfx + ".weight"], dX or None, lddx, beta_dx,
+                            self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n,
+                            self._cnt[self.cur], N_COUNTERS, self.s)
 
     def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx):
         ws = self.ws
