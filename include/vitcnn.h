@@ -70,6 +70,10 @@ VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
 /* out[c] = beta*out[c] + sum_r X[r*ldx + c]  (bias gradients; fixed-order two-stage) */
 VC_API int vc_colsum(int R, int C, const float* X, long ldx, float* out, float beta,
                      float* ws, long ws_floats, hipStream_t stream);
+/* The same with >= ceil(C/64) zeroed arrival counters (left zero; per stream): the partials are
+ * reduced in the last-arriving block of each column group, no second launch. */
+VC_API int vc_colsum_ex(int R, int C, const float* X, long ldx, float* out, float beta,
+                        float* ws, long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream);
 
 /* ---------------------------------------------------------------- normalisation
  * LayerNorm over the last dim (nn.LayerNorm eps=1e-6 via build_norm_layer,
@@ -80,6 +84,11 @@ VC_API int vc_layernorm_fwd(int R, int C, const float* x, long ldx, const float*
 VC_API int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
                             const float* mean, const float* rstd, float* dx, long lddx, float beta_dx,
                             float* dw, float* db, float beta_w, float* ws, long ws_floats, hipStream_t stream);
+/* The same with dx = res + LNgrad: the residual gradient is read from res (left untouched). */
+VC_API int vc_layernorm_bwd_res(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
+                                const float* mean, const float* rstd, const float* res, long ldr, float* dx,
+                                long lddx, float* dw, float* db, float beta_w, float* ws, long ws_floats,
+                                hipStream_t stream);
 
 /* BatchNorm2d over channels-last rows (torch train/eval semantics, eps, momentum):
  * ms_conv_bn_relu.bn (Mutimodality_Mamba7.py:1039), FusionLayer BN (:1103, :1129),

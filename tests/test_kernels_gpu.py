@@ -137,6 +137,54 @@ def test_colsum(L, ws):
     assert rel_err(out.cpu().numpy(), (X.sum(0) + 1).numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("R,C", [(51840, 72), (64, 81 * 144), (256, 72 * 16), (3000, 130), (5, 7)])
+def test_colsum_ticketed_is_bit_identical(L, ws, R, C):
+    """vc_colsum_ex (last-arriving block of each column group reduces) == vc_colsum (separate
+    reduction launch), bit for bit, twice in a row (counters left zero), and against fp64"""
+    X = rnd(R, C, seed=R + C)
+    Xd = X.to(DEV)
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    outs = []
+    for ex in (False, True, True):
+        out = torch.full((C,), 0.25, device=DEV)
+        if ex:
+            L.vc_colsum_ex(R, C, P(Xd), C, P(out), 2.0, P(ws), ws.numel(), P(cnt), cnt.numel(), S())
+        else:
+            L.vc_colsum(R, C, P(Xd), C, P(out), 2.0, P(ws), ws.numel(), S())
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+        assert int(cnt.abs().sum()) == 0
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert rel_err(outs[0].numpy(), (X.double().sum(0) + 0.5).numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("R,C", [(5184, 144), (3136, 256), (7, 144)])
+def test_layernorm_bwd_residual_is_bit_identical(L, ws, R, C):
+    """vc_layernorm_bwd_res (dx = res + LN grad, res untouched) == vc_layernorm_bwd with dx preset to res
+    and beta_dx 1, bit for bit (dw / db accumulated with beta_w 1)"""
+    x, dy = (rnd(R, C, seed=3) + 0.5).to(DEV), rnd(R, C, seed=4).to(DEV)
+    w, b = (rnd(C, seed=5) + 1).to(DEV), rnd(C, seed=6).to(DEV)
+    res = rnd(R, C, seed=7).to(DEV)
+    res0 = res.clone()
+    y, mean, rstd = torch.empty(R, C, device=DEV), torch.empty(R, device=DEV), torch.empty(R, device=DEV)
+    L.vc_layernorm_fwd(R, C, P(x), C, P(w), P(b), 1e-6, P(y), C, P(mean), P(rstd), S())
+    outs = []
+    for variant in (0, 1):
+        dx = res.clone() if variant == 0 else torch.full((R, C), float("nan"), device=DEV)
+        dw, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), -0.5, device=DEV)
+        if variant == 0:
+            L.vc_layernorm_bwd(R, C, P(dy), C, P(x), C, P(w), P(mean), P(rstd), P(dx), C, 1.0, P(dw), P(db), 1.0,
+                               P(ws), ws.numel(), S())
+        else:
+            L.vc_layernorm_bwd_res(R, C, P(dy), C, P(x), C, P(w), P(mean), P(rstd), P(res), C, P(dx), C, P(dw),
+                                   P(db), 1.0, P(ws), ws.numel(), S())
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (dx, dw, db)])
+    assert torch.equal(res.cpu(), res0.cpu())
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+
+
 @pytest.mark.parametrize("R,C", [(5184, 144), (3136, 256), (100, 256), (7, 144)])
 def test_layernorm_fwd_bwd(L, ws, R, C):
     x = rnd(R, C, seed=13, scale=3.0) + 0.5

@@ -262,20 +262,56 @@ __global__ __launch_bounds__(64) void splitk_reduce(GemmArgs g) {
   store_out(g, b, m, n, s);
 }
 
-// stage 1 of a column sum: block (cx, ry) sums rows [ry*rows_per, ...) of 64 columns
+// Column sums: block (cx, ry) sums rows [ry*rows_per, ...) of 64 columns (4 row lanes, combined in
+// order).  One row block (P == 1) writes out directly; else it writes part[ry][Cn] and the fixed-order
+// reduction over the P partials (colsum_reduce: 4 partial lanes p = l, l+4, ..., then the lanes in
+// order) runs in the last-arriving block of the column group (cnt) or in colsum_final.
+__device__ __forceinline__ void colsum_reduce(int P, int Cn, const float* __restrict__ part, int cx,
+                                              float* __restrict__ out, float beta) {
+  __shared__ float shr[4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = cx * 64 + cl;
+  float s = 0.f;
+  if (c < Cn) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += 4) s += part[(long)p * Cn + c];
+  }
+  shr[pl][cl] = s;
+  __syncthreads();
+  if (pl == 0 && c < Cn)
+    out[c] = (beta != 0.f ? beta * out[c] : 0.f) + ((shr[0][cl] + shr[1][cl]) + (shr[2][cl] + shr[3][cl]));
+}
+
 __global__ __launch_bounds__(256) void colsum_partial(int R, int Cn, const float* __restrict__ X, long ldx,
-                                                      int rows_per, float* __restrict__ part) {
+                                                      int rows_per, float* __restrict__ part,
+                                                      unsigned int* __restrict__ cnt, float* __restrict__ out,
+                                                      float beta) {
   __shared__ float sh[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int cl = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + cl;
   const int rl = threadIdx.x >> 6;
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(R, r0 + rows_per);
   float s = 0.f;
-  if (c < Cn)
+  if (c < Cn) {
+#pragma unroll 4
     for (int r = r0 + rl; r < r1; r += 4) s += X[(long)r * ldx + c];
-  sh[rl][threadIdx.x & 63] = s;
+  }
+  sh[rl][cl] = s;
   __syncthreads();
-  if (rl == 0 && c < Cn) part[(long)blockIdx.y * Cn + c] = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
+  if (gridDim.y == 1) {
+    if (rl == 0 && c < Cn)
+      out[c] = (beta != 0.f ? beta * out[c] : 0.f) + ((sh[0][cl] + sh[1][cl]) + (sh[2][cl] + sh[3][cl]));
+    return;
+  }
+  if (rl == 0 && c < Cn) part[(long)blockIdx.y * Cn + c] = (sh[0][cl] + sh[1][cl]) + (sh[2][cl] + sh[3][cl]);
+  if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
+  colsum_reduce(gridDim.y, Cn, part, blockIdx.x, out, beta);
+}
+
+__global__ __launch_bounds__(256) void colsum_final(int P, int Cn, const float* __restrict__ part,
+                                                    float* __restrict__ out, float beta) {
+  colsum_reduce(P, Cn, part, blockIdx.x, out, beta);
 }
 
 }  // namespace
@@ -908,25 +944,34 @@ VC_EXPORT int vc_gemm(int transA, int transB, int M, int N, int K, float alpha,
                     bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, nullptr, 0, stream);
 }
 
-// out[c] = beta * out[c] + sum_r X[r * ldx + c]   (deterministic two-stage; ws >= 2048 * ceil(C/64)*64)
-VC_EXPORT int vc_colsum(int R, int Cn, const float* X, long ldx, float* out, float beta, float* ws, long ws_floats,
-                        hipStream_t stream) {
+// out[c] = beta * out[c] + sum_r X[r * ldx + c]   (deterministic: fixed-order partials).  counters
+// (optional): >= ceil(Cn/64) zeroed arrival counters (left zero) -- the partials are then reduced in
+// the last-arriving block of each column group instead of a second launch.
+VC_EXPORT int vc_colsum_ex(int R, int Cn, const float* X, long ldx, float* out, float beta, float* ws, long ws_floats,
+                           unsigned int* counters, int n_counters, hipStream_t stream) {
   VC_REQUIRE(R >= 0 && Cn >= 0);
   if (Cn == 0) return VC_OK;
-  // ~64-128 rows per partial block, at most 512 partials, then a 16x16 parallel final sum
-  int rows_per = std::max(64, vc_cdiv(R, 512));
+  // ~64-128 rows per partial block, at most 128 partials (the reduction reads P/4 per thread)
+  int rows_per = std::max(64, vc_cdiv(R, 128));
   int P = std::max(1, vc_cdiv(R, rows_per));
-  while ((long)P * Cn > ws_floats && rows_per < (1 << 30)) {
+  while (P > 1 && (long)P * Cn > ws_floats && rows_per < (1 << 30)) {
     rows_per *= 2;
     P = std::max(1, vc_cdiv(R, rows_per));
   }
-  VC_REQUIRE((long)P * Cn <= ws_floats);
-  if (P == 1) {  // small R: a single pass writes the result directly
-    hipLaunchKernelGGL(colsum_partial, dim3(vc_cdiv(Cn, 64), 1), dim3(256), 0, stream, R, Cn, X, ldx, rows_per, ws);
-    VC_CHECK_LAUNCH();
-    return launch_sum_rows(1, Cn, ws, Cn, 0, out, beta, stream);
-  }
-  hipLaunchKernelGGL(colsum_partial, dim3(vc_cdiv(Cn, 64), P), dim3(256), 0, stream, R, Cn, X, ldx, rows_per, ws);
+  VC_REQUIRE(P == 1 || (long)P * Cn <= ws_floats);
+  VC_REQUIRE(P <= 65535);
+  unsigned int* cnt = (P > 1 && counters && n_counters >= vc_cdiv(Cn, 64)) ? counters : nullptr;
+  hipLaunchKernelGGL(colsum_partial, dim3(vc_cdiv(Cn, 64), P), dim3(256), 0, stream, R, Cn, X, ldx, rows_per, ws, cnt,
+                     out, beta);
   VC_CHECK_LAUNCH();
-  return launch_sum_rows(P, Cn, ws, Cn, 0, out, beta, stream);
+  if (P > 1 && !cnt) {
+    hipLaunchKernelGGL(colsum_final, dim3(vc_cdiv(Cn, 64)), dim3(256), 0, stream, P, Cn, ws, out, beta);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
+VC_EXPORT int vc_colsum(int R, int Cn, const float* X, long ldx, float* out, float beta, float* ws, long ws_floats,
+                        hipStream_t stream) {
+  return vc_colsum_ex(R, Cn, X, ldx, out, beta, ws, ws_floats, nullptr, 0, stream);
 }

@@ -50,12 +50,15 @@ __global__ __launch_bounds__(256) void ln_fwd(int R, int C, const float* __restr
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w ; per-block partial dw / db
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w ; per-block partial dw / db.
+// The result goes to dx as res + v (res given: a residual gradient read from another buffer) or
+// beta_dx * dx + v.
 __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, const float* __restrict__ dy,
                                               long lddy, const float* __restrict__ x, long ldx,
                                               const float* __restrict__ w, const float* __restrict__ mean,
                                               const float* __restrict__ rstd, float* __restrict__ dx, long lddx,
-                                              float beta_dx, float* __restrict__ part) {
+                                              float beta_dx, const float* __restrict__ res, long ldr,
+                                              float* __restrict__ part) {
   __shared__ float sh[4][2][512];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float pw[LN_MAXV], pb[LN_MAXV];
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, 
       if (c < C) {
         float v = rs * (g[j] - sg - xh[j] * sgx);
         float* p = dx + r * lddx + c;
-        *p = (beta_dx != 0.f ? *p * beta_dx : 0.f) + v;
+        *p = (res ? res[r * ldr + c] : (beta_dx != 0.f ? *p * beta_dx : 0.f)) + v;
       }
     }
   }
@@ -328,18 +331,19 @@ VC_EXPORT int vc_layernorm_fwd(int R, int C, const float* x, long ldx, const flo
   return VC_OK;
 }
 
-// dx = beta_dx*dx + LNgrad;  dw = beta_w*dw + sum dy*xhat;  db = beta_w*db + sum dy
-VC_EXPORT int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
-                               const float* mean, const float* rstd, float* dx, long lddx, float beta_dx, float* dw,
-                               float* db, float beta_w, float* ws, long ws_floats, hipStream_t stream) {
+static int layernorm_bwd(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
+                         const float* mean, const float* rstd, const float* res, long ldr, float* dx, long lddx,
+                         float beta_dx, float* dw, float* db, float beta_w, float* ws, long ws_floats,
+                         hipStream_t stream) {
   VC_REQUIRE(C > 0 && C <= 64 * LN_MAXV && R >= 0);
   if (R == 0) return VC_OK;
   int rows_per = std::max(16, vc_cdiv(R, 256));
   while ((long)vc_cdiv(R, rows_per) * 2 * C > ws_floats) rows_per *= 2;
   const int P = vc_cdiv(R, rows_per);
   hipLaunchKernelGGL(ln_bwd, dim3(P), dim3(256), 0, stream, R, C, rows_per, dy, lddy, x, ldx, w, mean, rstd, dx,
-                     lddx, beta_dx, ws);
+                     lddx, beta_dx, res, ldr, ws);
   VC_CHECK_LAUNCH();
+  // the [P][2C] partials: 16 columns x 16 partial lanes per block, in parallel over the columns
   if (dw && db == dw + C) return launch_sum_rows(P, 2 * C, ws, (long)2 * C, 0L, dw, beta_w, stream);  // adjacent
   if (dw) {
     int rc = launch_sum_rows(P, C, ws, (long)2 * C, 0L, dw, beta_w, stream);
@@ -350,6 +354,24 @@ VC_EXPORT int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const f
     if (rc) return rc;
   }
   return VC_OK;
+}
+
+// dx = beta_dx*dx + LNgrad;  dw = beta_w*dw + sum dy*xhat;  db = beta_w*db + sum dy
+VC_EXPORT int vc_layernorm_bwd(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
+                               const float* mean, const float* rstd, float* dx, long lddx, float beta_dx, float* dw,
+                               float* db, float beta_w, float* ws, long ws_floats, hipStream_t stream) {
+  return layernorm_bwd(R, C, dy, lddy, x, ldx, w, mean, rstd, nullptr, 0, dx, lddx, beta_dx, dw, db, beta_w, ws,
+                       ws_floats, stream);
+}
+
+// dx = res + LNgrad (a residual gradient from another buffer, which stays untouched)
+VC_EXPORT int vc_layernorm_bwd_res(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
+                                   const float* mean, const float* rstd, const float* res, long ldr, float* dx,
+                                   long lddx, float* dw, float* db, float beta_w, float* ws, long ws_floats,
+                                   hipStream_t stream) {
+  VC_REQUIRE(res != nullptr);
+  return layernorm_bwd(R, C, dy, lddy, x, ldx, w, mean, rstd, res, ldr, dx, lddx, 0.f, dw, db, beta_w, ws, ws_floats,
+                       stream);
 }
 
 // Train: batch statistics -> save_mean / save_invstd, running stats updated (if run_mean).

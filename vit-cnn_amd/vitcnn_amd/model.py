@@ -43,11 +43,15 @@ WGRAD_LANE = 2             # backward: lane 0's deferred weight gradients (lane 
 # BN affine costs more VALU than the small im2col matrices cost bandwidth); FusAtNet, whose col
 # matrices reach 611 MB, always uses the implicit GEMM
 _IMPLICIT_CONV = os.environ.get("VITCNN_IMPLICIT_CONV", "0") == "1"
-_DEFER_WGRAD = os.environ.get("VITCNN_DEFER_WGRAD", "0") == "1"   # measured slower (2.39 -> 2.63 ms): each cross-lane graph edge costs more than the overlap gains
+# lane-0 weight gradients are batched and issued on the weight-gradient lane at a few flush points
+# (one fork each); forking each one separately measured slower (2.39 -> 2.63 ms: every cross-lane
+# graph edge costs more than one GEMM's overlap gains)
+_DEFER_WGRAD = os.environ.get("VITCNN_DEFER_WGRAD", "1") == "1"
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 _LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
+_TRACER = None   # launch-structure recorder of tools/critical_path.py (None in normal runs)
 
 UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
                    "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
@@ -370,7 +374,7 @@ class _Program:
 
     def __init__(self, model: Multimodality_Mamba, device, B, train, mode):
         self.m = model
-        self.L = lib()
+        self.L = lib() if _TRACER is None else _TRACER.wrap(lib(), self)
         self.B = int(B)
         self.train = 1 if train else 0
         self.ws = model._workspace(device, B, ("train" if train else "eval", mode))
@@ -390,6 +394,7 @@ class _Program:
         self._ev_lane = {}
         self.lanes_on = _LANES
         self.wgrad_tail = None
+        self.pending_wgrads = []
         _, self.P, self.BUF, self.I64 = model._ptrs()
         self.device = device
 
@@ -431,6 +436,8 @@ class _Program:
         e = self._event()
         e.record(self.streams[self.cur])
         self._ev_lane[id(e)] = self.cur
+        if _TRACER is not None:
+            _TRACER.mark(e, self.cur)
         return e
 
     def wait(self, *events):
@@ -441,6 +448,8 @@ class _Program:
             if self._ev_lane.get(id(e)) == self.cur:
                 continue
             self.streams[self.cur].wait_event(e)
+            if _TRACER is not None:
+                _TRACER.wait(e, self.cur)
 
     @contextlib.contextmanager
     def lane(self, i, *after):
@@ -459,6 +468,9 @@ class _Program:
             e = self._event()
             e.record(self.streams[i])
             self.streams[0].wait_event(e)
+            if _TRACER is not None:
+                _TRACER.mark(e, i)
+                _TRACER.wait(e, 0)
 
     # ---------------------------------------------------------------- gemm wrappers
     def mm_nt(self, M, N, K, A, lda, W, ldw, C, ldc, bias=0, alpha=1.0, beta=0.0, add=0, add_ld=0, add_mod=0,
@@ -479,7 +491,7 @@ class _Program:
                        bias_grad or None)
 
     def colsum(self, R, C, X, ldx, out, beta=0.0):
-        self.L.vc_colsum(R, C, X, ldx, out, beta, self.scr_p, self.scr_n, self.s)
+        self.L.vc_colsum_ex(R, C, X, ldx, out, beta, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
 
     # ---------------------------------------------------------------- building blocks (forward)
     def bn_stats(self, pfx, X, ldx, M, C, tag):
@@ -683,8 +695,14 @@ class _Program:
                             self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n,
                             self._cnt[self.cur], N_COUNTERS, self.s)
 
-    def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx):
+    def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx, res=0):
+        """dX = beta_dx * dX + LN grad, or res + LN grad (res: a residual gradient in another buffer)"""
         ws = self.ws
+        if res:
+            self.L.vc_layernorm_bwd_res(R, C, dY, C, X, C, self.P[pfx + ".weight"], ws.f(tag + ".m", R),
+                                        ws.f(tag + ".r", R), res, C, dX, C, self.G[pfx + ".weight"],
+                                        self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n, self.s)
+            return
         self.L.vc_layernorm_bwd(R, C, dY, C, X, C, self.P[pfx + ".weight"], ws.f(tag + ".m", R), ws.f(tag + ".r", R),
                                 dX, C, beta_dx, self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p,
                                 self.scr_n, self.s)
@@ -692,23 +710,35 @@ class _Program:
     def linear_bwd(self, wname, bname, dY, M, N, K, X, ldx, dX, beta_dx, lddy=None, defer=False):
         """Y[M,N] = X[M,K] W[N,K]^T + b:  dW = dY^T X, db = colsum(dY), dX (+)= dY W.
 
-        defer (lane 0 only): the weight gradient (and its split-K combine) runs on the weight-gradient
-        lane, forked from here, so the data gradient — the only part the rest of the backward waits
-        for — follows at once on lane 0.  Returns the wgrad lane's event after it (or None); the
-        caller must wait on it before anything overwrites dY or X."""
+        defer (lane 0 only): the weight gradient is queued (self.defer_wgrad) and issued on the
+        weight-gradient lane at the next flush_wgrads(), so the data gradient -- the only part the rest
+        of the backward waits for -- follows at once on lane 0.  The caller guarantees that nothing
+        writes dY or X again in this backward (they are read whenever the weight-gradient lane gets
+        there, up to the final join)."""
         lddy = lddy or N
-        ev = None
-        if defer and _DEFER_WGRAD and self.lanes_on and self.cur == 0:
-            e = self.mark()
-            with self.lane(WGRAD_LANE, e):
-                self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K, bias_grad=self.G[bname] if bname else 0)
-                ev = self.mark()
-            self.wgrad_tail = ev
-        else:
-            self.mm_tn(N, K, M, dY, lddy, X, ldx, self.G[wname], K, bias_grad=self.G[bname] if bname else 0)
+        self.defer_wgrad(defer, N, K, M, dY, lddy, X, ldx, self.G[wname], K, self.G[bname] if bname else 0)
         if dX:
             self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
-        return ev
+
+    def defer_wgrad(self, defer, M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=0):
+        """C[M,N] = A^T B (a weight gradient, mm_tn), now or -- defer on lane 0 with lanes on -- at the next
+        flush_wgrads()"""
+        if defer and _DEFER_WGRAD and self.lanes_on and self.cur == 0:
+            self.pending_wgrads.append((M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad))
+        else:
+            self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad)
+
+    def flush_wgrads(self):
+        """issue the queued weight gradients on the weight-gradient lane, forked once from lane 0 here;
+        wgrad_tail = that lane's event after them"""
+        if not self.pending_wgrads:
+            return
+        e = self.mark()
+        with self.lane(WGRAD_LANE, e):
+            for M, N, K, A, lda, Bm, ldb, C, ldc, bg in self.pending_wgrads:
+                self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bg)
+            self.wgrad_tail = self.mark()
+        self.pending_wgrads = []
 
     def wgrad_events(self):
         """the weight-gradient lane's latest event, as a list (empty if nothing was deferred)"""
@@ -842,14 +872,15 @@ class _Program:
         T2, dT = f(pfx + ".T2", rows * E), f(pfx + ".dT", rows * E)
         self.ln_bwd(gv + ".ln1", pfx + ".G", dG, T2, rows, E, dT, 0.0)
         YS, dYS = f(pfx + ".YS", rows * D), f(pfx + ".dYS", rows * D)
-        # its weight gradient reads dT, which the pre_norm backward below accumulates into
-        e_outw = self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0, defer=True)
+        # (the pre_norm backward below writes the residual sum to dTt, so dT stays as this reads it)
+        self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0, defer=True)
         U, XD, XZ = f(pfx + ".U", NDIR * rows * D), f(pfx + ".XD", NDIR * rows * XW), f(pfx + ".XZ", rows * 2 * D)
         Y, YP = f(pfx + ".Y", NDIR * rows * D), f(pfx + ".YP", rows * D)
         dU, dDTL = f(pfx + ".dU", NDIR * rows * D), f(pfx + ".dDTL", NDIR * rows * D)
         dXD, dXZ, dYP = f(pfx + ".dXD", NDIR * rows * XW), f(pfx + ".dXZ", rows * 2 * D), f(pfx + ".dYP", rows * D)
         # SiLU(z) gate (token-wise): dyp and the z half of dxz
         self.L.vc_mamba_gate_bwd(B, L_, D, XZ, YP, dYS, dYP, dXZ, self.s)
+        self.flush_wgrads()   # fusion, change_dim, out_proj: alongside the scan backward
         self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
                                  P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], Y, dYP,
                                  f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR)),
@@ -858,13 +889,7 @@ class _Program:
         nr = NDIR * rows
         # dt_proj: dt_lin = xdbl[:, :R] W_dt^T + b_dt
         # (the weight gradient reads dDTL and XD's dt-rank columns; the data gradient writes dXD's)
-        if _DEFER_WGRAD and self.lanes_on and self.cur == 0:
-            e = self.mark()
-            with self.lane(WGRAD_LANE, e):
-                self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, bias_grad=G[mx + ".dt_proj.bias"])
-                self.wgrad_tail = self.mark()
-        else:
-            self.mm_tn(D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, bias_grad=G[mx + ".dt_proj.bias"])
+        self.defer_wgrad(True, D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, G[mx + ".dt_proj.bias"])
         self.mm_nn(nr, R, D, dDTL, D, P[mx + ".dt_proj.weight"], R, dXD, XW)
         # x_proj: xdbl = u W_x^T
         self.linear_bwd(mx + ".x_proj.weight", None, dXD, nr, XW, D, U, D, dU, 1.0, defer=True)
@@ -873,18 +898,17 @@ class _Program:
                                     self.scr_n, self.s)
         Xn, dXn = f(pfx + ".Xn", rows * E), f(pfx + ".dXn", rows * E)
         self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0, defer=True)
-        T = f(pfx + ".T", rows * E)
-        if e_outw is not None:
-            self.wait(e_outw)
-        self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dT, 1.0)   # dT = residual + LN grad
+        self.flush_wgrads()   # dt_proj, x_proj, in_proj
+        T, dTt = f(pfx + ".T", rows * E), f(pfx + ".dTt", rows * E)
+        self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dTt, 0.0, res=dT)   # dTt = dT + LN grad
         if dX:
             self.wait(e_ch)
-            self.mm_nn(rows, Cin, E, dT, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
+            self.mm_nn(rows, Cin, E, dTt, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
         # pos_embed and patch_embed weight gradients: off the critical path
         e = self.mark()
         with self.lane(WGRAD_LANE if _DEFER_WGRAD else 0, e):
-            self.colsum(B, L_ * E, dT, L_ * E, G[gv + ".pos_embed"])
-            self.mm_tn(E, Cin, rows, dT, E, X, Cin, G[gv + ".patch_embed.projection.weight"], Cin)
+            self.colsum(B, L_ * E, dTt, L_ * E, G[gv + ".pos_embed"])
+            self.mm_tn(E, Cin, rows, dTt, E, X, Cin, G[gv + ".patch_embed.projection.weight"], Cin)
             if self.lanes_on and _DEFER_WGRAD:
                 self.wgrad_tail = self.mark()
 
@@ -925,11 +949,14 @@ class _Program:
             self.conv_bn_relu3_bwd("lidar1", self.LX, Pp, m.c2, 16, dL1, 0, 0.0)
             e_l3 = self.mark()
         # classifier + fusion2 (lane 0 so far) and fusion1 + LiDAR (lane 3): the "tail" bucket
+        if bucket_hook is not None:
+            self.flush_wgrads()   # fusion2's weight gradient belongs to the tail bucket
         self.bucket_ready(bucket_hook, "tail", e_l3, *self.wgrad_events())
         self.block_bwd(m.hsi2, "hsi2", self.H1, Pp - 2, dH2, dH1, e_f1)
         # block_bwd joined its lane-1 chain before dH1; its deferred weight gradients end at wgrad_tail
         self.bucket_ready(bucket_hook, "hsi2", *self.wgrad_events())
         self.block_bwd(m.hsi1, "hsi1", self.X0, Pp, dH1, None, None)
+        self.flush_wgrads()
         self.join_lanes()
         self.bucket_ready(bucket_hook, "hsi1")
         return grad
