@@ -67,6 +67,15 @@ VC_API int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha, 
  * state for tuning tools (tools/gemm_sweep.py), not for concurrent use. */
 VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
 
+/* Grouped launches: the fp32 (k-major kernel) GEMMs issued through vc_gemm / vc_gemm_ex on `stream`
+ * between vc_gemm_group_begin and vc_gemm_group_end are recorded and launched together as one grid
+ * (up to 8 per launch) plus one grouped split-K reduce -- a horizontal fusion for independent
+ * products (a layer's weight and data gradients, parallel branches).  The problems of a group must
+ * not depend on each other; each takes its own slice of the workspace and arrival counters passed
+ * to it.  Other GEMMs (bf16, long-K) and other streams launch at once.  Host-thread state. */
+VC_API int vc_gemm_group_begin(hipStream_t stream);
+VC_API int vc_gemm_group_end(void);
+
 /* out[c] = beta*out[c] + sum_r X[r*ldx + c]  (bias gradients; fixed-order two-stage) */
 VC_API int vc_colsum(int R, int C, const float* X, long ldx, float* out, float beta,
                      float* ws, long ws_floats, hipStream_t stream);

@@ -280,6 +280,69 @@ def test_batchnorm_ticketed_reduction_is_bit_identical(L, ws, M, C, relu):
             assert torch.equal(a, b)
 
 
+GROUP_PROBLEMS = [
+    # ta, tb, M, N, K, batch, bias_grad, beta  (weight / data gradients, batched TokenLearner, split-K)
+    (1, 0, 144, 256, 5184, 1, True, 0.0),
+    (0, 0, 5184, 144, 256, 1, False, 1.0),
+    (0, 1, 3136, 72, 256, 1, False, 0.0),
+    (1, 0, 81, 256, 49, 64, False, 0.0),
+    (0, 1, 49, 81, 256, 64, False, 0.0),
+    (1, 0, 72, 9, 51840, 1, True, 0.0),
+    (0, 0, 37, 29, 1000, 1, False, 0.5),
+    (1, 1, 50, 70, 300, 1, False, 0.0),
+    (0, 0, 64, 64, 64, 1, False, 0.0),
+]
+
+
+@pytest.mark.parametrize("n", [2, 3, 9])
+def test_gemm_group_is_bit_identical(L, ws, n):
+    """vc_gemm_group_begin / _end (one grouped grid + one grouped split-K reduce, 8 problems per launch)
+    == the same GEMMs launched one by one, bit for bit, including the in-launch combine's counters"""
+    probs = GROUP_PROBLEMS[:n]
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    ins, outs = [], []
+    for i, (ta, tb, M, N, K, batch, bg, beta) in enumerate(probs):
+        A = (rnd(batch, K, M, seed=50 + i) if ta else rnd(batch, M, K, seed=50 + i)).to(DEV)
+        B = (rnd(batch, N, K, seed=70 + i) if tb else rnd(batch, K, N, seed=70 + i)).to(DEV)
+        ins.append((A, B))
+    for grouped in (False, True, True):
+        res = []
+        if grouped:
+            L.vc_gemm_group_begin(S())
+        for i, (ta, tb, M, N, K, batch, bg, beta) in enumerate(probs):
+            A, B = ins[i]
+            C = rnd(batch, M, N, seed=90 + i).to(DEV)
+            bgr = torch.full((M,), 0.25, device=DEV) if bg else None
+            L.vc_gemm_ex(ta, tb, M, N, K, 1.0, P(A), M if ta else K, A[0].numel(), P(B), K if tb else N, B[0].numel(),
+                         beta, P(C), N, C[0].numel(), batch, None, None, 0, 0, F_LEGACY, P(bgr), P(ws), ws.numel(),
+                         P(cnt), cnt.numel(), S())
+            res.append((C, bgr))
+        if grouped:
+            L.vc_gemm_group_end()
+        torch.cuda.synchronize()
+        outs.append([(c.cpu(), b.cpu() if b is not None else None) for c, b in res])
+        assert int(cnt.abs().sum()) == 0
+    for o in outs[1:]:
+        for (c0, b0), (c1, b1) in zip(outs[0], o):
+            assert torch.equal(c0, c1)
+            assert b0 is None or torch.equal(b0, b1)
+    # and the first problem against a float64 product
+    ta, tb, M, N, K, batch, bg, beta = probs[0]
+    A, B = ins[0]
+    ref = (A[0].double().cpu().T if ta else A[0].double().cpu()) @ (B[0].double().cpu().T if tb else B[0].double().cpu())
+    ref = ref + beta * rnd(batch, M, N, seed=90)[0].double()
+    assert rel_err(outs[1][0][0][0].numpy(), ref.numpy()) < 1e-5
+
+
+def test_gemm_group_misuse_raises(L):
+    L.vc_gemm_group_begin(S())
+    with pytest.raises(RuntimeError):
+        L.vc_gemm_group_begin(S())
+    L.vc_gemm_group_end()
+    with pytest.raises(RuntimeError):
+        L.vc_gemm_group_end()
+
+
 @pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("ta,tb,M,N,K,bgrad", [(1, 0, 72, 9, 51840, True), (1, 0, 256, 1296, 3136, True),
                                                (0, 1, 3136, 256, 1296, False), (1, 0, 41, 72, 51840, False),

@@ -83,15 +83,17 @@ __device__ __forceinline__ void tile_idx(int tid, int e, int& r, int& k) {
   }
 }
 
+// One 64x64 output tile (bx, by) of K slice / batch bz; tn x tm tiles per slice (the arrival-counter
+// index of the in-launch combine).  Shared by the single-problem kernel and the grouped one, which
+// own the LDS (As, Bs: BK * LDS_STRIDE floats each, `last`: one int).
 template <bool TA, bool TB, bool VA, bool VB>
-__global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
-  __shared__ float As[BK * LDS_STRIDE];
-  __shared__ float Bs[BK * LDS_STRIDE];
+__device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by, int bz, int tn, int tm,
+                                              float* __restrict__ As, float* __restrict__ Bs, int* last) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int zb = blockIdx.z / g.nsplit, zs = blockIdx.z % g.nsplit;
+  const int n0 = bx * BN, m0 = by * BM;
+  const int zb = bz / g.nsplit, zs = bz % g.nsplit;
   const int kbeg = zs * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
   const float* A = g.A + (long)zb * g.sA;
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
         const int m = m0 + wm * 32 + mi * 16 + fk * 4 + r;
         const int n = n0 + wn * 32 + ni * 16 + fr;
         if (m < g.M && n < g.Ne) {
-          if (g.nsplit > 1) g.part[((long)blockIdx.z * g.M + m) * g.Ne + n] = acc[mi][ni][r];
+          if (g.nsplit > 1) g.part[((long)bz * g.M + m) * g.Ne + n] = acc[mi][ni][r];
           else store_out(g, zb, m, n, acc[mi][ni][r]);
         }
       }
@@ -217,18 +219,17 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
   // the tile's last arriver acquires and sums all slices in fixed z order — the same order as
   // splitk_reduce, so results do not depend on which slice arrives last — then re-zeroes the
   // counter for the next launch on this stream.
-  __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int tile = (zb * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  const int tile = (zb * tm + by) * tn + bx;
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(&g.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == (unsigned)(g.nsplit - 1));
+    *last = (t == (unsigned)(g.nsplit - 1));
   }
   __syncthreads();
-  if (!last) return;
+  if (!*last) return;
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -246,6 +247,97 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
     store_out(g, zb, m, n, sum);
   }
   if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool TA, bool TB, bool VA, bool VB>
+__global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
+  __shared__ float As[BK * LDS_STRIDE];
+  __shared__ float Bs[BK * LDS_STRIDE];
+  __shared__ int last;
+  gemm_f32_tile<TA, TB, VA, VB>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, As, Bs, &last);
+}
+
+// Grouped launch: up to GROUP_MAX independent problems in one grid (a horizontal fusion of GEMMs that
+// would otherwise be separate launches on one stream).  Block b belongs to the problem p with
+// start[p] <= b < start[p + 1] and runs its tile (b - start[p]) in (x fastest, y, z) order; the
+// (TA, TB, VA, VB) variant is a runtime switch (registers: the largest variant's).
+constexpr int GROUP_MAX = 8;
+struct GemmGroup {
+  int n;
+  int start[GROUP_MAX + 1];
+  int tn[GROUP_MAX], tm[GROUP_MAX], variant[GROUP_MAX];
+  GemmArgs g[GROUP_MAX];
+};
+
+// The kernel arguments are indexed with constants only (an unrolled select), so the problem's
+// descriptor is read with scalar loads from the argument segment instead of a dynamically indexed
+// private copy.
+struct GroupSel {
+  GemmArgs g;
+  int start, tn, tm, variant;
+};
+
+__device__ __forceinline__ GroupSel group_select(const GemmGroup& G, int b) {
+  GroupSel s;
+  s.g = G.g[0];
+  s.start = G.start[0];
+  s.tn = G.tn[0];
+  s.tm = G.tm[0];
+  s.variant = G.variant[0];
+#pragma unroll
+  for (int k = 1; k < GROUP_MAX; ++k)
+    if (k < G.n && b >= G.start[k]) {
+      s.g = G.g[k];
+      s.start = G.start[k];
+      s.tn = G.tn[k];
+      s.tm = G.tm[k];
+      s.variant = G.variant[k];
+    }
+  return s;
+}
+
+__global__ __launch_bounds__(256) void gemm_f32_group(GemmGroup G) {
+  __shared__ float As[BK * LDS_STRIDE];
+  __shared__ float Bs[BK * LDS_STRIDE];
+  __shared__ int last;
+  const int b = blockIdx.x;
+  const GroupSel s = group_select(G, b);
+  const int local = b - s.start;
+  const int tn = s.tn, tm = s.tm;
+  const int bx = local % tn, by = (local / tn) % tm, bz = local / (tn * tm);
+  const GemmArgs& g = s.g;
+#define VC_TILE(V_, TA_, TB_, VA_, VB_) \
+  case V_: gemm_f32_tile<TA_, TB_, VA_, VB_>(g, bx, by, bz, tn, tm, As, Bs, &last); break;
+  switch (s.variant) {
+    VC_TILE(0, false, false, false, false) VC_TILE(1, false, false, false, true)
+    VC_TILE(2, false, false, true, false) VC_TILE(3, false, false, true, true)
+    VC_TILE(4, false, true, false, false) VC_TILE(5, false, true, false, true)
+    VC_TILE(6, false, true, true, false) VC_TILE(7, false, true, true, true)
+    VC_TILE(8, true, false, false, false) VC_TILE(9, true, false, false, true)
+    VC_TILE(10, true, false, true, false) VC_TILE(11, true, false, true, true)
+    VC_TILE(12, true, true, false, false) VC_TILE(13, true, true, false, true)
+    VC_TILE(14, true, true, true, false) VC_TILE(15, true, true, true, true)
+    default: break;
+  }
+#undef VC_TILE
+}
+
+// grouped split-K reduce: block b of problem p covers 64 output columns of one row (as splitk_reduce)
+__global__ __launch_bounds__(64) void splitk_reduce_group(GemmGroup G) {
+  const int b = blockIdx.x;
+  const GroupSel sel = group_select(G, b);
+  const GemmArgs& g = sel.g;
+  const int local = b - sel.start;
+  const int nx = (g.Ne + 63) / 64;
+  const int n = (local % nx) * 64 + threadIdx.x;
+  if (n >= g.Ne) return;
+  const int m = (local / nx) % g.M, bb = local / (nx * g.M);
+  const long slab = (long)g.M * g.Ne;
+  const float* pp = g.part + (long)bb * g.nsplit * slab + (long)m * g.Ne + n;
+  float s = 0.f;
+#pragma unroll 8
+  for (int z = 0; z < g.nsplit; ++z) s += pp[z * slab];
+  store_out(g, bb, m, n, s);
 }
 
 // grid (ceil(Ne/64), M, batch): one thread per output element, no index division; the
@@ -772,13 +864,21 @@ static long g2_combine_limit() {
   return v;
 }
 
-// the k-major fp32 kernel (LDS [k][row], 16x16x4 f32)
-static int launch_legacy(int transA, int transB, int M, int N, int K, float alpha,
-                         const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
-                         float beta, float* C, long ldc, long strideC, int batch,
-                         const float* bias, const float* addend, long add_ld, int add_mod, int flags,
-                         float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
-                         int n_counters, hipStream_t stream) {
+// the k-major fp32 kernel (LDS [k][row], 16x16x4 f32): launch configuration of one problem
+struct LegacyPlan {
+  GemmArgs g;
+  int tn, tm, nz, variant;
+  bool reduce;        // separate split-K reduce launch
+  long ws_floats;     // split-K slab floats used
+  int counters;       // arrival counters used (in-launch combine)
+};
+
+static LegacyPlan plan_legacy(int transA, int transB, int M, int N, int K, float alpha,
+                              const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                              float beta, float* C, long ldc, long strideC, int batch,
+                              const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                              float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                              int n_counters) {
   Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, flags};
   const int Ne = N + (bias_grad ? 1 : 0);
   const int tn = vc_cdiv(Ne, BN), tm = vc_cdiv(M, BM);
@@ -806,27 +906,145 @@ static int launch_legacy(int transA, int transB, int M, int N, int K, float alph
   const long slab_bytes = (long)nsplit * std::min(BM, M) * std::min(BN, Ne) * 4;
   unsigned int* cnt =
       (nsplit > 1 && tile_counters && tiles <= n_counters && slab_bytes <= 4096) ? tile_counters : nullptr;
-  GemmArgs g{M, N, K, Ne, k_chunk, nsplit, A, lda, strideA, B, ldb, strideB, C, ldc, strideC, bias_grad, ws, cnt, epi};
-  dim3 grid(tn, tm, batch * nsplit), block(256);
+  LegacyPlan pl;
+  pl.g = GemmArgs{M, N, K, Ne, k_chunk, nsplit, A, lda, strideA, B, ldb, strideB, C, ldc, strideC, bias_grad, ws, cnt,
+                  epi};
+  pl.tn = tn;
+  pl.tm = tm;
+  pl.nz = batch * nsplit;
   const bool va = ((uintptr_t)A % 16 == 0) && (lda % 4 == 0) && (batch == 1 || strideA % 4 == 0);
   const bool vb = ((uintptr_t)B % 16 == 0) && (ldb % 4 == 0) && (batch == 1 || strideB % 4 == 0);
-#define VC_LAUNCH_GEMM(TA_, TB_)                                                                           \
-  do {                                                                                                     \
-    if (va && vb) hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, true, true>), grid, block, 0, stream, g);    \
-    else if (va) hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, true, false>), grid, block, 0, stream, g);    \
-    else if (vb) hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, false, true>), grid, block, 0, stream, g);    \
-    else hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, false, false>), grid, block, 0, stream, g);           \
-  } while (0)
-  if (transA && transB) VC_LAUNCH_GEMM(true, true);
-  else if (transA) VC_LAUNCH_GEMM(true, false);
-  else if (transB) VC_LAUNCH_GEMM(false, true);
-  else VC_LAUNCH_GEMM(false, false);
-#undef VC_LAUNCH_GEMM
+  pl.variant = (transA ? 8 : 0) | (transB ? 4 : 0) | (va ? 2 : 0) | (vb ? 1 : 0);
+  pl.reduce = nsplit > 1 && !cnt;
+  pl.ws_floats = nsplit > 1 ? (long)nsplit * batch * M * Ne : 0;
+  pl.counters = cnt ? (int)tiles : 0;
+  return pl;
+}
+
+static int launch_plan(const LegacyPlan& pl, hipStream_t stream) {
+  const GemmArgs& g = pl.g;
+  dim3 grid(pl.tn, pl.tm, pl.nz), block(256);
+#define VC_L(V_, TA_, TB_, VA_, VB_) \
+  case V_: hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, VA_, VB_>), grid, block, 0, stream, g); break;
+  switch (pl.variant) {
+    VC_L(0, false, false, false, false) VC_L(1, false, false, false, true)
+    VC_L(2, false, false, true, false) VC_L(3, false, false, true, true)
+    VC_L(4, false, true, false, false) VC_L(5, false, true, false, true)
+    VC_L(6, false, true, true, false) VC_L(7, false, true, true, true)
+    VC_L(8, true, false, false, false) VC_L(9, true, false, false, true)
+    VC_L(10, true, false, true, false) VC_L(11, true, false, true, true)
+    VC_L(12, true, true, false, false) VC_L(13, true, true, false, true)
+    VC_L(14, true, true, true, false) VC_L(15, true, true, true, true)
+    default: return VC_EINVAL;
+  }
+#undef VC_L
   VC_CHECK_LAUNCH();
-  if (nsplit > 1 && !cnt) {
-    hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(Ne, 64), M, batch), dim3(64), 0, stream, g);
+  if (pl.reduce) {
+    hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(g.Ne, 64), g.M, pl.nz / g.nsplit), dim3(64), 0, stream, g);
     VC_CHECK_LAUNCH();
   }
+  return VC_OK;
+}
+
+// ---- grouped launches (vc_gemm_group_begin / _end): the fp32 k-major problems issued in between
+// on the group's stream are recorded and launched as one gemm_f32_group grid (plus one grouped
+// split-K reduce); each takes its own slice of the workspace and of the arrival counters.
+struct GroupState {
+  bool active = false;
+  hipStream_t stream = nullptr;
+  int n = 0;
+  LegacyPlan plans[GROUP_MAX];
+  long ws_used = 0;
+  int cnt_used = 0;
+  int err = 0;
+};
+static thread_local GroupState g_group;
+
+static int group_flush() {
+  GroupState& st = g_group;
+  const int n = st.n;
+  st.n = 0;
+  st.ws_used = 0;
+  st.cnt_used = 0;
+  if (n == 0) return VC_OK;
+  if (n == 1) return launch_plan(st.plans[0], st.stream);
+  GemmGroup G, R;
+  G.n = n;
+  R.n = 0;
+  long total = 0, rtotal = 0;
+  for (int p = 0; p < n; ++p) {
+    const LegacyPlan& pl = st.plans[p];
+    G.start[p] = (int)total;
+    G.tn[p] = pl.tn;
+    G.tm[p] = pl.tm;
+    G.variant[p] = pl.variant;
+    G.g[p] = pl.g;
+    total += (long)pl.tn * pl.tm * pl.nz;
+    if (pl.reduce) {
+      R.start[R.n] = (int)rtotal;
+      R.g[R.n] = pl.g;
+      R.tn[R.n] = R.tm[R.n] = R.variant[R.n] = 0;
+      ++R.n;
+      rtotal += (long)vc_cdiv(pl.g.Ne, 64) * pl.g.M * (pl.nz / pl.g.nsplit);
+    }
+  }
+  G.start[n] = (int)total;
+  VC_REQUIRE(total < (1L << 31) && rtotal < (1L << 31));
+  hipLaunchKernelGGL(gemm_f32_group, dim3((unsigned)total), dim3(256), 0, st.stream, G);
+  VC_CHECK_LAUNCH();
+  if (R.n) {
+    R.start[R.n] = (int)rtotal;
+    hipLaunchKernelGGL(splitk_reduce_group, dim3((unsigned)rtotal), dim3(64), 0, st.stream, R);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
+VC_EXPORT int vc_gemm_group_begin(hipStream_t stream) {
+  VC_REQUIRE(!g_group.active);
+  g_group.active = true;
+  g_group.stream = stream;
+  g_group.n = 0;
+  g_group.ws_used = 0;
+  g_group.cnt_used = 0;
+  g_group.err = 0;
+  return VC_OK;
+}
+
+VC_EXPORT int vc_gemm_group_end(void) {
+  VC_REQUIRE(g_group.active);
+  g_group.active = false;
+  const int err = g_group.err;
+  const int rc = group_flush();
+  return err ? err : rc;
+}
+
+static int launch_legacy(int transA, int transB, int M, int N, int K, float alpha,
+                         const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                         float beta, float* C, long ldc, long strideC, int batch,
+                         const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                         float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                         int n_counters, hipStream_t stream) {
+  GroupState& st = g_group;
+  if (!st.active || stream != st.stream)
+    return launch_plan(plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc,
+                                   strideC, batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats,
+                                   tile_counters, n_counters),
+                       stream);
+  if (st.n == GROUP_MAX) {
+    const int rc = group_flush();
+    if (rc) return rc;
+  }
+  // this problem's slices of the workspace and the counters follow the earlier problems' slices
+  float* wsp = ws ? ws + st.ws_used : nullptr;
+  const long wsn = ws ? ws_floats - st.ws_used : 0;
+  unsigned int* cp = tile_counters ? tile_counters + st.cnt_used : nullptr;
+  const int cn = tile_counters ? n_counters - st.cnt_used : 0;
+  LegacyPlan pl = plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
+                              batch, bias, addend, add_ld, add_mod, flags, bias_grad, wsp, wsn, cp, cn);
+  st.ws_used += (pl.ws_floats + 63) / 64 * 64;
+  st.cnt_used += pl.counters;
+  st.plans[st.n++] = pl;
   return VC_OK;
 }
 

@@ -52,6 +52,7 @@ N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 _LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
 _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in normal runs)
+_GROUP = os.environ.get("VITCNN_GEMM_GROUP", "1") != "0"   # grouped launches of independent fp32 GEMMs
 
 UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
                    "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
@@ -395,6 +396,7 @@ class _Program:
         self.lanes_on = _LANES
         self.wgrad_tail = None
         self.pending_wgrads = []
+        self._grouping = False
         _, self.P, self.BUF, self.I64 = model._ptrs()
         self.device = device
 
@@ -430,6 +432,21 @@ class _Program:
         if self.gemm_flags and not exact:
             args = args[:21] + (args[21] | self.gemm_flags,) + args[22:]
         self.L.vc_gemm_ex(*args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
+
+    @contextlib.contextmanager
+    def gemm_group(self):
+        """the fp32 GEMMs issued inside (on the current lane; they must be independent of each other)
+        launch as one grouped grid + one grouped split-K reduce (vc_gemm_group_begin / _end)"""
+        if not _GROUP or self.gemm_flags or self._grouping:   # nested: the outer group collects
+            yield
+            return
+        self.L.vc_gemm_group_begin(self.s)
+        self._grouping = True
+        try:
+            yield
+        finally:
+            self._grouping = False
+            self.L.vc_gemm_group_end()
 
     def mark(self):
         """event recorded on the current lane"""
@@ -631,10 +648,12 @@ class _Program:
         nl = pfx + ".FusionLayer.cross_attention"
         M = B * S
         TH = ws.f(pfx + ".TH", M * Ci)
-        self.mm_nt(M, Ci, Cout, Fl, Cout, P[nl + ".theta.weight"], Cout, TH, Ci, bias=P[nl + ".theta.bias"])
         PG = ws.f(pfx + ".PG", M * 2 * Ci)
-        self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, PG, 2 * Ci, bias=P[nl + ".phi.0.bias"])
-        self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".g.0.weight"], Cout, PG + F32 * Ci, 2 * Ci, bias=P[nl + ".g.0.bias"])
+        with self.gemm_group():
+            self.mm_nt(M, Ci, Cout, Fl, Cout, P[nl + ".theta.weight"], Cout, TH, Ci, bias=P[nl + ".theta.bias"])
+            self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, PG, 2 * Ci, bias=P[nl + ".phi.0.bias"])
+            self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".g.0.weight"], Cout, PG + F32 * Ci, 2 * Ci,
+                       bias=P[nl + ".g.0.bias"])
         PP = ws.f(pfx + ".PP", B * Pk * 2 * Ci)
         PA = ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr()
         self.L.vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, PG, 2 * Ci, PP, PA, self.s)
@@ -716,9 +735,10 @@ class _Program:
         writes dY or X again in this backward (they are read whenever the weight-gradient lane gets
         there, up to the final join)."""
         lddy = lddy or N
-        self.defer_wgrad(defer, N, K, M, dY, lddy, X, ldx, self.G[wname], K, self.G[bname] if bname else 0)
-        if dX:
-            self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
+        with self.gemm_group():
+            self.defer_wgrad(defer, N, K, M, dY, lddy, X, ldx, self.G[wname], K, self.G[bname] if bname else 0)
+            if dX:
+                self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
 
     def defer_wgrad(self, defer, M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=0):
         """C[M,N] = A^T B (a weight gradient, mm_tn), now or -- defer on lane 0 with lanes on -- at the next
@@ -735,8 +755,9 @@ class _Program:
             return
         e = self.mark()
         with self.lane(WGRAD_LANE, e):
-            for M, N, K, A, lda, Bm, ldb, C, ldc, bg in self.pending_wgrads:
-                self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bg)
+            with self.gemm_group():
+                for M, N, K, A, lda, Bm, ldb, C, ldc, bg in self.pending_wgrads:
+                    self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bg)
             self.wgrad_tail = self.mark()
         self.pending_wgrads = []
 
@@ -788,10 +809,11 @@ class _Program:
         rows = B * L_
         a, st = ws.f(pfx + ".a", B * S * L_), ws.get(pfx + ".st", 2 * S, torch.float64).data_ptr()
         da = ws.f(pfx + ".da", B * S * L_)
-        self.gemm(0, 1, S, L_, C, 1.0 / L_, dZ, C, S * C, X, C, L_ * C, 0.0, da, L_, S * L_, B, None, None, 0, 0,
-                       0, None)
-        self.gemm(1, 0, L_, C, S, 1.0 / L_, a, L_, S * L_, dZ, C, S * C, 0.0, dX, C, L_ * C, B, None, None, 0, 0,
-                       0, None)
+        with self.gemm_group():
+            self.gemm(0, 1, S, L_, C, 1.0 / L_, dZ, C, S * C, X, C, L_ * C, 0.0, da, L_, S * L_, B, None, None, 0, 0,
+                      0, None)
+            self.gemm(1, 0, L_, C, S, 1.0 / L_, a, L_, S * L_, dZ, C, S * C, 0.0, dX, C, L_ * C, B, None, None, 0, 0,
+                      0, None)
         df = ws.f(pfx + ".df", S * rows)
         par = self.P[pfx + ".tokenizers.0.conv.0.weight"]
         self.L.vc_tl_attn_bwd(self.train, B, L_, S, ws.f(pfx + ".mx", rows), ws.f(pfx + ".avg", rows), par, st, da, df,
@@ -854,11 +876,12 @@ class _Program:
             self.ln_bwd(pfx + ".ln4", pfx + ".Fc", dFc, Zc, M, Cout, dZc, 0.0)
             CF, dCF = f(pfx + ".CF", rows * Cout), f(pfx + ".dCF", rows * Cout)
             self.token_learner_bwd(pfx + ".channel_token", CF, L_, Cout, S, dZc, dCF)
-            self.linear_bwd(pfx + ".channel_feature.weight", pfx + ".channel_feature.bias", dCF, rows, Cout, Cin, X,
-                            Cin, 0, 0.0)
-            if dX:
-                self.mm_nn(rows, Cin, Cout, dCF, Cout, self.P[pfx + ".channel_feature.weight"], Cin, dX, Cin,
-                           beta=1.0)
+            with self.gemm_group():
+                self.linear_bwd(pfx + ".channel_feature.weight", pfx + ".channel_feature.bias", dCF, rows, Cout,
+                                Cin, X, Cin, 0, 0.0)
+                if dX:
+                    self.mm_nn(rows, Cin, Cout, dCF, Cout, self.P[pfx + ".channel_feature.weight"], Cin, dX, Cin,
+                               beta=1.0)
             e_ch = self.mark()
         # global feature: ln3 -> TokenLearner -> change_dim
         Zg, dZg = f(pfx + ".global_feature.Z", M * Cout), f(pfx + ".dZg", M * Cout)
