@@ -864,6 +864,17 @@ static long g2_combine_limit() {
   return v;
 }
 
+// largest per-tile slab volume (bytes) the k-major kernel's last-arriving slice combines in-launch;
+// VITCNN_LEGACY_COMBINE overrides it for measurements
+static long legacy_combine_limit() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("VITCNN_LEGACY_COMBINE");
+    v = e ? atol(e) : 4096;
+  }
+  return v;
+}
+
 // the k-major fp32 kernel (LDS [k][row], 16x16x4 f32): launch configuration of one problem
 struct LegacyPlan {
   GemmArgs g;
@@ -904,8 +915,9 @@ static LegacyPlan plan_legacy(int transA, int transB, int M, int N, int K, float
   // (<= 4 KB of slabs per tile, measured: tools/gemm_census.py); wider splits keep the parallel
   // reduce kernel
   const long slab_bytes = (long)nsplit * std::min(BM, M) * std::min(BN, Ne) * 4;
-  unsigned int* cnt =
-      (nsplit > 1 && tile_counters && tiles <= n_counters && slab_bytes <= 4096) ? tile_counters : nullptr;
+  unsigned int* cnt = (nsplit > 1 && tile_counters && tiles <= n_counters && slab_bytes <= legacy_combine_limit())
+                          ? tile_counters
+                          : nullptr;
   LegacyPlan pl;
   pl.g = GemmArgs{M, N, K, Ne, k_chunk, nsplit, A, lda, strideA, B, ldb, strideB, C, ldc, strideC, bias_grad, ws, cnt,
                   epi};

@@ -53,6 +53,8 @@ N_COUNTERS = 1 << 16       # split-K tile counters per stream
 _LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
 _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in normal runs)
 _GROUP = os.environ.get("VITCNN_GEMM_GROUP", "1") != "0"   # grouped launches of independent fp32 GEMMs
+_LANE_MAP = [int(v) for v in os.environ.get("VITCNN_LANE_MAP", "").split(",") if v]   # measurement switch
+_BN_TICKETS = os.environ.get("VITCNN_BN_TICKETS", "0") == "1"   # BN reductions in the last-arriving block: measured ~1% slower (every arrival is an agent-scope release = L2 writeback)
 
 UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
                    "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
@@ -384,6 +386,8 @@ class _Program:
         scr = model._scratch(device, B)
         lanes = model._side_lanes(device)
         self.streams = [torch.cuda.current_stream(device)] + [st for st, _ in lanes]
+        if _LANE_MAP:   # logical lane -> stream (lanes sharing a stream run in issue order)
+            self.streams = [self.streams[_LANE_MAP[i]] for i in range(len(self.streams))]
         self._raw = [st.cuda_stream for st in self.streams]
         self._scr = [(scr.data_ptr(), scr.numel())] + [(t.data_ptr(), t.numel()) for _, t in lanes]
         self._cnt = [t.data_ptr() for t in model._tile_counters(device)]
@@ -462,7 +466,8 @@ class _Program:
         (tools/graph_probe*.py): a side lane is forked by waiting on a lane-0 event before it waits
         on another side lane's event, and a lane never waits on its own event (a no-op anyway)."""
         for e in events:
-            if self._ev_lane.get(id(e)) == self.cur:
+            src = self._ev_lane.get(id(e))
+            if src is not None and self.streams[src] is self.streams[self.cur]:
                 continue
             self.streams[self.cur].wait_event(e)
             if _TRACER is not None:
@@ -482,6 +487,8 @@ class _Program:
         """lane 0 waits for everything issued on the side lanes"""
         assert self.cur == 0
         for i in range(1, len(self.streams)):
+            if any(self.streams[i] is self.streams[j] for j in range(i)):
+                continue   # a stream shared with an earlier lane (VITCNN_LANE_MAP)
             e = self._event()
             e.record(self.streams[i])
             self.streams[0].wait_event(e)
@@ -515,8 +522,8 @@ class _Program:
         ws = self.ws
         mean, inv = ws.f(tag + ".bm", C), ws.f(tag + ".bi", C)
         self.L.vc_bn_stats_ex(self.train, M, C, X, ldx, BN_EPS, BN_MOM, mean, inv, self.BUF[pfx + ".running_mean"],
-                              self.BUF[pfx + ".running_var"], self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS,
-                              self.s)
+                              self.BUF[pfx + ".running_var"], self.scr_p, self.scr_n,
+                              self._cnt[self.cur] if _BN_TICKETS else None, N_COUNTERS, self.s)
         return mean, inv
 
     def layernorm(self, pfx, X, R, C, tag):
@@ -712,7 +719,7 @@ class _Program:
         self.L.vc_bn_bwd_ex(self.train, M, C, dY, lddy, X, ldx, relu_out or None, C, ws.f(tag + ".bm", C),
                             ws.f(tag + ".bi", C), self.P[pfx + ".weight"], dX or None, lddx, beta_dx,
                             self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n,
-                            self._cnt[self.cur], N_COUNTERS, self.s)
+                            self._cnt[self.cur] if _BN_TICKETS else None, N_COUNTERS, self.s)
 
     def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx, res=0):
         """dX = beta_dx * dX + LN grad, or res + LN grad (res: a residual gradient in another buffer)"""
