@@ -98,6 +98,14 @@ VC_API int vc_layernorm_bwd_res(int R, int C, const float* dy, long lddy, const 
                                 const float* mean, const float* rstd, const float* res, long ldr, float* dx,
                                 long lddx, float* dw, float* db, float beta_w, float* ws, long ws_floats,
                                 hipStream_t stream);
+/* Split form: dx now (res + LN grad, or beta_dx * dx + LN grad when res is null) with the dw / db
+ * partials left in `part`; the parameter reduction later (same R, C, part_floats), e.g. on another
+ * stream off the critical path.  Together bit-identical to vc_layernorm_bwd. */
+VC_API int vc_layernorm_bwd_dx(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
+                               const float* mean, const float* rstd, const float* res, long ldr, float* dx,
+                               long lddx, float beta_dx, float* part, long part_floats, hipStream_t stream);
+VC_API int vc_layernorm_bwd_params(int R, int C, const float* part, long part_floats, float* dw, float* db,
+                                   float beta_w, hipStream_t stream);
 
 /* BatchNorm2d over channels-last rows (torch train/eval semantics, eps, momentum):
  * ms_conv_bn_relu.bn (Mutimodality_Mamba7.py:1039), FusionLayer BN (:1103, :1129),
@@ -193,6 +201,11 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
                              const float* Dskip, const float* gate_logits, const float* yp, const float* dyp,
                              const float* ckpt, float* du, float* ddt_lin, float* dxdbl, float* dA_log,
                              float* dDskip, float* dgate_logits, float* ws, long ws_floats, hipStream_t stream);
+/* The parameter reductions of vc_mamba_scan_bwd (dA_log, D, gate logits) from the per-sequence partials a
+ * call with null parameter outputs left at the head of its ws; run later / elsewhere, bit-identical. */
+VC_API int vc_mamba_scan_bwd_params(int B, int D, int ndir, const float* gate_logits, const float* ws,
+                                    float* dA_log, float* dDskip, float* dgate_logits, float* scratch,
+                                    long scratch_floats, hipStream_t stream);
 /* backward of gather + conv1d + SiLU: du is turned into dpre in place; the x half of dxz [B*L, 2D]
  * is overwritten (summed over the directions); conv weight [D,1,4] / bias [D] grads overwritten */
 VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order, const int* inv_order,

@@ -183,6 +183,17 @@ def test_layernorm_bwd_residual_is_bit_identical(L, ws, R, C):
     assert torch.equal(res.cpu(), res0.cpu())
     for a_, b_ in zip(*outs):
         assert torch.equal(a_, b_)
+    # the split form (dx now, the parameter reduction later from a buffer of its own) is the same
+    part_n = 256 * 2 * C
+    part = torch.full((part_n,), float("nan"), device=DEV)
+    dx = torch.full((R, C), float("nan"), device=DEV)
+    dw, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), -0.5, device=DEV)
+    L.vc_layernorm_bwd_dx(R, C, P(dy), C, P(x), C, P(w), P(mean), P(rstd), P(res), C, P(dx), C, 0.0, P(part), part_n,
+                          S())
+    L.vc_layernorm_bwd_params(R, C, P(part), part_n, P(dw), P(db), 1.0, S())
+    torch.cuda.synchronize()
+    for a_, b_ in zip(outs[0], (dx.cpu(), dw.cpu(), db.cpu())):
+        assert torch.equal(a_, b_)
 
 
 @pytest.mark.parametrize("R,C", [(5184, 144), (3136, 256), (100, 256), (7, 144)])

@@ -111,6 +111,18 @@ def test_mamba_kernels_vs_float64(L, D, E, use_ckpt):
     lib.vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
                           P(gate_d), P(Y), P(dYP), P(CKP) if use_ckpt else None, P(dU), P(dDTL), P(dXD), P(dA),
                           P(dDs), P(dG), P(ws), ws.numel(), s)
+    if use_ckpt:
+        # split form: partials left in a buffer of their own, reduced by vc_mamba_scan_bwd_params (the
+        # model's deferred path) == the fused call, bit for bit; du / d(dt_lin) / dxdbl rewritten identically
+        nseq = ndir * B
+        spn = nseq * D * N + nseq * D + nseq
+        sp = torch.full((spn,), float("nan"), device=DEV)
+        lib.vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
+                              P(gate_d), P(Y), P(dYP), P(CKP), P(dU), P(dDTL), P(dXD), None, None, None, P(sp), spn, s)
+        dA2, dD2, dG2 = torch.empty(D, N, device=DEV), torch.empty(D, device=DEV), torch.empty(ndir, device=DEV)
+        lib.vc_mamba_scan_bwd_params(B, D, ndir, P(gate_d), P(sp), P(dA2), P(dD2), P(dG2), P(ws), ws.numel(), s)
+        torch.cuda.synchronize()
+        assert torch.equal(dA2.cpu(), dA.cpu()) and torch.equal(dD2.cpu(), dDs.cpu()) and torch.equal(dG2.cpu(), dG.cpu())
     dWdt, dbdt = torch.empty(D, R, device=DEV), torch.empty(D, device=DEV)
     lib.vc_gemm(0, 0, rows, R, D, 1.0, P(dDTL), D, 0, P(wdt_d), R, 0, 0.0, P(dXD), XW, 0, 1, None, None, 0, 0, 0,
                 None, P(ws), ws.numel(), s)

@@ -608,6 +608,21 @@ VC_API int vc_mamba_gate_bwd(int B, int L, int D, const float* xz, const float* 
   return VC_OK;
 }
 
+static int scan_param_reduce(int B, int D, int ndir, const float* gate_logits, const float* p_a, const float* p_d,
+                             const float* p_g, float* dA_log, float* dDskip, float* dgate_logits, float* scratch,
+                             long scratch_floats, hipStream_t stream) {
+  const int nseq = ndir * B;
+  int rc = dA_log ? vc_colsum(nseq, D * NST, p_a, (long)D * NST, dA_log, 0.f, scratch, scratch_floats, stream) : 0;
+  if (rc) return rc;
+  rc = dDskip ? vc_colsum(nseq, D, p_d, (long)D, dDskip, 0.f, scratch, scratch_floats, stream) : 0;
+  if (rc) return rc;
+  if (!dgate_logits) return VC_OK;
+  // dg partials are laid out [k][b]: per direction B contiguous values
+  hipLaunchKernelGGL(gate_grad, dim3(1), dim3(256), 0, stream, ndir, B, gate_logits, p_g, dgate_logits);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
 // Backward of scan + gate-weighted combine, given dyp = d(YP) per token (vc_mamba_gate_bwd).
 // Writes du, ddt_lin (per sequence position), the B/C columns of dxdbl (ld R+2N), and
 // dA_log / dD / d(gate logits) (overwrite).  ckpt: the segment states vc_mamba_scan_fwd stored
@@ -655,16 +670,25 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   else if (R == 16) hipLaunchKernelGGL(scan_bwd<16>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
   else hipLaunchKernelGGL(scan_bwd<0>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
   VC_CHECK_LAUNCH();
-  // the three parameter-gradient outputs are optional (the per-sequence partials stay in ws)
-  int rc = dA_log ? vc_colsum(nseq, D * NST, p_a, (long)D * NST, dA_log, 0.f, p_rest, rest, stream) : 0;
-  if (rc) return rc;
-  rc = dDskip ? vc_colsum(nseq, D, p_d, (long)D, dDskip, 0.f, p_rest, rest, stream) : 0;
-  if (rc) return rc;
-  if (!dgate_logits) return VC_OK;
-  // dg partials are laid out [k][b]: per direction B contiguous values
-  hipLaunchKernelGGL(gate_grad, dim3(1), dim3(256), 0, stream, ndir, B, gate_logits, p_g, dgate_logits);
-  VC_CHECK_LAUNCH();
-  return VC_OK;
+  // the three parameter-gradient outputs are optional (the per-sequence partials stay in ws, for
+  // vc_mamba_scan_bwd_params)
+  return scan_param_reduce(B, D, ndir, gate_logits, p_a, p_d, p_g, dA_log, dDskip, dgate_logits, p_rest, rest, stream);
+}
+
+// The parameter-gradient reductions of vc_mamba_scan_bwd, run separately (later, or on another
+// stream): ws is the workspace a vc_mamba_scan_bwd call with null dA_log / dDskip / dgate_logits left
+// its per-sequence partials in (it must not have been written since; given ckpt, ws_floats as then).
+// scratch: the column sums' temporary.  Bit-identical to the fused call.
+VC_API int vc_mamba_scan_bwd_params(int B, int D, int ndir, const float* gate_logits, const float* ws,
+                                    float* dA_log, float* dDskip, float* dgate_logits, float* scratch,
+                                    long scratch_floats, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && D > 0 && ndir > 0 && ws);
+  const int nseq = ndir * B;
+  const float* p_a = ws;
+  const float* p_d = p_a + (long)nseq * D * NST;
+  const float* p_g = p_d + (long)nseq * D;
+  return scan_param_reduce(B, D, ndir, gate_logits, p_a, p_d, p_g, dA_log, dDskip, dgate_logits, scratch,
+                           scratch_floats, stream);
 }
 
 // Backward of the direction gather + causal conv1d + SiLU.  dpre overwrites du in place;

@@ -331,14 +331,20 @@ VC_EXPORT int vc_layernorm_fwd(int R, int C, const float* x, long ldx, const flo
   return VC_OK;
 }
 
+// rows per ln_bwd block (P = ceil(R / rows_per) partial rows of 2C floats)
+static int ln_partial_rows(int R, int C, long part_floats) {
+  int rows_per = std::max(16, vc_cdiv(R, 256));
+  while ((long)vc_cdiv(R, rows_per) * 2 * C > part_floats) rows_per *= 2;
+  return rows_per;
+}
+
 static int layernorm_bwd(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
                          const float* mean, const float* rstd, const float* res, long ldr, float* dx, long lddx,
                          float beta_dx, float* dw, float* db, float beta_w, float* ws, long ws_floats,
                          hipStream_t stream) {
   VC_REQUIRE(C > 0 && C <= 64 * LN_MAXV && R >= 0);
   if (R == 0) return VC_OK;
-  int rows_per = std::max(16, vc_cdiv(R, 256));
-  while ((long)vc_cdiv(R, rows_per) * 2 * C > ws_floats) rows_per *= 2;
+  const int rows_per = ln_partial_rows(R, C, ws_floats);
   const int P = vc_cdiv(R, rows_per);
   hipLaunchKernelGGL(ln_bwd, dim3(P), dim3(256), 0, stream, R, C, rows_per, dy, lddy, x, ldx, w, mean, rstd, dx,
                      lddx, beta_dx, res, ldr, ws);
@@ -353,6 +359,36 @@ static int layernorm_bwd(int R, int C, const float* dy, long lddy, const float* 
     int rc = launch_sum_rows(P, C, ws, (long)2 * C, (long)C, db, beta_w, stream);
     if (rc) return rc;
   }
+  return VC_OK;
+}
+
+// Split form (the parameter reduction can run later, elsewhere): vc_layernorm_bwd_dx writes dx
+// (= res + LN grad when res is given, else beta_dx * dx + LN grad) and leaves the per-block dw / db
+// partials in `part`; vc_layernorm_bwd_params sums those partials (same R, C, part_floats) into
+// dw = beta_w * dw + ..., db = beta_w * db + ...  Together they equal vc_layernorm_bwd bit for bit.
+VC_EXPORT int vc_layernorm_bwd_dx(int R, int C, const float* dy, long lddy, const float* x, long ldx, const float* w,
+                                  const float* mean, const float* rstd, const float* res, long ldr, float* dx,
+                                  long lddx, float beta_dx, float* part, long part_floats, hipStream_t stream) {
+  VC_REQUIRE(C > 0 && C <= 64 * LN_MAXV && R > 0 && part);
+  const int rows_per = ln_partial_rows(R, C, part_floats);
+  const int P = vc_cdiv(R, rows_per);
+  VC_REQUIRE((long)P * 2 * C <= part_floats);
+  hipLaunchKernelGGL(ln_bwd, dim3(P), dim3(256), 0, stream, R, C, rows_per, dy, lddy, x, ldx, w, mean, rstd, dx,
+                     lddx, beta_dx, res, ldr, part);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_EXPORT int vc_layernorm_bwd_params(int R, int C, const float* part, long part_floats, float* dw, float* db,
+                                      float beta_w, hipStream_t stream) {
+  VC_REQUIRE(C > 0 && C <= 64 * LN_MAXV && R > 0 && part);
+  const int P = vc_cdiv(R, ln_partial_rows(R, C, part_floats));
+  if (dw && db == dw + C) return launch_sum_rows(P, 2 * C, part, (long)2 * C, 0L, dw, beta_w, stream);
+  if (dw) {
+    int rc = launch_sum_rows(P, C, part, (long)2 * C, 0L, dw, beta_w, stream);
+    if (rc) return rc;
+  }
+  if (db) return launch_sum_rows(P, C, part, (long)2 * C, (long)C, db, beta_w, stream);
   return VC_OK;
 }
 

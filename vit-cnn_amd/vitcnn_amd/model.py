@@ -721,9 +721,20 @@ class _Program:
                             self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n,
                             self._cnt[self.cur] if _BN_TICKETS else None, N_COUNTERS, self.s)
 
-    def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx, res=0):
-        """dX = beta_dx * dX + LN grad, or res + LN grad (res: a residual gradient in another buffer)"""
+    def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx, res=0, defer=False):
+        """dX = beta_dx * dX + LN grad, or res + LN grad (res: a residual gradient in another buffer).
+        defer (lane 0): dX now, the weight / bias gradient reduction queued for the weight-gradient
+        lane (its partials kept in a buffer of their own)"""
         ws = self.ws
+        if self._deferring(defer):
+            part_n = 256 * 2 * C   # >= the kernel's partial rows, so the same split as vc_layernorm_bwd
+            part = ws.f(tag + ".lnpart", part_n)
+            self.L.vc_layernorm_bwd_dx(R, C, dY, C, X, C, self.P[pfx + ".weight"], ws.f(tag + ".m", R),
+                                       ws.f(tag + ".r", R), res or None, C, dX, C, beta_dx, part, part_n, self.s)
+            gw, gb = self.G[pfx + ".weight"], self.G[pfx + ".bias"]
+            self.pending_wgrads.append(
+                lambda: self.L.vc_layernorm_bwd_params(R, C, part, part_n, gw, gb, 0.0, self.s))
+            return
         if res:
             self.L.vc_layernorm_bwd_res(R, C, dY, C, X, C, self.P[pfx + ".weight"], ws.f(tag + ".m", R),
                                         ws.f(tag + ".r", R), res, C, dX, C, self.G[pfx + ".weight"],
@@ -747,24 +758,29 @@ class _Program:
             if dX:
                 self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
 
+    def _deferring(self, defer):
+        return defer and _DEFER_WGRAD and self.lanes_on and self.cur == 0
+
     def defer_wgrad(self, defer, M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=0):
         """C[M,N] = A^T B (a weight gradient, mm_tn), now or -- defer on lane 0 with lanes on -- at the next
         flush_wgrads()"""
-        if defer and _DEFER_WGRAD and self.lanes_on and self.cur == 0:
-            self.pending_wgrads.append((M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad))
+        if self._deferring(defer):
+            self.pending_wgrads.append(
+                lambda: self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad))
         else:
             self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad)
 
     def flush_wgrads(self):
-        """issue the queued weight gradients on the weight-gradient lane, forked once from lane 0 here;
-        wgrad_tail = that lane's event after them"""
+        """issue the queued parameter-gradient work (weight-gradient GEMMs, grouped; LayerNorm and scan
+        parameter reductions) on the weight-gradient lane, forked once from lane 0 here; wgrad_tail =
+        that lane's event after them"""
         if not self.pending_wgrads:
             return
         e = self.mark()
         with self.lane(WGRAD_LANE, e):
             with self.gemm_group():
-                for M, N, K, A, lda, Bm, ldb, C, ldc, bg in self.pending_wgrads:
-                    self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bg)
+                for fn in self.pending_wgrads:
+                    fn()
             self.wgrad_tail = self.mark()
         self.pending_wgrads = []
 
@@ -892,7 +908,7 @@ class _Program:
             e_ch = self.mark()
         # global feature: ln3 -> TokenLearner -> change_dim
         Zg, dZg = f(pfx + ".global_feature.Z", M * Cout), f(pfx + ".dZg", M * Cout)
-        self.ln_bwd(pfx + ".ln3", pfx + ".Fg", dFg, Zg, M, Cout, dZg, 0.0)
+        self.ln_bwd(pfx + ".ln3", pfx + ".Fg", dFg, Zg, M, Cout, dZg, 0.0, defer=True)
         CD, dCD = f(pfx + ".CD", rows * Cout), f(pfx + ".dCD", rows * Cout)
         self.token_learner_bwd(pfx + ".global_feature", CD, L_, Cout, S, dZg, dCD)
         Gm, dG = f(pfx + ".G", rows * E), f(pfx + ".dG", rows * E)
@@ -900,7 +916,7 @@ class _Program:
                         defer=True)
         # hsiMamba: ln1 -> out_proj -> scan/combine -> x_proj/dt_proj -> conv -> in_proj -> pre_norm -> patch_embed
         T2, dT = f(pfx + ".T2", rows * E), f(pfx + ".dT", rows * E)
-        self.ln_bwd(gv + ".ln1", pfx + ".G", dG, T2, rows, E, dT, 0.0)
+        self.ln_bwd(gv + ".ln1", pfx + ".G", dG, T2, rows, E, dT, 0.0, defer=True)
         YS, dYS = f(pfx + ".YS", rows * D), f(pfx + ".dYS", rows * D)
         # (the pre_norm backward below writes the residual sum to dTt, so dT stays as this reads it)
         self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0, defer=True)
@@ -911,11 +927,25 @@ class _Program:
         # SiLU(z) gate (token-wise): dyp and the z half of dxz
         self.L.vc_mamba_gate_bwd(B, L_, D, XZ, YP, dYS, dYP, dXZ, self.s)
         self.flush_wgrads()   # fusion, change_dim, out_proj: alongside the scan backward
-        self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
-                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], Y, dYP,
-                                 f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR)),
-                                 dU, dDTL, dXD, G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"], self.scr_p,
-                                 self.scr_n, self.s)
+        CKPb = f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR))
+        if self._deferring(True):
+            # the per-sequence dA_log / D / gate partials stay in a buffer of their own; their
+            # reductions go with the next weight-gradient flush
+            nseq = NDIR * B
+            spn = nseq * D * 16 + nseq * D + nseq
+            sp = f(pfx + ".scanpart", spn)
+            self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
+                                     P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], Y,
+                                     dYP, CKPb, dU, dDTL, dXD, None, None, None, sp, spn, self.s)
+            gl, ga, gd, gg = P[gv + ".weights"], G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"]
+            self.pending_wgrads.append(
+                lambda: self.L.vc_mamba_scan_bwd_params(B, D, NDIR, gl, sp, ga, gd, gg, self.scr_p, self.scr_n,
+                                                        self.s))
+        else:
+            self.L.vc_mamba_scan_bwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
+                                     P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], Y,
+                                     dYP, CKPb, dU, dDTL, dXD, G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"],
+                                     self.scr_p, self.scr_n, self.s)
         nr = NDIR * rows
         # dt_proj: dt_lin = xdbl[:, :R] W_dt^T + b_dt
         # (the weight gradient reads dDTL and XD's dt-rank columns; the data gradient writes dXD's)
@@ -930,7 +960,7 @@ class _Program:
         self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0, defer=True)
         self.flush_wgrads()   # dt_proj, x_proj, in_proj
         T, dTt = f(pfx + ".T", rows * E), f(pfx + ".dTt", rows * E)
-        self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dTt, 0.0, res=dT)   # dTt = dT + LN grad
+        self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dTt, 0.0, res=dT, defer=True)   # dT + LN grad
         if dX:
             self.wait(e_ch)
             self.mm_nn(rows, Cin, E, dTt, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
@@ -984,6 +1014,8 @@ class _Program:
         self.bucket_ready(bucket_hook, "tail", e_l3, *self.wgrad_events())
         self.block_bwd(m.hsi2, "hsi2", self.H1, Pp - 2, dH2, dH1, e_f1)
         # block_bwd joined its lane-1 chain before dH1; its deferred weight gradients end at wgrad_tail
+        if bucket_hook is not None:
+            self.flush_wgrads()   # hsi2's pre_norm parameter reduction is still queued
         self.bucket_ready(bucket_hook, "hsi2", *self.wgrad_events())
         self.block_bwd(m.hsi1, "hsi1", self.X0, Pp, dH1, None, None)
         self.flush_wgrads()
