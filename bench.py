@@ -79,15 +79,19 @@ def time_kernel(fn, reps, stream):
 
 def _traffic_from_profile(kernel_key):
     """HBM bytes per launch of `kernel_key` from the committed PMC profile (rocprofv3 --pmc
-    FETCH_SIZE and WRITE_SIZE, separate passes; tools/pmc_collect.sh -> profiles/r01_pmc.json),
+    FETCH_SIZE and WRITE_SIZE, separate passes; tools/pmc_step.sh -> profiles/r02_pmc.json, the round-1
+    tools/pmc_collect.sh -> profiles/r01_pmc.json before it),
     or None when no profile of this kernel is committed."""
-    path = os.path.join(REPO, "profiles", "r01_pmc.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        prof = json.load(f)
-    k = prof.get("kernels", {}).get(kernel_key)
-    return None if k is None else k.get("hbm_bytes_per_launch")
+    for name in ("r02_pmc.json", "r01_pmc.json"):   # the latest committed profile that has the kernel
+        path = os.path.join(REPO, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            prof = json.load(f)
+        k = prof.get("kernels", {}).get(kernel_key)
+        if k is not None:
+            return k.get("hbm_bytes_per_launch")
+    return None
 
 
 def batch_assembly_ms(step, hsi, lidar, target, dev, steps, seed):
