@@ -114,6 +114,11 @@ VC_API int vc_layernorm_bwd_params(int R, int C, const float* part, long part_fl
 VC_API int vc_bn_stats(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
                        float* save_mean, float* save_invstd, float* run_mean, float* run_var,
                        float* ws, long ws_floats, hipStream_t stream);
+/* stats + apply in one call (train: the partials kernel + a channel-tiled apply that reduces them itself,
+ * two launches; eval: from the running statistics); bit-identical to vc_bn_stats + vc_bn_apply */
+VC_API int vc_bn_forward(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                         float* save_mean, float* save_invstd, float* run_mean, float* run_var, const float* w,
+                         const float* b, int relu, float* y, long ldy, float* ws, long ws_floats, hipStream_t stream);
 VC_API int vc_bn_apply(long M, int C, const float* x, long ldx, const float* mean, const float* invstd,
                        const float* w, const float* b, int relu, float* y, long ldy, hipStream_t stream);
 VC_API int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,

@@ -254,6 +254,30 @@ def test_batchnorm_train_fwd_bwd(L, ws, M, C, relu):
     assert rel_err(db.cpu().numpy(), br.grad.numpy()) < 1e-4
 
 
+@pytest.mark.parametrize("train", [1, 0])
+@pytest.mark.parametrize("M,C,relu", [(5184, 144, 0), (3136, 256, 1), (1600, 16, 1), (37, 200, 1)])
+def test_bn_forward_fused_is_bit_identical(L, ws, train, M, C, relu):
+    """vc_bn_forward (partials + a channel-tiled apply that reduces them itself) == vc_bn_stats +
+    vc_bn_apply: y, save_mean / save_invstd and the running statistics, bit for bit"""
+    x = (rnd(M, C, seed=61, scale=2.0) + 3.0).to(DEV)
+    w, b = (rnd(C, seed=62) + 1.0).to(DEV), rnd(C, seed=63).to(DEV)
+    outs = []
+    for fused in (False, True):
+        rm, rv = (rnd(C, seed=64) * 0.1).to(DEV), (rnd(C, seed=65).abs() + 0.5).to(DEV)
+        mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        y = torch.full((M, C), float("nan"), device=DEV)
+        if fused:
+            L.vc_bn_forward(train, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(w), P(b), relu, P(y), C,
+                            P(ws), ws.numel(), S())
+        else:
+            L.vc_bn_stats(train, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(ws), ws.numel(), S())
+            L.vc_bn_apply(M, C, P(x), C, P(mean), P(inv), P(w), P(b), relu, P(y), C, S())
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (y, mean, inv, rm, rv)])
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+
+
 @pytest.mark.parametrize("M,C,relu", [(5184, 144, 0), (3136, 512, 1), (5184, 1, 0), (1600, 16, 1), (37, 200, 1)])
 def test_batchnorm_ticketed_reduction_is_bit_identical(L, ws, M, C, relu):
     """vc_bn_stats_ex / vc_bn_bwd_ex (the last-arriving partial block of each channel group reduces)

@@ -123,10 +123,31 @@ __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, 
 // rows into part[p][2][C]; the reduction over the P partials runs in a fixed order (4 partial lanes
 // p = l, l+4, ..., then the 4 lanes in order), either in the last-arriving partial block of each
 // 64-channel group (tickets: no second launch) or in bn_stats_final (same code, same result).
-__device__ __forceinline__ void bn_stats_reduce(int P, int C, long M, const float* __restrict__ x,
-                                                const double* __restrict__ part, int cx, float eps, float momentum,
-                                                float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                                float* __restrict__ run_mean, float* __restrict__ run_var) {
+// The elementwise BN arithmetic, spelled with explicit fmaf so that every kernel using it (separate or
+// fused final + apply) rounds identically whatever the surrounding code lets the compiler contract.
+__device__ __forceinline__ float bn_fwd_elem(float xv, float mean, float invstd, float w, float b) {
+#pragma clang fp contract(off)
+  return fmaf((xv - mean) * invstd, w, b);
+}
+// (fp contraction off inside: the caller's products a1 = s1 / M, a2 = s2 / M are never fused into the
+// subtraction, whichever way the surrounding kernel hoists them): dx = w * invstd * (dyv - a1 - xhat * a2)
+__device__ __forceinline__ float bn_bwd_elem(float d, float xv, float mean, float invstd, float w, float a1,
+                                             float a2) {
+#pragma clang fp contract(off)
+  const float xh = (xv - mean) * invstd;
+  return (w * invstd) * fmaf(-xh, a2, d - a1);
+}
+// dx = beta_dx * dx + v, the accumulation rounded once per element in every kernel
+__device__ __forceinline__ void bn_dx_store(float* p, float beta_dx, float v) {
+  *p = beta_dx != 0.f ? fmaf(beta_dx, *p, v) : v;
+}
+
+// The fixed-order reduction of the [P][2][C] fp64 partials of channel group cx (block = 64 channels x
+// 4 partial lanes): on return (after a barrier) tot[0][cl] / tot[1][cl] hold channel cx*64+cl's two sums,
+// visible to every thread of the block.  Every consumer (the separate final kernels and the fused
+// apply kernels) sums in this one order, so their results agree bit for bit.
+__device__ __forceinline__ void bn_part_sums(int P, int C, const double* __restrict__ part, int cx,
+                                             double (*tot)[64]) {
   __shared__ double shr[2][4][64];
   const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const int c = cx * 64 + cl;
@@ -141,20 +162,76 @@ __device__ __forceinline__ void bn_stats_reduce(int P, int C, long M, const floa
   shr[0][pl][cl] = s1;
   shr[1][pl][cl] = s2;
   __syncthreads();
-  if (pl != 0 || c >= C) return;
-  s1 = shr[0][0][cl] + shr[0][1][cl] + shr[0][2][cl] + shr[0][3][cl];
-  s2 = shr[1][0][cl] + shr[1][1][cl] + shr[1][2][cl] + shr[1][3][cl];
+  if (pl == 0) {
+    tot[0][cl] = shr[0][0][cl] + shr[0][1][cl] + shr[0][2][cl] + shr[0][3][cl];
+    tot[1][cl] = shr[1][0][cl] + shr[1][1][cl] + shr[1][2][cl] + shr[1][3][cl];
+  }
+  __syncthreads();
+}
+
+// mean / invstd of channel c from its sums (shift k = x[0, c]); writes save_* and the running stats
+__device__ __forceinline__ void bn_stats_from_sums(double s1, double s2, int c, long M, const float* __restrict__ x,
+                                                   float eps, float momentum, float& mean_f, float& invstd_f,
+                                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                   float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                   bool write) {
   const double d = s1 / (double)M;
   const double var = fmax(s2 / (double)M - d * d, 0.0);
   const double mean = (double)x[c] + d;
-  save_mean[c] = (float)mean;
-  save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  mean_f = (float)mean;
+  invstd_f = (float)(1.0 / sqrt(var + (double)eps));
+  if (!write) return;
+  save_mean[c] = mean_f;
+  save_invstd[c] = invstd_f;
   if (run_mean) {
     const double unb = M > 1 ? var * ((double)M / (double)(M - 1)) : var;
     run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mean);
     run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
   }
 }
+
+__device__ __forceinline__ void bn_stats_reduce(int P, int C, long M, const float* __restrict__ x,
+                                                const double* __restrict__ part, int cx, float eps, float momentum,
+                                                float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                float* __restrict__ run_mean, float* __restrict__ run_var) {
+  __shared__ double tot[2][64];
+  bn_part_sums(P, C, part, cx, tot);
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = cx * 64 + cl;
+  if (pl != 0 || c >= C) return;
+  float mf, isf;
+  bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
+                     run_var, true);
+}
+
+// Fused final + apply (train mode): grid (ceil(C/64), ceil(M/rows_per_block)); every block reduces
+// the channel group's partials itself (bn_part_sums), the blocks of row 0 write save_* and the running
+// statistics, and all apply y = relu?((x - mean) * invstd * w + b) to their rows.
+__global__ __launch_bounds__(256) void bn_apply_stats(int M, int C, const float* __restrict__ x, long ldx, int P,
+                                                      const double* __restrict__ part, float eps, float momentum,
+                                                      float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                      float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      int relu, float* __restrict__ y, long ldy, int rows_per_block) {
+  __shared__ double tot[2][64];
+  bn_part_sums(P, C, part, blockIdx.x, tot);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  if (c >= C) return;
+  float mf, isf;
+  bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
+                     run_var, blockIdx.y == 0 && rl == 0);
+  const float bc = b[c];
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min((long)M, r0 + rows_per_block);
+  for (long r = r0 + rl; r < r1; r += 4) {
+    float v = bn_fwd_elem(x[r * ldx + c], mf, isf, w[c], bc);
+    if (relu) v = fmaxf(v, 0.f);
+    y[r * ldy + c] = v;
+  }
+}
+
+
 
 // grid (ceil(C/64), P); cnt (optional) = one zeroed arrival counter per 64-channel group
 __global__ __launch_bounds__(256) void bn_stats_sums(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
@@ -211,7 +288,7 @@ __global__ void bn_apply(int total, FastDiv fC, const float* __restrict__ x, lon
   if (idx >= total) return;
   int c;
   const long r = fdivmod(idx, fC, c);
-  float v = (x[r * ldx + c] - mean[c]) * invstd[c] * w[c] + b[c];
+  float v = bn_fwd_elem(x[r * ldx + c], mean[c], invstd[c], w[c], b[c]);
   if (relu) v = fmaxf(v, 0.f);
   y[r * ldy + c] = v;
 }
@@ -223,23 +300,12 @@ __global__ void bn_apply(int total, FastDiv fC, const float* __restrict__ x, lon
 __device__ __forceinline__ void bn_bwd_reduce(int P, int C, const double* __restrict__ part, int cx,
                                               double* __restrict__ sums, float* __restrict__ dw,
                                               float* __restrict__ db, float beta_w) {
-  __shared__ double shr[2][4][64];
+  __shared__ double tot[2][64];
+  bn_part_sums(P, C, part, cx, tot);
   const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const int c = cx * 64 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-#pragma unroll 4
-    for (int p = pl; p < P; p += 4) {
-      s1 += part[(long)p * 2 * C + c];
-      s2 += part[(long)p * 2 * C + C + c];
-    }
-  }
-  shr[0][pl][cl] = s1;
-  shr[1][pl][cl] = s2;
-  __syncthreads();
   if (pl != 0 || c >= C) return;
-  s1 = shr[0][0][cl] + shr[0][1][cl] + shr[0][2][cl] + shr[0][3][cl];
-  s2 = shr[1][0][cl] + shr[1][1][cl] + shr[1][2][cl] + shr[1][3][cl];
+  const double s1 = tot[0][cl], s2 = tot[1][cl];
   sums[c] = s1;
   sums[C + c] = s2;
   if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)s2;
@@ -287,6 +353,43 @@ __global__ __launch_bounds__(256) void bn_bwd_final(int P, int C, const double* 
   bn_bwd_reduce(P, C, part, blockIdx.x, sums, dw, db, beta_w);
 }
 
+// Fused final + apply of the BN backward: grid (ceil(C/64), ceil(M/rows_per_block)); every block
+// reduces the channel group's partials itself (bn_part_sums), the blocks of row 0 write dw / db, and
+// all write dx = beta_dx*dx + w*invstd*(dyv - s1/M - xhat*s2/M) (train) or w*invstd*dyv (eval) for
+// their rows -- the same arithmetic as bn_bwd_final + bn_bwd_apply.
+__global__ __launch_bounds__(256) void bn_bwd_apply_sums(int train, int M, int C, const float* __restrict__ dy,
+                                                         long lddy, const float* __restrict__ x, long ldx,
+                                                         const float* __restrict__ relu_out, long ldo,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ w, int P,
+                                                         const double* __restrict__ part, float* __restrict__ dx,
+                                                         long lddx, float beta_dx, float* __restrict__ dw,
+                                                         float* __restrict__ db, float beta_w, int rows_per_block) {
+  __shared__ double tot[2][64];
+  bn_part_sums(P, C, part, blockIdx.x, tot);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  if (c >= C) return;
+  const double s1 = tot[0][cl], s2 = tot[1][cl];
+  if (blockIdx.y == 0 && rl == 0) {
+    if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)s2;
+    if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
+  }
+  const float is = invstd[c], mu = mean[c], wc = w[c];
+  const float invM = 1.f / (float)M;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min((long)M, r0 + rows_per_block);
+  for (long r = r0 + rl; r < r1; r += 4) {
+    float d = dy[r * lddy + c];
+    if (relu_out && !(relu_out[r * ldo + c] > 0.f)) d = 0.f;
+    float v;
+    if (train) v = bn_bwd_elem(d, x[r * ldx + c], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
+    else v = (wc * is) * d;
+    bn_dx_store(dx + r * lddx + c, beta_dx, v);
+  }
+}
+
 // train: dx = w*invstd*(dyv - s1/M - xhat*s2/M);  eval (sums == null): dx = w*invstd*dyv
 __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, long lddy, const float* __restrict__ x,
                              long ldx, const float* __restrict__ relu_out, long ldo, const float* __restrict__ mean,
@@ -303,17 +406,18 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
   float v;
   if (sums) {
     const float invM = 1.f / (float)M;
-    const float xh = (x[r * ldx + c] - mean[c]) * is;
-    v = w[c] * is * (d - (float)sums[c] * invM - xh * ((float)sums[C + c] * invM));
+    v = bn_bwd_elem(d, x[r * ldx + c], mean[c], is, w[c], (float)sums[c] * invM,
+                    (float)sums[C + c] * invM);
   } else {
-    v = w[c] * is * d;
+    v = (w[c] * is) * d;
   }
-  float* p = dx + r * lddx + c;
-  *p = (beta_dx != 0.f ? beta_dx * *p : 0.f) + v;
+  bn_dx_store(dx + r * lddx + c, beta_dx, v);
 }
 
 // rows per partial block: at most 64 partials per 64-channel group (the fixed-order reduction reads
 // P/4 of them per thread), at least 32 rows each, fewer partials if the fp64 workspace is short
+constexpr int BN_APPLY_ROWS = 64;   // rows per block of the fused (partials-reducing) apply kernels
+
 int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
   int rows_per = std::max<long>(32, (M + 63) / 64);
   while ((long)vc_cdiv(M, rows_per) * 2 * C + reserve_doubles > ws_doubles && rows_per < (1 << 29)) rows_per *= 2;
@@ -449,6 +553,36 @@ VC_EXPORT int vc_bn_stats(int train, long M, int C, const float* x, long ldx, fl
                         nullptr, 0, stream);
 }
 
+// BatchNorm forward in one call: train -> batch statistics (partials) + the fused final/apply kernel
+// (save_* and running stats written as vc_bn_stats does, y as vc_bn_apply: two launches); eval ->
+// save_* from the running statistics + apply.  Bit-identical to vc_bn_stats + vc_bn_apply.
+VC_EXPORT int vc_bn_forward(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                            float* save_mean, float* save_invstd, float* run_mean, float* run_var, const float* w,
+                            const float* b, int relu, float* y, long ldy, float* ws, long ws_floats,
+                            hipStream_t stream) {
+  VC_REQUIRE(C > 0 && M >= 0);
+  if (!train || M == 0) {
+    int rc = vc_bn_stats(train, M, C, x, ldx, eps, momentum, save_mean, save_invstd, run_mean, run_var, ws, ws_floats,
+                         stream);
+    if (rc) return rc;
+    return vc_bn_apply(M, C, x, ldx, save_mean, save_invstd, w, b, relu, y, ldy, stream);
+  }
+  VC_REQUIRE(M < (1L << 31) && ((uintptr_t)ws & 7) == 0);
+  double* wsd = reinterpret_cast<double*>(ws);
+  const long ws_doubles = ws_floats / 2;
+  const int rows_per = bn_rows_per(M, C, ws_doubles, 0);
+  const int P = vc_cdiv(M, rows_per);
+  VC_REQUIRE((long)P * C * 2 <= ws_doubles && P <= 65535);
+  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
+                     (unsigned int*)nullptr, eps, momentum, save_mean, save_invstd, run_mean, run_var);
+  VC_CHECK_LAUNCH();
+  const int rpb = BN_APPLY_ROWS;
+  hipLaunchKernelGGL(bn_apply_stats, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(256), 0, stream, (int)M, C, x, ldx,
+                     P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy, rpb);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
 VC_EXPORT int vc_bn_apply(long M, int C, const float* x, long ldx, const float* mean, const float* invstd,
                           const float* w, const float* b, int relu, float* y, long ldy, hipStream_t stream) {
   VC_REQUIRE(C > 0 && M >= 0);
@@ -480,6 +614,14 @@ VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy,
   hipLaunchKernelGGL(bn_bwd_sums, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, dy, lddy, x, ldx,
                      relu_out, ldo, mean, invstd, rows_per, wsd, cnt, sums, dw, db, beta_w);
   VC_CHECK_LAUNCH();
+  if (!cnt && dx) {   // the channel-tiled apply reduces the partials itself: one launch fewer
+    const int rpb = BN_APPLY_ROWS;
+    hipLaunchKernelGGL(bn_bwd_apply_sums, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(256), 0, stream, train,
+                       (int)M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, w, P, wsd, dx, lddx, beta_dx, dw,
+                       db, beta_w, rpb);
+    VC_CHECK_LAUNCH();
+    return VC_OK;
+  }
   if (!cnt) {
     hipLaunchKernelGGL(bn_bwd_final, dim3(vc_cdiv(C, 64)), dim3(256), 0, stream, P, C, wsd, sums, dw, db, beta_w);
     VC_CHECK_LAUNCH();

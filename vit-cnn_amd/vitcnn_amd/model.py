@@ -556,10 +556,12 @@ class _Program:
         """Sequential(Conv2d 1x1, BatchNorm2d, ReLU) (FusionLayer of GLfusionBlock / fusionBlock)."""
         pre = self.ws.f(seq + ".pre", M * Cout)
         self.mm_nt(M, Cout, Cin, X, Cin, self.P[seq + ".0.weight"], Cin, pre, Cout, bias=self.P[seq + ".0.bias"])
-        mean, inv = self.bn_stats(seq + ".1", pre, Cout, M, Cout, seq + ".1")
-        out = self.ws.f(seq + ".out", M * Cout)
-        self.L.vc_bn_apply(M, Cout, pre, Cout, mean, inv, self.P[seq + ".1.weight"], self.P[seq + ".1.bias"], 1, out,
-                           Cout, self.s)
+        tag, ws = seq + ".1", self.ws
+        mean, inv = ws.f(tag + ".bm", Cout), ws.f(tag + ".bi", Cout)
+        out = ws.f(seq + ".out", M * Cout)
+        self.L.vc_bn_forward(self.train, M, Cout, pre, Cout, BN_EPS, BN_MOM, mean, inv,
+                             self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"], self.P[tag + ".weight"],
+                             self.P[tag + ".bias"], 1, out, Cout, self.scr_p, self.scr_n, self.s)
         return out
 
     def fusion(self, pfx, X1, C1, X2, C2, M, Cout):
