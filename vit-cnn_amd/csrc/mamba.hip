@@ -252,6 +252,18 @@ __device__ __forceinline__ float reduce_scatter8_row(const float (&v)[8]) {
   return w + dpp_mov<0xB1>(w);
 }
 
+// raw buffer access (MUBUF, vector memory): a resource over [p, p + bytes), 32-bit byte offsets;
+// loads past the end return 0, stores past the end are dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
 struct ScanBwdOut {
   float* du;        // [nseq*L, D]
   float* ddtl;      // [nseq*L, D]  grad of W_dt dtr + b_dt (pre-softplus)
@@ -294,18 +306,29 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
   // global operands of a segment: the entering state, u, the gathered d(yp) and yp (for the gate
   // gradient); the next segment's are loaded while this one is computed
   float hn[NQ], un[SCK], dn[SCK], yn[SCK];
+  // The segment operands and the du / d(dt_lin) outputs go through buffer resources over this
+  // sequence's rows: 32-bit offsets (no 64-bit address arithmetic per access), and the hardware range
+  // check returns 0 for out-of-range loads / drops out-of-range stores, which takes the place of the
+  // padding-token (t >= L) and padding-channel (d >= D) guards: such lanes get an offset past the end.
+  const unsigned seq_bytes = (unsigned)(a.L * a.D * 4);
+  const auto r_u = buf_rsrc(a.u + base * a.D, seq_bytes);
+  const auto r_yp = buf_rsrc(yp + base * a.D, seq_bytes);
+  const auto r_dyp = buf_rsrc(dyp + (long)b * a.L * a.D, seq_bytes);
+  const auto r_du = buf_rsrc(o.du + base * a.D, seq_bytes);
+  const auto r_ddtl = buf_rsrc(o.ddtl + base * a.D, seq_bytes);
+  const auto r_ck = buf_rsrc(ckpt + (long)s * nseg * NST * a.D, (unsigned)(nseg * NST * a.D * 4));
+  const unsigned lane_b = valid ? (unsigned)d * 4u : 0x80000000u;   // invalid lanes: out of range
   auto load_seg = [&](int c) {
     const int t0 = c * SCK;
-    const float* cp = ckpt + ((long)(s * nseg + c) * NST + NQ * q) * a.D + dc;
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) hn[j] = valid ? cp[(long)j * a.D] : 0.f;
+    for (int j = 0; j < NQ; ++j) hn[j] = buf_ld(r_ck, (unsigned)((c * NST + NQ * q + j) * a.D * 4) + lane_b);
 #pragma unroll
     for (int i = 0; i < SCK; ++i) {
       const int t = t0 + i;
-      const bool in = valid && t < a.L;
-      un[i] = in ? a.u[(base + t) * a.D + dc] : 0.f;
-      dn[i] = in ? dyp[((long)b * a.L + ord[t]) * a.D + dc] : 0.f;
-      yn[i] = in ? yp[(base + t) * a.D + dc] : 0.f;
+      const unsigned row = (unsigned)(t * a.D * 4) + lane_b;   // t >= L: past the end
+      un[i] = buf_ld(r_u, row);
+      dn[i] = buf_ld(r_dyp, (unsigned)((t < a.L ? ord[t] : a.L) * a.D * 4) + lane_b);
+      yn[i] = buf_ld(r_yp, row);
     }
   };
   __syncthreads();   // ord
@@ -362,10 +385,11 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
         dh[j] = dhn * dAs[i][j];                               // carried to t - 1
       }
       cross_row_sum2(S, qa);   // sums over the 16 states (the wave's 4 rows)
-      if (valid && t < a.L) {   // the 4 rows store identical values
-        o.du[(base + t) * a.D + d] = dt * S + Dd * dy;
+      {   // the 4 rows store identical values; padding tokens / channels fall out of range
+        const unsigned row = (unsigned)(t * a.D * 4) + lane_b;
+        buf_st(r_du, row, dt * S + Dd * dy);
         // softplus'(dt_lin) = sigmoid(dt_lin) = 1 - exp(-softplus(dt_lin))
-        o.ddtl[(base + t) * a.D + d] = (qa * LN2 + ut * S) * -expm1_c(-dt);
+        buf_st(r_ddtl, row, (qa * LN2 + ut * S) * -expm1_c(-dt));
       }
       if (q == 0) dD_acc += dy * ut;
       rb[(wave * SCK + i) * 32 + col] = reduce_scatter8_row(v);   // lanes 2j, 2j+1 store the same
