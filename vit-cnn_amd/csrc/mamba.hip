@@ -128,6 +128,18 @@ static size_t seq_lds_floats(int L, int R, int Dp) {
   return Lp * (2 * NST + Dp + R);
 }
 
+// raw buffer access (MUBUF, vector memory): a resource over [p, p + bytes), 32-bit byte offsets;
+// loads past the end return 0, stores past the end are dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
 template <int RT>
 __device__ __forceinline__ void stage_seq(const ScanArgs& a, int s, const SeqLds& m, int Lp, int Dp) {
   const int R = RT ? RT : a.R;
@@ -136,21 +148,20 @@ __device__ __forceinline__ void stage_seq(const ScanArgs& a, int s, const SeqLds
   const int n = a.L * XW, tot = Lp * XW;
   const int nt = blockDim.x;
   constexpr int SB = 8;
+  // rows past L read 0 (buffer range check); each element's LDS destination is selected, not branched
+  const auto r_src = buf_rsrc(src, (unsigned)(n * 4));
   for (int base = 0; base < tot; base += SB * nt) {
     float v[SB];
 #pragma unroll
-    for (int j = 0; j < SB; ++j) {
-      const int i = base + j * nt + threadIdx.x;
-      v[j] = i < n ? src[i] : 0.f;
-    }
+    for (int j = 0; j < SB; ++j) v[j] = buf_ld(r_src, (unsigned)(base + j * nt + threadIdx.x) * 4u);
 #pragma unroll
     for (int j = 0; j < SB; ++j) {
       const int i = base + j * nt + threadIdx.x;
       if (i < tot) {
         const int t = i / XW, col = i - t * XW;
-        if (col < R) m.xr[t * R + col] = v[j];
-        else if (col < R + NST) m.Bs[t * NST + col - R] = v[j];
-        else m.Cs[t * NST + col - R - NST] = v[j];
+        float* dst = col < R ? m.xr + t * R + col
+                             : (col < R + NST ? m.Bs + t * NST + (col - R) : m.Cs + t * NST + (col - R - NST));
+        *dst = v[j];
       }
     }
   }
@@ -190,24 +201,27 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
   for (int j = 0; j < NQ; ++j) A2[j] = valid ? -__expf(a.alog[dc * NST + NQ * q + j]) * LOG2E : 0.f;
   const float Dd = valid ? a.dskip[dc] : 0.f;
   stage_seq<RT>(a, s, m, Lp, Dp);
-  const float* ub = a.u + (long)s * a.L * a.D + dc;
+  // buffer resources over this sequence's rows (as in scan_bwd): padding tokens / channels and null
+  // outputs (a zero-sized resource) fall out of range -- loads give 0, stores are dropped
+  const unsigned seq_bytes = (unsigned)(a.L * a.D * 4);
+  const unsigned lane_b = valid ? (unsigned)d * 4u : 0x80000000u;
+  const auto r_u = buf_rsrc(a.u + (long)s * a.L * a.D, seq_bytes);
+  const auto r_y = buf_rsrc(y ? y + (long)s * a.L * a.D : nullptr, y ? seq_bytes : 0u);
+  const auto r_ck = buf_rsrc(ckpt ? ckpt + (long)s * nseg * NST * a.D : nullptr,
+                             ckpt ? (unsigned)(nseg * NST * a.D * 4) : 0u);
   float h[NQ] = {0.f, 0.f, 0.f, 0.f};
   float un[SCK];
 #pragma unroll
-  for (int i = 0; i < SCK; ++i) un[i] = valid && i < a.L ? ub[(long)i * a.D] : 0.f;
+  for (int i = 0; i < SCK; ++i) un[i] = buf_ld(r_u, (unsigned)(i * a.D * 4) + lane_b);
   for (int c = 0; c < nseg; ++c) {
     const int t0 = c * SCK;
-    if (ckpt && valid) {
-      float* cp = ckpt + ((long)(s * nseg + c) * NST + NQ * q) * a.D + d;
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) cp[(long)j * a.D] = h[j];
-    }
+    for (int j = 0; j < NQ; ++j) buf_st(r_ck, (unsigned)((c * NST + NQ * q + j) * a.D * 4) + lane_b, h[j]);
     float uc[SCK];
 #pragma unroll
     for (int i = 0; i < SCK; ++i) {
       uc[i] = un[i];
-      const int tn = t0 + SCK + i;
-      un[i] = valid && tn < a.L ? ub[(long)tn * a.D] : 0.f;   // prefetch the next segment
+      un[i] = buf_ld(r_u, (unsigned)((t0 + SCK + i) * a.D * 4) + lane_b);   // prefetch the next segment
     }
 #pragma unroll
     for (int i = 0; i < SCK; ++i) {
@@ -224,7 +238,7 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
       h[3] = fmaf(dtu, bv.w, __builtin_amdgcn_exp2f(dt * A2[3]) * h[3]);
       const float yt = cross_row_sum(fmaf(h[3], cv.w, fmaf(h[2], cv.z, fmaf(h[1], cv.y, h[0] * cv.x)))) + Dd * uc[i];
       // the 4 rows hold the same value: an unconditional store of identical bytes
-      if (y && valid && t < a.L) y[((long)s * a.L + t) * a.D + d] = yt;
+      buf_st(r_y, (unsigned)(t * a.D * 4) + lane_b, yt);
     }
   }
 }
@@ -250,18 +264,6 @@ __device__ __forceinline__ float reduce_scatter8_row(const float (&v)[8]) {
   const float keep = b1 ? z[1] : z[0], send = b1 ? z[0] : z[1];
   const float w = keep + dpp_mov<0x4E>(send);
   return w + dpp_mov<0xB1>(w);
-}
-
-// raw buffer access (MUBUF, vector memory): a resource over [p, p + bytes), 32-bit byte offsets;
-// loads past the end return 0, stores past the end are dropped
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
 }
 
 struct ScanBwdOut {
