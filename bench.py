@@ -77,21 +77,32 @@ def time_kernel(fn, reps, stream):
     return s.elapsed_time(e) / reps * 1e-3
 
 
-def _traffic_from_profile(kernel_key):
-    """HBM bytes per launch of `kernel_key` from the committed PMC profile (rocprofv3 --pmc
-    FETCH_SIZE and WRITE_SIZE, separate passes; tools/pmc_step.sh -> profiles/r02_pmc.json, the round-1
-    tools/pmc_collect.sh -> profiles/r01_pmc.json before it),
-    or None when no profile of this kernel is committed."""
-    for name in ("r02_pmc.json", "r01_pmc.json"):   # the latest committed profile that has the kernel
+PMC_PROFILES = ("r02_pmc_s4.json", "r02_pmc.json", "r01_pmc.json")   # newest first
+
+
+def _pmc_from_profile(kernel_key):
+    """Per-launch PMC record of `kernel_key` from the newest committed profile that has it
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ passes, separate runs: tools/pmc_step.sh ->
+    tools/pmc_summary_json.py -> profiles/r02_pmc_s4.json; tools/pmc_to_json.py before it), or None."""
+    for name in PMC_PROFILES:
         path = os.path.join(REPO, "profiles", name)
         if not os.path.exists(path):
             continue
         with open(path) as f:
             prof = json.load(f)
-        k = prof.get("kernels", {}).get(kernel_key)
-        if k is not None:
-            return k.get("hbm_bytes_per_launch")
+        kernels = prof.get("kernels", {})
+        # "scan_bwd<9>" also names the instantiations with further template arguments ("scan_bwd<9, true>")
+        hits = [v for n, v in kernels.items() if n == kernel_key or n.startswith(kernel_key[:-1] + ",")]
+        if hits:
+            return dict(hits[0], profile="profiles/" + name)
     return None
+
+
+def _traffic_from_profile(kernel_key):
+    """HBM bytes per launch of `kernel_key` (2 x FETCH_SIZE + WRITE_SIZE, the round-1 correction) from
+    the committed PMC profile, or None when no profile of this kernel is committed."""
+    k = _pmc_from_profile(kernel_key)
+    return None if k is None else k.get("hbm_bytes_per_launch")
 
 
 def batch_assembly_ms(step, hsi, lidar, target, dev, steps, seed):
@@ -168,10 +179,22 @@ def dominant_kernel_roofline(model, batch, reps):
     algo = 4.0 * (nr * D * 2 + nr * XW + rows * D + ckpt + nr * D * 2 + nr * 32)
     achieved = algo / t / 1e9
     traffic = _traffic_from_profile("scan_bwd<9>")
+    # the same launch against its two other bounds: compulsory HBM bytes only (the 4-token state
+    # checkpoints the forward writes for it excluded), and VALU issue (the committed PMC profile's
+    # SQ_INSTS_VALU per launch x 4 cycles / 1024 SIMDs at 2.4 GHz = the time the instructions need
+    # with every SIMD issuing every cycle)
+    compulsory = algo - 4.0 * ckpt
+    pmc = _pmc_from_profile("scan_bwd<9>") or {}
+    valu_us = pmc.get("valu_issue_bound_us")
     return {"kernel": "scan_bwd<9> (hsi1 selective-scan backward, 640 seq x 81 tokens x 72 ch x 16 states)",
             "bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic, "avg_launch_us": round(t * 1e6, 2),
-            "algorithmic_bytes_per_launch": algo}
+            "algorithmic_bytes_per_launch": algo,
+            "compulsory": {"bytes_per_launch": compulsory, "achieved": round(compulsory / t / 1e9, 2),
+                           "frac": round(compulsory / t / 1e9 / PEAK_HBM_GBS, 5)},
+            "valu_issue": None if valu_us is None else {
+                "insts_per_launch": pmc.get("SQ_INSTS_VALU"), "bound_us": round(valu_us, 2),
+                "frac": round(valu_us / (t * 1e6), 4), "profile": pmc.get("profile")}}
 
 
 def gemm_roofline(model, batch, reps):

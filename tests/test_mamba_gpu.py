@@ -5,6 +5,7 @@ The reference semantics (transformers MambaMixer fallback, modeling_mamba.py:175
 the same inputs; the HIP kernels must match to fp32 accuracy (1e-4 relative to each tensor's max).
 """
 import math
+import os
 
 import pytest
 import torch
@@ -123,6 +124,19 @@ def test_mamba_kernels_vs_float64(L, D, E, use_ckpt):
         lib.vc_mamba_scan_bwd_params(B, D, ndir, P(gate_d), P(sp), P(dA2), P(dD2), P(dG2), P(ws), ws.numel(), s)
         torch.cuda.synchronize()
         assert torch.equal(dA2.cpu(), dA.cpu()) and torch.equal(dD2.cpu(), dDs.cpu()) and torch.equal(dG2.cpu(), dG.cpu())
+        # the dB / dC reduce-scatter's two forms (bank-masked DPP adds, default; selects + DPP,
+        # VITCNN_SCAN_SELECT_RS=1) pair the same lanes in the same order: bit-identical outputs
+        outs = [t.clone() for t in (dU, dDTL, dXD)]
+        os.environ["VITCNN_SCAN_SELECT_RS"] = "1"
+        try:
+            lib.vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
+                                  P(gate_d), P(Y), P(dYP), P(CKP), P(dU), P(dDTL), P(dXD), None, None, None, P(sp),
+                                  spn, s)
+            torch.cuda.synchronize()
+        finally:
+            del os.environ["VITCNN_SCAN_SELECT_RS"]
+        for a_, b_ in zip(outs, (dU, dDTL, dXD)):
+            assert torch.equal(a_, b_)
     dWdt, dbdt = torch.empty(D, R, device=DEV), torch.empty(D, device=DEV)
     lib.vc_gemm(0, 0, rows, R, D, 1.0, P(dDTL), D, 0, P(wdt_d), R, 0, 0.0, P(dXD), XW, 0, 1, None, None, 0, 0, 0,
                 None, P(ws), ws.numel(), s)

@@ -79,6 +79,7 @@ def test_muufl_gradients(muufl):
     assert not bad, bad[:5]
 
 
+@pytest.mark.timeout(400)   # up to three B = 64 CPU oracle steps (two of them float64) on the box's 16 cores
 def test_muufl_b64_parity():
     """Config 4's batch (B = 64 per GPU, [64,64,11,11] + [64,2,11,11], 12 classes): HIP logits and loss
     within 1e-3 relative of the fp32 oracle, argmax identical where the top-2 margin exceeds 2e-3 of the
@@ -130,11 +131,13 @@ def test_muufl_b64_parity():
         st64 = O.make_state(sd64)
         masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(),
                            relu_masks_from_workspace(m, Bb), pooled=tl_pooled_from_workspace(m, Bb))
-        st64r = O.make_state(sd64)
-        O.train_step(st64r, hsi.double(), lidar.double(), target, w.double())
-        for n, g in cand:
-            e64 = float((g - st64[n].grad).norm())
-            own = float((state[n].grad.double() - st64r[n].grad).norm())
-            if not (e64 <= 1e-3 * norms[n] + 5e-5 * gmax or e64 <= 3.0 * own + 5e-5 * gmax):
-                bad.append((n, e64, own, norms[n]))
+        far = [(n, float((g - st64[n].grad).norm())) for n, g in cand]
+        far = [(n, e64) for n, e64 in far if not e64 <= 1e-3 * norms[n] + 5e-5 * gmax]
+        if far:   # the plain float64 step (the fp32 CPU reference's own error) only when it is needed
+            st64r = O.make_state(sd64)
+            O.train_step(st64r, hsi.double(), lidar.double(), target, w.double())
+            for n, e64 in far:
+                own = float((state[n].grad.double() - st64r[n].grad).norm())
+                if not e64 <= 3.0 * own + 5e-5 * gmax:
+                    bad.append((n, e64, own, norms[n]))
     assert not bad, bad[:5]

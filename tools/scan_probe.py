@@ -76,6 +76,11 @@ def main():
                                     ckp, f(pfx + ".dU", nr * D), f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW),
                                     None, None, None, prog.scr_p, prog.scr_n, st.cuda_stream)
             print(f"    scan_bwd kernel, {NDIR * b:4d} sequences: {timed(bwd_b, reps, st):7.1f} us", flush=True)
+        # the select-based dB / dC reduce-scatter (A/B against the bank-masked default)
+        os.environ["VITCNN_SCAN_SELECT_RS"] = "1"
+        print(f"    scan_bwd kernel, select reduce-scatter: {timed(lambda: bwd_b(64), reps, st):7.1f} us",
+              flush=True)
+        del os.environ["VITCNN_SCAN_SELECT_RS"]
 
 
 if __name__ == "__main__":

@@ -125,6 +125,28 @@ __device__ __forceinline__ void cross_row_sum2(float& a, float& b) {
   b = __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
+// Reduce-scatter of 4 per-lane values over the 4 rows of a wave: lane (row r, column c) returns
+// v_r summed over the 4 rows at column c, in cross_row_sum's order ((r0 + r1) + (r2 + r3)), so each
+// total is bit-identical to cross_row_sum(v_r).  permlane16_swap(v0, v1) + add leaves v0's row-pair
+// sums in the even rows and v1's in the odd rows (likewise v2 / v3); a permlane32_swap of the two
+// results + add completes row r's value r: 3 swaps + 3 adds for four totals instead of 8 + 8.
+__device__ __forceinline__ float row_scatter4(float v0, float v1, float v2, float v3) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v0), __builtin_bit_cast(unsigned, v1),
+                                                  false, false);
+  const float x01 = __builtin_bit_cast(float, (unsigned)p[0]) + __builtin_bit_cast(float, (unsigned)p[1]);
+  const auto q = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v2), __builtin_bit_cast(unsigned, v3),
+                                                  false, false);
+  const float x23 = __builtin_bit_cast(float, (unsigned)q[0]) + __builtin_bit_cast(float, (unsigned)q[1]);
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x01), __builtin_bit_cast(unsigned, x23),
+                                                  false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+// a[r] for the lane's row r = lane >> 4 (register selects, no memory)
+__device__ __forceinline__ float row_select4(const float (&a)[4], int r) {
+  return r == 0 ? a[0] : (r == 1 ? a[1] : (r == 2 ? a[2] : a[3]));
+}
+
 // In-launch "last arriver" of a group of n blocks that each published a partial result (the split-K
 // combine's protocol, cdna_hip_programming.md "In-launch split-K reduction"): the block's global
 // stores are drained and released at agent scope, thread 0 takes a ticket from *cnt; the block that

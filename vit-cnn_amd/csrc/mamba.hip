@@ -94,6 +94,9 @@ constexpr int NQ = 4;                   // states per lane
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 __device__ __forceinline__ int seg_count(int L) { return (L + SCK - 1) / SCK; }
 
 // softplus(beta = 1, threshold = 20) with an accurate log1p: log1p(e) = log(1 + e) * e / ((1 + e) - 1)
@@ -108,7 +111,9 @@ __device__ __forceinline__ float softplus_c(float x) {
 // < 5e-8 relative), exp(x) - 1 elsewhere
 __device__ __forceinline__ float expm1_c(float x) {
   const float p = x * (1.f + x * (0.5f + x * (1.f / 6 + x * (1.f / 24 + x * (1.f / 120 + x * (1.f / 720))))));
-  return fabsf(x) < 0.25f ? p : __builtin_amdgcn_exp2f(x * LOG2E) - 1.f;
+  float e = __builtin_amdgcn_exp2f(x * LOG2E) - 1.f;
+  asm volatile("" : "+v"(e));   // both sides computed, then a select: no divergent branch
+  return fabsf(x) < 0.25f ? p : e;
 }
 
 // LDS image of one sequence (Lp = SCK * segments tokens; rows L..Lp-1 zero):
@@ -223,6 +228,7 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
       uc[i] = un[i];
       un[i] = buf_ld(r_u, (unsigned)((t0 + SCK + i) * a.D * 4) + lane_b);   // prefetch the next segment
     }
+    float yv[SCK];   // this lane's 4-state partial of C_t . h_t per token
 #pragma unroll
     for (int i = 0; i < SCK; ++i) {
       const int t = t0 + i;
@@ -236,10 +242,12 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
       h[1] = fmaf(dtu, bv.y, __builtin_amdgcn_exp2f(dt * A2[1]) * h[1]);
       h[2] = fmaf(dtu, bv.z, __builtin_amdgcn_exp2f(dt * A2[2]) * h[2]);
       h[3] = fmaf(dtu, bv.w, __builtin_amdgcn_exp2f(dt * A2[3]) * h[3]);
-      const float yt = cross_row_sum(fmaf(h[3], cv.w, fmaf(h[2], cv.z, fmaf(h[1], cv.y, h[0] * cv.x)))) + Dd * uc[i];
-      // the 4 rows hold the same value: an unconditional store of identical bytes
-      buf_st(r_y, (unsigned)(t * a.D * 4) + lane_b, yt);
+      yv[i] = fmaf(h[3], cv.w, fmaf(h[2], cv.z, fmaf(h[1], cv.y, h[0] * cv.x)));
     }
+    // the segment's 4 cross-row sums as one reduce-scatter: row q finishes token t0 + q and stores
+    // it (one store per segment; padding tokens fall out of range)
+    const float yt = row_scatter4(yv[0], yv[1], yv[2], yv[3]) + Dd * row_select4(uc, q);
+    buf_st(r_y, (unsigned)((t0 + q) * a.D * 4) + lane_b, yt);
   }
 }
 
@@ -266,6 +274,47 @@ __device__ __forceinline__ float reduce_scatter8_row(const float (&v)[8]) {
   return w + dpp_mov<0xB1>(w);
 }
 
+// The first two stages of reduce_scatter8_row without the selects: the lanes that keep value a and
+// the lanes that keep value b sit in different 4-lane banks (bit 3: banks 0,1 vs 2,3; bit 2: banks
+// 0,2 vs 1,3), so each output is two bank-masked DPP adds (own + partner's same value), each lane
+// written by exactly one of them.  Same partners and operand order as reduce_scatter8_row, so the
+// result is bit-identical.  s_nop 1: the DPP operands may have been written by the two preceding VALU
+// instructions.
+template <int CTRL_ASM>
+__device__ __forceinline__ float dpp_pair_add(float a, float b);
+template <>
+__device__ __forceinline__ float dpp_pair_add<0>(float a, float b) {   // row_mirror, bit 3
+  float r;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %1, %1 row_mirror row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %2, %2 row_mirror row_mask:0xf bank_mask:0xc bound_ctrl:1"
+      : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+template <>
+__device__ __forceinline__ float dpp_pair_add<1>(float a, float b) {   // row_half_mirror, bit 2
+  float r;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0x5 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xa bound_ctrl:1"
+      : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float reduce_scatter8_row_bm(const float (&v)[8]) {
+  const int l = threadIdx.x & 15;
+  const bool b1 = l & 2;
+  float y4[4], z[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y4[j] = dpp_pair_add<0>(v[j], v[j + 4]);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) z[j] = dpp_pair_add<1>(y4[j], y4[j + 2]);
+  const float keep = b1 ? z[1] : z[0], send = b1 ? z[0] : z[1];
+  const float w = keep + dpp_mov<0x4E>(send);
+  return w + dpp_mov<0xB1>(w);
+}
+
 struct ScanBwdOut {
   float* du;        // [nseq*L, D]
   float* ddtl;      // [nseq*L, D]  grad of W_dt dtr + b_dt (pre-softplus)
@@ -275,7 +324,7 @@ struct ScanBwdOut {
   float* dg_part;   // [nseq]
 };
 
-template <int RT>
+template <int RT, bool BM>
 __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
                                                 const float* __restrict__ yp, const float* __restrict__ dyp,
                                                 const float* __restrict__ ckpt, ScanBwdOut o) {
@@ -303,7 +352,9 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
   // the dB/dC column this lane's reduce-scatter total belongs to
   const int vi = cl >> 1;
   const int col = vi < 4 ? NQ * q + vi : NST + NQ * q + vi - 4;
-  float dh[NQ] = {0.f, 0.f, 0.f, 0.f}, dAacc[NQ] = {0.f, 0.f, 0.f, 0.f};
+  // the lane's 4 states as two packed pairs (v_pk_fma_f32 / v_pk_mul_f32: two states per instruction)
+  const f2 A2v[2] = {f2{A2[0], A2[1]}, f2{A2[2], A2[3]}};
+  f2 dh[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, dAacc[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
   float dD_acc = 0.f, dg_acc = 0.f;
   // global operands of a segment: the entering state, u, the gathered d(yp) and yp (for the gate
   // gradient); the next segment's are loaded while this one is computed
@@ -319,6 +370,7 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
   const auto r_du = buf_rsrc(o.du + base * a.D, seq_bytes);
   const auto r_ddtl = buf_rsrc(o.ddtl + base * a.D, seq_bytes);
   const auto r_ck = buf_rsrc(ckpt + (long)s * nseg * NST * a.D, (unsigned)(nseg * NST * a.D * 4));
+  const auto r_dx = buf_rsrc(o.dxdbl + base * XW, (unsigned)(a.L * XW * 4));
   const unsigned lane_b = valid ? (unsigned)d * 4u : 0x80000000u;   // invalid lanes: out of range
   auto load_seg = [&](int c) {
     const int t0 = c * SCK;
@@ -337,10 +389,10 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
   load_seg(nseg - 1);
   for (int c = nseg - 1; c >= 0; --c) {
     const int t0 = c * SCK;
-    float hs[SCK + 1][NQ];   // hs[i] = state entering token t0 + i
+    f2 hs[SCK + 1][2];   // hs[i] = state entering token t0 + i
     float uc[SCK], dyr[SCK];
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) hs[0][j] = hn[j];
+    hs[0][0] = f2{hn[0], hn[1]};
+    hs[0][1] = f2{hn[2], hn[3]};
 #pragma unroll
     for (int i = 0; i < SCK; ++i) {
       uc[i] = un[i];
@@ -348,53 +400,64 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
       dg_acc += dyr[i] * yn[i];
     }
     if (c > 0) load_seg(c - 1);
-    // recompute the segment's states as the forward did (keep exp(dt A) for the reverse sweep)
-    float dAs[SCK][NQ];
+    // recompute the segment's states as the forward did, element for element (keep exp(dt A) for the
+    // reverse sweep)
+    f2 dAs[SCK][2];
 #pragma unroll
     for (int i = 0; i < SCK; ++i) {
       const int t = t0 + i;
       const float4 bv = *reinterpret_cast<const float4*>(m.Bs + t * NST + NQ * q);
       const float dt = m.dts[t * Dp + d];
       const float dtu = dt * uc[i];
-      const float bb[NQ] = {bv.x, bv.y, bv.z, bv.w};
+      const f2 bb[2] = {f2{bv.x, bv.y}, f2{bv.z, bv.w}};
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) {
-        dAs[i][j] = __builtin_amdgcn_exp2f(dt * A2[j]);
-        hs[i + 1][j] = fmaf(dtu, bb[j], dAs[i][j] * hs[i][j]);
+      for (int p = 0; p < 2; ++p) {
+        const f2 e = f2{dt, dt} * A2v[p];
+        dAs[i][p] = f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+        hs[i + 1][p] = fma2(f2{dtu, dtu}, bb[p], dAs[i][p] * hs[i][p]);
       }
     }
     // reverse sweep
     float* rb = red + (c & 1) * nw * SCK * 32;
+    float Sv[SCK], Qv[SCK];   // this lane's 4-state partials of S and qa per token
 #pragma unroll
     for (int i = SCK - 1; i >= 0; --i) {
       const int t = t0 + i;
       const float4 b4 = *reinterpret_cast<const float4*>(m.Bs + t * NST + NQ * q);
       const float4 c4 = *reinterpret_cast<const float4*>(m.Cs + t * NST + NQ * q);
-      const float bv[NQ] = {b4.x, b4.y, b4.z, b4.w}, cv[NQ] = {c4.x, c4.y, c4.z, c4.w};
+      const f2 bv[2] = {f2{b4.x, b4.y}, f2{b4.z, b4.w}}, cv[2] = {f2{c4.x, c4.y}, f2{c4.z, c4.w}};
       const float dt = m.dts[t * Dp + d], ut = uc[i], dy = g * dyr[i];
       const float dtu = dt * ut;
-      float v[8];
-      float S = 0.f, qa = 0.f;   // this lane's 4 terms of sum_n dhn B and sum_n (dL/d(dA) dA) A
+      const f2 dy2 = f2{dy, dy}, dt2 = f2{dt, dt}, dtu2 = f2{dtu, dtu};
+      f2 Sp, Qp, vB[2], vC[2];   // this lane's terms of sum_n dhn B and sum_n (dL/d(dA) dA) A, pairwise
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) {
-        const float dhn = fmaf(cv[j], dy, dh[j]);              // dL/dh_t
-        const float qq = dhn * (dAs[i][j] * hs[i][j]);         // dL/d(dA_t) * dA_t
-        dAacc[j] = fmaf(qq, dt, dAacc[j]);
-        qa = j ? fmaf(qq, A2[j], qa) : qq * A2[j];
-        S = j ? fmaf(dhn, bv[j], S) : dhn * bv[j];
-        v[j] = dhn * dtu;                                      // dL/dB_t[n], this channel
-        v[4 + j] = dy * hs[i + 1][j];                          // dL/dC_t[n], this channel
-        dh[j] = dhn * dAs[i][j];                               // carried to t - 1
+      for (int p = 0; p < 2; ++p) {
+        const f2 dhn = fma2(cv[p], dy2, dh[p]);                // dL/dh_t
+        const f2 qq = dhn * (dAs[i][p] * hs[i][p]);            // dL/d(dA_t) * dA_t
+        dAacc[p] = fma2(qq, dt2, dAacc[p]);
+        Qp = p ? fma2(qq, A2v[p], Qp) : qq * A2v[p];
+        Sp = p ? fma2(dhn, bv[p], Sp) : dhn * bv[p];
+        vB[p] = dhn * dtu2;                                    // dL/dB_t[n], this channel
+        vC[p] = dy2 * hs[i + 1][p];                            // dL/dC_t[n], this channel
+        dh[p] = dhn * dAs[i][p];                               // carried to t - 1
       }
-      cross_row_sum2(S, qa);   // sums over the 16 states (the wave's 4 rows)
-      {   // the 4 rows store identical values; padding tokens / channels fall out of range
-        const unsigned row = (unsigned)(t * a.D * 4) + lane_b;
-        buf_st(r_du, row, dt * S + Dd * dy);
-        // softplus'(dt_lin) = sigmoid(dt_lin) = 1 - exp(-softplus(dt_lin))
-        buf_st(r_ddtl, row, (qa * LN2 + ut * S) * -expm1_c(-dt));
-      }
-      if (q == 0) dD_acc += dy * ut;
-      rb[(wave * SCK + i) * 32 + col] = reduce_scatter8_row(v);   // lanes 2j, 2j+1 store the same
+      const float S = Sp.x + Sp.y, qa = Qp.x + Qp.y;
+      const float v[8] = {vB[0].x, vB[0].y, vB[1].x, vB[1].y, vC[0].x, vC[0].y, vC[1].x, vC[1].y};
+      Sv[i] = S;
+      Qv[i] = qa;
+      rb[(wave * SCK + i) * 32 + col] = BM ? reduce_scatter8_row_bm(v) : reduce_scatter8_row(v);   // lanes 2j, 2j+1 store the same
+    }
+    {   // the sums over the 16 states (the wave's 4 rows) of the segment's 4 tokens as one
+        // reduce-scatter: row q finishes token t0 + q (padding tokens / channels fall out of range;
+        // their u and d(yp) loaded as 0)
+      const float S = row_scatter4(Sv[0], Sv[1], Sv[2], Sv[3]);
+      const float qa = row_scatter4(Qv[0], Qv[1], Qv[2], Qv[3]);
+      const float dt = m.dts[(t0 + q) * Dp + d], ut = row_select4(uc, q), dy = g * row_select4(dyr, q);
+      const unsigned row = (unsigned)((t0 + q) * a.D * 4) + lane_b;
+      buf_st(r_du, row, dt * S + Dd * dy);
+      // softplus'(dt_lin) = sigmoid(dt_lin) = 1 - exp(-softplus(dt_lin))
+      buf_st(r_ddtl, row, (qa * LN2 + ut * S) * -expm1_c(-dt));
+      dD_acc += dy * ut;   // row q's tokens; the rows are summed at the end
     }
     // one barrier per segment: the partials alternate between two buffers, so the next segment's
     // stores (other buffer) need no barrier behind this combine; the one after them orders the
@@ -402,17 +465,23 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
     __syncthreads();
     for (int j = threadIdx.x; j < SCK * 32; j += blockDim.x) {
       const int i = j >> 5, cc = j & 31, t = t0 + i;
-      if (t < a.L) {
-        float sum = 0.f;
-        for (int ww = 0; ww < nw; ++ww) sum += rb[(ww * SCK + i) * 32 + cc];
-        o.dxdbl[(base + t) * XW + R + cc] = sum;
-      }
+      // the nw (<= 8) partials read together, then summed in wave order; tokens t >= L fall out of
+      // the output resource's range
+      float pv[8];
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) pv[ww] = ww < nw ? rb[(ww * SCK + i) * 32 + cc] : 0.f;
+      float sum = pv[0];
+#pragma unroll
+      for (int ww = 1; ww < 8; ++ww)
+        if (ww < nw) sum += pv[ww];
+      buf_st(r_dx, (unsigned)(t * XW + R + cc) * 4u, sum);
     }
   }
+  dD_acc = cross_row_sum(dD_acc);
   if (valid) {
     float* dap = o.da_part + ((long)s * a.D + d) * NST + NQ * q;
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) dap[j] = dAacc[j] * A2[j] * LN2;   // dL/dA_log = dL/dA * A
+    for (int j = 0; j < NQ; ++j) dap[j] = dAacc[j >> 1][j & 1] * A2[j] * LN2;   // dL/dA_log = dL/dA * A
     if (q == 0) o.dd_part[(long)s * a.D + d] = dD_acc;
   }
   const float v = wave_sum(q == 0 ? dg_acc : 0.f);
@@ -692,9 +761,19 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
     ckpt = p_ck;
   }
   ScanBwdOut o{du, ddt_lin, dxdbl, p_a, p_d, p_g};
-  if (R == 9) hipLaunchKernelGGL(scan_bwd<9>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
-  else if (R == 16) hipLaunchKernelGGL(scan_bwd<16>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
-  else hipLaunchKernelGGL(scan_bwd<0>, grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o);
+  // dB / dC reduce-scatter: bank-masked DPP adds (default) or the select-based form
+  // (VITCNN_SCAN_SELECT_RS=1, read per call; bit-identical, kept for the A/B measurement and its test)
+  const char* sel_env = getenv("VITCNN_SCAN_SELECT_RS");
+  const bool bm = !(sel_env && atoi(sel_env));
+#define VC_SCAN_BWD(RV)                                                                                     \
+  do {                                                                                                      \
+    if (bm) hipLaunchKernelGGL((scan_bwd<RV, true>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o); \
+    else hipLaunchKernelGGL((scan_bwd<RV, false>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o); \
+  } while (0)
+  if (R == 9) VC_SCAN_BWD(9);
+  else if (R == 16) VC_SCAN_BWD(16);
+  else VC_SCAN_BWD(0);
+#undef VC_SCAN_BWD
   VC_CHECK_LAUNCH();
   // the three parameter-gradient outputs are optional (the per-sequence partials stay in ws, for
   // vc_mamba_scan_bwd_params)

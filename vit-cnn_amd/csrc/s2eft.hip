@@ -74,6 +74,8 @@ __global__ void strip_cls(int B, int N, int D, const float* __restrict__ dX, flo
 }
 
 // ------------------------------------------------------------------ attention core (dim_head 16)
+constexpr float ATT_LOG2E = 1.4426950408889634f;
+constexpr float ATT_LN2 = 0.6931471805599453f;
 // One block per (b, h) with ceil(T/16) waves (256 blocks x 10 waves at config 5), so the head's K/V (and
 // for the backward Q, dO, lse, rowsum(dO*O)) are staged into LDS (sized to T) once per head.  P is never stored: the forward saves lse per row.
 // Forward on the matrix cores (v_mfma_f32_16x16x4_f32).  A wave owns 16 queries of one (b, h) and walks
@@ -104,6 +106,9 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
   const int qi = min(q0 + c, T - 1);
   // B operand of S^T: Q^T[d = 4g + s][q = c]
   const f32x4 qv = *(const f32x4*)(base + (long)qi * ld + h * 16 + g * 4);
+  // softmax in the base-2 domain: scores pre-scaled by log2(e), so every exponential is one v_exp_f32
+  // (expf's range reduction would cost ~10 VALU per score); lse is stored in natural log as before
+  const float scale2 = scale * ATT_LOG2E;
   float m = -INFINITY, l = 0.f;
   f32x4 o = {0.f, 0.f, 0.f, 0.f};          // O^T[d = 4g + r][q = c]
   for (int k0 = 0; k0 < T; k0 += 16) {
@@ -118,18 +123,18 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
     float tm = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      sv[r] = (k0 + 4 * g + r < T) ? st[r] * scale : -INFINITY;
+      sv[r] = (k0 + 4 * g + r < T) ? st[r] * scale2 : -INFINITY;
       tm = fmaxf(tm, sv[r]);
     }
     tm = fmaxf(tm, __shfl_xor(tm, 16, 64));
     tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
     const float mn = fmaxf(m, tm);
-    const float corr = (m == -INFINITY) ? 0.f : expf(m - mn);
+    const float corr = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
     m = mn;
     float pv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      pv[r] = (sv[r] == -INFINITY) ? 0.f : expf(sv[r] - mn);
+      pv[r] = (sv[r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sv[r] - mn);
       l = l * (r == 0 ? corr : 1.f) + pv[r];
     }
     o *= corr;
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
   if (q0 + c >= T) return;
   const float rl = 1.0f / l;
   *(f32x4*)(out + ((long)b * T + q0 + c) * ldo + h * 16 + g * 4) = o * rl;
-  if (g == 0) lse[((long)b * H + h) * T + q0 + c] = m + logf(l);
+  if (g == 0) lse[((long)b * H + h) * T + q0 + c] = m * ATT_LN2 + logf(l);
 }
 
 // Backward on MFMA, same tile scheme as the forward.  dS = P * (dP - rowsum(dO*O)), P recomputed
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
     v = group16_sum(v);
     if (d == 0 && idx < T * 16) {
       Ds[r] = v;
-      Ls[r] = lse[((long)b * H + h) * T + r];
+      Ls[r] = lse[((long)b * H + h) * T + r] * ATT_LOG2E;   // base-2 lse
     }
   }
   __syncthreads();
@@ -204,6 +209,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   const int ri = min(r0 + c, T - 1);
   {  // pass 1: dq of queries r0 .. r0 + 15 (query c of this lane)
     const f32x4 qv = Qs[ri * 4 + g], gv = dOs[ri * 4 + g];
+    const float scale2 = scale * ATT_LOG2E;
     const float lq = Ls[ri], dq_ = Ds[ri];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};  // dQ^T[d = 4g + r][q = c]
     for (int k0 = 0; k0 < T; k0 += 16) {
@@ -215,7 +221,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bool valid = k0 + 4 * g + r < T;
-        const float p = valid ? expf(st[r] * scale - lq) : 0.f;
+        const float p = valid ? __builtin_amdgcn_exp2f(fmaf(st[r], scale2, -lq)) : 0.f;
         ds[r] = p * (dpt[r] - dq_);
       }
 #pragma unroll
@@ -228,6 +234,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   }
   {  // pass 2: dk, dv of keys r0 .. r0 + 15 (key c of this lane)
     const f32x4 kv = Ks[ri * 4 + g], vv = Vs[ri * 4 + g];
+    const float scale2 = scale * ATT_LOG2E;
     f32x4 adk = {0.f, 0.f, 0.f, 0.f}, adv = {0.f, 0.f, 0.f, 0.f};  // dK^T / dV^T [d = 4g + r][key = c]
     for (int q0 = 0; q0 < T; q0 += 16) {
       const int qq = min(q0 + c, T - 1);
@@ -240,7 +247,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
         const int q = q0 + 4 * g + r;
         const bool valid = q < T;
         const int qc = valid ? q : T - 1;
-        const float p = valid ? expf(sm[r] * scale - Ls[qc]) : 0.f;
+        const float p = valid ? __builtin_amdgcn_exp2f(fmaf(sm[r], scale2, -Ls[qc])) : 0.f;
         pr[r] = p;
         ds[r] = p * (dp[r] - Ds[qc]);
       }
