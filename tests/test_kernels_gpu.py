@@ -30,6 +30,9 @@ def S():
     return torch.cuda.current_stream().cuda_stream
 
 
+S_ = S   # for tests whose own shape argument is named S
+
+
 def P(t):
     return t.data_ptr() if t is not None else None
 
@@ -432,3 +435,32 @@ def test_weighted_cross_entropy(L, B, ncls):
     torch.cuda.synchronize()
     assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
     assert rel_err(dl.cpu().numpy(), lr.grad.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("B,S,Pk,Ci", [(3, 49, 9, 128), (2, 25, 4, 72), (2, 81, 16, 64), (2, 49, 9, 70), (1, 7, 1, 4),
+                                       (300, 49, 9, 128), (260, 25, 4, 72)])
+def test_nonlocal_attention_fwd_bwd(L, B, S, Pk, Ci):
+    """vc_nonlocal_attn_fwd / _bwd (NONLocalBlock2D core, Mutimodality_Mamba7.py:140-159: unscaled
+    theta . phi^T, softmax over the pooled keys, att . g) vs torch float64 autograd.  Ci % 4 == 0 takes the
+    MFMA backward (S^T = phi theta^T tiles, 16 keys x 16 queries) and, from B = 256, the MFMA forward;
+    Ci = 70 the wave-per-row kernels."""
+    theta = rnd(B * S, Ci, seed=51)
+    pooled = rnd(B * Pk, 2 * Ci, seed=52)
+    dout = rnd(B * S, Ci, seed=53)
+    th = theta.double().view(B, S, Ci).requires_grad_(True)
+    pp = pooled.double().view(B, Pk, 2 * Ci).requires_grad_(True)
+    att_ref = torch.softmax(th @ pp[..., :Ci].transpose(1, 2), dim=-1)
+    o_ref = att_ref @ pp[..., Ci:]
+    o_ref.backward(dout.double().view(B, S, Ci))
+    td, pd, dd = theta.to(DEV), pooled.to(DEV), dout.to(DEV)
+    att = torch.full((B * S * Pk,), float("nan"), device=DEV)
+    o = torch.full((B * S, Ci), float("nan"), device=DEV)
+    dth = torch.full((B * S, Ci), float("nan"), device=DEV)
+    dpp = torch.full((B * Pk, 2 * Ci), float("nan"), device=DEV)
+    assert L.vc_nonlocal_attn_fwd(B, S, Pk, Ci, P(td), P(pd), P(att), P(o), S_()) == 0
+    assert L.vc_nonlocal_attn_bwd(B, S, Pk, Ci, P(td), P(pd), P(att), P(dd), P(dth), P(dpp), S_()) == 0
+    torch.cuda.synchronize()
+    assert rel_err(att.cpu().view(B, S, Pk).numpy(), att_ref.detach().numpy()) < 1e-5
+    assert rel_err(o.cpu().view(B, S, Ci).numpy(), o_ref.detach().numpy()) < 1e-5
+    assert rel_err(dth.cpu().view(B, S, Ci).numpy(), th.grad.numpy()) < 1e-5
+    assert rel_err(dpp.cpu().view(B, Pk, 2 * Ci).numpy(), pp.grad.numpy()) < 1e-5

@@ -27,26 +27,43 @@ namespace {
 
 constexpr int NST = 16;     // ssm state size (config state_size=16, Mutimodality_Mamba7.py:316)
 
-// one thread per (k, b, t, d); index decomposition with launch-time FastDivs (no integer divide)
-__global__ void dirconv_fwd(int total, FastDiv fD, FastDiv fL, FastDiv fB, const int* __restrict__ order,
-                            const float* __restrict__ xz, const float* __restrict__ cw, const float* __restrict__ cb,
-                            float* __restrict__ u) {
+// Direction gather + causal conv1d + SiLU.  A thread owns DC_T consecutive tokens of one (direction,
+// sample, channel) and slides the 4-tap window along them, so each gathered input is loaded once
+// (a thread per output would load it 4 times, with 4 order-table reads); lanes run along the channels
+// (coalesced rows).  Index decomposition with launch-time FastDivs.  A tap before the sequence start
+// contributes fma(w, 0, pre) = pre, i.e. it is skipped as in the reference's left zero padding.
+constexpr int DC_T = 8;
+__global__ void dirconv_fwd_run(int total, FastDiv fD, FastDiv fC, FastDiv fB, int L, const int* __restrict__ order,
+                                const float* __restrict__ xz, const float* __restrict__ cw,
+                                const float* __restrict__ cb, float* __restrict__ u) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int D = fD.div, L = fL.div;
-  int d, t, b;
-  const int st = fdivmod(idx, fD, d);
-  const int s = fdivmod(st, fL, t);
-  const int k = fdivmod(s, fB, b);
+  const int D = fD.div;
+  int d, c, b;
+  const int sc = fdivmod(idx, fD, d);
+  const int sq = fdivmod(sc, fC, c);
+  const int k = fdivmod(sq, fB, b);
   const int* ord = order + k * L;
   const float* xb = xz + (long)b * L * (2 * D) + d;
-  float pre = cb[d];
+  const float w0 = cw[d * 4], w1 = cw[d * 4 + 1], w2 = cw[d * 4 + 2], w3 = cw[d * 4 + 3], bias = cb[d];
+  const int t0 = c * DC_T;
+  float x[DC_T + 3];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int tau = t - 3 + j;
-    if (tau >= 0) pre += cw[d * 4 + j] * xb[ord[tau] * (2 * D)];
+  for (int i = 0; i < DC_T + 3; ++i) {
+    const int tau = t0 - 3 + i;
+    x[i] = (tau >= 0 && tau < L) ? xb[ord[tau] * (2 * D)] : 0.f;
   }
-  u[idx] = silu_f(pre);
+  float* ub = u + ((long)sq * L + t0) * D + d;
+#pragma unroll
+  for (int i = 0; i < DC_T; ++i) {
+    if (t0 + i < L) {
+      float pre = fmaf(w0, x[i], bias);
+      pre = fmaf(w1, x[i + 1], pre);
+      pre = fmaf(w2, x[i + 2], pre);
+      pre = fmaf(w3, x[i + 3], pre);
+      ub[(long)i * D] = silu_f(pre);
+    }
+  }
 }
 
 __device__ __forceinline__ float gate_softmax(const float* logits, int ndir, int k) {
@@ -327,15 +344,16 @@ struct ScanBwdOut {
 template <int RT, bool BM>
 __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
                                                 const float* __restrict__ yp, const float* __restrict__ dyp,
-                                                const float* __restrict__ ckpt, ScanBwdOut o) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // SeqLds, red [2][nw][SCK][32], [nw]
+                                                const float* __restrict__ ckpt, ScanBwdOut o, int rbs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // SeqLds, red [2 rbs][nw][SCK][32], [nw], ord
   const int R = RT ? RT : a.R;
   const int XW = R + 2 * NST;
   const int nseg = seg_count(a.L), Lp = nseg * SCK;
   const int nw = blockDim.x >> 6, Dp = nw * 16;
   const SeqLds m(smem, Lp, R, Dp);
   float* red = m.xr + Lp * R;
-  int* ord = reinterpret_cast<int*>(red + 2 * nw * SCK * 32 + nw);   // [L] this direction's order
+  const int nbuf = 2 * rbs;   // partial buffers: a combine every rbs segments, double-buffered
+  int* ord = reinterpret_cast<int*>(red + nbuf * nw * SCK * 32 + nw);   // [L] this direction's order
   const int s = blockIdx.x, k = s / a.B, b = s - k * a.B;
   for (int t = threadIdx.x; t < a.L; t += blockDim.x) ord[t] = a.order[k * a.L + t];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, cl = lane & 15;
@@ -418,7 +436,7 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
       }
     }
     // reverse sweep
-    float* rb = red + (c & 1) * nw * SCK * 32;
+    float* rb = red + (c % nbuf) * nw * SCK * 32;
     float Sv[SCK], Qv[SCK];   // this lane's 4-state partials of S and qa per token
 #pragma unroll
     for (int i = SCK - 1; i >= 0; --i) {
@@ -459,22 +477,26 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
       buf_st(r_ddtl, row, (qa * LN2 + ut * S) * -expm1_c(-dt));
       dD_acc += dy * ut;   // row q's tokens; the rows are summed at the end
     }
-    // one barrier per segment: the partials alternate between two buffers, so the next segment's
-    // stores (other buffer) need no barrier behind this combine; the one after them orders the
-    // reuse of this buffer two segments later
-    __syncthreads();
-    for (int j = threadIdx.x; j < SCK * 32; j += blockDim.x) {
-      const int i = j >> 5, cc = j & 31, t = t0 + i;
-      // the nw (<= 8) partials read together, then summed in wave order; tokens t >= L fall out of
-      // the output resource's range
-      float pv[8];
+    // one barrier per rbs segments: segment c's partials go to buffer c % (2 rbs), so the next rbs
+    // segments' stores (the other half of the buffers) need no barrier behind this combine; the
+    // combine after them orders the reuse of these buffers
+    if (c % rbs == 0) {
+      __syncthreads();
+      for (int j = threadIdx.x; j < rbs * SCK * 32; j += blockDim.x) {
+        const int cs = c + j / (SCK * 32), jj = j % (SCK * 32);
+        const int i = jj >> 5, cc = jj & 31, t = cs * SCK + i;
+        const float* rbc = red + (cs % nbuf) * nw * SCK * 32;
+        // the nw (<= 8) partials read together, then summed in wave order; tokens t >= L (and
+        // segments past the last) fall out of the output resource's range
+        float pv[8];
 #pragma unroll
-      for (int ww = 0; ww < 8; ++ww) pv[ww] = ww < nw ? rb[(ww * SCK + i) * 32 + cc] : 0.f;
-      float sum = pv[0];
+        for (int ww = 0; ww < 8; ++ww) pv[ww] = ww < nw ? rbc[(ww * SCK + i) * 32 + cc] : 0.f;
+        float sum = pv[0];
 #pragma unroll
-      for (int ww = 1; ww < 8; ++ww)
-        if (ww < nw) sum += pv[ww];
-      buf_st(r_dx, (unsigned)(t * XW + R + cc) * 4u, sum);
+        for (int ww = 1; ww < 8; ++ww)
+          if (ww < nw) sum += pv[ww];
+        buf_st(r_dx, (unsigned)(t * XW + R + cc) * 4u, sum);
+      }
     }
   }
   dD_acc = cross_row_sum(dD_acc);
@@ -485,7 +507,7 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
     if (q == 0) o.dd_part[(long)s * a.D + d] = dD_acc;
   }
   const float v = wave_sum(q == 0 ? dg_acc : 0.f);
-  float* rg = red + 2 * nw * SCK * 32;
+  float* rg = red + nbuf * nw * SCK * 32;
   if (lane == 0) rg[wave] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -558,6 +580,10 @@ __global__ __launch_bounds__(256) void gate_grad(int ndir, int per_dir, const fl
 
 
 // dxz[b,l,d] = sum_k sum_j w[d,j] dpre[k,b,inv_k(l)+3-j,d]   (the x half; gate_bwd writes the z half)
+// dxz[b, l, d] = sum_k sum_j w[d, j] dpre[k, b, inv_k(l) + 3 - j, d].  All ndir (<= MAXK) order-table
+// entries are read first and the 4 ndir taps issued after them (one round of dependent loads instead
+// of ndir); taps past the sequence end read as 0.  Same accumulation order for every ndir.
+template <int MAXK>
 __global__ void dirconv_bwd_gather(int total, FastDiv fD, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
                                    const float* __restrict__ cw, const float* __restrict__ dpre,
                                    float* __restrict__ dxz) {
@@ -571,58 +597,77 @@ __global__ void dirconv_bwd_gather(int total, FastDiv fD, FastDiv fL, int B, int
 #pragma unroll
   for (int j = 0; j < 4; ++j) w[j] = cw[d * 4 + j];
   float acc = 0.f;
-  for (int kk = 0; kk < ndir; ++kk) {
-    const int tk = inv[kk * L + l];
-    const float* base = dpre + (long)(kk * B + b) * L * D + d;
+  for (int k0 = 0; k0 < ndir; k0 += MAXK) {
+    int tk[MAXK];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = tk + 3 - j;
-      if (t < L) acc += w[j] * base[t * D];
+    for (int kk = 0; kk < MAXK; ++kk) tk[kk] = k0 + kk < ndir ? inv[(k0 + kk) * L + l] : L;
+    float v[MAXK][4];
+#pragma unroll
+    for (int kk = 0; kk < MAXK; ++kk) {
+      const float* base = dpre + (long)((k0 + kk) * B + b) * L * D + d;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = tk[kk] + 3 - j;
+        v[kk][j] = t < L ? base[(long)t * D] : 0.f;
+      }
     }
+#pragma unroll
+    for (int kk = 0; kk < MAXK; ++kk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = fmaf(w[j], v[kk][j], acc);
   }
   dxz[(long)bl * 2 * D + d] = acc;
 }
 
-// Fused SiLU backward + conv1d weight/bias partial sums over a chunk of (seq, t) rows:
-//   dpre = du * SiLU'(pre) (pre recomputed from the 4 gathered taps, written in place over du),
-//   part[p][d*4 + j] = sum dpre * x_{t-3+j},  part[p][4D + d] = sum dpre
-// block = 16 channels x 16 row lanes (64-B row segments, 16 independent streams per channel)
-__global__ __launch_bounds__(256) void dirconv_bwd_wgrad(int D, FastDiv fL, FastDiv fB, const int* __restrict__ order,
-                                                         const float* __restrict__ xz, const float* __restrict__ cw,
-                                                         const float* __restrict__ cb, float* __restrict__ du,
-                                                         int rows, int rows_per, float* __restrict__ part) {
+// Fused SiLU backward + conv1d weight/bias partial sums over a chunk of (seq, token-run) items:
+//   dpre = du * SiLU'(pre) (pre recomputed from the 4 gathered taps as dirconv_fwd_run does, written in
+//   place over du), part[p][d*4 + j] = sum dpre * x_{t-3+j},  part[p][4D + d] = sum dpre
+// block = 16 channels x 16 item lanes; an item is DC_T consecutive tokens of one sequence, walked with
+// the forward's sliding tap window (each gathered input loaded once).  Fixed order, deterministic.
+__global__ __launch_bounds__(256) void dirconv_bwd_wgrad(int D, int L, FastDiv fC, FastDiv fB,
+                                                         const int* __restrict__ order, const float* __restrict__ xz,
+                                                         const float* __restrict__ cw, const float* __restrict__ cb,
+                                                         float* __restrict__ du, int items, int items_per,
+                                                         float* __restrict__ part) {
   __shared__ float sh[5][16][17];
   const int dlc = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int d = blockIdx.x * 16 + dlc;
-  const int L = fL.div;
-  const int r0 = blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
+  const int i0 = blockIdx.y * items_per, i1 = min(items, i0 + items_per);
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if (d < D) {
-    float w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = cw[d * 4 + j];
-    const float bias = cb[d];
-    for (int r = r0 + rl; r < r1; r += 16) {
-      int t, b;
-      const int s = fdivmod(r, fL, t);
-      const int k = fdivmod(s, fB, b);
+    const float w0 = cw[d * 4], w1 = cw[d * 4 + 1], w2 = cw[d * 4 + 2], w3 = cw[d * 4 + 3], bias = cb[d];
+    for (int it = i0 + rl; it < i1; it += 16) {
+      int c, b;
+      const int sq = fdivmod(it, fC, c);
+      const int k = fdivmod(sq, fB, b);
       const int* ord = order + k * L;
       const float* xb = xz + (long)b * L * (2 * D) + d;
-      float x[4];
-      float pre = bias;
+      const int t0 = c * DC_T;
+      float x[DC_T + 3];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int tau = t - 3 + j;
-        x[j] = tau >= 0 ? xb[ord[tau] * (2 * D)] : 0.f;
-        pre += w[j] * x[j];
+      for (int i = 0; i < DC_T + 3; ++i) {
+        const int tau = t0 - 3 + i;
+        x[i] = (tau >= 0 && tau < L) ? xb[ord[tau] * (2 * D)] : 0.f;
       }
-      const float sg = sigmoid_f(pre);
-      float* gp = du + (long)r * D + d;
-      const float g = *gp * sg * (1.f + pre * (1.f - sg));
-      *gp = g;
-      acc[4] += g;
+      float* gp = du + ((long)sq * L + t0) * D + d;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] += g * x[j];
+      for (int i = 0; i < DC_T; ++i) {
+        if (t0 + i < L) {
+          float pre = fmaf(w0, x[i], bias);
+          pre = fmaf(w1, x[i + 1], pre);
+          pre = fmaf(w2, x[i + 2], pre);
+          pre = fmaf(w3, x[i + 3], pre);
+          const float sg = sigmoid_f(pre);
+          const float g = gp[(long)i * D] * sg * (1.f + pre * (1.f - sg));
+          gp[(long)i * D] = g;
+          acc[4] += g;
+          // taps before the sequence start are 0 (the forward skipped them)
+          acc[0] += g * x[i];
+          acc[1] += g * x[i + 1];
+          acc[2] += g * x[i + 2];
+          acc[3] += g * x[i + 3];
+        }
+      }
     }
   }
 #pragma unroll
@@ -648,8 +693,11 @@ VC_API int vc_mamba_dirconv_fwd(int B, int L, int D, int ndir, const int* order,
   if (total == 0) return VC_OK;
   VC_REQUIRE_I32(total);
   VC_REQUIRE_I32((long)B * L * 2 * D);
-  hipLaunchKernelGGL(dirconv_fwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(D),
-                     make_fastdiv(L), make_fastdiv(B), order, xz, conv_w, conv_b, u);
+  const int nch = vc_cdiv(L, DC_T);
+  const long runs = (long)ndir * B * nch * D;
+  VC_REQUIRE_I32(runs);
+  hipLaunchKernelGGL(dirconv_fwd_run, dim3(vc_cdiv(runs, 256)), dim3(256), 0, stream, (int)runs, make_fastdiv(D),
+                     make_fastdiv(nch), make_fastdiv(B), L, order, xz, conv_w, conv_b, u);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -741,7 +789,13 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   VC_REQUIRE(need_a + need_d + need_g + need_ck <= ws_floats);
   const int nw = vc_cdiv(D, 16);
   VC_REQUIRE(nw <= 8);
-  const size_t sm = sizeof(float) * (seq_lds_floats(L, R, nw * 16) + 2 * nw * SCK * 32 + nw + L);
+  // dB / dC partial combine every rbs segments (VITCNN_SCAN_RBS, default 2), when the LDS still holds
+  // three blocks per CU; else every segment
+  const char* rbs_env = getenv("VITCNN_SCAN_RBS");
+  int rbs = rbs_env ? std::max(1, std::min(4, atoi(rbs_env))) : 2;
+  auto lds_bytes = [&](int r) { return sizeof(float) * (seq_lds_floats(L, R, nw * 16) + 2 * r * nw * SCK * 32 + nw + L); };
+  while (rbs > 1 && lds_bytes(rbs) > 160 * 1024 / 3 && lds_bytes(1) <= 160 * 1024 / 3) --rbs;
+  const size_t sm = lds_bytes(rbs);
   VC_REQUIRE(sm <= 160 * 1024);
   VC_REQUIRE_I32((long)nseq * L * (R + 2 * NST));
   float* p_a = ws;
@@ -767,8 +821,8 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   const bool bm = !(sel_env && atoi(sel_env));
 #define VC_SCAN_BWD(RV)                                                                                     \
   do {                                                                                                      \
-    if (bm) hipLaunchKernelGGL((scan_bwd<RV, true>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o); \
-    else hipLaunchKernelGGL((scan_bwd<RV, false>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o); \
+    if (bm) hipLaunchKernelGGL((scan_bwd<RV, true>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs); \
+    else hipLaunchKernelGGL((scan_bwd<RV, false>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs); \
   } while (0)
   if (R == 9) VC_SCAN_BWD(9);
   else if (R == 16) VC_SCAN_BWD(16);
@@ -805,15 +859,21 @@ VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order,
   VC_REQUIRE(B > 0 && L > 0 && D > 0 && ndir > 0);
   const long rows = (long)ndir * B * L;
   VC_REQUIRE_I32(rows * D);
-  int rows_per = std::max<long>(64, (rows + 255) / 256);
-  while ((long)vc_cdiv(rows, rows_per) * D * 5 > ws_floats) rows_per *= 2;
-  const int P = vc_cdiv(rows, rows_per);
-  hipLaunchKernelGGL(dirconv_bwd_wgrad, dim3(vc_cdiv(D, 16), P), dim3(256), 0, stream, D, make_fastdiv(L),
-                     make_fastdiv(B), order, xz, conv_w, conv_b, du, (int)rows, rows_per, ws);
+  const int nch = vc_cdiv(L, DC_T);
+  const long items = (long)ndir * B * nch;   // DC_T-token runs
+  int items_per = std::max<long>(16, (items + 255) / 256);
+  while ((long)vc_cdiv(items, items_per) * D * 5 > ws_floats) items_per *= 2;
+  const int P = vc_cdiv(items, items_per);
+  hipLaunchKernelGGL(dirconv_bwd_wgrad, dim3(vc_cdiv(D, 16), P), dim3(256), 0, stream, D, L, make_fastdiv(nch),
+                     make_fastdiv(B), order, xz, conv_w, conv_b, du, (int)items, items_per, ws);
   VC_CHECK_LAUNCH();
   const long tot2 = (long)B * L * D;
-  hipLaunchKernelGGL(dirconv_bwd_gather, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, (int)tot2,
-                     make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, conv_w, du, dxz);
+  if (ndir <= 10)   // the model's 10 scan orders: one round of loads
+    hipLaunchKernelGGL(dirconv_bwd_gather<10>, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, (int)tot2,
+                       make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, conv_w, du, dxz);
+  else
+    hipLaunchKernelGGL(dirconv_bwd_gather<4>, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, (int)tot2,
+                       make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, conv_w, du, dxz);
   VC_CHECK_LAUNCH();
   if (dconv_b == dconv_w + 4L * D) return launch_sum_rows(P, 5 * D, ws, 5L * D, 0L, dconv_w, 0.f, stream);
   int rc = launch_sum_rows(P, 4 * D, ws, 5L * D, 0L, dconv_w, 0.f, stream);
