@@ -81,6 +81,10 @@ def main():
         print(f"    scan_bwd kernel, select reduce-scatter: {timed(lambda: bwd_b(64), reps, st):7.1f} us",
               flush=True)
         del os.environ["VITCNN_SCAN_SELECT_RS"]
+        # the dB / dC partial combine after every segment (A/B against every second segment, the default)
+        os.environ["VITCNN_SCAN_RBS"] = "1"
+        print(f"    scan_bwd kernel, combine every segment: {timed(lambda: bwd_b(64), reps, st):7.1f} us", flush=True)
+        del os.environ["VITCNN_SCAN_RBS"]
 
 
 if __name__ == "__main__":
