@@ -85,11 +85,24 @@ __global__ __launch_bounds__(256) void head_fwd(int S1, int S2, int C, int ncls,
   for (int c0 = 0; c0 < C; c0 += 64) {
     const int c = c0 + cl;
     float s1 = 0.f, s2 = 0.f;
-    if (c < C) {   // unrolled: a thread's loads of the chunk are in flight together
-#pragma unroll 4
-      for (int p = rg; p < S1; p += 4) s1 += f1[((long)b * S1 + p) * C + c];
-#pragma unroll 4
-      for (int q = rg; q < S2; q += 4) s2 += f2[((long)b * S2 + q) * C + c];
+    if (c < C) {
+      // a thread's first HR rows of each map are loaded before any is summed (one round of dependent
+      // HBM loads instead of one per 4 rows; the sums keep the row order), the rest (S > 4 HR) in a loop
+      constexpr int HR = 24;
+      float v1[HR], v2[HR];
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {
+        const int p = rg + 4 * i;
+        v1[i] = p < S1 ? f1[((long)b * S1 + p) * C + c] : 0.f;
+        v2[i] = p < S2 ? f2[((long)b * S2 + p) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < HR; ++i) {
+        if (rg + 4 * i < S1) s1 += v1[i];
+        if (rg + 4 * i < S2) s2 += v2[i];
+      }
+      for (int p = rg + 4 * HR; p < S1; p += 4) s1 += f1[((long)b * S1 + p) * C + c];
+      for (int q = rg + 4 * HR; q < S2; q += 4) s2 += f2[((long)b * S2 + q) * C + c];
     }
     red[rg * 64 + cl] = s1 / (float)S1 + s2 / (float)S2;
     __syncthreads();

@@ -990,7 +990,9 @@ class _Program:
         self.lanes_on = lanes and _LANES and os.environ.get("VITCNN_LANES_BWD", "1") != "0"
         grad = out if out is not None else torch.empty(m._n_params, dtype=torch.float32, device=self.device)
         if m._n_params > m._n_active:  # parameters the reference forward never uses get no gradient
-            self.L.vc_fill(m._n_params - m._n_active, grad.data_ptr() + F32 * m._n_active, 0.0, self.s)
+            # (off lane 0's chain: nothing reads this range before the final join)
+            with self.lane(3, self.mark()):
+                self.L.vc_fill(m._n_params - m._n_active, grad.data_ptr() + F32 * m._n_active, 0.0, self.s)
         gb = grad.data_ptr()
         self.G = {n: gb + F32 * o for n, o in m._poff.items()}
         Pp = m.patch
