@@ -12,6 +12,7 @@
 namespace {
 
 constexpr int LN_MAXV = 8;  // C <= 512
+constexpr int NB = 8;       // rows (or partials) per lane whose loads a BatchNorm kernel issues together
 
 __global__ __launch_bounds__(256) void ln_fwd(int R, int C, const float* __restrict__ x, long ldx,
                                               const float* __restrict__ w, const float* __restrict__ b, float eps,
@@ -66,28 +67,50 @@ __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, 
   for (int j = 0; j < LN_MAXV; ++j) pw[j] = pb[j] = 0.f;
   const long rbeg = (long)blockIdx.x * rows_per_block;
   const long rend = min((long)R, rbeg + rows_per_block);
-  for (long r = rbeg + wv; r < rend; r += 4) {
-    const float mu = mean[r], rs = rstd[r];
-    float xh[LN_MAXV], g[LN_MAXV];
-    float sg = 0.f, sgx = 0.f;
+  // two rows (r, r + 4) per iteration: both rows' loads and both pairs of wave sums are independent,
+  // so their latencies overlap; the partial dw / db take row r's terms before row r + 4's, as a
+  // one-row loop would (bit-identical)
+  for (long r = rbeg + wv; r < rend; r += 8) {
+    const bool two = r + 4 < rend;
+    const long r2 = two ? r + 4 : r;
+    const float mu = mean[r], rs = rstd[r], mu2 = mean[r2], rs2 = rstd[r2];
+    float xh[LN_MAXV], g[LN_MAXV], dd[LN_MAXV], xh2[LN_MAXV], g2[LN_MAXV], dd2[LN_MAXV];
+    float sg = 0.f, sgx = 0.f, sg2 = 0.f, sgx2 = 0.f;
 #pragma unroll
     for (int j = 0; j < LN_MAXV; ++j) {
       int c = lane + 64 * j;
-      float d = 0.f, xv = 0.f, wc = 0.f;
+      float d = 0.f, xv = 0.f, wc = 0.f, d2 = 0.f, xv2 = 0.f;
       if (c < C) {
         d = dy[r * lddy + c];
         xv = x[r * ldx + c];
         wc = w[c];
+        d2 = dy[r2 * lddy + c];
+        xv2 = x[r2 * ldx + c];
       }
       xh[j] = (xv - mu) * rs;
       g[j] = d * wc;
+      dd[j] = d;
       sg += g[j];
       sgx += g[j] * xh[j];
-      pw[j] += d * xh[j];
-      pb[j] += d;
+      xh2[j] = (xv2 - mu2) * rs2;
+      g2[j] = d2 * wc;
+      dd2[j] = d2;
+      sg2 += g2[j];
+      sgx2 += g2[j] * xh2[j];
     }
     sg = wave_sum(sg) / C;
     sgx = wave_sum(sgx) / C;
+    sg2 = wave_sum(sg2) / C;
+    sgx2 = wave_sum(sgx2) / C;
+#pragma unroll
+    for (int j = 0; j < LN_MAXV; ++j) {
+      pw[j] += dd[j] * xh[j];
+      pb[j] += dd[j];
+      if (two) {
+        pw[j] += dd2[j] * xh2[j];
+        pb[j] += dd2[j];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < LN_MAXV; ++j) {
       int c = lane + 64 * j;
@@ -95,6 +118,11 @@ __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, 
         float v = rs * (g[j] - sg - xh[j] * sgx);
         float* p = dx + r * lddx + c;
         *p = (res ? res[r * ldr + c] : (beta_dx != 0.f ? *p * beta_dx : 0.f)) + v;
+        if (two) {
+          float v2 = rs2 * (g2[j] - sg2 - xh2[j] * sgx2);
+          float* p2 = dx + r2 * lddx + c;
+          *p2 = (res ? res[r2 * ldr + c] : (beta_dx != 0.f ? *p2 * beta_dx : 0.f)) + v2;
+        }
       }
     }
   }
@@ -153,10 +181,22 @@ __device__ __forceinline__ void bn_part_sums(int P, int C, const double* __restr
   const int c = cx * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
-#pragma unroll 4
-    for (int p = pl; p < P; p += 4) {
-      s1 += part[(long)p * 2 * C + c];
-      s2 += part[(long)p * 2 * C + C + c];
+    // NB partials per lane loaded before they are summed (one round of dependent loads per batch of
+    // NB instead of one per 4); the sums keep the partial order
+    for (int p0 = pl; p0 < P; p0 += 4 * NB) {
+      double a[NB], bq[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int p = p0 + 4 * i;
+        a[i] = p < P ? part[(long)p * 2 * C + c] : 0.0;
+        bq[i] = p < P ? part[(long)p * 2 * C + C + c] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        if (p0 + 4 * i < P) {
+          s1 += a[i];
+          s2 += bq[i];
+        }
     }
   }
   shr[0][pl][cl] = s1;
@@ -224,10 +264,18 @@ __global__ __launch_bounds__(256) void bn_apply_stats(int M, int C, const float*
   const float bc = b[c];
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min((long)M, r0 + rows_per_block);
-  for (long r = r0 + rl; r < r1; r += 4) {
-    float v = bn_fwd_elem(x[r * ldx + c], mf, isf, w[c], bc);
-    if (relu) v = fmaxf(v, 0.f);
-    y[r * ldy + c] = v;
+  const float wc = w[c];
+  for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight
+    float xv[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) xv[i] = rb + 4 * i < r1 ? x[(rb + 4 * i) * ldx + c] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (rb + 4 * i < r1) {
+        float v = bn_fwd_elem(xv[i], mf, isf, wc, bc);
+        if (relu) v = fmaxf(v, 0.f);
+        y[(rb + 4 * i) * ldy + c] = v;
+      }
   }
 }
 
@@ -247,11 +295,17 @@ __global__ __launch_bounds__(256) void bn_stats_sums(int M, int C, const float* 
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const double k = x[c];
-#pragma unroll 4
-    for (long r = r0 + rl; r < r1; r += 4) {
-      const double d = (double)x[r * ldx + c] - k;
-      s1 += d;
-      s2 = fma(d, d, s2);
+    for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight, summed in row order
+      float v[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) v[i] = rb + 4 * i < r1 ? x[(rb + 4 * i) * ldx + c] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        if (rb + 4 * i < r1) {
+          const double d = (double)v[i] - k;
+          s1 += d;
+          s2 = fma(d, d, s2);
+        }
     }
   }
   sh[0][rl][cl] = s1;
@@ -327,12 +381,24 @@ __global__ __launch_bounds__(256) void bn_bwd_sums(int M, int C, const float* __
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const float mu = mean[c], is = invstd[c];
-#pragma unroll 4
-    for (long r = r0 + rl; r < r1; r += 4) {
-      float d = dy[r * lddy + c];
-      if (relu_out && !(relu_out[r * ldo + c] > 0.f)) d = 0.f;
-      s1 += d;
-      s2 += (double)d * ((x[r * ldx + c] - mu) * is);
+    for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight, summed in row order
+      float dv[NB], xv[NB], ov[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const long r = rb + 4 * i;
+        const bool ok = r < r1;
+        dv[i] = ok ? dy[r * lddy + c] : 0.f;
+        xv[i] = ok ? x[r * ldx + c] : 0.f;
+        ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        if (rb + 4 * i < r1) {
+          float d = dv[i];
+          if (relu_out && !(ov[i] > 0.f)) d = 0.f;
+          s1 += d;
+          s2 += (double)d * ((xv[i] - mu) * is);
+        }
     }
   }
   sh[0][rl][cl] = s1;
@@ -380,13 +446,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_sums(int train, int M, int C
   const float invM = 1.f / (float)M;
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min((long)M, r0 + rows_per_block);
-  for (long r = r0 + rl; r < r1; r += 4) {
-    float d = dy[r * lddy + c];
-    if (relu_out && !(relu_out[r * ldo + c] > 0.f)) d = 0.f;
-    float v;
-    if (train) v = bn_bwd_elem(d, x[r * ldx + c], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
-    else v = (wc * is) * d;
-    bn_dx_store(dx + r * lddx + c, beta_dx, v);
+  for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight
+    float dv[NB], xv[NB], ov[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const long r = rb + 4 * i;
+      const bool ok = r < r1;
+      dv[i] = ok ? dy[r * lddy + c] : 0.f;
+      xv[i] = ok && train ? x[r * ldx + c] : 0.f;
+      ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (rb + 4 * i < r1) {
+        float d = dv[i];
+        if (relu_out && !(ov[i] > 0.f)) d = 0.f;
+        float v;
+        if (train) v = bn_bwd_elem(d, xv[i], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
+        else v = (wc * is) * d;
+        bn_dx_store(dx + (rb + 4 * i) * lddx + c, beta_dx, v);
+      }
   }
 }
 
