@@ -25,12 +25,21 @@ __global__ __launch_bounds__(256) void pixel_stats(long M, int C, const float* _
   const float* xr = x + r * ldx;
   float best = -INFINITY, s = 0.f;
   int bi = 0x7fffffff;
-  for (int c = lane; c < C; c += 64) {
-    const float v = xr[c];
-    s += v;
-    if (v > best) {
-      best = v;
-      bi = c;
+  for (int c0 = lane; c0 < C; c0 += 64 * 8) {   // 8 of the lane's channels loaded, then scanned in order
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = c0 + 64 * j < C ? xr[c0 + 64 * j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + 64 * j;
+      if (c < C) {
+        const float v = xv[j];
+        s += v;
+        if (v > best) {
+          best = v;
+          bi = c;
+        }
+      }
     }
   }
 #pragma unroll
@@ -70,18 +79,48 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 
 // the token's 2->1 conv output for pixel i, in fp64: BN(1) normalises values with a tiny spread
 // around a large mean, so the fp32 rounding of the conv would be amplified by 1/std
+__device__ __forceinline__ double tl_fv(float m, float v, float w0, float w1, float bc) {
+  return (double)w0 * m + (double)w1 * v + (double)bc;
+}
 __device__ __forceinline__ double tl_f(const float* __restrict__ mx, const float* __restrict__ avg, long i, float w0,
                                        float w1, float bc) {
-  return (double)w0 * mx[i] + (double)w1 * avg[i] + (double)bc;
+  return tl_fv(mx[i], avg[i], w0, w1, bc);
 }
 
 // the token's BN(1) output for pixel i: forward, backward and vc_tl_relu_mask share this one
 // expression, so they take identical ReLU decisions
+__device__ __forceinline__ float tl_bnv(float m, float v, float w0, float w1, float bc, double mean, double invstd,
+                                        float gam, float bet, double& xh) {
+  xh = (tl_fv(m, v, w0, w1, bc) - mean) * invstd;
+  return (float)xh * gam + bet;
+}
 __device__ __forceinline__ float tl_bn(const float* __restrict__ mx, const float* __restrict__ avg, long i, float w0,
                                        float w1, float bc, double mean, double invstd, float gam, float bet,
                                        double& xh) {
-  xh = (tl_f(mx, avg, i, w0, w1, bc) - mean) * invstd;
-  return (float)xh * gam + bet;
+  return tl_bnv(mx[i], avg[i], w0, w1, bc, mean, invstd, gam, bet, xh);
+}
+
+// A token block's pass over its n elements i = threadIdx.x + TLT * k in increasing k: the (mx, avg)
+// pairs of NBT consecutive k are loaded before any is used (one round of dependent loads per NBT
+// elements instead of one per element), then fn(i, mx[i], avg[i]) runs in the same element order as
+// a plain loop, so every accumulation is bit-identical to it.
+constexpr int NBT = 8;
+template <typename Fn>
+__device__ __forceinline__ void tl_pass(long n, const float* __restrict__ mx, const float* __restrict__ avg, Fn fn) {
+  for (long i0 = threadIdx.x; i0 < n; i0 += (long)TLT * NBT) {
+    float m[NBT], v[NBT];
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) {
+      const long i = i0 + (long)TLT * j;
+      m[j] = i < n ? mx[i] : 0.f;
+      v[j] = i < n ? avg[i] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) {
+      const long i = i0 + (long)TLT * j;
+      if (i < n) fn(i, m[j], v[j]);
+    }
+  }
 }
 
 // one block per token s; a[(b*S + s)*HW + p]
@@ -97,13 +136,13 @@ __global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S
   double mean, invstd;
   if (train) {
     double acc = 0.0;
-    for (long i = threadIdx.x; i < n; i += TLT) acc += tl_f(mx, avg, i, w0, w1, bc);
+    tl_pass(n, mx, avg, [&](long, float m, float v) { acc += tl_fv(m, v, w0, w1, bc); });
     mean = block_sum(acc, red) / (double)n;
     double q = 0.0;
-    for (long i = threadIdx.x; i < n; i += TLT) {
-      const double d = tl_f(mx, avg, i, w0, w1, bc) - mean;
+    tl_pass(n, mx, avg, [&](long, float m, float v) {
+      const double d = tl_fv(m, v, w0, w1, bc) - mean;
       q += d * d;
-    }
+    });
     const double m2 = block_sum(q, red);
     const double var = m2 / (double)n;
     invstd = 1.0 / sqrt(var + (double)eps);
@@ -122,12 +161,12 @@ __global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S
     stats[2 * s] = mean;
     stats[2 * s + 1] = invstd;
   }
-  for (long i = threadIdx.x; i < n; i += TLT) {
+  tl_pass(n, mx, avg, [&](long i, float m, float v) {
     double xh;
-    const float bn = tl_bn(mx, avg, i, w0, w1, bc, mean, invstd, gam, bet, xh);
+    const float bn = tl_bnv(m, v, w0, w1, bc, mean, invstd, gam, bet, xh);
     const long b = i / HW, q = i % HW;
     a[((long)b * S + s) * HW + q] = sigmoid_f(fmaxf(bn, 0.f));
-  }
+  });
 }
 
 // one block per token: da -> df[s][i] (grad of the 2->1 conv output) + the token's 5 param grads
@@ -141,37 +180,56 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S
   const float w0 = p[0], w1 = p[1], bc = p[2], gam = p[3], bet = p[4];
   const double mean = stats[2 * s], invstd = stats[2 * s + 1];
   const long n = (long)B * HW;
+  // da[b, s, q] of element i = b * HW + q, loaded with the element's (mx, avg) (same batching and
+  // element order as tl_pass)
+  auto pass = [&](auto fn) {
+    for (long i0 = threadIdx.x; i0 < n; i0 += (long)TLT * NBT) {
+      float m[NBT], v[NBT], g[NBT];
+#pragma unroll
+      for (int j = 0; j < NBT; ++j) {
+        const long i = i0 + (long)TLT * j;
+        const bool ok = i < n;
+        const long b = ok ? i / HW : 0, q = ok ? i % HW : 0;
+        m[j] = ok ? mx[i] : 0.f;
+        v[j] = ok ? avg[i] : 0.f;
+        g[j] = ok ? da[((long)b * S + s) * HW + q] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < NBT; ++j) {
+        const long i = i0 + (long)TLT * j;
+        if (i < n) fn(i, m[j], v[j], g[j]);
+      }
+    }
+  };
   double s1 = 0.0, s2 = 0.0;
-  for (long i = threadIdx.x; i < n; i += TLT) {
+  pass([&](long, float m, float v, float dav) {
     double xh;
-    const float bn = tl_bn(mx, avg, i, w0, w1, bc, mean, invstd, gam, bet, xh);
-    const long b = i / HW, q = i % HW;
+    const float bn = tl_bnv(m, v, w0, w1, bc, mean, invstd, gam, bet, xh);
     float g1 = 0.f;
     if (bn > 0.f) {
       const float sg = sigmoid_f(bn);
-      g1 = da[((long)b * S + s) * HW + q] * sg * (1.f - sg);
+      g1 = dav * sg * (1.f - sg);
     }
     s1 += g1;
     s2 += g1 * xh;
-  }
+  });
   s1 = block_sum(s1, red);
   s2 = block_sum(s2, red);
   double gw0 = 0.0, gw1 = 0.0, gb = 0.0;
-  for (long i = threadIdx.x; i < n; i += TLT) {
+  pass([&](long i, float m, float v, float dav) {
     double xh;
-    const float bn = tl_bn(mx, avg, i, w0, w1, bc, mean, invstd, gam, bet, xh);
-    const long b = i / HW, q = i % HW;
+    const float bn = tl_bnv(m, v, w0, w1, bc, mean, invstd, gam, bet, xh);
     float g1 = 0.f;
     if (bn > 0.f) {
       const float sg = sigmoid_f(bn);
-      g1 = da[((long)b * S + s) * HW + q] * sg * (1.f - sg);
+      g1 = dav * sg * (1.f - sg);
     }
     const double d = train ? gam * invstd * (g1 - s1 / (double)n - xh * s2 / (double)n) : gam * invstd * g1;
     df[(long)s * n + i] = (float)d;
-    gw0 += d * mx[i];
-    gw1 += d * avg[i];
+    gw0 += d * m;
+    gw1 += d * v;
     gb += d;
-  }
+  });
   gw0 = block_sum(gw0, red);
   gw1 = block_sum(gw1, red);
   gb = block_sum(gb, red);
