@@ -23,18 +23,47 @@ __global__ __launch_bounds__(512) void gate_fwd(int N, int C, const float* __res
   float* msk = sh + 2 * N;
   const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* xb = x + (long)b * N * C;
-  for (int r = wave; r < N; r += 8) {
-    float s = 0.f, m = -INFINITY;
-    for (int c = lane; c < C; c += 64) {
-      const float v = xb[(long)r * C + c];
-      s += v;
-      m = fmaxf(m, v);
+  // GR rows per wave at a time (rows r, r + 8, ...): their loads are in flight together and their
+  // reductions interleave; each row's sum / max keep the one-row order (bit-identical)
+  constexpr int GR = 4, CV = 4;   // CV: a lane's channels per row held in registers (C <= 256)
+  for (int r0 = wave; r0 < N; r0 += 8 * GR) {
+    float v[GR][CV];
+#pragma unroll
+    for (int g = 0; g < GR; ++g)
+#pragma unroll
+      for (int j = 0; j < CV; ++j) {
+        const int r = r0 + 8 * g, c = lane + 64 * j;
+        v[g][j] = (r < N && c < C) ? xb[(long)r * C + c] : 0.f;
+      }
+    float s[GR], m[GR];
+#pragma unroll
+    for (int g = 0; g < GR; ++g) {
+      s[g] = 0.f;
+      m[g] = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < CV; ++j)
+        if (lane + 64 * j < C) {
+          s[g] += v[g][j];
+          m[g] = fmaxf(m[g], v[g][j]);
+        }
+      for (int c = lane + 64 * CV; c < C; c += 64) {   // channels beyond 64 * CV (not at config 5)
+        const float vv = r0 + 8 * g < N ? xb[(long)(r0 + 8 * g) * C + c] : 0.f;
+        s[g] += vv;
+        m[g] = fmaxf(m[g], vv);
+      }
     }
-    s = wave_sum(s);
-    m = wave_max(m);
+#pragma unroll
+    for (int g = 0; g < GR; ++g) {
+      s[g] = wave_sum(s[g]);
+      m[g] = wave_max(m[g]);
+    }
     if (lane == 0) {
-      avg[r] = s / (float)C;
-      mx[r] = m;
+#pragma unroll
+      for (int g = 0; g < GR; ++g)
+        if (r0 + 8 * g < N) {
+          avg[r0 + 8 * g] = s[g] / (float)C;
+          mx[r0 + 8 * g] = m[g];
+        }
     }
   }
   __syncthreads();
