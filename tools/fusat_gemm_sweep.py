@@ -14,7 +14,9 @@ from vitcnn_amd._lib import lib  # noqa: E402
 from vitcnn_amd.fusatnet import FusAtNet  # noqa: E402
 from vitcnn_amd.losses import CrossEntropyLoss  # noqa: E402
 
-CONFIGS = [(0, 0), (64, 64), (128, 64), (64, 128), (128, 128)]
+CONFIGS = [(0, 0, 0), (64, 64, 0), (128, 64, 0), (64, 128, 0), (128, 128, 0)]
+if os.environ.get("SWEEP_NSPLIT"):   # (bm, bn) automatic, forced split-K counts instead of tiles
+    CONFIGS = [(0, 0, 0)] + [(0, 0, int(v)) for v in os.environ["SWEEP_NSPLIT"].split(",")]
 
 
 def main():
@@ -45,7 +47,7 @@ def main():
         shapes.setdefault(key, []).append(a)
 
     def time_call(a, cfg):
-        L.vc_gemm_tune(cfg[0], cfg[1], 0, 0, -1)
+        L.vc_gemm_tune(cfg[0], cfg[1], cfg[2], 0, -1)
         args = list(a[:-1]) + [st.cuda_stream]
         for _ in range(2):
             raw(*args)
@@ -60,8 +62,8 @@ def main():
 
     tot = [0.0] * len(CONFIGS)
     best = 0.0
-    print(f"{len(calls)} GEMM calls, {len(shapes)} shapes; times in us per call; configs (bm,bn) {CONFIGS}")
-    print("  tA tB      M      N      K batch count  " + "  ".join(f"{c[0]:>3d}x{c[1]:<3d}" for c in CONFIGS) +
+    print(f"{len(calls)} GEMM calls, {len(shapes)} shapes; times in us per call; configs (bm,bn,nsplit) {CONFIGS}")
+    print("  tA tB      M      N      K batch count  " + "  ".join(f"{c[0]:>3d}x{c[1]:<3d}/{c[2]:<2d}" for c in CONFIGS) +
           "   TF(auto)")
     for key, lst in shapes.items():
         ts = [time_call(lst[0], c) for c in CONFIGS]
@@ -72,7 +74,7 @@ def main():
         ta, tb, M, N, K, batch = key
         print(f"  {ta:2d} {tb:2d} {M:6d} {N:6d} {K:6d} {batch:5d} {n:5d}  " + "  ".join(f"{v:7.1f}" for v in ts) +
               f"   {2.0 * M * N * K * batch / ts[0] * 1e-6:7.1f}", flush=True)
-    print("summed over the step (us): " + "  ".join(f"{c[0]}x{c[1]}: {v:.0f}" for c, v in zip(CONFIGS, tot)) +
+    print("summed over the step (us): " + "  ".join(f"{c[0]}x{c[1]}/{c[2]}: {v:.0f}" for c, v in zip(CONFIGS, tot)) +
           f"  best-of: {best:.0f}")
 
 
