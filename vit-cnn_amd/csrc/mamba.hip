@@ -533,6 +533,10 @@ __global__ void gate_bwd(int total, FastDiv fD, const float* __restrict__ xz, co
   dxz[(long)r * 2 * D + D + d] = g * ypsum[idx] * sg * (1.f + z * (1.f - sg));
 }
 
+// YP[b, l, :] = sum_k softmax(gate)_k y[k, b, inv_k(l), :], ysum = YP * SiLU(z).  The ndir (<= MAXK)
+// order-table entries are read first and the gathered rows after them (one round of dependent loads
+// instead of ndir), then summed in direction order.
+template <int MAXK>
 __global__ void combine_fwd(int total, FastDiv fD, FastDiv fL, int B, int ndir, const int* __restrict__ inv,
                             const float* __restrict__ logits, const float* __restrict__ y,
                             const float* __restrict__ xz, float* __restrict__ ypsum, float* __restrict__ out) {
@@ -548,9 +552,20 @@ __global__ void combine_fwd(int total, FastDiv fD, FastDiv fL, int B, int ndir, 
   for (int i = 0; i < ndir; ++i) den += __expf(logits[i] - mx);
   const float rden = 1.f / den;
   float acc = 0.f;
-  for (int kk = 0; kk < ndir; ++kk) {
-    const float gk = __expf(logits[kk] - mx) * rden;
-    acc += gk * y[((long)(kk * B + b) * L + inv[kk * L + l]) * D + d];
+  for (int k0 = 0; k0 < ndir; k0 += MAXK) {
+    int tk[MAXK];
+#pragma unroll
+    for (int kk = 0; kk < MAXK; ++kk) tk[kk] = k0 + kk < ndir ? inv[(k0 + kk) * L + l] : 0;
+    float yv[MAXK];
+#pragma unroll
+    for (int kk = 0; kk < MAXK; ++kk)
+      yv[kk] = k0 + kk < ndir ? y[((long)((k0 + kk) * B + b) * L + tk[kk]) * D + d] : 0.f;
+#pragma unroll
+    for (int kk = 0; kk < MAXK; ++kk)
+      if (k0 + kk < ndir) {
+        const float gk = __expf(logits[k0 + kk] - mx) * rden;
+        acc += gk * yv[kk];
+      }
   }
   ypsum[idx] = acc;
   out[idx] = acc * silu_f(xz[(long)bl * 2 * D + D + d]);
@@ -733,8 +748,12 @@ VC_API int vc_mamba_combine_fwd(int B, int L, int D, int ndir, const int* inv_or
   long total = (long)B * L * D;
   if (total == 0) return VC_OK;
   VC_REQUIRE_I32((long)ndir * total);
-  hipLaunchKernelGGL(combine_fwd, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(D),
-                     make_fastdiv(L), B, ndir, inv_order, gate_logits, y, xz, ypsum, ysum);
+  if (ndir <= 10)   // the model's 10 scan orders
+    hipLaunchKernelGGL(combine_fwd<10>, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total,
+                       make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, gate_logits, y, xz, ypsum, ysum);
+  else
+    hipLaunchKernelGGL(combine_fwd<4>, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total,
+                       make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, gate_logits, y, xz, ypsum, ysum);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
