@@ -124,7 +124,7 @@ __device__ __forceinline__ void tl_pass(long n, const float* __restrict__ mx, co
 }
 
 // one block per token s; a[(b*S + s)*HW + p]
-__global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S, const float* __restrict__ mx,
+__global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, FastDiv fHW, int S, const float* __restrict__ mx,
                                                 const float* __restrict__ avg, const float* __restrict__ par,
                                                 float* __restrict__ buf, float eps, float momentum,
                                                 double* __restrict__ stats, float* __restrict__ a) {
@@ -164,13 +164,14 @@ __global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, int S
   tl_pass(n, mx, avg, [&](long i, float m, float v) {
     double xh;
     const float bn = tl_bnv(m, v, w0, w1, bc, mean, invstd, gam, bet, xh);
-    const long b = i / HW, q = i % HW;
+    int q;
+    const long b = fdivmod((int)i, fHW, q);   // n = B * HW < 2^31 (launcher): 32-bit magic division
     a[((long)b * S + s) * HW + q] = sigmoid_f(fmaxf(bn, 0.f));
   });
 }
 
 // one block per token: da -> df[s][i] (grad of the 2->1 conv output) + the token's 5 param grads
-__global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S, const float* __restrict__ mx,
+__global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, FastDiv fHW, int S, const float* __restrict__ mx,
                                                 const float* __restrict__ avg, const float* __restrict__ par,
                                                 const double* __restrict__ stats, const float* __restrict__ da,
                                                 float* __restrict__ df, float* __restrict__ gpar) {
@@ -189,7 +190,8 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S
       for (int j = 0; j < NBT; ++j) {
         const long i = i0 + (long)TLT * j;
         const bool ok = i < n;
-        const long b = ok ? i / HW : 0, q = ok ? i % HW : 0;
+        int q = 0;
+        const long b = ok ? fdivmod((int)i, fHW, q) : 0;
         m[j] = ok ? mx[i] : 0.f;
         v[j] = ok ? avg[i] : 0.f;
         g[j] = ok ? da[((long)b * S + s) * HW + q] : 0.f;
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, int S
 }
 
 // mask[(b*S + s)*HW + q] = (BN(1) output > 0): the ReLU decisions attn_fwd / attn_bwd took
-__global__ __launch_bounds__(256) void attn_mask(int B, int HW, int S, const float* __restrict__ mx,
+__global__ __launch_bounds__(256) void attn_mask(int B, int HW, FastDiv fHW, int S, const float* __restrict__ mx,
                                                  const float* __restrict__ avg, const float* __restrict__ par,
                                                  const double* __restrict__ stats, unsigned char* __restrict__ mask) {
   const int s = blockIdx.y;
@@ -253,7 +255,9 @@ __global__ __launch_bounds__(256) void attn_mask(int B, int HW, int S, const flo
   const float* p = par + (long)s * TPAR;
   double xh;
   const float bn = tl_bn(mx, avg, i, p[0], p[1], p[2], stats[2 * s], stats[2 * s + 1], p[3], p[4], xh);
-  mask[((i / HW) * S + s) * HW + i % HW] = bn > 0.f ? 1 : 0;
+  int q;
+  const long bq = fdivmod((int)i, fHW, q);
+  mask[(bq * S + s) * HW + q] = bn > 0.f ? 1 : 0;
 }
 
 // dx[i, c] += davg/C + (c == argmax ? dmx : 0),  dmx / davg summed over the S tokens
@@ -290,7 +294,8 @@ VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx,
 VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
                           float* bn_buffers, float eps, float momentum, double* stats, float* a, hipStream_t stream) {
   VC_REQUIRE(B > 0 && HW > 0 && S > 0);
-  hipLaunchKernelGGL(attn_fwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, S, mx, avg, params, bn_buffers, eps,
+  VC_REQUIRE_I32((long)B * HW);
+  hipLaunchKernelGGL(attn_fwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, make_fastdiv(HW), S, mx, avg, params, bn_buffers, eps,
                      momentum, stats, a);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -299,7 +304,8 @@ VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, cons
 VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
                           const double* stats, const float* da, float* df, float* dparams, hipStream_t stream) {
   VC_REQUIRE(B > 0 && HW > 0 && S > 0);
-  hipLaunchKernelGGL(attn_bwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, S, mx, avg, params, stats, da, df,
+  VC_REQUIRE_I32((long)B * HW);
+  hipLaunchKernelGGL(attn_bwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, make_fastdiv(HW), S, mx, avg, params, stats, da, df,
                      dparams);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -308,7 +314,8 @@ VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, cons
 VC_API int vc_tl_relu_mask(int B, int HW, int S, const float* mx, const float* avg, const float* params,
                            const double* stats, unsigned char* mask, hipStream_t stream) {
   VC_REQUIRE(B > 0 && HW > 0 && S > 0);
-  hipLaunchKernelGGL(attn_mask, dim3(vc_cdiv((long)B * HW, 256), S), dim3(256), 0, stream, B, HW, S, mx, avg, params,
+  VC_REQUIRE_I32((long)B * HW);
+  hipLaunchKernelGGL(attn_mask, dim3(vc_cdiv((long)B * HW, 256), S), dim3(256), 0, stream, B, HW, make_fastdiv(HW), S, mx, avg, params,
                      stats, mask);
   VC_CHECK_LAUNCH();
   return VC_OK;
