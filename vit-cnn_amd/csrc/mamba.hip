@@ -222,7 +222,6 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
 #pragma unroll
   for (int j = 0; j < NQ; ++j) A2[j] = valid ? -__expf(a.alog[dc * NST + NQ * q + j]) * LOG2E : 0.f;
   const float Dd = valid ? a.dskip[dc] : 0.f;
-  stage_seq<RT>(a, s, m, Lp, Dp);
   // buffer resources over this sequence's rows (as in scan_bwd): padding tokens / channels and null
   // outputs (a zero-sized resource) fall out of range -- loads give 0, stores are dropped
   const unsigned seq_bytes = (unsigned)(a.L * a.D * 4);
@@ -235,6 +234,7 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
   float un[SCK];
 #pragma unroll
   for (int i = 0; i < SCK; ++i) un[i] = buf_ld(r_u, (unsigned)(i * a.D * 4) + lane_b);
+  stage_seq<RT>(a, s, m, Lp, Dp);   // the first segment's u loads are in flight meanwhile
   for (int c = 0; c < nseg; ++c) {
     const int t0 = c * SCK;
 #pragma unroll
@@ -365,7 +365,6 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
 #pragma unroll
   for (int j = 0; j < NQ; ++j) A2[j] = valid ? -__expf(a.alog[dc * NST + NQ * q + j]) * LOG2E : 0.f;
   const float Dd = valid ? a.dskip[dc] : 0.f;
-  stage_seq<RT>(a, s, m, Lp, Dp);
   const long base = (long)s * a.L;
   // the dB/dC column this lane's reduce-scatter total belongs to
   const int vi = cl >> 1;
@@ -404,7 +403,8 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
     }
   };
   __syncthreads();   // ord
-  load_seg(nseg - 1);
+  load_seg(nseg - 1);   // the last segment's operands are in flight while the sequence is staged
+  stage_seq<RT>(a, s, m, Lp, Dp);
   for (int c = nseg - 1; c >= 0; --c) {
     const int t0 = c * SCK;
     f2 hs[SCK + 1][2];   // hs[i] = state entering token t0 + i
