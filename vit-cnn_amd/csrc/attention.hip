@@ -149,8 +149,7 @@ __device__ __forceinline__ f32x4 ld4_or0(const float* base, long ld, bool row_ok
 }
 // cross-row max / sum over the 4 lane groups (lanes c, c+16, c+32, c+48)
 __device__ __forceinline__ float xrow_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
+  return cross_row_max(v);
 }
 
 constexpr int NLW = 4;   // waves (16-query tiles) per forward block

@@ -142,6 +142,17 @@ __device__ __forceinline__ float row_scatter4(float v0, float v1, float v2, floa
   return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
+// max over the 4 rows of a wave for every column (lane & 15), all lanes get it: the permlane16 /
+// permlane32 half swaps of cross_row_sum with fmaxf (exact, so identical to the __shfl_xor form)
+__device__ __forceinline__ float cross_row_max(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = fmaxf(__builtin_bit_cast(float, (unsigned)p[0]), __builtin_bit_cast(float, (unsigned)p[1]));
+  const unsigned w = __builtin_bit_cast(unsigned, v);
+  const auto q = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)q[0]), __builtin_bit_cast(float, (unsigned)q[1]));
+}
+
 // a[r] for the lane's row r = lane >> 4 (register selects, no memory)
 __device__ __forceinline__ float row_select4(const float (&a)[4], int r) {
   return r == 0 ? a[0] : (r == 1 ? a[1] : (r == 2 ? a[2] : a[3]));

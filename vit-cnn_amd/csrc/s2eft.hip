@@ -155,8 +155,7 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
       sv[r] = (k0 + 4 * g + r < T) ? st[r] * scale2 : -INFINITY;
       tm = fmaxf(tm, sv[r]);
     }
-    tm = fmaxf(tm, __shfl_xor(tm, 16, 64));
-    tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+    tm = cross_row_max(tm);
     const float mn = fmaxf(m, tm);
     const float corr = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
     m = mn;
@@ -174,8 +173,7 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
       o = __builtin_amdgcn_mfma_f32_16x16x4f32(Vf[kk * 16 + c], pv[s2], o, 0, 0, 0);
     }
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = cross_row_sum(l);   // same order as the xor-16 then xor-32 shuffles
   if (q0 + c >= T) return;
   const float rl = 1.0f / l;
   *(f32x4*)(out + ((long)b * T + q0 + c) * ldo + h * 16 + g * 4) = o * rl;
