@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the bucketed RCCL exchange even at N = 1 (world-1 process group)")
     ap.add_argument("--no-f1", action="store_true")
+    ap.add_argument("--no-train-loop", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
 
@@ -105,20 +106,35 @@ def _traffic_from_profile(kernel_key):
     return None if k is None else k.get("hbm_bytes_per_launch")
 
 
+_SCENE = {}
+
+
+def synthetic_scene(seed, labelled_frac=1.0):
+    """A Houston2013-size synthetic scene (349 x 1905 pixels, 144 HSI + 1 LiDAR bands, U[0,1) like the
+    reference's per-band min-max normalisation, datasets.py:125-133) and a ground-truth map with
+    classes 1..15 on `labelled_frac` of the pixels (0 = unlabelled elsewhere); generated once per seed."""
+    key = (seed, labelled_frac)
+    if key not in _SCENE:
+        rng = np.random.default_rng(seed)
+        W, H = 349, 1905
+        img1 = rng.random((W, H, 144), dtype=np.float32)
+        img2 = rng.random((W, H, 1), dtype=np.float32)
+        gt = rng.integers(1, 16, size=(W, H))
+        if labelled_frac < 1.0:
+            gt[rng.random((W, H)) >= labelled_frac] = 0
+        _SCENE[key] = (img1, img2, gt)
+    return _SCENE[key]
+
+
 def batch_assembly_ms(step, hsi, lidar, target, dev, steps, seed):
     """ms per training step when every batch is assembled on the device (vitcnn_amd.window.PatchBatcher:
     vc_patch_gather of B windows + flip / rot90 codes, datasets.py:511-593) from a synthetic
     HBM-resident 349 x 1905 cube with a uniform ground-truth map, then copied into the captured
     step's input buffers."""
     from vitcnn_amd.window import PatchBatcher
-    rng = np.random.default_rng(seed)
-    W, H = 349, 1905
-    img1 = rng.random((W, H, hsi.shape[1]), dtype=np.float32)
-    img2 = rng.random((W, H, lidar.shape[1]), dtype=np.float32)
-    gt = rng.integers(0, 16, size=(W, H))
+    img1, img2, gt = synthetic_scene(seed)
     batcher = PatchBatcher(img1, img2, gt, hsi.shape[-1], ignored_labels=(0,), batch_size=hsi.shape[0],
                            flip_augmentation=True, device=dev, seed=seed)
-    del img1, img2
     it = iter(batcher)
 
     def asm_step():
@@ -136,6 +152,56 @@ def batch_assembly_ms(step, hsi, lidar, target, dev, steps, seed):
         asm_step()
     torch.cuda.synchronize(dev)
     return (time.perf_counter() - t0) / steps * 1e3
+
+
+def train_loop_leg(dev, epochs, seed, headline_ms):
+    """the rate the reference's main.py sees through the plugin surface --
+    `vitcnn_amd.model_utils.train` (model_utils.py:854-1045) with the model, AdamW, weighted CE and
+    StepLR of `get_model("Multimodality_Mamba")`, over a `PatchBatcher` loader (MultiModalX batches of
+    64 gathered on the device from the HBM-resident synthetic scene, 2 % of its pixels labelled:
+    ~13.3k patches = 208 batches per epoch, the last one short), `epochs` epochs, display every 100
+    iterations, best / final checkpoints written (into a temporary directory).  Reported: the whole
+    call (first batch of each shape eager, graph captures, checkpoints) and the steady state (epochs
+    after the first), against the headline step."""
+    import shutil
+    import tempfile
+    from vitcnn_amd import model_utils as mu
+    from vitcnn_amd.window import PatchBatcher
+    img1, img2, gt = synthetic_scene(seed, labelled_frac=0.02)
+    torch.manual_seed(0)
+    net, opt, crit, kw = mu.get_model("Multimodality_Mamba", n_classes=16, n_bands=(144, 1), ignored_labels=[0],
+                                      dataset="synthetic", device=dev)
+    loader = PatchBatcher(img1, img2, gt, 9, ignored_labels=(0,), batch_size=kw["batch_size"],
+                          flip_augmentation=kw["flip_augmentation"], device=dev, seed=seed)
+    cwd = os.getcwd()
+    tmp = tempfile.mkdtemp(prefix="vitcnn_train_leg_")
+    try:
+        os.chdir(tmp)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        mu.train("bench", 0, None, net, opt, crit, loader, epochs, scheduler=kw["scheduler"], display_iter=100,
+                 device=dev)
+        torch.cuda.synchronize(dev)
+        total = time.perf_counter() - t0
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp, ignore_errors=True)
+    st = mu.train.last_stats
+    ep = st["epochs"]
+    patches = sum(e["patches"] for e in ep)
+    steady = ep[1:] if len(ep) > 1 else ep
+    sp, ss = sum(e["patches"] for e in steady), sum(e["seconds"] for e in steady)
+    steady_v = sp / ss
+    ms_step = ss / sum(e["batches"] for e in steady) * 1e3
+    return {"workload": "model_utils.train(): get_model('Multimodality_Mamba') defaults (AdamW 8e-4, weighted CE, "
+                        "StepLR), PatchBatcher loader over the synthetic 349x1905 scene (2 % labelled), B=64, "
+                        f"{epochs} epochs, display every 100 iterations, checkpoints written",
+            "launch": st["launch"], "value": round(steady_v, 1), "unit": "patches/s",
+            "ms_per_batch_steady": round(ms_step, 4), "steady_epochs": len(steady),
+            "value_whole_call": round(patches / total, 1), "seconds_whole_call": round(total, 3),
+            "batches_per_epoch": ep[0]["batches"], "patches_per_epoch": ep[0]["patches"],
+            "vs_headline_step": round(headline_ms / ms_step, 4),
+            "final_loss": round(float(st["losses"][-1]), 6)}
 
 
 def dominant_kernel_roofline(model, batch, reps):
@@ -347,9 +413,7 @@ def s2eft_leg(dev, steps, cpu_steps):
     except RuntimeError as e:  # reported in the line, never silent
         launch = f"eager (graph capture failed: {str(e)[:80]})"
         step = eager_step
-    for _ in range(3):
-        step()
-    torch.cuda.synchronize(dev)
+    warm(step, dev, WARM_S)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -358,11 +422,12 @@ def s2eft_leg(dev, steps, cpu_steps):
     out = {"workload": "S2EFT (CAF, depth 5, 4 heads x 16, dim 64) train step, x [64,145,147], 16 classes",
            "value": round(64 / ms * 1e3, 1), "unit": "patches/s", "ms_per_step": round(ms, 4), "dtype": "fp32",
            "launch": launch}
-    if cpu_steps > 0:
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+
+    def cpu_leg():   # run after every GPU leg
         from oracle import s2eft_oracle as O
         threads = cpu_threads()
         torch.set_num_threads(threads)
-        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         O.train_step(sd, x, t, w)
         t0 = time.perf_counter()
         for _ in range(cpu_steps):
@@ -370,7 +435,7 @@ def s2eft_leg(dev, steps, cpu_steps):
         dt = (time.perf_counter() - t0) / cpu_steps
         out["cpu_baseline"] = {"value": round(64 / dt, 2), "unit": "patches/s", "cores": threads, "kind": "port",
                                "sample": f"{cpu_steps} B=64 fwd+bwd steps of oracle/s2eft_oracle.py"}
-    return out
+    return out, (cpu_leg if cpu_steps > 0 else None)
 
 
 def muufl_leg(dev, steps):
@@ -401,9 +466,7 @@ def muufl_leg(dev, steps):
     with torch.cuda.graph(graph):
         fused_train_step(m, crit, hsi, lidar, tgt)
         opt.step()
-    for _ in range(3):
-        graph.replay()
-    torch.cuda.synchronize(dev)
+    warm(graph.replay, dev, WARM_S)
     t0 = time.perf_counter()
     for _ in range(steps):
         graph.replay()
@@ -470,9 +533,7 @@ def fusat_leg(dev, steps, cpu):
         launch = f"eager (graph capture failed: {str(e)[:80]})"
         torch.cuda.synchronize(dev)
         step = eager_step
-    for _ in range(2):
-        step()
-    torch.cuda.synchronize(dev)
+    warm(step, dev, WARM_S)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -486,13 +547,14 @@ def fusat_leg(dev, steps, cpu):
            "forward": {"value": round(64 / ms_fwd * 1e3, 1), "unit": "patches/s (train-mode forward)",
                        "ms_per_batch": round(ms_fwd, 3), "achieved_tflops": round(tf_fwd, 2),
                        "mfma_frac": round(tf_fwd / PEAK_FP32_MFMA_TFLOPS, 4)}}
-    if cpu:
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    tc, wc = tgt[:4].cpu(), w.cpu()
+
+    def cpu_leg():   # run after every GPU leg
         from oracle import fusat_oracle as O
         threads = cpu_threads()
         torch.set_num_threads(threads)
-        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         params = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
-        tc, wc = tgt[:4].cpu(), w.cpu()
 
         def cpu_step():
             for v in params.values():
@@ -503,7 +565,7 @@ def fusat_leg(dev, steps, cpu):
         out["cpu_baseline"] = {"value": round(4 / med, 2), "unit": "patches/s", "cores": threads, "kind": "port",
                                "sample": "median of 3 B=4 training steps (forward + autograd backward) of "
                                          "oracle/fusat_oracle.py after 1 warm-up"}
-    return out
+    return out, (cpu_leg if cpu else None)
 
 
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (not the 2:1-sparsity figure)
@@ -564,11 +626,32 @@ def build_step(dev, precision, world, rank, batch, exchange, warmup, use_graph):
     return step, model, (hsi, lidar, target), holder, launch
 
 
-def time_steps(step, dev, steps, world):
-    """K steps bracketed by barrier + synchronize on both sides; max over ranks."""
-    for _ in range(3):
+WARM_S = 0.4   # untimed replays before every timed leg
+
+
+def warm(step, dev, seconds, world=1):
+    """Untimed replays for at least `seconds`, so no timed leg starts cold (GPU clocks, caches, the
+    allocator) whatever ran before it.  The count is fixed from a 5-step probe and agreed over the
+    ranks (max), since the replayed step may hold collectives every rank must issue equally often."""
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(5):
         step()
     torch.cuda.synchronize(dev)
+    per = max((time.perf_counter() - t0) / 5, 1e-5)
+    n = torch.tensor([int(seconds / per) + 1], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(n, op=dist.ReduceOp.MAX)
+    for _ in range(int(n.item())):
+        step()
+    torch.cuda.synchronize(dev)
+    return 5 + int(n.item())
+
+
+def time_steps(step, dev, steps, world, warm_s=WARM_S):
+    """K steps bracketed by barrier + synchronize on both sides; max over ranks.  Preceded by
+    `warm_s` seconds of untimed replays."""
+    warm(step, dev, warm_s, world)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -635,7 +718,7 @@ def precision_leg(dev, precision, steps, warmup, reps):
     return out
 
 
-def f1_leg(dev, cpu):
+def f1_leg(dev, seed, cpu):
     """Row F1: whole-image inference, model_utils.test (model_utils.py:1067-1132)
     over a Houston2013-size synthetic scene (349 x 1905, 144 + 1 bands, 9x9 windows, stride 1:
     646,877 windows), eval-mode BatchNorm (running statistics), device-side window gather and fp64
@@ -645,13 +728,11 @@ def f1_leg(dev, cpu):
     from vitcnn_amd.window import SlidingWindowInference
     torch.manual_seed(0)
     m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16).to(dev)
-    rng = np.random.default_rng(5)
-    img1 = rng.random((349, 1905, 144), dtype=np.float32)
-    img2 = rng.random((349, 1905, 1), dtype=np.float32)
+    img1, img2, _ = synthetic_scene(seed)
     # warm-up on a small crop builds the eval workspaces of the batch sizes the full run uses
-    SlidingWindowInference(m, img1[:80, :80], img2[:80, :80], 9, 1, 16, dev).run(batch_size=64)
+    for _ in range(3):
+        SlidingWindowInference(m, img1[:80, :80], img2[:80, :80], 9, 1, 16, dev).run(batch_size=64)
     runner = SlidingWindowInference(m, img1, img2, 9, 1, 16, dev)
-    del img1, img2
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     probs = runner.run(batch_size=64)
@@ -660,18 +741,20 @@ def f1_leg(dev, cpu):
                        "forward, fp64 centre accumulation (incl. the probability map's copy to the host)",
            "windows": runner.n, "value": round(runner.n / el, 1), "unit": "windows/s", "seconds": round(el, 3),
            "dtype": "fp32", "probs_finite": bool(np.isfinite(probs).all())}
-    if cpu:
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+
+    def cpu_leg():   # run after every GPU leg
         from oracle import vitcnn_oracle as O
         threads = cpu_threads()
         torch.set_num_threads(threads)
-        st = O.make_state(m.cpu().state_dict(), requires_grad=False)
+        st = O.make_state(sd, requires_grad=False)
         x1, x2, _ = synthetic(64, 77, "cpu")
         P = O.Params(st, training=False)
         with torch.no_grad():
             med, _ = timed_median(lambda: O.forward(P, x1, x2), 2, 3)
         out["cpu_baseline"] = {"value": round(64 / med, 2), "unit": "windows/s", "cores": threads, "kind": "port",
                                "sample": "median of 3 eval-mode B=64 forwards of oracle/vitcnn_oracle.py after 2 warm-up"}
-    return out
+    return out, (cpu_leg if cpu else None)
 
 
 def main():
@@ -697,6 +780,7 @@ def main():
     loss_val = float(holder["loss"].item())
 
     # reference-loop variant: loss.item() host sync every step (model_utils.py:936)
+    warm(step, dev, WARM_S / 2, world)
     t1 = time.perf_counter()
     nsync = min(args.steps, 50)
     for _ in range(nsync):
@@ -729,6 +813,7 @@ def main():
                                          "RCCL all-reduce of 3 head-first buckets on a side stream, overlapped "
                                          "with the backward; 1/world folded into AdamW")},
         "ms_per_step_with_loss_item": round(ms_sync, 4),
+        "value_with_loss_item": round(world * args.batch / ms_sync * 1e3, 1),
         "ms_per_step_with_batch_assembly": round(ms_asm, 4),
         "value_with_batch_assembly": round(world * args.batch / ms_asm * 1e3, 1),
         "final_loss": round(loss_val, 6),
@@ -736,23 +821,34 @@ def main():
         "roofline": roof,
         "roofline_gemm": roof_gemm,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log(f"CPU baseline: {args.cpu_warmup} + {args.cpu_steps} oracle steps on {cpu_threads()} threads")
-        out["cpu_baseline"] = cpu_baseline(args.cpu_warmup, args.cpu_steps)
+    cpu_legs = []
     if world == 1 and not args.no_s2eft:
         other = "bf16" if args.precision == "fp32" else "fp32"
         log(f"{other} leg")
         out["config2_bf16" if other == "bf16" else "parity_fp32"] = precision_leg(
             dev, other, min(args.steps, 50), args.warmup, args.kernel_reps)
         log("config 5: S2EFT leg")
-        out["config5_s2eft"] = s2eft_leg(dev, min(args.steps, 50), 0 if args.no_cpu_baseline else 5)
+        out["config5_s2eft"], c = s2eft_leg(dev, min(args.steps, 50), 0 if args.no_cpu_baseline else 5)
+        cpu_legs.append(c)
         log("config 5: FusAtNet leg")
-        out["config5_fusatnet"] = fusat_leg(dev, 5, not args.no_cpu_baseline)
+        out["config5_fusatnet"], c = fusat_leg(dev, 5, not args.no_cpu_baseline)
+        cpu_legs.append(c)
         log("config 4: MUUFL leg")
         out["config4_muufl"] = muufl_leg(dev, min(args.steps, 50))
     if world == 1 and not args.no_f1:
         log("F1: whole-image test()")
-        out["f1_test"] = f1_leg(dev, not args.no_cpu_baseline)
+        out["f1_test"], c = f1_leg(dev, 1000 + rank, not args.no_cpu_baseline)
+        cpu_legs.append(c)
+    if world == 1 and not args.no_train_loop:
+        log("train(): the plugin-surface loop over a PatchBatcher loader")
+        out["value_via_train_loop"] = train_loop_leg(dev, 3, 1000 + rank, elapsed / args.steps * 1e3)
+    # the CPU baselines last: minutes of all-core CPU work that must not precede a timed GPU leg
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log(f"CPU baseline: {args.cpu_warmup} + {args.cpu_steps} oracle steps on {cpu_threads()} threads")
+        out["cpu_baseline"] = cpu_baseline(args.cpu_warmup, args.cpu_steps)
+        for c in cpu_legs:
+            if c is not None:
+                c()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

@@ -301,6 +301,19 @@ VC_API int vc_patch_gather(int W, int H, int C, int P, const float* cube, const 
  * mode of model_utils.py:1126-1128; windows are distinct, so no two i share a centre) */
 VC_API int vc_center_accumulate(int W, int H, int P, int ncls, const int* corners, long k0, int step, int n,
                                 const float* logits, double* probs, hipStream_t stream);
+/* MultiModalX radiation / mixture noise (datasets.py:529-545, applied at :565-568 to the HSI patch
+ * after flip / rot90), in place on gathered patches x [n][C][P][P]:
+ *   rad[i] != 0:  x = rad[i] * x + N/25                                   (radiation_noise)
+ *   mix[2i] > 0:  x = (a1 * x + a2 * d2) / (a1 + a2) + N/25, (a1, a2) = mix[2i..2i+1]  (mixture_noise)
+ * d2[c][p] = cube[pix[off[v] + r]][c], v = (int)lab[i][p] the (transformed) label window, r uniform in
+ * [0, off[v+1] - off[v]) per (sample, pixel) -- the reference's np.random.choice over the samples of
+ * class v; an empty class (ignored labels) leaves d2 = 0.  pix: x * H + y pixel indices of the cube.
+ * N: standard normals and r from a counter-based hash of (seed, gid0 + i, stream, element) -- the
+ * host draws the per-sample decisions and alphas in the reference's RNG order; the per-element fields
+ * are drawn on the device. */
+VC_API int vc_patch_noise(int n, int C, int P, int H, float* x, const float* lab, const float* rad,
+                          const float* mix, const int* off, const int* pix, int nlab, const float* cube,
+                          unsigned long long seed, long long gid0, hipStream_t stream);
 
 /* ---------------------------------------------------------------- classification metrics
  * Confusion matrix of a prediction map (utils.py:585-663 metrics(), counting step :596-611):

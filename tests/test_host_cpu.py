@@ -156,6 +156,7 @@ def test_window_xform_codes_follow_reference_distribution():
     from vitcnn_amd.window import PatchBatcher
     pb = PatchBatcher.__new__(PatchBatcher)
     pb.flip, pb.P, pb.rng = True, 9, np.random.RandomState(0)
+    pb.radiation = pb.mixture = False
     codes = pb.xform_codes(20000)
     flips = (codes & 3) != 0
     rots = (codes >> 2) != 0
@@ -163,3 +164,24 @@ def test_window_xform_codes_follow_reference_distribution():
     # P(flip branch) = 0.5 * P(at least one of h/v) = 0.375; P(rotate) = 0.25
     assert abs(flips.mean() - 0.375) < 0.02 and abs(rots.mean() - 0.25) < 0.02
     assert set(np.unique(codes >> 2).tolist()) <= {0, 1, 2, 3}
+
+
+def test_to_same_device_keeps_workspaces_and_binding():
+    """.to() onto the device the model is already on must not free the workspaces: train() calls
+    net.to(device) on entry, and hipGraphs captured by an earlier train() call write into them (a
+    rebind there freed memory a replayed graph then wrote to).  A real move, a scratch growth or a
+    re-flatten bumps the binding generation the TrainStepper checks before replaying."""
+    from vitcnn_amd import Multimodality_Mamba
+    m = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
+    ws = m._workspace("cpu", 4, ("train", "grad"))
+    gen = m._bind_gen
+    m.to("cpu")
+    m.to(torch.device("cpu"))
+    assert m._bind_gen == gen and m._ws.get(("cpu", 4, ("train", "grad"))) is ws
+    m._scratch("cpu", 4)
+    m._scratch("cpu", 4096)                       # grows: the old scratch is gone
+    assert m._bind_gen == gen + 1
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m.load_state_dict(sd, assign=True)
+    m._ensure_flat()
+    assert m._bind_gen == gen + 2 and not m._ws

@@ -137,10 +137,142 @@ def test_train_and_val_over_device_batches(tmp_path, monkeypatch):
     model, opt, crit, hp = mu.get_model("Multimodality_Mamba", n_classes=16, n_bands=(144, 1), ignored_labels=[0],
                                         dataset="synthetic", device=torch.device(DEV))
     loader = PatchBatcher(img1, img2, gt, 9, ignored_labels=[0], batch_size=64, flip_augmentation=True, device=DEV)
-    loader.dataset = loader  # train() reads data_loader.dataset.name like a DataLoader
     best = mu.train("t", 0, None, model, opt, crit, loader, 1, scheduler=hp["scheduler"], display_iter=0,
                     device=torch.device(DEV))
     assert best is not None and set(best.keys()) == set(model.state_dict().keys())
     acc = mu.val(model, loader, device=DEV)
     assert 0.0 <= acc <= 1.0
     assert all(np.isfinite(v.float().cpu().numpy()).all() for v in model.state_dict().values())
+
+
+def test_test_whole_image_production_batch_matches_reference_loop():
+    """test() at its production batch -- a 26 x 26 scene = 324 windows goes through
+    the model as ONE batch of 324 (>= 256: the MFMA NonLocal forward `nl_fwd_mfma` and every B >= 256
+    kernel configuration run) -- against the reference loop evaluated by the CPU oracle: 1e-3
+    relative on the probability map, argmax bit-exact on every window centre."""
+    _need_gpu()
+    from oracle import vitcnn_oracle as O
+    from vitcnn_amd import model_utils as mu
+    rng = np.random.default_rng(17)
+    W = H = 26
+    P = 9
+    img1 = rng.random((W, H, 144), dtype=np.float32)
+    img2 = rng.random((W, H, 1), dtype=np.float32)
+    sd = hash_state_dict()
+    # running statistics away from their init values, so eval-mode BatchNorm normalises for real
+    g = torch.Generator().manual_seed(3)
+    for k, v in sd.items():
+        if k.endswith("running_mean"):
+            sd[k] = torch.rand(v.shape, generator=g) * 0.2 - 0.1
+        elif k.endswith("running_var"):
+            sd[k] = torch.rand(v.shape, generator=g) + 0.5
+    model, _, _, hp = mu.get_model("Multimodality_Mamba", n_classes=16, n_bands=(144, 1), ignored_labels=[0],
+                                   dataset="synthetic", device=torch.device(DEV))
+    model.load_state_dict(sd)
+    hp["test_stride"] = 1
+    wins = _ref_windows(W, H, P, 1)
+    assert len(wins) == 324
+    probs = mu.test(0, model, img1, img2, hp)
+    x1 = torch.from_numpy(np.stack([img1[x:x + P, y:y + P].transpose(2, 0, 1) for x, y in wins]))
+    x2 = torch.from_numpy(np.stack([img2[x:x + P, y:y + P].transpose(2, 0, 1) for x, y in wins]))
+    st = O.make_state(sd, requires_grad=False)
+    with torch.no_grad():
+        ref_logits = O.forward(O.Params(st, training=False), x1, x2).numpy()
+    ref = np.zeros((W, H, 16))
+    for (x, y), lg in zip(wins, ref_logits):
+        ref[x + P // 2, y + P // 2] += lg
+    err = np.abs(probs - ref).max() / np.abs(ref).max()
+    assert err < 1e-3, err
+    hit = ref.any(-1)
+    assert len(set(ref.argmax(-1)[hit].tolist())) > 1      # the class indices vary over the scene
+    assert np.array_equal(probs.argmax(-1)[hit], ref.argmax(-1)[hit])
+
+
+def _noise_batcher(rad, mix, seed=5):
+    from vitcnn_amd.window import PatchBatcher
+    rng = np.random.default_rng(seed)
+    W, H = 40, 36
+    img1 = rng.random((W, H, 144), dtype=np.float32)
+    img2 = rng.random((W, H, 1), dtype=np.float32)
+    gt = rng.integers(0, 6, size=(W, H))
+    pb = PatchBatcher(img1, img2, gt, 9, ignored_labels=[0], batch_size=64, flip_augmentation=True, device=DEV,
+                      seed=seed, radiation_augmentation=rad, mixture_augmentation=mix)
+    return pb, img1, gt
+
+
+def test_patch_noise_exact_given_the_draws():
+    """vc_patch_noise == the CPU restatement (oracle/patch_noise_oracle.py) of datasets.py:529-545 fed the
+    same host decisions, transformed label windows and hash fields; and the mixture's candidate table
+    pairs the unshuffled labels with the shuffled indices as the reference does (:505-506, :540-543)."""
+    _need_gpu()
+    from oracle import patch_noise_oracle as NO
+    pb, img1, gt = _noise_batcher(True, True)
+    # the candidate table: class v -> idx_shuffled[j] over j with labels_unshuffled[j] == v
+    mask = gt != 0
+    xs, ys = np.nonzero(mask)
+    keep = (xs > 4) & (xs < gt.shape[0] - 4) & (ys > 4) & (ys < gt.shape[1] - 4)
+    idx = np.stack([xs[keep], ys[keep]], axis=1)
+    labels = gt[idx[:, 0], idx[:, 1]]
+    sh = idx.copy()
+    np.random.RandomState(5).shuffle(sh)
+    off, pix = pb.mix_off.cpu().numpy(), pb.mix_pix.cpu().numpy()
+    for v in range(1, 6):
+        want = sorted((sh[labels == v][:, 0] * gt.shape[1] + sh[labels == v][:, 1]).tolist())
+        assert sorted(pix[off[v]:off[v + 1]].tolist()) == want
+    assert off[1] == off[0]                                   # the ignored class has no candidates
+    # one batch with forced decisions: every sample noised one way or the other
+    from vitcnn_amd._lib import lib
+    n = 12
+    s = torch.cuda.current_stream().cuda_stream
+    cor = pb.corners[:n]
+    codes = np.array([0, 1, 2, 3, 4, 8, 12, 0, 1, 4, 2, 0], dtype=np.uint8)
+    xd = torch.from_numpy(codes).to(DEV)
+    x1 = torch.empty(n, 144, 9, 9, device=DEV)
+    lib().vc_patch_gather(pb.W, pb.H, 144, 9, pb.c1.data_ptr(), cor.data_ptr(), 0, 0, n, xd.data_ptr(), x1.data_ptr(), s)
+    clean = x1.clone()
+    rad = np.array([1.05, 0, 0.93, 0, 1.0, 0, 0, 0.9, 0, 1.1, 0, 0], dtype=np.float32)
+    mix = np.zeros((n, 2), dtype=np.float32)
+    mix[[1, 2, 5, 6, 8, 11]] = [[0.5, 0.3], [0.02, 0.9], [1.0, 1.0], [0.2, 0.7], [0.9, 0.01], [0.4, 0.4]]
+    pb.gid = 1000
+    pb.apply_noise(x1, cor, xd.data_ptr(), rad, mix, s)
+    lab = pb._last_noise[2].cpu().numpy().reshape(n, 9, 9)
+    torch.cuda.synchronize()
+    cube = img1.reshape(-1, 144)
+    ref = NO.apply_noise(clean.cpu().numpy(), lab, rad, mix, off, pix, cube, pb.seed, 1000)
+    got = x1.cpu().numpy()
+    assert np.abs(got - ref).max() < 2e-5
+    assert np.array_equal(got[[3, 10]], clean.cpu().numpy()[[3, 10]])   # samples without a draw stay untouched
+    # the label windows are the transformed gt windows
+    for i in range(n):
+        x, y = pb.centers[i] - 4
+        assert np.array_equal(lab[i], _np_xform(gt[x:x + 9, y:y + 9, None], codes[i])[:, :, 0].astype(np.float32))
+
+
+def test_patch_noise_distribution():
+    """radiation p 0.1 and mixture p 0.2 per sample (datasets.py:565-568); the noise fields are
+    N(0, 1) / 25; alpha ~ U(0.9, 1.1), a1, a2 ~ U(0.01, 1)."""
+    _need_gpu()
+    pb, _, _ = _noise_batcher(True, True, seed=9)
+    codes, rad, mix = pb.decisions(20000)
+    assert abs((rad != 0).mean() - 0.1) < 0.01 and abs((mix[:, 0] > 0).mean() - 0.2) < 0.012
+    r = rad[rad != 0]
+    assert r.min() >= 0.9 and r.max() <= 1.1 and abs(r.mean() - 1.0) < 0.005
+    m = mix[mix[:, 0] > 0]
+    assert m.min() >= 0.01 and m.max() <= 1.0
+    # the radiation field: x' - alpha x = N / 25 over many elements
+    from vitcnn_amd._lib import lib
+    pb2, _, _ = _noise_batcher(True, False, seed=9)
+    n = 64
+    x = torch.zeros(n, 144, 9, 9, device=DEV)
+    rad = np.full(n, 1.0, dtype=np.float32)
+    pb2.apply_noise(x, pb2.corners[:n], None, rad, np.zeros((n, 2), dtype=np.float32),
+                    torch.cuda.current_stream().cuda_stream)
+    z = x.cpu().numpy().reshape(-1) * 25
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+    assert abs(np.mean(z ** 4) - 3.0) < 0.05                  # normal kurtosis
+    # batches iterate with the noise on, finite
+    tot = 0
+    for x1, x2, t in pb:
+        assert torch.isfinite(x1).all()
+        tot += x1.shape[0]
+    assert tot == len(pb.centers)

@@ -90,6 +90,60 @@ __global__ void center_accumulate(Win w, int ncls, const int* __restrict__ corne
   probs[((long)(x + h) * w.H + (y + h)) * ncls + c] += (double)logits[e];
 }
 
+// Counter-based randomness of the noise augmentations: splitmix64 finaliser over
+// (seed, global sample id, stream, element).  oracle/patch_noise_oracle.py restates it.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ unsigned long long noise_key(unsigned long long seed, long long gid, int stream) {
+  return mix64(seed ^ mix64(((unsigned long long)gid << 2) | (unsigned long long)stream));
+}
+// standard normal (Box-Muller on two 24-bit uniforms in (0, 1))
+__device__ __forceinline__ float gauss(unsigned long long key, int e) {
+  const unsigned long long r = mix64(key + (unsigned long long)e);
+  const float u1 = ((float)(r >> 40) + 0.5f) * (1.f / 16777216.f);
+  const float u2 = ((float)(r & 0xFFFFFFull) + 0.5f) * (1.f / 16777216.f);
+  return sqrtf(-2.f * logf(u1)) * cosf(6.283185307179586f * u2);
+}
+
+// one thread per element of x (sample-major, then channel, then pixel): coalesced reads / writes of
+// the patches; the mixture source spectrum is a gather of one cube row (band-contiguous) per pixel
+__global__ __launch_bounds__(256) void patch_noise(int total, FastDiv fCPP, FastDiv fPP, int C, int H,
+                                                   float* __restrict__ x, const float* __restrict__ lab,
+                                                   const float* __restrict__ rad, const float* __restrict__ mix,
+                                                   const int* __restrict__ off, const int* __restrict__ pix, int nlab,
+                                                   const float* __restrict__ cube, unsigned long long seed,
+                                                   long long gid0) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int PP = fPP.div;
+  int rem, c, p;
+  const int s = fdivmod(idx, fCPP, rem);
+  c = fdivmod(rem, fPP, p);
+  const float a = rad[s], a1 = mix[2 * s], a2 = mix[2 * s + 1];
+  if (a == 0.f && !(a1 > 0.f)) return;
+  float v = x[idx];
+  const long long gid = gid0 + s;
+  if (a != 0.f) v = fmaf(a, v, 0.04f * gauss(noise_key(seed, gid, 0), c * PP + p));
+  if (a1 > 0.f) {
+    const int lv = (int)lab[(long)s * PP + p];
+    float d2 = 0.f;
+    if (lv >= 0 && lv < nlab) {
+      const int o0 = off[lv], cnt = off[lv + 1] - o0;
+      if (cnt > 0) {
+        const unsigned long long r = mix64(noise_key(seed, gid, 2) + (unsigned long long)p);
+        const int j = (int)((r >> 32) % (unsigned long long)cnt);
+        d2 = cube[(long)pix[o0 + j] * C + c];
+      }
+    }
+    v = (a1 * v + a2 * d2) / (a1 + a2) + 0.04f * gauss(noise_key(seed, gid, 1), c * PP + p);
+  }
+  x[idx] = v;
+}
+
 // number of sliding-window positions along one axis (utils.py:389-399)
 long axis_count(int L, int P, int step) {
   const int off = (L - P) % step;
@@ -127,6 +181,21 @@ VC_EXPORT int vc_patch_gather(int W, int H, int C, int P, const float* cube, con
   const Win w = make_win(W, H, P, corners ? 1 : step);
   hipLaunchKernelGGL(patch_gather, dim3(n), dim3(256), P * P * (CT + 1) * sizeof(float), stream, w, C, cube,
                      corners, k0, xform, out);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_EXPORT int vc_patch_noise(int n, int C, int P, int H, float* x, const float* lab, const float* rad,
+                             const float* mix, const int* off, const int* pix, int nlab, const float* cube,
+                             unsigned long long seed, long long gid0, hipStream_t stream) {
+  VC_REQUIRE(n >= 0 && C > 0 && P > 0 && H > 0 && nlab >= 0 && x && rad && mix);
+  VC_REQUIRE(nlab == 0 || (lab && off && pix && cube));
+  if (n == 0) return VC_OK;
+  const long total = (long)n * C * P * P;
+  VC_REQUIRE_I32(total);
+  hipLaunchKernelGGL(patch_noise, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total,
+                     make_fastdiv(C * P * P), make_fastdiv(P * P), C, H, x, lab, rad, mix, off, pix, nlab, cube, seed,
+                     gid0);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

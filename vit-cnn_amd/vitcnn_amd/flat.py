@@ -17,6 +17,46 @@ import torch.nn as nn
 F32 = 4
 
 
+def expose_grad_views(model):
+    """Point every parameter's .grad at its slice of the flat gradient (`flat_params.grad`), so torch
+    optimizers (e.g. the reference's torch.optim.Adam(model.parameters()), model_utils.py:109-118),
+    gradient clipping or inspection see the gradient the hand-written backward wrote.  A no-op when
+    the views are current, or when the model is trained by vitcnn_amd.optim.AdamW (which reads the
+    flat gradient and clears `_grad_views`: ~1000 views per ViT-CNN step would cost milliseconds)."""
+    if not getattr(model, "_grad_views", True):
+        return
+    g = model._flat_store.grad
+    if g is None:
+        return
+    base = g.data_ptr()
+    names = model._pnames if hasattr(model, "_pnames") else list(model._pmods)
+    first, last = model._pmods[names[0]], model._pmods[names[-1]]
+    p0, p1 = first[0]._parameters[first[1]], last[0]._parameters[last[1]]
+    if p0.grad is not None and p1.grad is not None and p0.grad.data_ptr() == base + F32 * model._poff[names[0]] \
+            and p1.grad.data_ptr() == base + F32 * model._poff[names[-1]]:
+        return
+    n_active = model._n_active
+    for n in names:
+        m, pn = model._pmods[n]
+        p = m._parameters[pn]
+        o = model._poff[n]
+        # parameters the forward never uses (ViT-CNN's hsiMamba.tokenlearner / ln3) get no gradient,
+        # as under the reference's autograd
+        p.grad = g[o:o + p.numel()].view(p.shape) if o < n_active else None
+
+
+def install_grad_views(model):
+    """Register expose_grad_views as the flat buffer's post-accumulate hook (autograd backward)."""
+    me = weakref.ref(model)
+
+    def hook(_t):
+        m = me()
+        if m is not None:
+            expose_grad_views(m)
+
+    model._flat_store.register_post_accumulate_grad_hook(hook)
+
+
 class FlatParams:
     """Mixin for an nn.Module whose parameters live in one flat buffer; call `_build_flat()` at the end
     of __init__.  Provides flat_params, n_active_params, _ensure_flat (re-pack after a parameter was
@@ -45,6 +85,7 @@ class FlatParams:
 
     def _rebind(self, flat):
         object.__setattr__(self, "_flat_store", flat.detach().requires_grad_(True))
+        install_grad_views(self)
         base = self._flat_store.detach()
         for n, (m, pn) in self._pmods.items():
             p = m._parameters[pn]

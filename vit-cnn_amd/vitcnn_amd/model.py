@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 
 from ._lib import lib
+from .flat import install_grad_views
 from .layers import ConvBnReluParams, FusionParams, GlobalLocalParams
 from .scan_orders import scan_orders
 
@@ -177,6 +178,7 @@ class Multimodality_Mamba(nn.Module):
 
     def _rebind(self, flat, bflat, iflat):
         object.__setattr__(self, "_flat_store", flat.detach().requires_grad_(True))
+        install_grad_views(self)
         object.__setattr__(self, "_bflat", bflat)
         object.__setattr__(self, "_iflat", iflat)
         base = self._flat_store.detach()
@@ -197,6 +199,9 @@ class Multimodality_Mamba(nn.Module):
         self._ptr_cache = None
         self._ws = {}
         self._dev_cache = {}
+        # every rebind frees the workspaces / device tables: hipGraphs captured before it are stale
+        # (TrainStepper compares this generation before replaying)
+        self._bind_gen = getattr(self, "_bind_gen", 0) + 1
 
     def _flat_intact(self):
         base = self._flat_store.data_ptr()
@@ -220,7 +225,13 @@ class Multimodality_Mamba(nn.Module):
         flat = fn(self._flat_store.detach())
         if flat.dtype != torch.float32:
             raise RuntimeError("ViT-CNN MI355X path computes in fp32 master weights; dtype casts are not supported")
-        self._rebind(flat, fn(self._bflat), fn(self._iflat))
+        bflat, iflat = fn(self._bflat), fn(self._iflat)
+        if flat.data_ptr() == self._flat_store.data_ptr() and bflat.data_ptr() == self._bflat.data_ptr() and \
+                iflat.data_ptr() == self._iflat.data_ptr():
+            # .to(the device it is on): nothing moves, and the workspaces -- which captured hipGraphs of
+            # the step (vitcnn_amd.step.TrainStepper) write into -- must stay alive
+            return self
+        self._rebind(flat, bflat, iflat)
         return self
 
     def set_precision(self, precision: str):
@@ -294,6 +305,8 @@ class Multimodality_Mamba(nn.Module):
         key = "scratch"
         t = self._dev_cache.get(str(device), {}).get(key)
         if t is None or t.numel() < need:
+            if t is not None:
+                self._bind_gen += 1   # the old scratch is freed: graphs captured with it are stale
             t = torch.empty(need, dtype=torch.float32, device=device)
             self._device_tables(device)[key] = t
         return t

@@ -156,56 +156,96 @@ def save_model(savename, model, model_name, dataset_name, train_state, type, **k
     return path
 
 
+def _stepper(net, optimizer, criterion):
+    """the model's TrainStepper for this optimizer / criterion (kept across train() calls, so the
+    captured per-shape graphs are reused)"""
+    from .step import TrainStepper
+    st = getattr(net, "_vc_stepper", None)
+    if st is None or st.opt is not optimizer or st.crit is not criterion or \
+            (st.exchange is None) == parallel.is_distributed():
+        st = TrainStepper(net, optimizer, criterion)
+        object.__setattr__(net, "_vc_stepper", st)
+    return st
+
+
 def train(savename, run, bands, net, optimizer, criterion, data_loader, epoch, scheduler=None, display_iter=100,
           device=torch.device("cpu"), display=None, val_loader=None, supervision="full"):
-    """Training loop of model_utils.py:854-1045 (per-iteration loss.item(), scheduler per epoch,
-    best-state tracking, best/final checkpoints).  `display` (visdom) is optional here."""
+    """Training loop of model_utils.py:854-1045: per batch one optimizer step (zero_grad, forward,
+    criterion, backward, step: :916-934), the loss recorded per iteration (:936-938) and its running
+    mean printed every `display_iter` iterations (:940-962), the scheduler stepped per epoch
+    (:997-1000), best-state tracking with best / final checkpoints (:1015-1043).  `display` (visdom)
+    is optional here.
+
+    The step is `vitcnn_amd.step.TrainStepper.step`: for ViT-CNN with the fused AdamW one hipGraph
+    replay per batch (captured per batch shape; data parallel: bucketed RCCL all-reduce inside it).
+    The per-iteration losses stay on the device and are read in one transfer at each display point
+    and at the epoch end (the reference's `loss.item()` host sync per iteration would stall the queue
+    every step); the recorded values are the same.
+
+    Data parallel (a process group with more than one rank): replicas start from rank 0's parameters,
+    a loader that is not already sharded is wrapped in `parallel.ShardedLoader` (every rank the same
+    number of batches: one gradient exchange per batch on every rank), and the per-epoch metric that
+    decides the best-state branch -- whose buffer broadcast is a collective -- is the mean over the
+    ranks (validation: accuracy over the union of the ranks' validation batches), so every rank takes
+    the same branch.  `train.last_stats` holds per-epoch wall times and batch counts."""
+    import time
     if criterion is None:
         raise Exception("Missing criterion. You must specify a loss function.")
     if supervision != "full":
         raise ValueError('supervision mode "{}" is unknown.'.format(supervision))
     net.to(device)
-    if parallel.is_distributed():
+    distributed = parallel.is_distributed()
+    if distributed:
         parallel.broadcast_parameters(net)       # replicas start identical (rank 0's values)
         if not parallel.is_sharded(data_loader):
             data_loader = parallel.ShardedLoader(data_loader, parallel.rank(), parallel.world())
+    stepper = _stepper(net, optimizer, criterion)
     save_epoch = 16 if epoch == 128 else (epoch // 20 if epoch > 20 else 1)
     best_val_acc = 0.0
     best_model_wts = None
     losses = []
     iter_ = 1
     val_accuracies = []
+    stats = {"epochs": [], "launch": None}
+    train.last_stats = stats
     for e in range(1, epoch + 1):
+        t_epoch = time.perf_counter()
         net.train()
+        pending = []          # device losses not yet read back
+        nb = npatch = 0
         avg_loss = 0.0
-        nb = 0
+        n_batches = len(data_loader)
         for batch_idx, (data, data2, target) in enumerate(data_loader):
-            data, data2, target = data.to(device), data2.to(device), target.to(device)
-            optimizer.zero_grad()
-            output = net(data, data2)
-            loss = criterion(output, target)
-            loss.backward()
-            parallel.allreduce_gradients(net, optimizer)
-            optimizer.step()
-            lv = loss.item()
-            avg_loss += lv
-            losses.append(lv)
+            loss = stepper.step(data, data2, target)
+            if stepper.fused:
+                loss = loss.clone()   # a replayed graph's loss buffer is overwritten by the next replay
+            pending.append(loss.detach())
             nb += 1
-            if display_iter and iter_ % display_iter == 0 and parallel.rank() == 0:
-                mean_loss = float(np.mean(losses[max(0, len(losses) - 101):]))
-                print("Train (epoch {}/{}) [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
-                    e, epoch, batch_idx * len(data), len(data) * len(data_loader),
-                    100.0 * batch_idx / max(len(data_loader), 1), mean_loss), flush=True)
-                if display is not None and hasattr(display, "line"):
-                    display.line(X=np.arange(len(losses)), Y=np.asarray(losses), win="loss")
+            npatch += int(target.shape[0])
+            if display_iter and iter_ % display_iter == 0:
+                vals = torch.stack(pending).tolist() if pending else []
+                pending = []
+                losses.extend(vals)
+                if parallel.rank() == 0:
+                    mean_loss = float(np.mean(losses[max(0, len(losses) - 101):]))
+                    print("Train (epoch {}/{}) [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
+                        e, epoch, batch_idx * len(data), len(data) * n_batches,
+                        100.0 * batch_idx / max(n_batches, 1), mean_loss), flush=True)
+                    if display is not None and hasattr(display, "line"):
+                        display.line(X=np.arange(len(losses)), Y=np.asarray(losses), win="loss")
             iter_ += 1
-        avg_loss /= max(nb, 1)
+        if pending:
+            losses.extend(torch.stack(pending).tolist())
+        avg_loss = float(np.sum(losses[len(losses) - nb:])) / max(nb, 1) if nb else 0.0
         if val_loader is not None:
-            val_acc = val(net, val_loader, device=device, supervision=supervision)
+            correct, total = _val_counts(net, val_loader, device)
+            if distributed:
+                correct, total = parallel.sum_over_ranks([correct, total])
+            val_acc = correct / total
             val_accuracies.append(val_acc)
             metric = -val_acc
         else:
-            metric = avg_loss
+            metric = parallel.mean_over_ranks(avg_loss) if distributed else avg_loss
         if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
             scheduler.step(metric)
         elif scheduler is not None:
@@ -221,6 +261,9 @@ def train(savename, run, bands, net, optimizer, criterion, data_loader, epoch, s
             parallel.broadcast_buffers(net)
             save_model(savename, net, camel_to_snake(str(net.__class__.__name__)), data_loader.dataset.name,
                        train_state="train", type="final_epoch", run=run, epoch=e, metric=abs(metric))
+        stats["epochs"].append({"seconds": time.perf_counter() - t_epoch, "batches": nb, "patches": npatch})
+        stats["launch"] = stepper.launch
+    stats["losses"] = losses
     return best_model_wts
 
 
@@ -229,6 +272,12 @@ def val(net, data_loader, device="cpu", supervision="full"):
     label.  Like the reference, the network is not switched to eval mode (it runs in whatever
     mode it is in — train mode when called from `train`).  The per-sample `.item()` loop becomes
     an on-device comparison with one host sync per batch."""
+    correct, total = _val_counts(net, data_loader, device)
+    return correct / total
+
+
+def _val_counts(net, data_loader, device):
+    """(correct, counted) of val(): the host counts, summed over ranks by train() under DP"""
     ignored = sorted(set(getattr(data_loader.dataset, "ignored_labels", [])))
     correct, total = 0, 0
     for data, data2, target in data_loader:
@@ -243,7 +292,7 @@ def val(net, data_loader, device="cpu", supervision="full"):
                 keep &= pred != lab
             correct += int(((pred == target.view(-1)) & keep).sum())
             total += int(keep.sum())
-    return correct / total
+    return correct, total
 
 
 def test(run, net, img1, img2, hyperparams):

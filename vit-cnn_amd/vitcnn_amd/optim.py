@@ -28,6 +28,24 @@ class AdamW(torch.optim.Optimizer):
         self.grad_scale = 1.0   # data-parallel: 1/world_size folded into the update
         self._dev = None
         self._hyper_vals = None
+        # the model need not expose per-parameter .grad views of its flat gradient (torch optimizers
+        # need them; this one reads the flat gradient)
+        owner()._grad_views = False
+
+    def sync_hyper(self):
+        """Copy lr / betas / eps / weight decay / grad_scale to the device tensor the kernel reads, if
+        they changed.  step() does this itself; a replayed hipGraph of the step does not run Python, so
+        the caller (vitcnn_amd.step.TrainStepper) calls it before every replay (a scheduler's new lr then
+        takes effect on the next step, as with torch.optim)."""
+        flat = self._owner().flat_params
+        st = self._device_state(flat)
+        grp = self.param_groups[0]
+        vals = (float(grp["lr"]), float(grp["betas"][0]), float(grp["betas"][1]), float(grp["eps"]),
+                float(grp["weight_decay"]), float(self.grad_scale))
+        if vals != self._hyper_vals:
+            st["hyper"].copy_(torch.tensor(vals, dtype=torch.float32))
+            self._hyper_vals = vals
+        return st
 
     def _device_state(self, flat):
         st = self._dev
@@ -47,13 +65,7 @@ class AdamW(torch.optim.Optimizer):
         g = flat.grad
         if g is None:
             return loss
-        st = self._device_state(flat)
-        grp = self.param_groups[0]
-        vals = (float(grp["lr"]), float(grp["betas"][0]), float(grp["betas"][1]), float(grp["eps"]),
-                float(grp["weight_decay"]), float(self.grad_scale))
-        if vals != self._hyper_vals:
-            st["hyper"].copy_(torch.tensor(vals, dtype=torch.float32))
-            self._hyper_vals = vals
+        st = self.sync_hyper()
         s = torch.cuda.current_stream(flat.device).cuda_stream
         lib().vc_adamw(model._n_active, flat.data_ptr(), g.data_ptr(), st["m"].data_ptr(), st["v"].data_ptr(),
                        st["hyper"].data_ptr(), st["step"].data_ptr(), s)

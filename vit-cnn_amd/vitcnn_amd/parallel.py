@@ -89,19 +89,28 @@ def allreduce_gradients(model, optimizer=None, group=None):
         return
     n = dist.get_world_size(group)
     if not hasattr(model, "flat_params"):
-        # per-parameter gradients (FusAtNet / torch modules): one flattened bucket over EVERY
-        # parameter that requires grad (zeros where backward produced none), so the bucket size
-        # and offsets are the same on every rank whatever the local graph touched
+        # per-parameter gradients (torch modules): one flattened bucket over EVERY parameter that
+        # requires grad (zeros where backward produced none), so the bucket size and offsets are the
+        # same on every rank whatever the local graph touched.  A has-gradient flag per parameter is
+        # summed first: a parameter no rank produced a gradient for keeps grad None (torch optimizers
+        # skip it, as single-process training does) instead of receiving zeros that weight decay /
+        # momentum would then act on.
         params = [p for p in model.parameters() if p.requires_grad]
         if not params:
             raise RuntimeError("allreduce_gradients: the model has no trainable parameters")
+        dev = params[0].device
+        has = torch.tensor([p.grad is not None for p in params], dtype=torch.int32, device=dev)
+        dist.all_reduce(has, op=dist.ReduceOp.SUM, group=group)
+        has = has.tolist()
         bucket = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
         bucket.mul_(1.0 / n)
         o = 0
-        for p in params:
+        for p, h in zip(params, has):
             v = bucket[o:o + p.numel()].view_as(p)
-            if p.grad is None:
+            if h == 0:
+                p.grad = None
+            elif p.grad is None:
                 p.grad = v.clone()
             else:
                 p.grad.copy_(v)
@@ -199,6 +208,29 @@ class GradExchange:
             self.grad.mul_(1.0 / n)
 
 
+def _scalar_device(group=None):
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+def mean_over_ranks(x: float, group=None) -> float:
+    """The mean of a host scalar over the ranks (every rank returns the same value): train() decides
+    its best-epoch branch -- which contains collectives -- on this, never on a rank-local number."""
+    if not is_distributed():
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_scalar_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return float(t.item()) / dist.get_world_size(group)
+
+
+def sum_over_ranks(values, group=None):
+    """Element-wise sum of a list of host numbers over the ranks (float64)."""
+    if not is_distributed():
+        return [float(v) for v in values]
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=_scalar_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t.tolist()
+
+
 def broadcast_parameters(model, src: int = 0, group=None):
     """Make every replica start from rank `src`'s parameters: one broadcast of the flat buffer, or of
     one flattened bucket for models without it."""
@@ -247,9 +279,14 @@ def shard_indices(n: int, rank_: int, world_: int, seed: int = 0, epoch: int = 0
 
 class ShardedLoader:
     """Wrap a reference-style DataLoader (batches of (data, data2, target)) so each rank iterates a
-    disjoint shard of its batches (batch b goes to rank b % world).  Used by train() when a process
-    group is up and the loader is not already sharded (a loader whose sampler is a
-    DistributedSampler, or whose dataset carries `rank`/`world` attributes, is)."""
+    disjoint shard of its batches: batch b goes to rank b % world, and the batch list is padded by
+    wrapping (as `shard_indices` / DistributedSampler pad their index lists) to ceil(n / world) * world,
+    so EVERY rank iterates the same number of batches -- train() issues one gradient all-reduce per
+    batch, and ranks with different batch counts would pair their collectives across epochs (or block
+    forever in the last one).  The wrapped batches are the first ones of the same pass (kept from it,
+    not re-drawn).  Used by train() when a process group is up and the loader is not already sharded
+    (a loader whose sampler is a DistributedSampler, or whose dataset carries `rank`/`world`
+    attributes, is)."""
 
     def __init__(self, loader, rank_: int, world_: int):
         self.loader, self.rank, self.world = loader, rank_, world_
@@ -257,12 +294,21 @@ class ShardedLoader:
 
     def __len__(self):
         n = len(self.loader)
-        return (n - self.rank + self.world - 1) // self.world
+        return -(-n // self.world) if n > 0 else 0
 
     def __iter__(self):
+        n = len(self.loader)
+        total = len(self) * self.world
+        # padded position n + j repeats batch j % n; this rank owns at most one of them (pad < world)
+        need = [j % n for j in range(total - n) if (n + j) % self.world == self.rank]
+        kept = {}
         for b, item in enumerate(self.loader):
+            if b in need:
+                kept[b] = item
             if b % self.world == self.rank:
                 yield item
+        for b in need:
+            yield kept[b]
 
 
 def is_sharded(loader) -> bool:

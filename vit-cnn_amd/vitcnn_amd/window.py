@@ -81,16 +81,31 @@ class PatchBatcher:
 
     Iterating yields (hsi [B,C1,P,P], lidar [B,C2,P,P], target [B] int64) on `device`, in the
     order of the shuffled `indices` (DataLoader(shuffle=False) over the dataset, as main.py builds
-    it).  `rank`/`world` select a disjoint shard for data parallelism."""
+    it).  `rank`/`world` select a disjoint shard for data parallelism.
+
+    Augmentations of MultiModalX.__getitem__ (datasets.py:559-568), per sample in the reference's
+    order and with its probabilities, the decisions drawn from one host RandomState in the reference's
+    call order: flip / rot90 (flip_augmentation, :511-526) folded into the gather; radiation noise
+    (p 0.1: alpha ~ U(0.9, 1.1), x = alpha x + N/25, :529-532) and mixture noise (p 0.2: a1, a2 ~
+    U(0.01, 1), x = (a1 x + a2 d2) / (a1 + a2) + N/25 with d2 the spectra of random same-class training
+    pixels, :534-545) on the HSI patch by `vc_patch_noise`.  The per-element normal fields and the
+    per-pixel same-class choices (the reference's np.random.normal(size=patch) / np.random.choice) are
+    drawn on the device from a counter-based hash, so the host stream differs from the reference's
+    after the first noisy sample (same distributions).  The mixture's source
+    pixel reproduces the reference's pairing of its UNshuffled label list with its shuffled index list
+    (datasets.py:505-506, :540-543): for class v the candidates are indices[j] over the positions j
+    with labels[j] == v."""
 
     def __init__(self, img1, img2, gt, patch_size: int, ignored_labels=(0,), batch_size: int = 64,
                  flip_augmentation: bool = False, device="cuda", seed: int = 0, rank: int = 0, world: int = 1,
-                 name: str = "synthetic"):
+                 name: str = "synthetic", radiation_augmentation: bool = False, mixture_augmentation: bool = False):
         self.device = torch.device(device)
         self.c1, self.c2 = _cube(img1, self.device), _cube(img2, self.device)
         self.P, self.bs, self.flip = int(patch_size), int(batch_size), bool(flip_augmentation)
+        self.radiation, self.mixture = bool(radiation_augmentation), bool(mixture_augmentation)
         self.ignored_labels = set(ignored_labels)
         self.name = name
+        self.seed = int(seed) & ((1 << 63) - 1)
         gt = np.asarray(gt)
         mask = np.ones_like(gt)
         for lab in self.ignored_labels:
@@ -99,32 +114,73 @@ class PatchBatcher:
         p = self.P // 2
         keep = (xs > p) & (xs < gt.shape[0] - p) & (ys > p) & (ys < gt.shape[1] - p)
         idx = np.stack([xs[keep], ys[keep]], axis=1)
+        labels_unshuffled = gt[idx[:, 0], idx[:, 1]].astype(np.int64)
         self.rng = np.random.RandomState(seed)
         self.rng.shuffle(idx)
+        self.W, self.H = int(self.c1.shape[0]), int(self.c1.shape[1])
+        if self.mixture:
+            self._mixture_tables(gt, idx, labels_unshuffled)
         idx = idx[rank::world] if world > 1 else idx
         self.centers = idx
         self.labels = torch.as_tensor(gt[idx[:, 0], idx[:, 1]].astype(np.int64)).to(self.device)
         corners = (idx - p).astype(np.int32)
         self.corners = torch.as_tensor(np.ascontiguousarray(corners)).to(self.device)
-        self.W, self.H = int(self.c1.shape[0]), int(self.c1.shape[1])
+        self.gid = 0     # samples drawn so far (the noise hash's counter)
+
+    def _mixture_tables(self, gt, idx_shuffled, labels_unshuffled):
+        """class v -> candidate source pixels idx_shuffled[j] for j with labels_unshuffled[j] == v, as
+        CSR (off [nlab + 1], pix = x * H + y); ignored classes get none (d2 stays 0, :539); the label
+        map as a float cube for the label-window gather"""
+        nlab = int(max(int(gt.max()), int(labels_unshuffled.max()) if len(labels_unshuffled) else 0)) + 1
+        order = np.argsort(labels_unshuffled, kind="stable")
+        counts = np.bincount(labels_unshuffled, minlength=nlab)
+        for lab in self.ignored_labels:
+            if 0 <= lab < nlab:
+                counts[lab] = 0
+        keep = np.isin(labels_unshuffled[order], list(self.ignored_labels), invert=True)
+        src = idx_shuffled[order[keep]]
+        off = np.zeros(nlab + 1, dtype=np.int32)
+        off[1:] = np.cumsum(counts)
+        self.nlab = nlab
+        self.mix_off = torch.as_tensor(off).to(self.device)
+        self.mix_pix = torch.as_tensor((src[:, 0] * self.H + src[:, 1]).astype(np.int32)).to(self.device)
+        self.gt_cube = torch.as_tensor(np.ascontiguousarray(gt, dtype=np.float32)[:, :, None]).to(self.device)
 
     def __len__(self):
         return -(-len(self.centers) // self.bs)
 
+    @property
+    def dataset(self):
+        """DataLoader-style access (train() reads data_loader.dataset.name / .ignored_labels)"""
+        return self
+
     def xform_codes(self, n: int) -> np.ndarray:
         """MultiModalX flip/rotate decisions (datasets.py:511-526, :559-564) as gather codes."""
+        return self.decisions(n)[0]
+
+    def decisions(self, n: int):
+        """(xform codes [n] u8, radiation alpha [n] f32 (0: none), mixture (a1, a2) [n, 2] f32 (0: none)):
+        per sample, in __getitem__'s order (datasets.py:559-568), from the batcher's RandomState"""
         codes = np.zeros(n, dtype=np.uint8)
-        if not self.flip or self.P <= 1:
-            return codes
+        rad = np.zeros(n, dtype=np.float32)
+        mix = np.zeros((n, 2), dtype=np.float32)
         r = self.rng
+        flip = self.flip and self.P > 1
+        if not (flip or self.radiation or self.mixture):
+            return codes, rad, mix
         for i in range(n):
-            if r.random_sample() > 0.5:
-                h = r.random_sample() > 0.5
-                v = r.random_sample() > 0.5
-                codes[i] = (1 if h else 0) | (2 if v else 0)
-            elif r.random_sample() > 0.5:
-                codes[i] = int(r.choice([1, 2, 3])) << 2
-        return codes
+            if flip:
+                if r.random_sample() > 0.5:
+                    h = r.random_sample() > 0.5
+                    v = r.random_sample() > 0.5
+                    codes[i] = (1 if h else 0) | (2 if v else 0)
+                elif r.random_sample() > 0.5:
+                    codes[i] = int(r.choice([1, 2, 3])) << 2
+            if self.radiation and r.random_sample() < 0.1:
+                rad[i] = r.uniform(0.9, 1.1)
+            if self.mixture and r.random_sample() < 0.2:
+                mix[i] = r.uniform(0.01, 1.0, size=2)
+        return codes, rad, mix
 
     def __iter__(self):
         L = lib()
@@ -135,11 +191,31 @@ class PatchBatcher:
             x1 = torch.empty(n, C1, P, P, device=self.device)
             x2 = torch.empty(n, C2, P, P, device=self.device)
             cor = self.corners[b0:b0 + n]
-            xf = None
-            if self.flip:
-                xf = torch.as_tensor(self.xform_codes(n)).to(self.device)
-            L.vc_patch_gather(self.W, self.H, C1, P, self.c1.data_ptr(), cor.data_ptr(), 0, 0, n,
-                              xf.data_ptr() if xf is not None else None, x1.data_ptr(), s)
-            L.vc_patch_gather(self.W, self.H, C2, P, self.c2.data_ptr(), cor.data_ptr(), 0, 0, n,
-                              xf.data_ptr() if xf is not None else None, x2.data_ptr(), s)
+            codes, rad, mix = self.decisions(n)
+            xf = torch.as_tensor(codes).to(self.device) if self.flip else None
+            xfp = xf.data_ptr() if xf is not None else None
+            L.vc_patch_gather(self.W, self.H, C1, P, self.c1.data_ptr(), cor.data_ptr(), 0, 0, n, xfp,
+                              x1.data_ptr(), s)
+            L.vc_patch_gather(self.W, self.H, C2, P, self.c2.data_ptr(), cor.data_ptr(), 0, 0, n, xfp,
+                              x2.data_ptr(), s)
+            if rad.any() or mix.any():
+                self.apply_noise(x1, cor, xfp, rad, mix, s)
+            self.gid += n
             yield x1, x2, self.labels[b0:b0 + n]
+
+    def apply_noise(self, x1, cor, xfp, rad, mix, stream):
+        L = lib()
+        n, C1, P = x1.shape[0], x1.shape[1], self.P
+        rad_d = torch.as_tensor(rad).to(self.device)
+        mix_d = torch.as_tensor(np.ascontiguousarray(mix)).to(self.device)
+        lab = off = pix = None
+        nlab = 0
+        if self.mixture:
+            lab = torch.empty(n, 1, P, P, device=self.device)
+            L.vc_patch_gather(self.W, self.H, 1, P, self.gt_cube.data_ptr(), cor.data_ptr(), 0, 0, n, xfp,
+                              lab.data_ptr(), stream)
+            off, pix, nlab = self.mix_off.data_ptr(), self.mix_pix.data_ptr(), self.nlab
+        L.vc_patch_noise(n, C1, P, self.H, x1.data_ptr(), lab.data_ptr() if lab is not None else None,
+                         rad_d.data_ptr(), mix_d.data_ptr(), off, pix, nlab, self.c1.data_ptr(), self.seed, self.gid,
+                         stream)
+        self._last_noise = (rad_d, mix_d, lab)   # keep the uploads alive until the kernel has run
