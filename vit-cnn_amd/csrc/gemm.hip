@@ -86,7 +86,7 @@ __device__ __forceinline__ void tile_idx(int tid, int e, int& r, int& k) {
 // One 64x64 output tile (bx, by) of K slice / batch bz; tn x tm tiles per slice (the arrival-counter
 // index of the in-launch combine).  Shared by the single-problem kernel and the grouped one, which
 // own the LDS (As, Bs: BK * LDS_STRIDE floats each, `last`: one int).
-template <bool TA, bool TB, bool VA, bool VB>
+template <bool TA, bool TB, bool VA, bool VB, int PD>
 __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by, int bz, int tn, int tm,
                                               float* __restrict__ As, float* __restrict__ Bs, int* last) {
   const int tid = threadIdx.x;
@@ -100,7 +100,11 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
   const float* Bp = g.B + (long)zb * g.sB;
   const bool ones = g.Ne > g.N;
 
-  float ra[NE], rb[NE];
+  // PD register sets of staged operand tiles: the global loads of k-tiles t+1 .. t+PD-1 are in
+  // flight while tile t is multiplied (the small-grid GEMMs of the step are bound by the load
+  // latency of their few k-tiles, not by the MFMAs); the k order and the MFMA sequence are those of
+  // PD = 1, so the results are bit-identical for every depth.
+  float ra[PD][NE], rb[PD][NE];
   auto a_at = [&](int gm, int gk) -> float {
     return (gm < g.M && gk < kend) ? (TA ? A[(long)gk * g.lda + gm] : A[(long)gm * g.lda + gk]) : 0.f;
   };
@@ -109,7 +113,7 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
     if (gn < g.N) return TB ? Bp[(long)gn * g.ldb + gk] : Bp[(long)gk * g.ldb + gn];
     return (ones && gn == g.N) ? 1.f : 0.f;
   };
-  auto load = [&](int k0) {
+  auto load = [&](int k0, float (&xa)[NE], float (&xb)[NE]) {
 #pragma unroll
     for (int v = 0; v < NE / 4; ++v) {
       if (VA) {
@@ -119,17 +123,17 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
         const bool full = TA ? (gk < kend && gm + 3 < g.M) : (gm < g.M && gk + 3 < kend);
         if (full) {
           const float4 x = *reinterpret_cast<const float4*>(TA ? A + (long)gk * g.lda + gm : A + (long)gm * g.lda + gk);
-          ra[4 * v] = x.x; ra[4 * v + 1] = x.y; ra[4 * v + 2] = x.z; ra[4 * v + 3] = x.w;
+          xa[4 * v] = x.x; xa[4 * v + 1] = x.y; xa[4 * v + 2] = x.z; xa[4 * v + 3] = x.w;
         } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ra[4 * v + i] = TA ? a_at(gm + i, gk) : a_at(gm, gk + i);
+          for (int i = 0; i < 4; ++i) xa[4 * v + i] = TA ? a_at(gm + i, gk) : a_at(gm, gk + i);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           int m, k;
           tile_idx<TA, false>(tid, 4 * v + i, m, k);
-          ra[4 * v + i] = a_at(m0 + m, k0 + k);
+          xa[4 * v + i] = a_at(m0 + m, k0 + k);
         }
       }
       if (VB) {
@@ -139,33 +143,33 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
         const bool full = TB ? (gn < g.N && gk + 3 < kend) : (gk < kend && gn + 3 < g.N);
         if (full) {
           const float4 x = *reinterpret_cast<const float4*>(TB ? Bp + (long)gn * g.ldb + gk : Bp + (long)gk * g.ldb + gn);
-          rb[4 * v] = x.x; rb[4 * v + 1] = x.y; rb[4 * v + 2] = x.z; rb[4 * v + 3] = x.w;
+          xb[4 * v] = x.x; xb[4 * v + 1] = x.y; xb[4 * v + 2] = x.z; xb[4 * v + 3] = x.w;
         } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) rb[4 * v + i] = TB ? b_at(gn, gk + i) : b_at(gn + i, gk);
+          for (int i = 0; i < 4; ++i) xb[4 * v + i] = TB ? b_at(gn, gk + i) : b_at(gn + i, gk);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           int n, k;
           tile_idx<!TB, false>(tid, 4 * v + i, n, k);
-          rb[4 * v + i] = b_at(n0 + n, k0 + k);
+          xb[4 * v + i] = b_at(n0 + n, k0 + k);
         }
       }
     }
   };
-  auto store = [&]() {
+  auto store = [&](const float (&xa)[NE], const float (&xb)[NE]) {
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       int m, k;
       tile_idx<TA, VA>(tid, e, m, k);
-      As[k * LDS_STRIDE + m] = ra[e];
+      As[k * LDS_STRIDE + m] = xa[e];
     }
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       int n, k;
       tile_idx<!TB, VB>(tid, e, n, k);
-      Bs[k * LDS_STRIDE + n] = rb[e];
+      Bs[k * LDS_STRIDE + n] = xb[e];
     }
   };
 
@@ -176,25 +180,32 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fk = lane >> 4;
-  if (kbeg < kend) {
-    load(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-      store();
-      __syncthreads();
-      if (k0 + BK < kend) load(k0 + BK);
+  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
 #pragma unroll
-      for (int ks = 0; ks < BK / 4; ++ks) {
-        const int kk = ks * 4 + fk;
-        const float a0 = As[kk * LDS_STRIDE + wm * 32 + fr];
-        const float a1 = As[kk * LDS_STRIDE + wm * 32 + 16 + fr];
-        const float b0 = Bs[kk * LDS_STRIDE + wn * 32 + fr];
-        const float b1 = Bs[kk * LDS_STRIDE + wn * 32 + 16 + fr];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+  for (int p = 0; p < PD; ++p)
+    if (p < nk) load(kbeg + p * BK, ra[p], rb[p]);
+  for (int t0 = 0; t0 < nk; t0 += PD) {
+#pragma unroll
+    for (int s = 0; s < PD; ++s) {
+      const int t = t0 + s;
+      if (t < nk) {
+        store(ra[s], rb[s]);
+        __syncthreads();
+        if (t + PD < nk) load(kbeg + (t + PD) * BK, ra[s], rb[s]);
+#pragma unroll
+        for (int ks = 0; ks < BK / 4; ++ks) {
+          const int kk = ks * 4 + fk;
+          const float a0 = As[kk * LDS_STRIDE + wm * 32 + fr];
+          const float a1 = As[kk * LDS_STRIDE + wm * 32 + 16 + fr];
+          const float b0 = Bs[kk * LDS_STRIDE + wn * 32 + fr];
+          const float b1 = Bs[kk * LDS_STRIDE + wn * 32 + 16 + fr];
+          acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
 
@@ -249,12 +260,12 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
   if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool TA, bool TB, bool VA, bool VB>
+template <bool TA, bool TB, bool VA, bool VB, int PD>
 __global__ __launch_bounds__(256) void gemm_f32_mfma(GemmArgs g) {
   __shared__ float As[BK * LDS_STRIDE];
   __shared__ float Bs[BK * LDS_STRIDE];
   __shared__ int last;
-  gemm_f32_tile<TA, TB, VA, VB>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, As, Bs, &last);
+  gemm_f32_tile<TA, TB, VA, VB, PD>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, As, Bs, &last);
 }
 
 // Grouped launch: up to GROUP_MAX independent problems in one grid (a horizontal fusion of GEMMs that
@@ -296,6 +307,7 @@ __device__ __forceinline__ GroupSel group_select(const GemmGroup& G, int b) {
   return s;
 }
 
+template <int PD>
 __global__ __launch_bounds__(256) void gemm_f32_group(GemmGroup G) {
   __shared__ float As[BK * LDS_STRIDE];
   __shared__ float Bs[BK * LDS_STRIDE];
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(256) void gemm_f32_group(GemmGroup G) {
   const int bx = local % tn, by = (local / tn) % tm, bz = local / (tn * tm);
   const GemmArgs& g = s.g;
 #define VC_TILE(V_, TA_, TB_, VA_, VB_) \
-  case V_: gemm_f32_tile<TA_, TB_, VA_, VB_>(g, bx, by, bz, tn, tm, As, Bs, &last); break;
+  case V_: gemm_f32_tile<TA_, TB_, VA_, VB_, PD>(g, bx, by, bz, tn, tm, As, Bs, &last); break;
   switch (s.variant) {
     VC_TILE(0, false, false, false, false) VC_TILE(1, false, false, false, true)
     VC_TILE(2, false, false, true, false) VC_TILE(3, false, false, true, true)
@@ -933,11 +945,23 @@ static LegacyPlan plan_legacy(int transA, int transB, int M, int N, int K, float
   return pl;
 }
 
-static int launch_plan(const LegacyPlan& pl, hipStream_t stream) {
+// register sets of staged k-tiles in the k-major kernel (VITCNN_GEMM_PD = 1..4 for measurements; every
+// depth gives bit-identical results)
+static int legacy_pd() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VITCNN_GEMM_PD");
+    v = e ? std::max(1, std::min(4, atoi(e))) : 3;
+  }
+  return v;
+}
+
+template <int PD>
+static int launch_plan_pd(const LegacyPlan& pl, hipStream_t stream) {
   const GemmArgs& g = pl.g;
   dim3 grid(pl.tn, pl.tm, pl.nz), block(256);
 #define VC_L(V_, TA_, TB_, VA_, VB_) \
-  case V_: hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, VA_, VB_>), grid, block, 0, stream, g); break;
+  case V_: hipLaunchKernelGGL((gemm_f32_mfma<TA_, TB_, VA_, VB_, PD>), grid, block, 0, stream, g); break;
   switch (pl.variant) {
     VC_L(0, false, false, false, false) VC_L(1, false, false, false, true)
     VC_L(2, false, false, true, false) VC_L(3, false, false, true, true)
@@ -956,6 +980,15 @@ static int launch_plan(const LegacyPlan& pl, hipStream_t stream) {
     VC_CHECK_LAUNCH();
   }
   return VC_OK;
+}
+
+static int launch_plan(const LegacyPlan& pl, hipStream_t stream) {
+  switch (legacy_pd()) {
+    case 1: return launch_plan_pd<1>(pl, stream);
+    case 2: return launch_plan_pd<2>(pl, stream);
+    case 4: return launch_plan_pd<4>(pl, stream);
+    default: return launch_plan_pd<3>(pl, stream);
+  }
 }
 
 // ---- grouped launches (vc_gemm_group_begin / _end): the fp32 k-major problems issued in between
@@ -1002,7 +1035,12 @@ static int group_flush() {
   }
   G.start[n] = (int)total;
   VC_REQUIRE(total < (1L << 31) && rtotal < (1L << 31));
-  hipLaunchKernelGGL(gemm_f32_group, dim3((unsigned)total), dim3(256), 0, st.stream, G);
+  switch (legacy_pd()) {
+    case 1: hipLaunchKernelGGL(gemm_f32_group<1>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
+    case 2: hipLaunchKernelGGL(gemm_f32_group<2>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
+    case 4: hipLaunchKernelGGL(gemm_f32_group<4>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
+    default: hipLaunchKernelGGL(gemm_f32_group<3>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
+  }
   VC_CHECK_LAUNCH();
   if (R.n) {
     R.start[R.n] = (int)rtotal;
