@@ -156,8 +156,13 @@ def test_test_whole_image_production_batch_matches_reference_loop():
     rng = np.random.default_rng(17)
     W = H = 26
     P = 9
-    img1 = rng.random((W, H, 144), dtype=np.float32)
-    img2 = rng.random((W, H, 1), dtype=np.float32)
+    # a scene of 9 regions with their own band profiles (i.i.d. pixels would give every window the same
+    # class: the network's eval output barely depends on white noise), so the class indices vary
+    xx, yy = np.meshgrid(np.arange(W), np.arange(H), indexing="ij")
+    region = (xx * 3 // W) * 3 + (yy * 3 // H)
+    prof = rng.random((9, 144), dtype=np.float32)
+    img1 = (0.7 * prof[region] + 0.3 * rng.random((W, H, 144), dtype=np.float32)).astype(np.float32)
+    img2 = (region[:, :, None] / 9.0 + 0.1 * rng.random((W, H, 1))).astype(np.float32)
     sd = hash_state_dict()
     # running statistics away from their init values, so eval-mode BatchNorm normalises for real
     g = torch.Generator().manual_seed(3)
@@ -166,6 +171,7 @@ def test_test_whole_image_production_batch_matches_reference_loop():
             sd[k] = torch.rand(v.shape, generator=g) * 0.2 - 0.1
         elif k.endswith("running_var"):
             sd[k] = torch.rand(v.shape, generator=g) + 0.5
+    sd["classifier.bias"] = torch.zeros(16)
     model, _, _, hp = mu.get_model("Multimodality_Mamba", n_classes=16, n_bands=(144, 1), ignored_labels=[0],
                                    dataset="synthetic", device=torch.device(DEV))
     model.load_state_dict(sd)

@@ -945,13 +945,15 @@ static LegacyPlan plan_legacy(int transA, int transB, int M, int N, int K, float
   return pl;
 }
 
-// register sets of staged k-tiles in the k-major kernel (VITCNN_GEMM_PD = 1..4 for measurements; every
-// depth gives bit-identical results)
+// register sets of staged k-tiles in the k-major kernel: 1.  Deeper sets (bit-identical results) measured
+// slower on the whole step -- PD 1 / 2 / 3 / 4: 2.148 / 2.19 / 2.19 / 2.245 ms (round 3,
+// tools/ab_env.sh, profiles/r03_ab_gemm_pd.log): the extra VGPRs cost more occupancy than the earlier
+// loads save latency.  VITCNN_GEMM_PD=2 selects the two-set build for measurements.
 static int legacy_pd() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("VITCNN_GEMM_PD");
-    v = e ? std::max(1, std::min(4, atoi(e))) : 3;
+    v = e ? std::max(1, std::min(2, atoi(e))) : 1;
   }
   return v;
 }
@@ -983,12 +985,7 @@ static int launch_plan_pd(const LegacyPlan& pl, hipStream_t stream) {
 }
 
 static int launch_plan(const LegacyPlan& pl, hipStream_t stream) {
-  switch (legacy_pd()) {
-    case 1: return launch_plan_pd<1>(pl, stream);
-    case 2: return launch_plan_pd<2>(pl, stream);
-    case 4: return launch_plan_pd<4>(pl, stream);
-    default: return launch_plan_pd<3>(pl, stream);
-  }
+  return legacy_pd() == 2 ? launch_plan_pd<2>(pl, stream) : launch_plan_pd<1>(pl, stream);
 }
 
 // ---- grouped launches (vc_gemm_group_begin / _end): the fp32 k-major problems issued in between
@@ -1035,12 +1032,8 @@ static int group_flush() {
   }
   G.start[n] = (int)total;
   VC_REQUIRE(total < (1L << 31) && rtotal < (1L << 31));
-  switch (legacy_pd()) {
-    case 1: hipLaunchKernelGGL(gemm_f32_group<1>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
-    case 2: hipLaunchKernelGGL(gemm_f32_group<2>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
-    case 4: hipLaunchKernelGGL(gemm_f32_group<4>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
-    default: hipLaunchKernelGGL(gemm_f32_group<3>, dim3((unsigned)total), dim3(256), 0, st.stream, G); break;
-  }
+  if (legacy_pd() == 2) hipLaunchKernelGGL(gemm_f32_group<2>, dim3((unsigned)total), dim3(256), 0, st.stream, G);
+  else hipLaunchKernelGGL(gemm_f32_group<1>, dim3((unsigned)total), dim3(256), 0, st.stream, G);
   VC_CHECK_LAUNCH();
   if (R.n) {
     R.start[R.n] = (int)rtotal;

@@ -258,6 +258,35 @@ class Multimodality_Mamba(nn.Module):
         in one of these two tensors (one broadcast each for data-parallel buffer sync)."""
         return self._bflat, self._iflat
 
+    def _state_layout(self):
+        """(key, buffer kind, offset, shape, numel) in state_dict() order, and state_dict's metadata"""
+        lay = getattr(self, "_sd_layout", None)
+        if lay is None:
+            sd = nn.Module.state_dict(self)
+            rows = []
+            for k, v in sd.items():
+                kind = "p" if k in self._poff else ("b" if k in self._boff else "i")
+                off = (self._poff if kind == "p" else self._boff if kind == "b" else self._ioff)[k]
+                rows.append((k, kind, off, tuple(v.shape), v.numel()))
+            lay = (rows, getattr(sd, "_metadata", None))
+            object.__setattr__(self, "_sd_layout", lay)
+        return lay
+
+    def snapshot_state_dict(self, device=None):
+        """state_dict() -- same keys, order, shapes and metadata -- whose values are views of ONE copy of
+        each flat buffer (three device copies instead of 1704 tensor copies): train()'s best-state copy
+        (model_utils.py:1017 deep-copies the state_dict every improving epoch) and save_model (one
+        device-to-host transfer).  `device`: where the copy goes (default: the model's device)."""
+        from collections import OrderedDict
+        rows, meta = self._state_layout()
+        src = {}
+        for kind, t in (("p", self._flat_store.detach()), ("b", self._bflat), ("i", self._iflat)):
+            src[kind] = t.clone() if device is None else t.to(device, copy=True)
+        out = OrderedDict((k, src[kind][o:o + n].view(shape)) for k, kind, o, shape, n in rows)
+        if meta is not None:
+            out._metadata = meta
+        return out
+
     def zero_grad(self, set_to_none: bool = True):
         super().zero_grad(set_to_none=set_to_none)
         if set_to_none:
