@@ -13,7 +13,7 @@ import bench  # noqa: E402
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    out = bench.fusat_leg(torch.device("cuda", 0), steps, False)
+    out, _ = bench.fusat_leg(torch.device("cuda", 0), steps, False)
     print(json.dumps(out), flush=True)
 
 
