@@ -162,6 +162,24 @@ VC_API int vc_conv3x3_wgrad(int B, int H, int W, int C, int O, int pad, const fl
                             float beta, float* dweight, float* dbias, float* ws, long ws_floats, hipStream_t stream);
 VC_API int vc_conv3x3_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy, const float* weight,
                             float beta, float* dx, long lddx, float* ws, long ws_floats, hipStream_t stream);
+/* FusAtNet's 3x3 convs (FusAtNet.py:10-62, :168-186; stride 1, pad 0 or 1, channels-last rows) as
+ * implicit GEMMs over a TAP-MAJOR contraction index k = tap * C + c (conv_tap.hip): operand tiles are
+ * row gathers (one input row per output pixel and tap), no im2col matrix, no col2im.  Weights in
+ * tap-major layouts made by vc_conv3x3_pack from the torch layout w [O][C][3][3]:
+ *   mode 0: Wt [O][9][C] (fwd; also the layout of wgrad's output)   mode 1: W2 [9][O][C] (dgrad)
+ *   mode 2: w = beta w + Wt unpacked (a tap-major weight gradient back to the torch layout)
+ *   fwd:   y [B*OH*OW] (ld ldy) = conv(x) + bias (bias may be null)
+ *   wgrad: dWt [O][9][C] = sum over output pixels of dy x (overwritten; the bias gradient is colsum(dy))
+ *   dgrad: dx (ld lddx) = beta dx + the conv's input gradient for dy
+ * ws: split-K slabs when the tile grid is small (fixed-order sums; may be null: no split). */
+VC_API int vc_conv3x3_pack(int O, int C, int mode, const float* src, float* dst, float beta, hipStream_t stream);
+VC_API int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* wt,
+                              const float* bias, float* y, long ldy, float* ws, long ws_floats, hipStream_t stream);
+VC_API int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* dy,
+                                long lddy, float* dwt, float* ws, long ws_floats, hipStream_t stream);
+VC_API int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,
+                                const float* w2, float beta, float* dx, long lddx, float* ws, long ws_floats,
+                                hipStream_t stream);
 /* gradient of vc_im2col3x3 w.r.t. its (post-BN) input, gather form: dx [B,H,W,C] overwritten */
 VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx, hipStream_t stream);
 

@@ -206,3 +206,35 @@ def test_fusat_fused_adam_matches_torch_adam():
     named = dict(m.named_parameters())
     for p, k in zip(ref_params, ref):
         assert torch.allclose(named[k].detach(), p.detach(), rtol=1e-5, atol=1e-6), k
+
+
+@pytest.mark.gpu
+def test_fusat_trains_with_the_reference_torch_adam():
+    """the reference's own optimizer, torch.optim.Adam(model.parameters()) (model_utils.py:
+    109-118), trains the flat-buffer model: after backward every parameter's .grad is a view of the flat
+    gradient, so two torch-Adam steps equal two fused-Adam steps on an identical replica."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vitcnn_amd.losses import CrossEntropyLoss
+    from vitcnn_amd.optim import AdamW
+    a, b = _seeded().to("cuda").train(), _seeded().to("cuda").train()
+    topt = torch.optim.Adam(a.parameters(), lr=1e-3)
+    fopt = AdamW(b.parameters(), lr=1e-3, weight_decay=0.0)
+    g = torch.Generator().manual_seed(5)
+    x1, x2 = torch.rand(8, 144, 11, 11, generator=g).cuda(), torch.rand(8, 1, 11, 11, generator=g).cuda()
+    t = torch.randint(1, 16, (8,), generator=g).cuda()
+    crit = CrossEntropyLoss(weight=torch.ones(16, device="cuda"))
+    for _ in range(2):
+        for m, opt in ((a, topt), (b, fopt)):
+            opt.zero_grad()
+            crit(m(x1, x2), t).backward()
+            opt.step()
+    torch.cuda.synchronize()
+    pa = dict(a.named_parameters())
+    assert all(p.grad is not None for p in pa.values())
+    init = _seeded().state_dict()
+    moved = 0
+    for k, p in b.named_parameters():
+        assert torch.allclose(pa[k].detach(), p.detach(), rtol=1e-5, atol=1e-6), k
+        moved += int(not torch.equal(p.detach().cpu(), init[k]))
+    assert moved > 0

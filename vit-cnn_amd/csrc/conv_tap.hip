@@ -1,0 +1,379 @@
+// FusAtNet's 3x3 convolutions (stride 1, padding 0 or 1; FusAtNet.py:10-62 ConvUnit / ConvUnit_NP /
+// Residual_Unit, :168-186) as implicit GEMMs over a TAP-MAJOR contraction index k = tap * C + c.
+//
+// The im2col formulation (vc_im2col3x3_pad + vc_gemm) orders k channel-major (c * 9 + tap, the
+// torch weight layout), so every k-tile of the col matrix mixes channels and taps and has to be
+// materialised: for the 2193-channel concat of the fusion module that is 611 MB written and read
+// per conv, plus a col2im scatter in the backward.  With k tap-major, a k-tile of 32 consecutive k
+// is 32 consecutive channels of ONE tap, i.e. for every output pixel a contiguous 128-B piece of
+// one channels-last input row: the operand tile is a row GATHER with one address per row and tap,
+// loaded as float4s like a plain matrix.  No col matrix and no col2im: the data gradient is the
+// same gather over the output gradient with the mirrored tap offsets.  The weights are repacked
+// tap-major once per step (vc_conv3x3_pack).
+//
+//   fwd   : y[p][o]        = b[o] + sum_{tap,c} x[in(p,tap)][c] Wt[o][tap][c]      M = pixels, N = O,  K = 9C
+//   wgrad : dWt[o][tap][c] = sum_p dy[p][o] x[in(p,tap)][c]                        M = O, N = 9C,      K = pixels
+//   dgrad : dx[q][c]      (+)= sum_{tap,o} dy[out(q,tap)][o] W2[tap][o][c]         M = pixels, N = C,  K = 9O
+//
+// Block = 256 threads = 4 waves (2 x 2) over a 128 x 128 output tile, each wave 64 x 64 = 2 x 2
+// tiles of v_mfma_f32_32x32x2_f32 (f32 operands, exact f32 fma chains; 64-cycle issue; four
+// independent accumulators per wave).  k-tiles of 32 go through LDS as k-major images [k][row], so a
+// fragment read is 32 consecutive rows per half-wave (conflict-free): operands whose source rows are
+// k-contiguous are transposed by scalar stores into a pitch-129 image (a 32-lane group's 8 k-chunks x
+// 4 rows land in 32 distinct banks), k-outer sources are stored as float4s into a pitch-132 image.
+// One register set of the next k-tile's loads is in flight behind the MFMAs.  Against the 64 x 64
+// im2col GEMM the 128 x 128 tile halves the operand bytes per flop (the long-K convs were
+// operand-bandwidth-bound at ~50 TF/s).
+#include "common.h"
+
+namespace {
+
+constexpr int TM = 128, TN = 128, TK = 32;
+constexpr int PK = 129;   // LDS pitch of images transposed from k-contiguous rows
+constexpr int PO = 132;   // LDS pitch of images stored from k-outer rows
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum { FWD = 0, WGRAD = 1, DGRAD = 2 };
+
+struct TapArgs {
+  int H, W, C, O, pad, OH, OW;
+  int M, N;                // GEMM output extents (N: total output columns; wgrad 9C)
+  int P;                   // wgrad: number of output pixels (the contraction)
+  int nk;                  // k-tiles in all
+  int tpt;                 // fwd / dgrad: k-tiles per tap; wgrad: n-tiles per tap
+  int kper;                // k-tiles per split slice
+  const float* x;  long ldx;     // input activations (fwd, wgrad), channels-last rows
+  const float* dy; long lddy;    // output gradient (wgrad, dgrad), channels-last rows
+  const float* w;                // fwd: Wt [O][9][C]; dgrad: W2 [9][O][C]
+  const float* bias;             // fwd (optional)
+  float* out; long ldo;          // fwd: y [M][ldo]; wgrad: dWt [O][9C] (ldo = 9C); dgrad: dx [M][ldo]
+  float beta;                    // dgrad: dx = beta dx + ...
+  float* part;                   // split-K slabs [nsplit][M][N]
+  int vx, vdy, vw;               // float4 loads allowed (16-B aligned base, ld % 4 == 0)
+  FastDiv fOW, fOHW, fW, fHW;
+};
+
+__device__ __forceinline__ int tap_di(int tap) { return tap >= 6 ? 2 : (tap >= 3 ? 1 : 0); }
+
+// the output-pixel decomposition (fwd rows, wgrad k) and the input-pixel one (dgrad rows)
+__device__ __forceinline__ void split_out(const TapArgs& a, int p, int& b, int& i, int& j) {
+  int r1;
+  b = fdivmod(p, a.fOHW, r1);
+  i = fdivmod(r1, a.fOW, j);
+}
+__device__ __forceinline__ void split_in(const TapArgs& a, int q, int& b, int& i, int& j) {
+  int r1;
+  b = fdivmod(q, a.fHW, r1);
+  i = fdivmod(r1, a.fW, j);
+}
+// input row of output pixel (b, i, j) through tap t, -1 outside the (padded) image
+__device__ __forceinline__ int in_row(const TapArgs& a, int b, int i, int j, int tap) {
+  const int di = tap_di(tap), dj = tap - 3 * di;
+  const int y = i + di - a.pad, x = j + dj - a.pad;
+  return (b >= 0 && y >= 0 && y < a.H && x >= 0 && x < a.W) ? (b * a.H + y) * a.W + x : -1;
+}
+// output row reading input pixel (b, i, j) through tap t, -1 if none
+__device__ __forceinline__ int out_row(const TapArgs& a, int b, int i, int j, int tap) {
+  const int di = tap_di(tap), dj = tap - 3 * di;
+  const int y = i - di + a.pad, x = j - dj + a.pad;
+  return (b >= 0 && y >= 0 && y < a.OH && x >= 0 && x < a.OW) ? (b * a.OH + y) * a.OW + x : -1;
+}
+
+// 4 consecutive floats of row `row` (ld `ld`) from column c, columns >= cend read 0; row < 0 -> 0
+__device__ __forceinline__ void load4(const float* base, long ld, int row, int c, int cend, bool vec, float* v) {
+  if (row < 0) {
+    v[0] = v[1] = v[2] = v[3] = 0.f;
+    return;
+  }
+  const float* p = base + (long)row * ld + c;
+  if (vec && c + 3 < cend) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = c + e < cend ? p[e] : 0.f;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void conv_tap(TapArgs a) {
+  constexpr int PA = MODE == WGRAD ? PO : PK;   // A: dy^T (k-outer) for wgrad, row gathers (k-contiguous) else
+  constexpr int PB = MODE == FWD ? PK : PO;     // B: Wt rows (k-contiguous) for fwd, k-outer else
+  __shared__ __attribute__((aligned(16))) float As[TK * PA];
+  __shared__ __attribute__((aligned(16))) float Bs[TK * PB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, l31 = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.y * TM;
+  const int nt = blockIdx.x;
+  const int kt0 = blockIdx.z * a.kper, kt1 = min(a.nk, kt0 + a.kper);
+  const int ntap = MODE == WGRAD ? nt / a.tpt : 0;                       // wgrad: the n-tile's tap
+  const int n0 = MODE == WGRAD ? (nt - ntap * a.tpt) * TN : nt * TN;      // first channel / column
+  const int Kt = MODE == FWD ? a.C : a.O;                                  // per-tap k extent (fwd, dgrad)
+
+  // k-contiguous staging: rows kr + 32 i, k-chunk kc (4 consecutive k); k-outer staging: k rows
+  // ok + 8 i, column chunk oc (4 consecutive columns)
+  const int kr = tid >> 3, kc = tid & 7;
+  const int ok = tid >> 5, oc = tid & 31;
+  // fwd / dgrad: this thread's 4 gathered A rows, decomposed once (b = -1: past the last row)
+  int rb_[4], ri_[4], rj_[4];
+  if constexpr (MODE != WGRAD) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = m0 + kr + 32 * i;
+      if (r < a.M) {
+        if (MODE == FWD) split_out(a, r, rb_[i], ri_[i], rj_[i]);
+        else split_in(a, r, rb_[i], ri_[i], rj_[i]);
+      } else {
+        rb_[i] = -1; ri_[i] = rj_[i] = 0;
+      }
+    }
+  }
+
+  float ra[16], rbv[16];
+  auto load = [&](int kt) {
+    if constexpr (MODE == WGRAD) {
+      const int p0 = kt * TK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = p0 + ok + 8 * i;
+        // A(m = o, k = p) = dy[p][o]
+        load4(a.dy, a.lddy, p < a.P ? p : -1, m0 + 4 * oc, a.O, a.vdy, ra + 4 * i);
+        // B(k = p, n = (tap, c)) = x[in(p, tap)][c]
+        int row = -1;
+        if (p < a.P) {
+          int b, y, x;
+          split_out(a, p, b, y, x);
+          row = in_row(a, b, y, x, ntap);
+        }
+        load4(a.x, a.ldx, row, n0 + 4 * oc, a.C, a.vx, rbv + 4 * i);
+      }
+    } else {
+      const int tap = kt / a.tpt, c0 = (kt - tap * a.tpt) * TK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (MODE == FWD) {
+          const int row = in_row(a, rb_[i], ri_[i], rj_[i], tap);
+          load4(a.x, a.ldx, row, c0 + 4 * kc, Kt, a.vx, ra + 4 * i);
+          // B(k = (tap, c), n = o) = Wt[o][tap][c]: rows o = n0 + kr + 32 i
+          const int o = n0 + kr + 32 * i;
+          load4(a.w + (long)tap * a.C, 9L * a.C, o < a.O ? o : -1, c0 + 4 * kc, a.C, a.vw, rbv + 4 * i);
+        } else {
+          const int row = out_row(a, rb_[i], ri_[i], rj_[i], tap);
+          load4(a.dy, a.lddy, row, c0 + 4 * kc, Kt, a.vdy, ra + 4 * i);
+          // B(k = (tap, o), n = c) = W2[tap][o][c]: k rows o = c0 + ok + 8 i
+          const int o = c0 + ok + 8 * i;
+          load4(a.w + (long)tap * a.O * a.C, a.C, o < a.O ? o : -1, n0 + 4 * oc, a.C, a.vw, rbv + 4 * i);
+        }
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (MODE == WGRAD) {
+        *reinterpret_cast<float4*>(As + (ok + 8 * i) * PA + 4 * oc) =
+            make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[(4 * kc + e) * PA + kr + 32 * i] = ra[4 * i + e];
+      }
+      if constexpr (MODE == FWD) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Bs[(4 * kc + e) * PB + kr + 32 * i] = rbv[4 * i + e];
+      } else {
+        *reinterpret_cast<float4*>(Bs + (ok + 8 * i) * PB + 4 * oc) =
+            make_float4(rbv[4 * i], rbv[4 * i + 1], rbv[4 * i + 2], rbv[4 * i + 3]);
+      }
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (kt0 < kt1) {
+    load(kt0);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      store();
+      __syncthreads();
+      if (kt + 1 < kt1) load(kt + 1);
+#pragma unroll
+      for (int ks = 0; ks < TK / 2; ++ks) {
+        const int k = 2 * ks + h;
+        const float a0 = As[k * PA + wm * 64 + l31];
+        const float a1 = As[k * PA + wm * 64 + 32 + l31];
+        const float b0 = Bs[k * PB + wn * 64 + l31];
+        const float b1 = Bs[k * PB + wn * 64 + 32 + l31];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+
+  // C/D of 32x32: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int cl = n0 + wn * 64 + ni * 32 + l31;         // column within the tile's range
+        int col;
+        bool ok_ = row < a.M;
+        if (MODE == WGRAD) {
+          ok_ = ok_ && cl < a.C;
+          col = ntap * a.C + cl;
+        } else {
+          ok_ = ok_ && cl < (MODE == FWD ? a.O : a.C);
+          col = cl;
+        }
+        if (!ok_) continue;
+        const float v = acc[mi][ni][r];
+        if (split) {
+          a.part[((long)blockIdx.z * a.M + row) * a.N + col] = v;
+        } else {
+          float* o = a.out + (long)row * a.ldo + col;
+          if (MODE == FWD) *o = v + (a.bias ? a.bias[col] : 0.f);
+          else if (MODE == DGRAD) *o = (a.beta != 0.f ? a.beta * *o : 0.f) + v;
+          else *o = v;
+        }
+      }
+}
+
+// split-K combine in fixed slice order, then the mode's epilogue
+template <int MODE>
+__global__ __launch_bounds__(256) void conv_tap_reduce(TapArgs a, int nsplit) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)a.M * a.N) return;
+  const int row = (int)(e / a.N), col = (int)(e - (long)row * a.N);
+  const long slab = (long)a.M * a.N;
+  float s = 0.f;
+  for (int z = 0; z < nsplit; ++z) s += a.part[z * slab + e];
+  float* o = a.out + (long)row * a.ldo + col;
+  if (MODE == FWD) *o = s + (a.bias ? a.bias[col] : 0.f);
+  else if (MODE == DGRAD) *o = (a.beta != 0.f ? a.beta * *o : 0.f) + s;
+  else *o = s;
+}
+
+// weight layouts: w [O][C][9] (torch) <-> Wt [O][9][C] (mode 0) / W2 [9][O][C] (mode 1);
+// mode 2: w = beta w + unpack(Wt)
+__global__ __launch_bounds__(256) void conv_pack(int O, int C, int mode, const float* __restrict__ src,
+                                                 float* __restrict__ dst, float beta) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)O * C * 9;
+  if (e >= n) return;
+  // e indexes the torch layout: o, c, tap
+  const int tap = (int)(e % 9);
+  const long oc_ = e / 9;
+  const int c = (int)(oc_ % C), o = (int)(oc_ / C);
+  if (mode == 0) dst[((long)o * 9 + tap) * C + c] = src[e];
+  else if (mode == 1) dst[((long)tap * O + o) * C + c] = src[e];
+  else dst[e] = (beta != 0.f ? beta * dst[e] : 0.f) + src[((long)o * 9 + tap) * C + c];
+}
+
+bool vec_ok(const float* p, long ld) { return p && ((uintptr_t)p % 16 == 0) && (ld % 4 == 0); }
+
+template <int MODE>
+int launch_tap(TapArgs& a, int grid_n, int grid_m, float* ws, long ws_floats, hipStream_t stream) {
+  const long tiles = (long)grid_n * grid_m;
+  int nsplit = 1;
+  if (ws && tiles < 384 && a.nk >= 8) {
+    nsplit = (int)std::min<long>((768 + tiles - 1) / tiles, a.nk / 4);
+    while (nsplit > 1 && (long)nsplit * a.M * a.N > ws_floats) --nsplit;
+    nsplit = std::max(nsplit, 1);
+  }
+  a.kper = vc_cdiv(a.nk, nsplit);
+  nsplit = vc_cdiv(a.nk, a.kper);
+  a.part = nsplit > 1 ? ws : nullptr;
+  VC_REQUIRE(grid_m < 65536 && nsplit < 65536);
+  hipLaunchKernelGGL(conv_tap<MODE>, dim3(grid_n, grid_m, nsplit), dim3(256), 0, stream, a);
+  VC_CHECK_LAUNCH();
+  if (nsplit > 1) {
+    const long n = (long)a.M * a.N;
+    hipLaunchKernelGGL(conv_tap_reduce<MODE>, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, a, nsplit);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
+TapArgs geo(int B, int H, int W, int C, int O, int pad) {
+  TapArgs a{};
+  a.H = H; a.W = W; a.C = C; a.O = O; a.pad = pad;
+  a.OH = H + 2 * pad - 2; a.OW = W + 2 * pad - 2;
+  a.fOW = make_fastdiv(a.OW); a.fOHW = make_fastdiv(a.OH * a.OW);
+  a.fW = make_fastdiv(W); a.fHW = make_fastdiv(H * W);
+  (void)B;
+  return a;
+}
+
+}  // namespace
+
+VC_EXPORT int vc_conv3x3_pack(int O, int C, int mode, const float* src, float* dst, float beta, hipStream_t stream) {
+  VC_REQUIRE(O > 0 && C > 0 && mode >= 0 && mode <= 2 && src && dst);
+  const long n = (long)O * C * 9;
+  VC_REQUIRE_I32(n);
+  hipLaunchKernelGGL(conv_pack, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, O, C, mode, src, dst, beta);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_EXPORT int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* wt,
+                                 const float* bias, float* y, long ldy, float* ws, long ws_floats, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad && C > 0 && O > 0 && (pad == 0 || pad == 1));
+  VC_REQUIRE(x && wt && y && ldx >= C && ldy >= O);
+  TapArgs a = geo(B, H, W, C, O, pad);
+  a.M = B * a.OH * a.OW;
+  a.N = O;
+  VC_REQUIRE_I32((long)B * H * W * ldx);
+  VC_REQUIRE_I32((long)a.M * ldy);
+  a.tpt = vc_cdiv(C, TK);
+  a.nk = 9 * a.tpt;
+  a.x = x; a.ldx = ldx; a.w = wt; a.bias = bias; a.out = y; a.ldo = ldy;
+  a.vx = vec_ok(x, ldx); a.vw = vec_ok(wt, C);
+  return launch_tap<FWD>(a, vc_cdiv(O, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
+}
+
+VC_EXPORT int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
+                                   const float* dy, long lddy, float* dwt, float* ws, long ws_floats,
+                                   hipStream_t stream) {
+  VC_REQUIRE(B > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad && C > 0 && O > 0 && (pad == 0 || pad == 1));
+  VC_REQUIRE(x && dy && dwt && ldx >= C && lddy >= O);
+  TapArgs a = geo(B, H, W, C, O, pad);
+  a.M = O;
+  a.N = 9 * C;
+  a.P = B * a.OH * a.OW;
+  VC_REQUIRE_I32((long)B * H * W * ldx);
+  VC_REQUIRE_I32((long)a.P * lddy);
+  a.tpt = vc_cdiv(C, TN);
+  a.nk = vc_cdiv(a.P, TK);
+  a.x = x; a.ldx = ldx; a.dy = dy; a.lddy = lddy; a.out = dwt; a.ldo = 9L * C;
+  a.vx = vec_ok(x, ldx); a.vdy = vec_ok(dy, lddy);
+  return launch_tap<WGRAD>(a, 9 * a.tpt, vc_cdiv(O, TM), ws, ws_floats, stream);
+}
+
+VC_EXPORT int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,
+                                   const float* w2, float beta, float* dx, long lddx, float* ws, long ws_floats,
+                                   hipStream_t stream) {
+  VC_REQUIRE(B > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad && C > 0 && O > 0 && (pad == 0 || pad == 1));
+  VC_REQUIRE(dy && w2 && dx && lddy >= O && lddx >= C);
+  TapArgs a = geo(B, H, W, C, O, pad);
+  a.M = B * H * W;
+  a.N = C;
+  VC_REQUIRE_I32((long)a.M * lddx);
+  VC_REQUIRE_I32((long)B * a.OH * a.OW * lddy);
+  a.tpt = vc_cdiv(O, TK);
+  a.nk = 9 * a.tpt;
+  a.dy = dy; a.lddy = lddy; a.w = w2; a.out = dx; a.ldo = lddx; a.beta = beta;
+  a.vdy = vec_ok(dy, lddy); a.vw = vec_ok(w2, C);
+  return launch_tap<DGRAD>(a, vc_cdiv(C, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
+}

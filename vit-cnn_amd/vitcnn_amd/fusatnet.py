@@ -18,12 +18,18 @@ pooled-scale and product backwards); the parameter gradients land in one flat gr
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ._lib import lib
 from .flat import F32, FlatParams
 from .model import _IMPLICIT_CONV, N_COUNTERS
+
+# 3x3 convs: the tap-major implicit GEMM (vc_conv3x3_tap_*, conv_tap.hip) by default; VITCNN_FUSAT_IM2COL=1
+# restores the im2col + vc_gemm formulation of rounds 1-2 (measurements)
+_TAP_CONV = os.environ.get("VITCNN_FUSAT_IM2COL", "0") != "1"
 
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
 _COUNTER_BUFS = {}
@@ -242,15 +248,26 @@ class _Program:
                           bias_grad, self.scr.data_ptr(), self.SCRATCH, self.cnt, N_COUNTERS, self.s)
 
     def conv3(self, x, ldx, H, C, conv, pad):
-        """x [B,H,W,C] rows (ld ldx) -> conv3x3 + bias, [B,OH,OH,O] contiguous: vc_im2col3x3_pad + vc_gemm
-        (the im2col matrix is recomputed in the backward rather than kept), or the implicit GEMM
-        vc_conv3x3_* with VITCNN_IMPLICIT_CONV=1 (no col matrix; measured slower at B = 64)."""
+        """x [B,H,W,C] rows (ld ldx) -> conv3x3 + bias, [B,OH,OH,O] contiguous.
+
+        Default: the tap-major implicit GEMM (vc_conv3x3_tap_fwd / _wgrad / _dgrad): operand tiles are
+        gathered input rows, so neither an im2col matrix (611 MB for the 2193-channel concat) nor a
+        col2im pass exists; the weights are repacked tap-major per step (vc_conv3x3_pack, in the
+        captured graph) and the tap-major weight gradient unpacked into the flat gradient.
+        VITCNN_FUSAT_IM2COL=1: vc_im2col3x3_pad + vc_gemm (rounds 1-2); VITCNN_IMPLICIT_CONV=1 with it:
+        the element-gather implicit GEMM vc_conv3x3_*."""
         B, O = self.B, conv.out_channels
         OH = H + 2 * pad - 2
         M, K = B * OH * OH, C * 9
         L, scr = self.L, self.scr.data_ptr()
         y = self.new(B, OH, OH, O)
-        if _IMPLICIT_CONV:
+        if _TAP_CONV:
+            wt = self.new(O * K)
+            L.vc_conv3x3_pack(O, C, 0, conv.weight.data_ptr(), wt.data_ptr(), 0.0, self.s)
+            L.vc_conv3x3_tap_fwd(B, H, H, C, O, pad, x.data_ptr(), ldx, wt.data_ptr(), conv.bias.data_ptr(),
+                                 y.data_ptr(), O, scr, self.SCRATCH, self.s)
+            del wt
+        elif _IMPLICIT_CONV:
             L.vc_conv3x3_fwd(B, H, H, C, O, pad, x.data_ptr(), ldx, None, None, None, None, conv.weight.data_ptr(),
                              conv.bias.data_ptr(), 0, y.data_ptr(), O, scr, self.SCRATCH, self.s)
         else:
@@ -262,6 +279,18 @@ class _Program:
 
         def bwd():
             dy = self.grad_of(y)
+            if _TAP_CONV:
+                dwt = self.new(O * K)
+                L.vc_conv3x3_tap_wgrad(B, H, H, C, O, pad, x.data_ptr(), ldx, dy.data_ptr(), O, dwt.data_ptr(), scr,
+                                       self.SCRATCH, self.s)
+                L.vc_conv3x3_pack(O, C, 2, dwt.data_ptr(), self.pgrad(conv.weight), 0.0, self.s)
+                L.vc_colsum(M, O, dy.data_ptr(), O, self.pgrad(conv.bias), 0.0, scr, self.SCRATCH, self.s)
+                if id(x) not in self.no_grad_ids:
+                    w2 = dwt   # reused: the unpack above has read it (same stream)
+                    L.vc_conv3x3_pack(O, C, 1, conv.weight.data_ptr(), w2.data_ptr(), 0.0, self.s)
+                    L.vc_conv3x3_tap_dgrad(B, H, H, C, O, pad, dy.data_ptr(), O, w2.data_ptr(), 1.0,
+                                           self.grad_of(x).data_ptr(), ldx, scr, self.SCRATCH, self.s)
+                return
             if _IMPLICIT_CONV:
                 L.vc_conv3x3_wgrad(B, H, H, C, O, pad, x.data_ptr(), ldx, None, None, None, None, dy.data_ptr(), O,
                                    0.0, self.pgrad(conv.weight), self.pgrad(conv.bias), scr, self.SCRATCH, self.s)
@@ -387,27 +416,28 @@ class _Program:
         t = self.maxpool(t, H, 1024)
         Hp = H // 2
         Ct = c1 + c2 + 2048
-        cat = self.new(B, P, P, Ct)                                           # cat([x1, x2, Ms, Mt], 1)
+        Cp = (Ct + 3) // 4 * 4    # row stride of the concat: 16-B aligned rows (float4 gathers in conv_tap)
+        cat = self.new(B, P, P, Cp)                                           # cat([x1, x2, Ms, Mt], 1)
         self.cat = cat
-        L.vc_add2_2d(M, c1, x1.data_ptr(), c1, None, 0, cat.data_ptr(), Ct, 0.0, self.s)
-        L.vc_add2_2d(M, c2, x2.data_ptr(), c2, None, 0, cat.data_ptr() + F32 * c1, Ct, 0.0, self.s)
+        L.vc_add2_2d(M, c1, x1.data_ptr(), c1, None, 0, cat.data_ptr(), Cp, 0.0, self.s)
+        L.vc_add2_2d(M, c2, x2.data_ptr(), c2, None, 0, cat.data_ptr() + F32 * c1, Cp, 0.0, self.s)
         offs = F32 * (c1 + c2)
-        L.vc_pool_scale(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024, cat.data_ptr() + offs, Ct,
+        L.vc_pool_scale(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024, cat.data_ptr() + offs, Cp,
                         self.s)                                               # Ms
 
         def ms_bwd():
             dpooled = self.grad_of(t)
             L.vc_pool_scale_bwd(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024,
-                                self.grad_of(cat).data_ptr() + offs, Ct, self.grad_of(Fhs).data_ptr(), 1024,
+                                self.grad_of(cat).data_ptr() + offs, Cp, self.grad_of(Fhs).data_ptr(), 1024,
                                 dpooled.data_ptr(), self.s)
 
         self.record(ms_bwd, t, Fhs, cat)
         Sp = self.res_attention(x2, c2, P, c2, m.spatial_am)
         offt = F32 * (c1 + c2 + 1024)
-        self.mul(Sp, Fhs, M, 1024, cat.data_ptr() + offt, Ct,
-                 lambda: (self.grad_of(cat).data_ptr() + offt, Ct))           # Mt
-        Fm = self.six(cat, Ct, P, Ct, m.mfe)
-        Am = self.res_attention(cat, Ct, P, Ct, m.mam)
+        self.mul(Sp, Fhs, M, 1024, cat.data_ptr() + offt, Cp,
+                 lambda: (self.grad_of(cat).data_ptr() + offt, Cp))           # Mt
+        Fm = self.six(cat, Cp, P, Ct, m.mfe)
+        Am = self.res_attention(cat, Cp, P, Ct, m.mam)
         Fss = self.new(B, P, P, 1024) if self.grad else Fm
         self.mul(Fm, Am, M, 1024, Fss.data_ptr(), 1024, lambda: (self.grad_of(Fss).data_ptr(), 1024))
         self.keep[id(Fss)] = Fss
