@@ -166,7 +166,7 @@ VC_API int vc_conv3x3_dgrad(int B, int H, int W, int C, int O, int pad, const fl
  * implicit GEMMs over a TAP-MAJOR contraction index k = tap * C + c (conv_tap.hip): operand tiles are
  * row gathers (one input row per output pixel and tap), no im2col matrix, no col2im.  Weights in
  * tap-major layouts made by vc_conv3x3_pack from the torch layout w [O][C][3][3]:
- *   mode 0: Wt [O][9][C] (fwd; also the layout of wgrad's output)   mode 1: W2 [9][O][C] (dgrad)
+ *   mode 0: Wt [O][9][C] (fwd and dgrad; also the layout of wgrad's output)   mode 1: W2 [9][O][C]
  *   mode 2: w = beta w + Wt unpacked (a tap-major weight gradient back to the torch layout)
  *   fwd:   y [B*OH*OW] (ld ldy) = conv(x) + bias (bias may be null)
  *   wgrad: dWt [O][9][C] = sum over output pixels of dy x (overwritten; the bias gradient is colsum(dy))
@@ -178,7 +178,7 @@ VC_API int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, const 
 VC_API int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* dy,
                                 long lddy, float* dwt, float* ws, long ws_floats, hipStream_t stream);
 VC_API int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,
-                                const float* w2, float beta, float* dx, long lddx, float* ws, long ws_floats,
+                                const float* wt, float beta, float* dx, long lddx, float* ws, long ws_floats,
                                 hipStream_t stream);
 /* gradient of vc_im2col3x3 w.r.t. its (post-BN) input, gather form: dx [B,H,W,C] overwritten */
 VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx, hipStream_t stream);

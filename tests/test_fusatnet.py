@@ -109,7 +109,8 @@ def _flat_grads(m):
 def _backward_check(B, seed, ties=0):
     """HIP forward + backward at batch B vs torch autograd over the oracle (fp32) and a float64
     evaluation; every parameter gradient within 1e-3 of its norm (+1e-5 of the largest), or no worse
-    than 3x the fp32 reference's own error.  `ties`: how many tensors may instead sit within 3e-3 of
+    than 3x the fp32 reference's own error (at B = 4: its worst over ulp-level weight perturbations).
+    `ties`: how many tensors may instead sit within 3e-3 of
     their norm -- at B = 64 the classifier's last 3x3 conv (1x1 output, a train-mode BatchNorm over 64
     values per channel, then ReLU) has pre-activations within fp32 rounding of 0, and one flipped ReLU
     decision moves that conv's weight gradient (a sum over the 64 samples) by ~1.5e-3 of its norm; the
@@ -130,6 +131,19 @@ def _backward_check(B, seed, ties=0):
     params = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
     ref = O.forward(params, x1, x2, train=True)
     torch.nn.functional.cross_entropy(ref, t, weight=w).backward()
+    # the fp32 reference's own spread: at B = 4 (train-mode BatchNorm over 4 values per channel at the
+    # classifier's 1x1 output) a decision sits within fp32 rounding of its threshold -- weights moved by
+    # 1e-7 relative (about one ulp) move the CPU fp32 gradients from 4e-5 to 1.5e-3 / 3.5e-3 of their
+    # norm (every tensor below the classifier).  The yardstick is the worst of those reference runs.
+    spread = []
+    if B == 4:
+        for s in range(3):
+            gs = torch.Generator().manual_seed(s)
+            pp = {k: ((v * (1 + 1e-7 * torch.randn(v.shape, generator=gs, dtype=torch.float64).float()))
+                      if v.is_floating_point() and "running" not in k else v).clone()
+                      .requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+            torch.nn.functional.cross_entropy(O.forward(pp, x1, x2, train=True), t, weight=w).backward()
+            spread.append(pp)
     # float64 evaluation: the yardstick for "as accurate as the fp32 reference" (six train-mode
     # BatchNorms deep, the first convolution's weight gradient carries ~1e-3 relative fp32 noise)
     p64 = {k: (v.double() if v.is_floating_point() else v).clone().requires_grad_(v.is_floating_point() and
@@ -149,7 +163,7 @@ def _backward_check(B, seed, ties=0):
     for k, gk in grads.items():
         g64 = p64[k].grad
         err = float((gk.double() - g64).norm())
-        err32 = float((params[k].grad.double() - g64).norm())
+        err32 = max(float((r[k].grad.double() - g64).norm()) for r in [params] + spread)
         if not (err <= 1e-3 * float(g64.norm()) + 1e-5 * gmax or err <= 3.0 * err32 + 1e-5 * gmax):
             bad.append((k, err, err32, float(g64.norm())))
     if bad and os.path.isdir("gpurun_out"):

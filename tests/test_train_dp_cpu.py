@@ -166,6 +166,14 @@ def test_flat_model_exposes_per_parameter_grad_views():
     before = m.flat_params.detach().clone()
     opt.step()
     assert torch.allclose(before - m.flat_params.detach(), flat, rtol=1e-6, atol=1e-6)
+    # the torch optimizer's zero_grad (views -> None) also clears the flat gradient: the next backward
+    # starts from zero instead of accumulating onto the previous step's gradient
+    opt.zero_grad()
+    (m.flat_params * 2.0).sum().backward()
+    assert torch.equal(m.flat_params.grad, torch.full_like(flat, 2.0))
+    opt.zero_grad(set_to_none=False)
+    (m.flat_params * 3.0).sum().backward()
+    assert torch.equal(m.flat_params.grad, torch.full_like(flat, 3.0))
     # ViT-CNN: the never-used hsiMamba.tokenlearner / ln3 parameters get no gradient (as in the reference)
     v = Multimodality_Mamba(9, 1, 1, 144, 1, 32, 16)
     v.flat_params.sum().backward()

@@ -9,11 +9,11 @@
 // one channels-last input row: the operand tile is a row GATHER with one address per row and tap,
 // loaded as float4s like a plain matrix.  No col matrix and no col2im: the data gradient is the
 // same gather over the output gradient with the mirrored tap offsets.  The weights are repacked
-// tap-major once per step (vc_conv3x3_pack).
+// tap-major once per step (vc_conv3x3_pack); the backward reads the same repacked copy.
 //
 //   fwd   : y[p][o]        = b[o] + sum_{tap,c} x[in(p,tap)][c] Wt[o][tap][c]      M = pixels, N = O,  K = 9C
 //   wgrad : dWt[o][tap][c] = sum_p dy[p][o] x[in(p,tap)][c]                        M = O, N = 9C,      K = pixels
-//   dgrad : dx[q][c]      (+)= sum_{tap,o} dy[out(q,tap)][o] W2[tap][o][c]         M = pixels, N = C,  K = 9O
+//   dgrad : dx[q][c]      (+)= sum_{tap,o} dy[out(q,tap)][o] Wt[o][tap][c]         M = pixels, N = C,  K = 9O
 //
 // Block = 256 threads = 4 waves (2 x 2) over a 128 x 128 output tile, each wave 64 x 64 = 2 x 2
 // tiles of v_mfma_f32_32x32x2_f32 (f32 operands, exact f32 fma chains; 64-cycle issue; four
@@ -45,7 +45,7 @@ struct TapArgs {
   int kper;                // k-tiles per split slice
   const float* x;  long ldx;     // input activations (fwd, wgrad), channels-last rows
   const float* dy; long lddy;    // output gradient (wgrad, dgrad), channels-last rows
-  const float* w;                // fwd: Wt [O][9][C]; dgrad: W2 [9][O][C]
+  const float* w;                // Wt [O][9][C] (fwd, dgrad)
   const float* bias;             // fwd (optional)
   float* out; long ldo;          // fwd: y [M][ldo]; wgrad: dWt [O][9C] (ldo = 9C); dgrad: dx [M][ldo]
   float beta;                    // dgrad: dx = beta dx + ...
@@ -161,9 +161,10 @@ __global__ __launch_bounds__(256) void conv_tap(TapArgs a) {
         } else {
           const int row = out_row(a, rb_[i], ri_[i], rj_[i], tap);
           load4(a.dy, a.lddy, row, c0 + 4 * kc, Kt, a.vdy, ra + 4 * i);
-          // B(k = (tap, o), n = c) = W2[tap][o][c]: k rows o = c0 + ok + 8 i
+          // B(k = (tap, o), n = c) = Wt[o][tap][c] (the forward's layout read with row stride 9C):
+          // k rows o = c0 + ok + 8 i
           const int o = c0 + ok + 8 * i;
-          load4(a.w + (long)tap * a.O * a.C, a.C, o < a.O ? o : -1, n0 + 4 * oc, a.C, a.vw, rbv + 4 * i);
+          load4(a.w + (long)tap * a.C, 9L * a.C, o < a.O ? o : -1, n0 + 4 * oc, a.C, a.vw, rbv + 4 * i);
         }
       }
     }
@@ -285,12 +286,15 @@ bool vec_ok(const float* p, long ld) { return p && ((uintptr_t)p % 16 == 0) && (
 
 template <int MODE>
 int launch_tap(TapArgs& a, int grid_n, int grid_m, float* ws, long ws_floats, hipStream_t stream) {
+  // split K so the grid fills one round of resident blocks (256 CUs x 3 blocks: 164 VGPRs, 34 KB LDS)
+  // without a ragged second round; slices of >= 4 k-tiles; the slabs must fit the workspace
   const long tiles = (long)grid_n * grid_m;
   int nsplit = 1;
-  if (ws && tiles < 384 && a.nk >= 8) {
-    nsplit = (int)std::min<long>((768 + tiles - 1) / tiles, a.nk / 4);
+  static const char* no_split = getenv("VITCNN_TAP_NOSPLIT");
+  if (no_split && atoi(no_split)) ws = nullptr;
+  if (ws && tiles < 768 && a.nk >= 8) {
+    nsplit = (int)std::max<long>(1, std::min<long>(768 / tiles, a.nk / 4));
     while (nsplit > 1 && (long)nsplit * a.M * a.N > ws_floats) --nsplit;
-    nsplit = std::max(nsplit, 1);
   }
   a.kper = vc_cdiv(a.nk, nsplit);
   nsplit = vc_cdiv(a.nk, a.kper);
@@ -362,10 +366,10 @@ VC_EXPORT int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, c
 }
 
 VC_EXPORT int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,
-                                   const float* w2, float beta, float* dx, long lddx, float* ws, long ws_floats,
+                                   const float* wt, float beta, float* dx, long lddx, float* ws, long ws_floats,
                                    hipStream_t stream) {
   VC_REQUIRE(B > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad && C > 0 && O > 0 && (pad == 0 || pad == 1));
-  VC_REQUIRE(dy && w2 && dx && lddy >= O && lddx >= C);
+  VC_REQUIRE(dy && wt && dx && lddy >= O && lddx >= C);
   TapArgs a = geo(B, H, W, C, O, pad);
   a.M = B * H * W;
   a.N = C;
@@ -373,7 +377,7 @@ VC_EXPORT int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, c
   VC_REQUIRE_I32((long)B * a.OH * a.OW * lddy);
   a.tpt = vc_cdiv(O, TK);
   a.nk = 9 * a.tpt;
-  a.dy = dy; a.lddy = lddy; a.w = w2; a.out = dx; a.ldo = lddx; a.beta = beta;
-  a.vdy = vec_ok(dy, lddy); a.vw = vec_ok(w2, C);
+  a.dy = dy; a.lddy = lddy; a.w = wt; a.out = dx; a.ldo = lddx; a.beta = beta;
+  a.vdy = vec_ok(dy, lddy); a.vw = vec_ok(wt, C);
   return launch_tap<DGRAD>(a, vc_cdiv(C, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
 }

@@ -46,14 +46,28 @@ def expose_grad_views(model):
 
 
 def install_grad_views(model):
-    """Register expose_grad_views as the flat buffer's post-accumulate hook (autograd backward)."""
+    """Register expose_grad_views as the flat buffer's post-accumulate hook (autograd backward), and a
+    pre-accumulate hook that honours a torch optimizer's zero_grad(): that clears the per-parameter
+    views (grad = None) but cannot see the flat gradient, which autograd would otherwise keep
+    accumulating into -- so a flat gradient whose views were cleared is dropped before the new one
+    lands (zero_grad(set_to_none=False) zeroes the views, i.e. the flat gradient, in place)."""
     me = weakref.ref(model)
+
+    def pre(_g):
+        m = me()
+        if m is not None and getattr(m, "_grad_views", True) and m._flat_store.grad is not None:
+            names = m._pnames if hasattr(m, "_pnames") else list(m._pmods)
+            mod, pn = m._pmods[names[0]]
+            if mod._parameters[pn].grad is None:
+                m._flat_store.grad = None
+        return None
 
     def hook(_t):
         m = me()
         if m is not None:
             expose_grad_views(m)
 
+    model._flat_store.register_hook(pre)
     model._flat_store.register_post_accumulate_grad_hook(hook)
 
 

@@ -200,7 +200,8 @@ class _FusAtNetFunction(torch.autograd.Function):
 
 
 class _Program:
-    SCRATCH = 1 << 22
+    # floats: split-K slabs of the tap-major conv GEMMs (up to ~50 MB at B = 64)
+    SCRATCH = 1 << int(os.environ.get("VITCNN_FUSAT_SCRATCH_LOG2", "26"))
 
     def __init__(self, m: FusAtNet, x1, x2, grad: bool):
         self.m, self.L, self.dev = m, lib(), x1.device
@@ -261,12 +262,12 @@ class _Program:
         M, K = B * OH * OH, C * 9
         L, scr = self.L, self.scr.data_ptr()
         y = self.new(B, OH, OH, O)
+        wt = None
         if _TAP_CONV:
-            wt = self.new(O * K)
+            wt = self.new(O * K)     # tap-major copy of the weight, read again by the data gradient
             L.vc_conv3x3_pack(O, C, 0, conv.weight.data_ptr(), wt.data_ptr(), 0.0, self.s)
             L.vc_conv3x3_tap_fwd(B, H, H, C, O, pad, x.data_ptr(), ldx, wt.data_ptr(), conv.bias.data_ptr(),
                                  y.data_ptr(), O, scr, self.SCRATCH, self.s)
-            del wt
         elif _IMPLICIT_CONV:
             L.vc_conv3x3_fwd(B, H, H, C, O, pad, x.data_ptr(), ldx, None, None, None, None, conv.weight.data_ptr(),
                              conv.bias.data_ptr(), 0, y.data_ptr(), O, scr, self.SCRATCH, self.s)
@@ -286,9 +287,7 @@ class _Program:
                 L.vc_conv3x3_pack(O, C, 2, dwt.data_ptr(), self.pgrad(conv.weight), 0.0, self.s)
                 L.vc_colsum(M, O, dy.data_ptr(), O, self.pgrad(conv.bias), 0.0, scr, self.SCRATCH, self.s)
                 if id(x) not in self.no_grad_ids:
-                    w2 = dwt   # reused: the unpack above has read it (same stream)
-                    L.vc_conv3x3_pack(O, C, 1, conv.weight.data_ptr(), w2.data_ptr(), 0.0, self.s)
-                    L.vc_conv3x3_tap_dgrad(B, H, H, C, O, pad, dy.data_ptr(), O, w2.data_ptr(), 1.0,
+                    L.vc_conv3x3_tap_dgrad(B, H, H, C, O, pad, dy.data_ptr(), O, wt.data_ptr(), 1.0,
                                            self.grad_of(x).data_ptr(), ldx, scr, self.SCRATCH, self.s)
                 return
             if _IMPLICIT_CONV:
@@ -308,7 +307,7 @@ class _Program:
             self.gemm(0, 0, M, K, O, dy.data_ptr(), O, conv.weight.data_ptr(), K, 0.0, dcol.data_ptr(), K)
             L.vc_col2im3x3_pad(B, H, H, C, pad, dcol.data_ptr(), self.grad_of(x).data_ptr(), ldx, 1, self.s)
 
-        self.record(bwd, x, y)
+        self.record(bwd, x, y) if wt is None else self.record(bwd, x, y, wt)
         return y, OH
 
     def bn_relu(self, y, M, C, bn, relu=1):
