@@ -40,6 +40,9 @@ def _rel(a, b):
     (4, 11, 144, 256, 1, 144),     # FusAtNet B = 4: the HSI branches' first conv
     (4, 11, 1024, 256, 0, 1024),   # FusAtNet B = 4: the classifier's first (valid) conv
     (4, 3, 256, 1024, 0, 256),     # FusAtNet B = 4: the classifier's last 3x3 conv
+    (64, 11, 1024, 256, 0, 1024),  # FusAtNet B = 64: the classifier's convs
+    (64, 5, 256, 256, 0, 256),
+    (64, 3, 256, 1024, 0, 256),
 ])
 @pytest.mark.parametrize("ws_log2", [0, 22, 24])
 def test_conv_tap_fwd_wgrad_dgrad(B, H, C, O, pad, ldx, ws_log2):
