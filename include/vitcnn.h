@@ -166,8 +166,9 @@ VC_API int vc_conv3x3_dgrad(int B, int H, int W, int C, int O, int pad, const fl
  * implicit GEMMs over a TAP-MAJOR contraction index k = tap * C + c (conv_tap.hip): operand tiles are
  * row gathers (one input row per output pixel and tap), no im2col matrix, no col2im.  Weights in
  * tap-major layouts made by vc_conv3x3_pack from the torch layout w [O][C][3][3]:
- *   mode 0: Wt [O][9][C] (fwd and dgrad; also the layout of wgrad's output)   mode 1: W2 [9][O][C]
- *   mode 2: w = beta w + Wt unpacked (a tap-major weight gradient back to the torch layout)
+ *   mode 0: Wt [O][9][Cw] (fwd and dgrad), Cw = C rounded up to a multiple of 4, padding written 0
+ *           (16-B aligned rows: float4 operand loads at any C)                mode 1: W2 [9][O][C]
+ *   mode 2: w = beta w + dWt unpacked (wgrad's tap-major [O][9][C] gradient back to the torch layout)
  *   fwd:   y [B*OH*OW] (ld ldy) = conv(x) + bias (bias may be null)
  *   wgrad: dWt [O][9][C] = sum over output pixels of dy x (overwritten; the bias gradient is colsum(dy))
  *   dgrad: dx (ld lddx) = beta dx + the conv's input gradient for dy

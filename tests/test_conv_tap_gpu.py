@@ -74,7 +74,8 @@ def test_conv_tap_fwd_wgrad_dgrad(B, H, C, O, pad, ldx, ws_log2):
     s = torch.cuda.current_stream().cuda_stream
     ws = torch.empty(1 << ws_log2, device=DEV) if ws_log2 else None
     wsp, wsn = (ws.data_ptr(), ws.numel()) if ws_log2 else (None, 0)
-    wt = torch.empty(O * 9 * C, device=DEV)
+    Cw = (C + 3) // 4 * 4
+    wt = torch.full((O * 9 * Cw,), 5.0, device=DEV)   # the pack must write the padding (as 0)
     w2 = torch.empty(O * 9 * C, device=DEV)
     L.vc_conv3x3_pack(O, C, 0, wd.data_ptr(), wt.data_ptr(), 0.0, s)
     L.vc_conv3x3_pack(O, C, 1, wd.data_ptr(), w2.data_ptr(), 0.0, s)
@@ -93,7 +94,9 @@ def test_conv_tap_fwd_wgrad_dgrad(B, H, C, O, pad, ldx, ws_log2):
                            wsp, wsn, s)
     torch.cuda.synchronize()
     assert torch.equal(w2.cpu().reshape(9, O, C), w2_ref)
-    assert torch.equal(wt.cpu().reshape(O, 9, C), w.permute(0, 2, 3, 1).reshape(O, 9, C))
+    wt_ref = torch.zeros(O, 9, Cw)
+    wt_ref[:, :, :C] = w.permute(0, 2, 3, 1).reshape(O, 9, C)
+    assert torch.equal(wt.cpu().reshape(O, 9, Cw), wt_ref)
     tol = 2e-6 * (9 * max(C, O)) ** 0.5
     errs = (_rel(y.reshape(B, OH, OH, O), y_ref), _rel(dw, dw_ref), _rel(dx[:, :C].reshape(B, H, H, C), dx_ref),
             _nrel(y.reshape(B, OH, OH, O), y_ref), _nrel(dw, dw_ref), _nrel(dx[:, :C].reshape(B, H, H, C), dx_ref))

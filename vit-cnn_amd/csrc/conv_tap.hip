@@ -38,6 +38,7 @@ enum { FWD = 0, WGRAD = 1, DGRAD = 2 };
 
 struct TapArgs {
   int H, W, C, O, pad, OH, OW;
+  int Cw;                  // Wt row pitch per tap: C rounded up to 4 (zero padding)
   int M, N;                // GEMM output extents (N: total output columns; wgrad 9C)
   int P;                   // wgrad: number of output pixels (the contraction)
   int nk;                  // k-tiles in all
@@ -97,7 +98,7 @@ __device__ __forceinline__ void load4(const float* base, long ld, int row, int c
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void conv_tap(TapArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void conv_tap(TapArgs a) {
   constexpr int PA = MODE == WGRAD ? PO : PK;   // A: dy^T (k-outer) for wgrad, row gathers (k-contiguous) else
   constexpr int PB = MODE == FWD ? PK : PO;     // B: Wt rows (k-contiguous) for fwd, k-outer else
   __shared__ __attribute__((aligned(16))) float As[TK * PA];
@@ -157,14 +158,14 @@ __global__ __launch_bounds__(256) void conv_tap(TapArgs a) {
           load4(a.x, a.ldx, row, c0 + 4 * kc, Kt, a.vx, ra + 4 * i);
           // B(k = (tap, c), n = o) = Wt[o][tap][c]: rows o = n0 + kr + 32 i
           const int o = n0 + kr + 32 * i;
-          load4(a.w + (long)tap * a.C, 9L * a.C, o < a.O ? o : -1, c0 + 4 * kc, a.C, a.vw, rbv + 4 * i);
+          load4(a.w + (long)tap * a.Cw, 9L * a.Cw, o < a.O ? o : -1, c0 + 4 * kc, a.Cw, a.vw, rbv + 4 * i);
         } else {
           const int row = out_row(a, rb_[i], ri_[i], rj_[i], tap);
           load4(a.dy, a.lddy, row, c0 + 4 * kc, Kt, a.vdy, ra + 4 * i);
-          // B(k = (tap, o), n = c) = Wt[o][tap][c] (the forward's layout read with row stride 9C):
+          // B(k = (tap, o), n = c) = Wt[o][tap][c] (the forward's layout read with row stride 9 Cw):
           // k rows o = c0 + ok + 8 i
           const int o = c0 + ok + 8 * i;
-          load4(a.w + (long)tap * a.C, 9L * a.C, o < a.O ? o : -1, n0 + 4 * oc, a.C, a.vw, rbv + 4 * i);
+          load4(a.w + (long)tap * a.Cw, 9L * a.Cw, o < a.O ? o : -1, n0 + 4 * oc, a.Cw, a.vw, rbv + 4 * i);
         }
       }
     }
@@ -224,7 +225,10 @@ __global__ __launch_bounds__(256) void conv_tap(TapArgs a) {
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < 2; ++ni) {
+      // one 32x32 accumulator at a time: the data gradient's read of dx (beta) is not batched over
+      // all 64 outputs (that raised the kernel past 3 waves per SIMD)
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -249,6 +253,7 @@ __global__ __launch_bounds__(256) void conv_tap(TapArgs a) {
           else *o = v;
         }
       }
+    }
 }
 
 // split-K combine in fixed slice order, then the mode's epilogue
@@ -266,19 +271,28 @@ __global__ __launch_bounds__(256) void conv_tap_reduce(TapArgs a, int nsplit) {
   else *o = s;
 }
 
-// weight layouts: w [O][C][9] (torch) <-> Wt [O][9][C] (mode 0) / W2 [9][O][C] (mode 1);
-// mode 2: w = beta w + unpack(Wt)
+// weight layouts: w [O][C][9] (torch) -> Wt [O][9][Cw] (mode 0; Cw = C rounded up to 4, zero padding, so
+// the fwd / dgrad weight rows are 16-B aligned and load as float4 at any C) / W2 [9][O][C] (mode 1);
+// mode 2: w = beta w + unpack(dWt [O][9][C])
 __global__ __launch_bounds__(256) void conv_pack(int O, int C, int mode, const float* __restrict__ src,
                                                  float* __restrict__ dst, float beta) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (mode == 0) {   // e indexes Wt [O][9][Cw]: a gather from the torch layout, padding columns 0
+    const int Cw = (C + 3) & ~3;
+    if (e >= (long)O * 9 * Cw) return;
+    const int c = (int)(e % Cw);
+    const long ot = e / Cw;
+    const int tap = (int)(ot % 9), o = (int)(ot / 9);
+    dst[e] = c < C ? src[((long)o * C + c) * 9 + tap] : 0.f;
+    return;
+  }
   const long n = (long)O * C * 9;
   if (e >= n) return;
   // e indexes the torch layout: o, c, tap
   const int tap = (int)(e % 9);
   const long oc_ = e / 9;
   const int c = (int)(oc_ % C), o = (int)(oc_ / C);
-  if (mode == 0) dst[((long)o * 9 + tap) * C + c] = src[e];
-  else if (mode == 1) dst[((long)tap * O + o) * C + c] = src[e];
+  if (mode == 1) dst[((long)tap * O + o) * C + c] = src[e];
   else dst[e] = (beta != 0.f ? beta * dst[e] : 0.f) + src[((long)o * 9 + tap) * C + c];
 }
 
@@ -313,6 +327,7 @@ int launch_tap(TapArgs& a, int grid_n, int grid_m, float* ws, long ws_floats, hi
 TapArgs geo(int B, int H, int W, int C, int O, int pad) {
   TapArgs a{};
   a.H = H; a.W = W; a.C = C; a.O = O; a.pad = pad;
+  a.Cw = (C + 3) & ~3;
   a.OH = H + 2 * pad - 2; a.OW = W + 2 * pad - 2;
   a.fOW = make_fastdiv(a.OW); a.fOHW = make_fastdiv(a.OH * a.OW);
   a.fW = make_fastdiv(W); a.fHW = make_fastdiv(H * W);
@@ -324,7 +339,7 @@ TapArgs geo(int B, int H, int W, int C, int O, int pad) {
 
 VC_EXPORT int vc_conv3x3_pack(int O, int C, int mode, const float* src, float* dst, float beta, hipStream_t stream) {
   VC_REQUIRE(O > 0 && C > 0 && mode >= 0 && mode <= 2 && src && dst);
-  const long n = (long)O * C * 9;
+  const long n = (long)O * ((C + 3) & ~3) * 9;   // mode 0 writes the padded layout
   VC_REQUIRE_I32(n);
   hipLaunchKernelGGL(conv_pack, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, O, C, mode, src, dst, beta);
   VC_CHECK_LAUNCH();
@@ -343,7 +358,7 @@ VC_EXPORT int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, con
   a.tpt = vc_cdiv(C, TK);
   a.nk = 9 * a.tpt;
   a.x = x; a.ldx = ldx; a.w = wt; a.bias = bias; a.out = y; a.ldo = ldy;
-  a.vx = vec_ok(x, ldx); a.vw = vec_ok(wt, C);
+  a.vx = vec_ok(x, ldx); a.vw = vec_ok(wt, a.Cw);
   return launch_tap<FWD>(a, vc_cdiv(O, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
 }
 
@@ -378,6 +393,6 @@ VC_EXPORT int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, c
   a.tpt = vc_cdiv(O, TK);
   a.nk = 9 * a.tpt;
   a.dy = dy; a.lddy = lddy; a.w = wt; a.out = dx; a.ldo = lddx; a.beta = beta;
-  a.vdy = vec_ok(dy, lddy); a.vw = vec_ok(wt, C);
+  a.vdy = vec_ok(dy, lddy); a.vw = vec_ok(wt, a.Cw);
   return launch_tap<DGRAD>(a, vc_cdiv(C, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
 }

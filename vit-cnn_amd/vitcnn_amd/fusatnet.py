@@ -264,7 +264,7 @@ class _Program:
         y = self.new(B, OH, OH, O)
         wt = None
         if _TAP_CONV:
-            wt = self.new(O * K)     # tap-major copy of the weight, read again by the data gradient
+            wt = self.new(O * 9 * ((C + 3) // 4 * 4))   # tap-major weight (rows padded to 4), read again by dgrad
             L.vc_conv3x3_pack(O, C, 0, conv.weight.data_ptr(), wt.data_ptr(), 0.0, self.s)
             L.vc_conv3x3_tap_fwd(B, H, H, C, O, pad, x.data_ptr(), ldx, wt.data_ptr(), conv.bias.data_ptr(),
                                  y.data_ptr(), O, scr, self.SCRATCH, self.s)
