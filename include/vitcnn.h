@@ -235,6 +235,30 @@ VC_API int vc_mamba_scan_bwd_params(int B, int D, int ndir, const float* gate_lo
 VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order, const int* inv_order,
                                 const float* xz, const float* conv_w, const float* conv_b, float* du, float* dxz,
                                 float* dconv_w, float* dconv_b, float* ws, long ws_floats, hipStream_t stream);
+/* Fused forms (one launch each way per block on the critical chain; needs D % 4 == 0 and
+ * ceil((R+32)/16)*16 <= ceil(D/16)*16, true for the model's D = 72, R = 9):
+ * vc_mamba_scan_fwd_fused = vc_mamba_dirconv_fwd + xdbl = u x_proj_w^T (modeling_mamba.py:441-456) +
+ * vc_mamba_scan_fwd in one kernel; u [ndir*B*L, D] and xdbl [.., R+32] are written for the backward
+ * (u bit-identical to vc_mamba_dirconv_fwd). */
+VC_API int vc_mamba_scan_fwd_fused(int B, int L, int D, int R, int ndir, const float* xz, const int* order,
+                                   const float* conv_w, const float* conv_b, const float* x_proj_w,
+                                   const float* dt_w, const float* dt_b, const float* A_log, const float* Dskip,
+                                   float* u, float* xdbl, float* yp, float* ckpt, hipStream_t stream);
+/* vc_mamba_scan_bwd followed, per sequence, by the dt_proj / x_proj data gradients and the conv1d + SiLU
+ * backward: dxdbl complete (all R+32 columns), dpre = d(conv pre-activation) [ndir*B*L, D], ddt_lin as
+ * vc_mamba_scan_bwd, conv_part [ndir*B][5D] per-sequence conv weight / bias partials (reduce with
+ * vc_mamba_conv_params).  ckpt required.  The x half of dxz then comes from vc_mamba_dirconv_bwd_gather. */
+VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
+                                   const int* order, const float* xz, const float* conv_w, const float* conv_b,
+                                   const float* x_proj_w, const float* dt_w, const float* dt_b, const float* A_log,
+                                   const float* Dskip, const float* gate_logits, const float* yp, const float* dyp,
+                                   const float* ckpt, float* dpre, float* ddt_lin, float* dxdbl, float* conv_part,
+                                   float* dA_log, float* dDskip, float* dgate_logits, float* ws, long ws_floats,
+                                   hipStream_t stream);
+VC_API int vc_mamba_dirconv_bwd_gather(int B, int L, int D, int ndir, const int* inv_order, const float* conv_w,
+                                       const float* dpre, float* dxz, hipStream_t stream);
+VC_API int vc_mamba_conv_params(int B, int D, int ndir, const float* conv_part, float* dconv_w, float* dconv_b,
+                                hipStream_t stream);
 
 /* ---------------------------------------------------------------- TokenLearner
  * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64).  params: S x 5 floats

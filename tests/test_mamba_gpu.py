@@ -50,6 +50,100 @@ def _ref(xz, order, cw, cb, wx, wdt, bdt, alog, dsk, gate, B, L, D, R, ndir):
     return ys, leaves
 
 
+def _case(L, D, E):
+    """seeded float64 inputs of one mixer shape, the float64 reference output / gradients, and their
+    fp32 device copies"""
+    torch.manual_seed(0)
+    B, ndir, N = 2, 10, 16
+    R = math.ceil(E / 16)
+    XW = R + 2 * N
+    from vitcnn_amd.scan_orders import scan_orders, inverse
+    n = int(round(L ** 0.5))
+    orders = scan_orders(n)
+    order = torch.tensor(orders, dtype=torch.int64)
+    f64 = torch.float64
+    xz = torch.randn(B * L, 2 * D, dtype=f64)
+    cw, cb = torch.randn(D, 4, dtype=f64) * 0.5, torch.randn(D, dtype=f64) * 0.1
+    wx = torch.randn(XW, D, dtype=f64) / math.sqrt(D)
+    wdt, bdt = torch.randn(D, R, dtype=f64) / math.sqrt(R), torch.randn(D, dtype=f64) * 0.5 - 3.0
+    alog = torch.log(torch.arange(1, N + 1, dtype=f64)).repeat(D, 1) + 0.1 * torch.randn(D, N, dtype=f64)
+    dsk, gate = 1 + 0.2 * torch.randn(D, dtype=f64), torch.randn(ndir, dtype=f64)
+    dys = torch.randn(B * L, D, dtype=f64)
+    ys_ref, leaves = _ref(xz, order, cw, cb, wx, wdt, bdt, alog, dsk, gate, B, L, D, R, ndir)
+    (ys_ref.reshape(B * L, D) * dys).sum().backward()
+    d = lambda t: t.to(torch.float32).contiguous().to(DEV)  # noqa: E731
+    c = dict(B=B, ndir=ndir, N=N, R=R, XW=XW, ref=ys_ref.detach().reshape(B * L, D), leaves=leaves,
+             o32=torch.tensor(orders, dtype=torch.int32, device=DEV),
+             inv32=torch.tensor([inverse(o) for o in orders], dtype=torch.int32, device=DEV))
+    for nm, t in (("xz", xz), ("cw", cw), ("cb", cb), ("wx", wx), ("wdt", wdt), ("bdt", bdt), ("alog", alog),
+                  ("dsk", dsk), ("gate", gate), ("dys", dys)):
+        c[nm] = d(t)
+    return c
+
+
+def _grad_errs(got, leaves):
+    names = ["xz", "conv_w", "conv_b", "x_proj", "dt_w", "dt_b", "A_log", "D", "gate"]
+    errs = {}
+    for nm, g_, leaf in zip(names, got, leaves):
+        r = leaf.grad.reshape(g_.shape)
+        errs[nm] = float((g_.cpu().double() - r).abs().max() / r.abs().max())
+    return errs
+
+
+@pytest.mark.parametrize("L,D,E", [(81, 72, 144), (49, 72, 144), (121, 72, 144), (49, 128, 256), (25, 40, 80)])
+def test_mamba_fused_vs_float64(L, D, E):
+    """vc_mamba_scan_fwd_fused (direction conv + x_proj + scan in one launch) and vc_mamba_scan_bwd_fused
+    (+ dt_proj / x_proj data gradients + conv1d backward) + the direction gather + the conv parameter
+    reduction, against the same float64 reference as the separate kernels; U bit-identical to
+    vc_mamba_dirconv_fwd, xdbl equal to the x_proj GEMM's to fp32 rounding."""
+    lib = _lib()
+    c = _case(L, D, E)
+    B, ndir, N, R, XW = c["B"], c["ndir"], c["N"], c["R"], c["XW"]
+    s = torch.cuda.current_stream().cuda_stream
+    P = lambda t: t.data_ptr()  # noqa: E731
+    rows = ndir * B * L
+    U, XD, Y = torch.empty(rows, D, device=DEV), torch.empty(rows, XW, device=DEV), torch.empty(rows, D, device=DEV)
+    CKP = torch.empty(lib.vc_mamba_scan_ckpt_floats(B, L, D, ndir), device=DEV)
+    assert lib.vc_mamba_scan_fwd_fused(B, L, D, R, ndir, P(c["xz"]), P(c["o32"]), P(c["cw"]), P(c["cb"]), P(c["wx"]),
+                                       P(c["wdt"]), P(c["bdt"]), P(c["alog"]), P(c["dsk"]), P(U), P(XD), P(Y), P(CKP),
+                                       s) == 0
+    YS, YP = torch.empty(B * L, D, device=DEV), torch.empty(B * L, D, device=DEV)
+    lib.vc_mamba_combine_fwd(B, L, D, ndir, P(c["inv32"]), P(c["gate"]), P(Y), P(c["xz"]), P(YP), P(YS), s)
+    U2, XD2 = torch.empty_like(U), torch.empty_like(XD)
+    ws = torch.empty(1 << 24, device=DEV)
+    lib.vc_mamba_dirconv_fwd(B, L, D, ndir, P(c["o32"]), P(c["xz"]), P(c["cw"]), P(c["cb"]), P(U2), s)
+    lib.vc_gemm(0, 1, rows, XW, D, 1.0, P(U2), D, 0, P(c["wx"]), D, 0, 0.0, P(XD2), XW, 0, 1, None, None, 0, 0, 0,
+                None, P(ws), ws.numel(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(U, U2)
+    assert float((XD - XD2).abs().max() / XD2.abs().max()) < 1e-6
+    err = float((YS.cpu().double() - c["ref"]).abs().max() / c["ref"].abs().max())
+    assert err < 1e-5, ("forward", err)
+
+    dU, dDTL = (torch.full((rows, D), float("nan"), device=DEV) for _ in range(2))
+    dXD = torch.full((rows, XW), float("nan"), device=DEV)
+    dXZ = torch.full((B * L, 2 * D), float("nan"), device=DEV)
+    dYP = torch.empty(B * L, D, device=DEV)
+    CP = torch.full((ndir * B * 5 * D,), float("nan"), device=DEV)
+    dA, dDs, dG = torch.empty(D, N, device=DEV), torch.empty(D, device=DEV), torch.empty(ndir, device=DEV)
+    lib.vc_mamba_gate_bwd(B, L, D, P(c["xz"]), P(YP), P(c["dys"]), P(dYP), P(dXZ), s)
+    assert lib.vc_mamba_scan_bwd_fused(B, L, D, R, ndir, P(U), P(XD), P(c["o32"]), P(c["xz"]), P(c["cw"]), P(c["cb"]),
+                                       P(c["wx"]), P(c["wdt"]), P(c["bdt"]), P(c["alog"]), P(c["dsk"]), P(c["gate"]),
+                                       P(Y), P(dYP), P(CKP), P(dU), P(dDTL), P(dXD), P(CP), P(dA), P(dDs), P(dG), P(ws),
+                                       ws.numel(), s) == 0
+    lib.vc_mamba_dirconv_bwd_gather(B, L, D, ndir, P(c["inv32"]), P(c["cw"]), P(dU), P(dXZ), s)
+    dCW, dCB = torch.empty(D, 4, device=DEV), torch.empty(D, device=DEV)
+    lib.vc_mamba_conv_params(B, D, ndir, P(CP), P(dCW), P(dCB), s)
+    dWdt, dbdt, dWx = torch.empty(D, R, device=DEV), torch.empty(D, device=DEV), torch.empty(XW, D, device=DEV)
+    lib.vc_gemm(1, 0, D, R, rows, 1.0, P(dDTL), D, 0, P(XD), XW, 0, 0.0, P(dWdt), R, 0, 1, None, None, 0, 0, 0,
+                P(dbdt), P(ws), ws.numel(), s)
+    lib.vc_gemm(1, 0, XW, D, rows, 1.0, P(dXD), XW, 0, P(U), D, 0, 0.0, P(dWx), D, 0, 1, None, None, 0, 0, 0, None,
+                P(ws), ws.numel(), s)
+    torch.cuda.synchronize()
+    errs = _grad_errs([dXZ, dCW, dCB, dWx, dWdt, dbdt, dA, dDs, dG], c["leaves"])
+    assert max(errs.values()) < 1e-4, errs
+
+
 @pytest.mark.parametrize("L,D,E,use_ckpt", [(81, 72, 144, True), (49, 128, 256, True), (81, 72, 144, False),
                                             (121, 72, 144, True), (25, 40, 80, True)])
 def test_mamba_kernels_vs_float64(L, D, E, use_ckpt):

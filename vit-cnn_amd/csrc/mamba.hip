@@ -163,6 +163,9 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, f
 }
 
 template <int RT>
+__device__ __forceinline__ void stage_dt(const ScanArgs& a, const SeqLds& m, int Lp, int Dp);
+
+template <int RT>
 __device__ __forceinline__ void stage_seq(const ScanArgs& a, int s, const SeqLds& m, int Lp, int Dp) {
   const int R = RT ? RT : a.R;
   const int XW = R + 2 * NST;
@@ -187,8 +190,16 @@ __device__ __forceinline__ void stage_seq(const ScanArgs& a, int s, const SeqLds
       }
     }
   }
-  // dt for every (token, channel): the block has 4 * Dp threads, so thread i handles channel
-  // c = i % Dp of tokens i / Dp, i / Dp + 4, ...; its W_dt row and bias are loaded once
+  stage_dt<RT>(a, m, Lp, Dp);
+}
+
+// dt for every (token, channel) from the staged dt-rank columns m.xr (barriers on both sides): the block
+// has 4 * Dp threads, so thread i handles channel c = i % Dp of tokens i / Dp, i / Dp + 4, ...; its W_dt
+// row and bias are loaded once
+template <int RT>
+__device__ __forceinline__ void stage_dt(const ScanArgs& a, const SeqLds& m, int Lp, int Dp) {
+  const int R = RT ? RT : a.R;
+  const int nt = blockDim.x;
   const int c = threadIdx.x % Dp;
   const bool valid = c < a.D;
   const int cc = valid ? c : 0;
@@ -207,8 +218,121 @@ __device__ __forceinline__ void stage_seq(const ScanArgs& a, int s, const SeqLds
   __syncthreads();
 }
 
-template <int RT>
-__global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ y, float* __restrict__ ckpt) {
+// ---------------------------------------------------------------- fused front end (scan_fwd<RT, true>)
+// The direction conv and x_proj of a sequence computed inside the scan block, before its scan:
+//   phase 1  u[t, c] = SiLU(conv1d_k4(xz[b, order_k(t), c]) + bias) -> LDS image UD [Lp][Dp] (the dts
+//            region, not yet in use) and U in HBM (the backward reads it).  Thread (c = i % Dp, g = i / Dp)
+//            slides the 4-tap window along tokens [g nseg, (g + 1) nseg), each gathered input loaded once;
+//            the same fma order as dirconv_fwd_run, so U is bit-identical to the unfused path.
+//   phase 2  xdbl[t, j] = sum_c u[t, c] W_x[j, c] on v_mfma_f32_16x16x4_f32 (A = UD rows, B = W_x rows from
+//            L1 / L2; 16 x 16 output tiles of (token, j), k = channel in float4 steps: step s of lane
+//            group g pairs channel 16 kc + 4 g + s on both operands) -> the dt-rank / B / C columns of the
+//            LDS image and XD in HBM.
+//   phase 3  dt = softplus(W_dt xr + b) over UD (stage_dt).
+// Replaces the dirconv_fwd launch, the x_proj GEMM launch and the scan's staging of xdbl from HBM.
+struct FusedFwd {
+  const float* xz;       // [B*L, 2D] in_proj output (token order)
+  const float* conv_w;   // [D, 4]
+  const float* conv_b;   // [D]
+  const float* wx;       // [R+2N, D] x_proj weight
+  float* u;              // [nseq*L, D] out
+  float* xdbl;           // [nseq*L, R+2N] out
+};
+
+__device__ __forceinline__ float cf_ld(const float* p, int i, bool ok) { return ok ? p[i] : 0.f; }
+
+// phase 1: order table in `ord` (LDS, L ints) already staged; barrier after
+__device__ __forceinline__ void fused_conv_seq(const ScanArgs& a, const FusedFwd& f, int s, const int* ord,
+                                               float* UD, int nseg, int Dp) {
+  const int L = a.L, D = a.D;
+  const int b = s % a.B;
+  const int c = threadIdx.x % Dp, g = threadIdx.x / Dp;
+  const bool cv = c < D;
+  const int cc = cv ? c : 0;
+  const float w0 = cf_ld(f.conv_w, cc * 4, cv), w1 = cf_ld(f.conv_w, cc * 4 + 1, cv),
+              w2 = cf_ld(f.conv_w, cc * 4 + 2, cv), w3 = cf_ld(f.conv_w, cc * 4 + 3, cv),
+              bias = cf_ld(f.conv_b, cc, cv);
+  const float* xb = f.xz + (long)b * L * (2 * D) + cc;
+  float* ub = f.u + (long)s * L * D + cc;
+  const int t0 = g * nseg;
+  float x0, x1, x2;
+  {
+    float xv[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int tau = t0 - 3 + i;
+      xv[i] = (cv && tau >= 0 && tau < L) ? xb[ord[tau] * (2 * D)] : 0.f;
+    }
+    x0 = xv[0], x1 = xv[1], x2 = xv[2];
+  }
+  constexpr int CH = 8;   // gathered inputs loaded together
+  for (int i0 = 0; i0 < nseg; i0 += CH) {
+    float xv[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int t = t0 + i0 + i;
+      xv[i] = (cv && i0 + i < nseg && t < L) ? xb[ord[t] * (2 * D)] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int t = t0 + i0 + i;
+      if (i0 + i < nseg) {
+        float pre = fmaf(w0, x0, bias);
+        pre = fmaf(w1, x1, pre);
+        pre = fmaf(w2, x2, pre);
+        pre = fmaf(w3, xv[i], pre);
+        const bool ok = cv && t < L;
+        const float uu = ok ? silu_f(pre) : 0.f;
+        UD[t * Dp + c] = uu;
+        if (ok) ub[(long)t * D] = uu;
+        x0 = x1;
+        x1 = x2;
+        x2 = xv[i];
+      }
+    }
+  }
+}
+
+// phase 2 (after a barrier behind phase 1): xdbl = u W_x^T into the LDS columns and XD in HBM.  Needs D % 4 == 0.
+__device__ __forceinline__ void fused_xproj_seq(const ScanArgs& a, const FusedFwd& f, int s, const SeqLds& m,
+                                                const float* UD, int Lp, int Dp) {
+  const int R = a.R, XW = R + 2 * NST, D = a.D, L = a.L;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int ntm = (Lp + 15) / 16, ntj = (XW + 15) / 16, nkc = Dp / 16;
+  float* xd = f.xdbl + (long)s * L * XW;
+  for (int tile = wave; tile < ntm * ntj; tile += nw) {
+    const int tm = tile / ntj, tj = tile - tm * ntj;
+    const int ar = min(16 * tm + r, Lp - 1);   // A row = token (rows past Lp: clamped, discarded)
+    const int bj = min(16 * tj + r, XW - 1);   // B column = x_proj output j (clamped, discarded)
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nkc; ++kc) {
+      const int k0 = 16 * kc + 4 * g;
+      const f32x4 av = *reinterpret_cast<const f32x4*>(UD + ar * Dp + k0);
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 bv = k0 < D ? *reinterpret_cast<const f32x4*>(f.wx + (long)bj * D + k0) : z;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+    }
+    // C[t = 16 tm + 4 g + i][j = 16 tj + r]
+    const int j = 16 * tj + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 16 * tm + 4 * g + i;
+      if (t < Lp && j < XW) {
+        float* dst = j < R ? m.xr + t * R + j : (j < R + NST ? m.Bs + t * NST + (j - R) : m.Cs + t * NST + (j - R - NST));
+        *dst = acc[i];
+        if (t < L) xd[(long)t * XW + j] = acc[i];
+      }
+    }
+  }
+}
+
+template <int RT, bool FUSED>
+__global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ y, float* __restrict__ ckpt,
+                                                FusedFwd f) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int R = RT ? RT : a.R;
   const int nseg = seg_count(a.L), Lp = nseg * SCK;
@@ -232,9 +356,22 @@ __global__ __launch_bounds__(512) void scan_fwd(ScanArgs a, float* __restrict__ 
                              ckpt ? (unsigned)(nseg * NST * a.D * 4) : 0u);
   float h[NQ] = {0.f, 0.f, 0.f, 0.f};
   float un[SCK];
+  if (FUSED) {
+    int* ord = reinterpret_cast<int*>(m.xr + Lp * R);   // [L] this direction's token order
+    const int k = s / a.B;
+    for (int t = threadIdx.x; t < a.L; t += blockDim.x) ord[t] = a.order[k * a.L + t];
+    __syncthreads();
+    fused_conv_seq(a, f, s, ord, m.dts, nseg, Dp);
+    __syncthreads();   // UD complete; U in HBM visible to the block
 #pragma unroll
-  for (int i = 0; i < SCK; ++i) un[i] = buf_ld(r_u, (unsigned)(i * a.D * 4) + lane_b);
-  stage_seq<RT>(a, s, m, Lp, Dp);   // the first segment's u loads are in flight meanwhile
+    for (int i = 0; i < SCK; ++i) un[i] = buf_ld(r_u, (unsigned)(i * a.D * 4) + lane_b);
+    fused_xproj_seq(a, f, s, m, m.dts, Lp, Dp);
+    stage_dt<RT>(a, m, Lp, Dp);   // its leading barrier orders phase 2's UD reads before the dt writes
+  } else {
+#pragma unroll
+    for (int i = 0; i < SCK; ++i) un[i] = buf_ld(r_u, (unsigned)(i * a.D * 4) + lane_b);
+    stage_seq<RT>(a, s, m, Lp, Dp);   // the first segment's u loads are in flight meanwhile
+  }
   for (int c = 0; c < nseg; ++c) {
     const int t0 = c * SCK;
 #pragma unroll
@@ -332,6 +469,26 @@ __device__ __forceinline__ float reduce_scatter8_row_bm(const float (&v)[8]) {
   return w + dpp_mov<0xB1>(w);
 }
 
+// ---------------------------------------------------------------- fused tail (scan_bwd<RT, BM, true>)
+// After the reverse sweep the block holds its sequence's d(dt_lin) (over the dts region), dB / dC (over
+// Bs / Cs) in LDS, and du (the scan's part) in HBM.  The tail finishes the sequence's backward through
+// dt_proj, x_proj and the direction conv, replacing three launches (the dt_proj and x_proj data-gradient
+// GEMMs and dirconv_bwd_wgrad):
+//   (a) dxr[t, j] = sum_c ddtl[t, c] W_dt[c, j]            (v_mfma_f32_16x16x4_f32, k = channel)
+//   (b) du[t, c] += sum_j dxdbl[t, j] W_x[j, c]            (MFMA, k = j over the [Lp][XWp] image
+//                                                            dt-rank | dB | dC built over the dts region)
+//   (c) dpre = du SiLU'(pre), pre recomputed from the 4 gathered taps (dirconv_fwd_run's fma order),
+//       written over du; the conv weight / bias partials of the sequence, [nseq][5D] (c*4 + j | 4D + c),
+//       summed over tokens in a fixed order.
+// In (b) / (c) wave w owns channels 16 w .. 16 w + 15, so a channel's partials never leave its wave.
+struct FusedBwd {
+  const float* xz;       // [B*L, 2D]
+  const float* conv_w;   // [D, 4]
+  const float* conv_b;   // [D]
+  const float* wx;       // [R+2N, D]
+  float* conv_part;      // [nseq][5D] out
+};
+
 struct ScanBwdOut {
   float* du;        // [nseq*L, D]
   float* ddtl;      // [nseq*L, D]  grad of W_dt dtr + b_dt (pre-softplus)
@@ -341,10 +498,126 @@ struct ScanBwdOut {
   float* dg_part;   // [nseq]
 };
 
-template <int RT, bool BM>
+template <int RT>
+__device__ __forceinline__ void fused_bwd_tail(const ScanArgs& a, const FusedBwd& fb, const ScanBwdOut& o, int s,
+                                               int b, const SeqLds& m, const int* ord, int Lp, int Dp) {
+  const int R = RT ? RT : a.R, XW = R + 2 * NST, D = a.D, L = a.L;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int ntm = (Lp + 15) / 16, nkc = Dp / 16;
+  const long base = (long)s * L;
+  // (a) A = ddtl rows (dts region), B[k = c][col = j] = W_dt[c, j]
+  const int ntr = (R + 15) / 16;
+  for (int tile = wave; tile < ntm * ntr; tile += nw) {
+    const int tm = tile / ntr, tr = tile - tm * ntr;
+    const int ar = min(16 * tm + r, Lp - 1);
+    const int jc = 16 * tr + r;
+    const bool jok = jc < R;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nkc; ++kc) {
+      const int k0 = 16 * kc + 4 * g;
+      const f32x4 av = *reinterpret_cast<const f32x4*>(m.dts + ar * Dp + k0);
+      float bv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = (jok && k0 + e < D) ? a.wdt[(long)(k0 + e) * R + jc] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[3], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 16 * tm + 4 * g + i;
+      if (t < Lp && jok) {
+        m.xr[t * R + jc] = acc[i];
+        if (t < L) o.dxdbl[(base + t) * XW + jc] = acc[i];
+      }
+    }
+  }
+  __syncthreads();
+  // the dxdbl image [Lp][XWp] over the dts region (its d(dt_lin) consumed above)
+  const int XWp = (XW + 15) / 16 * 16;
+  float* XI = m.dts;
+  for (int idx = threadIdx.x; idx < Lp * XWp; idx += blockDim.x) {
+    const int t = idx / XWp, j = idx - t * XWp;
+    XI[idx] = j < R ? m.xr[t * R + j] : (j < R + NST ? m.Bs[t * NST + j - R] : (j < XW ? m.Cs[t * NST + j - R - NST] : 0.f));
+  }
+  __syncthreads();
+  // (b) + (c): lane channel dl = 16 wave + r; B[k = j][col = dl] = W_x[j, dl] held in registers
+  const int dl = 16 * wave + r;
+  const bool dok = dl < D;
+  const int dcl = dok ? dl : 0;
+  constexpr int NKX = RT ? (RT + 2 * NST + 15) / 16 : 6;   // k chunks of the image (<= 6, host check)
+  const int nkx = XWp / 16;
+  f32x4 bw[NKX];
+#pragma unroll
+  for (int kc = 0; kc < NKX; ++kc)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 16 * kc + 4 * g + e;
+      bw[kc][e] = (kc < nkx && dok && j < XW) ? fb.wx[(long)j * D + dcl] : 0.f;
+    }
+  const float w0 = cf_ld(fb.conv_w, dcl * 4, dok), w1 = cf_ld(fb.conv_w, dcl * 4 + 1, dok),
+              w2 = cf_ld(fb.conv_w, dcl * 4 + 2, dok), w3 = cf_ld(fb.conv_w, dcl * 4 + 3, dok),
+              bias = cf_ld(fb.conv_b, dcl, dok);
+  const float* xb = fb.xz + (long)b * L * (2 * D) + dcl;
+  float cacc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int tm = 0; tm < ntm; ++tm) {
+    const int ar = min(16 * tm + r, Lp - 1);
+    const int tq = 16 * tm + 4 * g;   // this lane's 4 tokens tq .. tq + 3
+    float xv[7];                      // gathered taps tq - 3 .. tq + 3 (issued before the MFMAs)
+#pragma unroll
+    for (int e = 0; e < 7; ++e) {
+      const int tau = tq - 3 + e;
+      xv[e] = (dok && tau >= 0 && tau < L) ? xb[ord[tau] * (2 * D)] : 0.f;
+    }
+    float dus[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dus[i] = (dok && tq + i < L) ? o.du[(base + tq + i) * D + dl] : 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < NKX; ++kc)
+      if (kc < nkx) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(XI + ar * XWp + 16 * kc + 4 * g);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bw[kc].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bw[kc].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bw[kc].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bw[kc].w, acc, 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = tq + i;
+      if (dok && t < L) {
+        float pre = fmaf(w0, xv[i], bias);
+        pre = fmaf(w1, xv[i + 1], pre);
+        pre = fmaf(w2, xv[i + 2], pre);
+        pre = fmaf(w3, xv[i + 3], pre);
+        const float sg = sigmoid_f(pre);
+        const float gd = (dus[i] + acc[i]) * sg * (1.f + pre * (1.f - sg));
+        o.du[(base + t) * D + dl] = gd;
+        cacc[4] += gd;
+        cacc[0] += gd * xv[i];
+        cacc[1] += gd * xv[i + 1];
+        cacc[2] += gd * xv[i + 2];
+        cacc[3] += gd * xv[i + 3];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 5; ++e) cacc[e] = cross_row_sum(cacc[e]);
+  if (g == 0 && dok) {
+    float* cp = fb.conv_part + (long)s * 5 * D;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cp[dl * 4 + e] = cacc[e];
+    cp[4 * D + dl] = cacc[4];
+  }
+}
+
+template <int RT, bool BM, bool FUSE>
 __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const float* __restrict__ gate_logits,
                                                 const float* __restrict__ yp, const float* __restrict__ dyp,
-                                                const float* __restrict__ ckpt, ScanBwdOut o, int rbs) {
+                                                const float* __restrict__ ckpt, ScanBwdOut o, int rbs,
+                                                FusedBwd fb) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // SeqLds, red [2 rbs][nw][SCK][32], [nw], ord
   const int R = RT ? RT : a.R;
   const int XW = R + 2 * NST;
@@ -474,7 +747,11 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
       const unsigned row = (unsigned)((t0 + q) * a.D * 4) + lane_b;
       buf_st(r_du, row, dt * S + Dd * dy);
       // softplus'(dt_lin) = sigmoid(dt_lin) = 1 - exp(-softplus(dt_lin))
-      buf_st(r_ddtl, row, (qa * LN2 + ut * S) * -expm1_c(-dt));
+      const float ddl = (qa * LN2 + ut * S) * -expm1_c(-dt);
+      buf_st(r_ddtl, row, ddl);
+      // fused tail: d(dt_lin) kept in LDS over this token's dt (read for the last time above, by this
+      // wave only: its channels)
+      if (FUSE) m.dts[(t0 + q) * Dp + d] = valid ? ddl : 0.f;
       dD_acc += dy * ut;   // row q's tokens; the rows are summed at the end
     }
     // one barrier per rbs segments: segment c's partials go to buffer c % (2 rbs), so the next rbs
@@ -496,6 +773,9 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
         for (int ww = 1; ww < 8; ++ww)
           if (ww < nw) sum += pv[ww];
         buf_st(r_dx, (unsigned)(t * XW + R + cc) * 4u, sum);
+        // fused tail: dB / dC kept in LDS over the token's B / C rows (swept by every wave before the
+        // barrier above; later segments read only their own rows)
+        if (FUSE && t < Lp) (cc < NST ? m.Bs + t * NST + cc : m.Cs + t * NST + (cc - NST))[0] = sum;
       }
     }
   }
@@ -515,6 +795,7 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
     for (int ww = 0; ww < nw; ++ww) sum += rg[ww];
     o.dg_part[s] = sum;
   }
+  if (FUSE) fused_bwd_tail<RT>(a, fb, o, s, b, m, ord, Lp, Dp);   // the barrier above: LDS images complete
 }
 
 // token-wise SiLU(z) gate of the combined output, backward:
@@ -735,9 +1016,9 @@ VC_API int vc_mamba_scan_fwd(int B, int L, int D, int R, int ndir, const float* 
   VC_REQUIRE(sm <= 160 * 1024);
   VC_REQUIRE_I32((long)ndir * B * L * (R + 2 * NST));
   ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
-  if (R == 9) hipLaunchKernelGGL(scan_fwd<9>, grid, block, sm, stream, a, y, ckpt);
-  else if (R == 16) hipLaunchKernelGGL(scan_fwd<16>, grid, block, sm, stream, a, y, ckpt);
-  else hipLaunchKernelGGL(scan_fwd<0>, grid, block, sm, stream, a, y, ckpt);
+  if (R == 9) hipLaunchKernelGGL((scan_fwd<9, false>), grid, block, sm, stream, a, y, ckpt, FusedFwd{});
+  else if (R == 16) hipLaunchKernelGGL((scan_fwd<16, false>), grid, block, sm, stream, a, y, ckpt, FusedFwd{});
+  else hipLaunchKernelGGL((scan_fwd<0, false>), grid, block, sm, stream, a, y, ckpt, FusedFwd{});
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -791,12 +1072,21 @@ static int scan_param_reduce(int B, int D, int ndir, const float* gate_logits, c
 // (null: they are recomputed into ws first).
 // ws needs (nseq*D*N + nseq*D + nseq + 2048*ceil(D*N/64)*64) floats (+ vc_mamba_scan_ckpt_floats
 // without ckpt).
-VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
-                             const int* order, const float* dt_w, const float* dt_b, const float* A_log,
-                             const float* Dskip, const float* gate_logits, const float* y, const float* dyp,
-                             const float* ckpt, float* du, float* ddt_lin, float* dxdbl, float* dA_log,
-                             float* dDskip, float* dgate_logits, float* ws, long ws_floats, hipStream_t stream) {
+// the fused front end / tail need float4 rows of W_x (D % 4 == 0) and the [Lp][XWp] dxdbl image inside
+// the [Lp][Dp] dts region, XWp <= 96 (the model: D = 72, R = 9 -> XWp = 48 <= Dp = 80)
+static bool scan_fusable(int D, int R) {
+  const int XWp = (R + 2 * NST + 15) / 16 * 16;
+  return D % 4 == 0 && XWp <= vc_cdiv(D, 16) * 16 && XWp <= 96;
+}
+
+static int scan_bwd_impl(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
+                         const int* order, const float* dt_w, const float* dt_b, const float* A_log,
+                         const float* Dskip, const float* gate_logits, const float* y, const float* dyp,
+                         const float* ckpt, float* du, float* ddt_lin, float* dxdbl, float* dA_log,
+                         float* dDskip, float* dgate_logits, float* ws, long ws_floats, const FusedBwd* fb,
+                         hipStream_t stream) {
   VC_REQUIRE(B > 0 && L > 0 && D > 0 && D <= 128 && R > 0 && R <= 64 && ndir > 0 && ndir <= 64);
+  VC_REQUIRE(!fb || (ckpt && scan_fusable(D, R)));
   const int nseq = ndir * B;
   const long need_a = (long)nseq * D * NST, need_d = (long)nseq * D, need_g = nseq;
   long need_ck = 0;
@@ -827,9 +1117,9 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   const dim3 grid(nseq), block(nw * 64);
   if (!ckpt) {
     const size_t smf = sizeof(float) * seq_lds_floats(L, R, nw * 16);
-    if (R == 9) hipLaunchKernelGGL(scan_fwd<9>, grid, block, smf, stream, a, nullptr, p_ck);
-    else if (R == 16) hipLaunchKernelGGL(scan_fwd<16>, grid, block, smf, stream, a, nullptr, p_ck);
-    else hipLaunchKernelGGL(scan_fwd<0>, grid, block, smf, stream, a, nullptr, p_ck);
+    if (R == 9) hipLaunchKernelGGL((scan_fwd<9, false>), grid, block, smf, stream, a, nullptr, p_ck, FusedFwd{});
+    else if (R == 16) hipLaunchKernelGGL((scan_fwd<16, false>), grid, block, smf, stream, a, nullptr, p_ck, FusedFwd{});
+    else hipLaunchKernelGGL((scan_fwd<0, false>), grid, block, smf, stream, a, nullptr, p_ck, FusedFwd{});
     VC_CHECK_LAUNCH();
     ckpt = p_ck;
   }
@@ -840,8 +1130,9 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   const bool bm = !(sel_env && atoi(sel_env));
 #define VC_SCAN_BWD(RV)                                                                                     \
   do {                                                                                                      \
-    if (bm) hipLaunchKernelGGL((scan_bwd<RV, true>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs); \
-    else hipLaunchKernelGGL((scan_bwd<RV, false>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs); \
+    if (fb) hipLaunchKernelGGL((scan_bwd<RV, true, true>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs, *fb); \
+    else if (bm) hipLaunchKernelGGL((scan_bwd<RV, true, false>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs, FusedBwd{}); \
+    else hipLaunchKernelGGL((scan_bwd<RV, false, false>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs, FusedBwd{}); \
   } while (0)
   if (R == 9) VC_SCAN_BWD(9);
   else if (R == 16) VC_SCAN_BWD(16);
@@ -851,6 +1142,77 @@ VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* 
   // the three parameter-gradient outputs are optional (the per-sequence partials stay in ws, for
   // vc_mamba_scan_bwd_params)
   return scan_param_reduce(B, D, ndir, gate_logits, p_a, p_d, p_g, dA_log, dDskip, dgate_logits, p_rest, rest, stream);
+}
+
+VC_API int vc_mamba_scan_bwd(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
+                             const int* order, const float* dt_w, const float* dt_b, const float* A_log,
+                             const float* Dskip, const float* gate_logits, const float* y, const float* dyp,
+                             const float* ckpt, float* du, float* ddt_lin, float* dxdbl, float* dA_log,
+                             float* dDskip, float* dgate_logits, float* ws, long ws_floats, hipStream_t stream) {
+  return scan_bwd_impl(B, L, D, R, ndir, u, xdbl, order, dt_w, dt_b, A_log, Dskip, gate_logits, y, dyp, ckpt, du,
+                       ddt_lin, dxdbl, dA_log, dDskip, dgate_logits, ws, ws_floats, nullptr, stream);
+}
+
+VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
+                                   const int* order, const float* xz, const float* conv_w, const float* conv_b,
+                                   const float* x_proj_w, const float* dt_w, const float* dt_b, const float* A_log,
+                                   const float* Dskip, const float* gate_logits, const float* y, const float* dyp,
+                                   const float* ckpt, float* dpre, float* ddt_lin, float* dxdbl, float* conv_part,
+                                   float* dA_log, float* dDskip, float* dgate_logits, float* ws, long ws_floats,
+                                   hipStream_t stream) {
+  VC_REQUIRE(xz && conv_w && conv_b && x_proj_w && conv_part);
+  VC_REQUIRE_I32((long)B * L * 2 * D);
+  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part};
+  return scan_bwd_impl(B, L, D, R, ndir, u, xdbl, order, dt_w, dt_b, A_log, Dskip, gate_logits, y, dyp, ckpt, dpre,
+                       ddt_lin, dxdbl, dA_log, dDskip, dgate_logits, ws, ws_floats, &fb, stream);
+}
+
+VC_API int vc_mamba_scan_fwd_fused(int B, int L, int D, int R, int ndir, const float* xz, const int* order,
+                                   const float* conv_w, const float* conv_b, const float* x_proj_w,
+                                   const float* dt_w, const float* dt_b, const float* A_log, const float* Dskip,
+                                   float* u, float* xdbl, float* y, float* ckpt, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && L > 0 && D > 0 && D <= 128 && R > 0 && R <= 64 && ndir > 0);
+  VC_REQUIRE(xz && order && conv_w && conv_b && x_proj_w && u && xdbl && scan_fusable(D, R));
+  const dim3 grid(ndir * B), block(vc_cdiv(D, 16) * 64);
+  VC_REQUIRE(block.x <= 512);
+  const size_t sm = sizeof(float) * (seq_lds_floats(L, R, block.x / 4) + L);   // + the order table
+  VC_REQUIRE(sm <= 160 * 1024);
+  VC_REQUIRE_I32((long)ndir * B * L * (R + 2 * NST));
+  VC_REQUIRE_I32((long)B * L * 2 * D);
+  const ScanArgs a{B, L, D, R, u, xdbl, order, dt_w, dt_b, A_log, Dskip};
+  const FusedFwd f{xz, conv_w, conv_b, x_proj_w, u, xdbl};
+  if (R == 9) hipLaunchKernelGGL((scan_fwd<9, true>), grid, block, sm, stream, a, y, ckpt, f);
+  else if (R == 16) hipLaunchKernelGGL((scan_fwd<16, true>), grid, block, sm, stream, a, y, ckpt, f);
+  else hipLaunchKernelGGL((scan_fwd<0, true>), grid, block, sm, stream, a, y, ckpt, f);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// the x half of dxz from the per-direction dpre (vc_mamba_scan_bwd_fused's output): dirconv_bwd_gather alone
+VC_API int vc_mamba_dirconv_bwd_gather(int B, int L, int D, int ndir, const int* inv_order, const float* conv_w,
+                                       const float* dpre, float* dxz, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && L > 0 && D > 0 && ndir > 0);
+  VC_REQUIRE_I32((long)ndir * B * L * D);
+  const long tot2 = (long)B * L * D;
+  if (ndir <= 10)
+    hipLaunchKernelGGL(dirconv_bwd_gather<10>, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, (int)tot2,
+                       make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, conv_w, dpre, dxz);
+  else
+    hipLaunchKernelGGL(dirconv_bwd_gather<4>, dim3(vc_cdiv(tot2, 256)), dim3(256), 0, stream, (int)tot2,
+                       make_fastdiv(D), make_fastdiv(L), B, ndir, inv_order, conv_w, dpre, dxz);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// conv1d weight [D,4] / bias [D] gradients (overwrite) from vc_mamba_scan_bwd_fused's per-sequence partials
+VC_API int vc_mamba_conv_params(int B, int D, int ndir, const float* conv_part, float* dconv_w, float* dconv_b,
+                                hipStream_t stream) {
+  VC_REQUIRE(B > 0 && D > 0 && ndir > 0 && conv_part && dconv_w && dconv_b);
+  const int nseq = ndir * B;
+  if (dconv_b == dconv_w + 4L * D) return launch_sum_rows(nseq, 5 * D, conv_part, 5L * D, 0L, dconv_w, 0.f, stream);
+  const int rc = launch_sum_rows(nseq, 4 * D, conv_part, 5L * D, 0L, dconv_w, 0.f, stream);
+  if (rc) return rc;
+  return launch_sum_rows(nseq, D, conv_part, 5L * D, 4L * D, dconv_b, 0.f, stream);
 }
 
 // The parameter-gradient reductions of vc_mamba_scan_bwd, run separately (later, or on another

@@ -52,6 +52,10 @@ _DEFER_WGRAD = os.environ.get("VITCNN_DEFER_WGRAD", "1") == "1"
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
+# the Mamba direction conv + x_proj folded into the scan launch and the dt_proj / x_proj data gradients +
+# conv1d backward into the scan backward's tail (vc_mamba_scan_fwd_fused / _bwd_fused); "0" restores the
+# separate launches (measurement switch, read per program)
+_SCAN_FUSED = os.environ.get("VITCNN_SCAN_FUSED", "1") != "0"
 _LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
 _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in normal runs)
 _GROUP = os.environ.get("VITCNN_GEMM_GROUP", "1") != "0"   # grouped launches of independent fp32 GEMMs
@@ -440,6 +444,7 @@ class _Program:
         self.gemm_flags = GEMM_BF16 if model.precision == "bf16" else 0
         # 3x3 convs as implicit GEMMs (fp32 only, opt-in); bf16 operands use im2col + the bf16 vc_gemm
         self.implicit_conv = not self.gemm_flags and _IMPLICIT_CONV
+        self.scan_fused = _SCAN_FUSED
         self.cur = 0
         self._gemm_i = 0
         self._ev_i = 0
@@ -657,15 +662,22 @@ class _Program:
         XZ = ws.f(pfx + ".XZ", rows * 2 * D)
         self.mm_nt(rows, 2 * D, E, Xn, E, P[mx + ".in_proj.weight"], E, XZ, 2 * D)
         U = ws.f(pfx + ".U", NDIR * rows * D)
-        self.L.vc_mamba_dirconv_fwd(B, L_, D, NDIR, order, XZ, P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"], U,
-                                    self.s)
         XD = ws.f(pfx + ".XD", NDIR * rows * XW)
-        self.mm_nt(NDIR * rows, XW, D, U, D, P[mx + ".x_proj.weight"], D, XD, XW)
         Y = ws.f(pfx + ".Y", NDIR * rows * D)
         # segment checkpoints of the scan state, kept for the backward (training with grad only)
         CKP = ws.f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR)) if self.ws_grad else None
-        self.L.vc_mamba_scan_fwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
-                                 P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], Y, CKP, self.s)
+        if self.scan_fused:
+            # direction conv + x_proj + scan as one launch (U and XD written for the backward)
+            self.L.vc_mamba_scan_fwd_fused(B, L_, D, R, NDIR, XZ, order, P[mx + ".conv1d.weight"],
+                                           P[mx + ".conv1d.bias"], P[mx + ".x_proj.weight"],
+                                           P[mx + ".dt_proj.weight"], P[mx + ".dt_proj.bias"], P[mx + ".A_log"],
+                                           P[mx + ".D"], U, XD, Y, CKP, self.s)
+        else:
+            self.L.vc_mamba_dirconv_fwd(B, L_, D, NDIR, order, XZ, P[mx + ".conv1d.weight"],
+                                        P[mx + ".conv1d.bias"], U, self.s)
+            self.mm_nt(NDIR * rows, XW, D, U, D, P[mx + ".x_proj.weight"], D, XD, XW)
+            self.L.vc_mamba_scan_fwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
+                                     P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], Y, CKP, self.s)
         YP, YS = ws.f(pfx + ".YP", rows * D), ws.f(pfx + ".YS", rows * D)
         self.L.vc_mamba_combine_fwd(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, XZ, YP, YS, self.s)
         T2 = ws.f(pfx + ".T2", rows * E)
@@ -986,6 +998,9 @@ class _Program:
         self.L.vc_mamba_gate_bwd(B, L_, D, XZ, YP, dYS, dYP, dXZ, self.s)
         self.flush_wgrads()   # fusion, change_dim, out_proj: alongside the scan backward
         CKPb = f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR))
+        if self.scan_fused:
+            self._scan_bwd_fused(pfx, gv, mx, B, L_, D, R, XW, order, inv, CKPb)
+            return self._block_bwd_tail(pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch)
         if self._deferring(True):
             # the per-sequence dA_log / D / gate partials stay in a buffer of their own; their
             # reductions go with the next weight-gradient flush
@@ -1014,9 +1029,52 @@ class _Program:
         self.L.vc_mamba_dirconv_bwd(B, L_, D, NDIR, order, inv, XZ, P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"],
                                     dU, dXZ, G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"], self.scr_p,
                                     self.scr_n, self.s)
+        self._block_bwd_tail(pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch)
+
+    def _scan_bwd_fused(self, pfx, gv, mx, B, L_, D, R, XW, order, inv, CKPb):
+        """scan backward + dt_proj / x_proj data gradients + conv1d / SiLU backward in one launch
+        (vc_mamba_scan_bwd_fused), the direction gather into dxz, and the parameter gradients (dt_proj,
+        x_proj, conv1d, A_log / D / gate) queued for the weight-gradient lane"""
+        ws, P, G, f = self.ws, self.P, self.G, self.ws.f
+        rows = B * L_
+        nr, nseq = NDIR * rows, NDIR * B
+        U, XD, XZ = f(pfx + ".U", nr * D), f(pfx + ".XD", nr * XW), f(pfx + ".XZ", rows * 2 * D)
+        Y, dYP = f(pfx + ".Y", nr * D), f(pfx + ".dYP", rows * D)
+        dU, dDTL, dXD, dXZ = f(pfx + ".dU", nr * D), f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW), f(
+            pfx + ".dXZ", rows * 2 * D)
+        CP = f(pfx + ".convpart", nseq * 5 * D)
+        defer = self._deferring(True)
+        spn = nseq * D * 16 + nseq * D + nseq
+        sp = f(pfx + ".scanpart", spn) if defer else self.scr_p
+        spn = spn if defer else self.scr_n
+        gl, ga, gd, gg = P[gv + ".weights"], G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"]
+        self.L.vc_mamba_scan_bwd_fused(B, L_, D, R, NDIR, U, XD, order, XZ, P[mx + ".conv1d.weight"],
+                                       P[mx + ".conv1d.bias"], P[mx + ".x_proj.weight"], P[mx + ".dt_proj.weight"],
+                                       P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], gl, Y, dYP, CKPb, dU,
+                                       dDTL, dXD, CP, None if defer else ga, None if defer else gd,
+                                       None if defer else gg, sp, spn, self.s)
+        if defer:
+            self.pending_wgrads.append(
+                lambda: self.L.vc_mamba_scan_bwd_params(B, D, NDIR, gl, sp, ga, gd, gg, self.scr_p, self.scr_n,
+                                                        self.s))
+        self.L.vc_mamba_dirconv_bwd_gather(B, L_, D, NDIR, inv, P[mx + ".conv1d.weight"], dU, dXZ, self.s)
+        # parameter gradients: dt_proj (dDTL, XD's dt-rank columns), x_proj (dXD, U), conv1d (partials)
+        self.defer_wgrad(True, D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, G[mx + ".dt_proj.bias"])
+        self.defer_wgrad(True, XW, D, nr, dXD, XW, U, D, G[mx + ".x_proj.weight"], D)
+        cw, cb = G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"]
+        if defer:
+            self.pending_wgrads.append(lambda: self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s))
+        else:
+            self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s)
+
+    def _block_bwd_tail(self, pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch):
+        """in_proj -> pre_norm -> patch_embed backward of a GlobalLocal block"""
+        ws, P, G, f = self.ws, self.P, self.G, self.ws.f
+        D = E // 2
+        dXZ = f(pfx + ".dXZ", rows * 2 * D)
         Xn, dXn = f(pfx + ".Xn", rows * E), f(pfx + ".dXn", rows * E)
         self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0, defer=True)
-        self.flush_wgrads()   # dt_proj, x_proj, in_proj
+        self.flush_wgrads()   # dt_proj, x_proj, conv1d, in_proj
         T, dTt = f(pfx + ".T", rows * E), f(pfx + ".dTt", rows * E)
         self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dTt, 0.0, res=dT, defer=True)   # dT + LN grad
         if dX:
