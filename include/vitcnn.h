@@ -235,19 +235,20 @@ VC_API int vc_mamba_scan_bwd_params(int B, int D, int ndir, const float* gate_lo
 VC_API int vc_mamba_dirconv_bwd(int B, int L, int D, int ndir, const int* order, const int* inv_order,
                                 const float* xz, const float* conv_w, const float* conv_b, float* du, float* dxz,
                                 float* dconv_w, float* dconv_b, float* ws, long ws_floats, hipStream_t stream);
-/* Fused forms (one launch each way per block on the critical chain; needs D % 4 == 0 and
- * ceil((R+32)/16)*16 <= ceil(D/16)*16, true for the model's D = 72, R = 9):
+/* Fused forms (one launch each way per block on the critical chain; needs D % 4 == 0 and R <= 16 --
+ * true for the model's (D, R) = (72, 9) and (128, 16)):
  * vc_mamba_scan_fwd_fused = vc_mamba_dirconv_fwd + xdbl = u x_proj_w^T (modeling_mamba.py:441-456) +
- * vc_mamba_scan_fwd in one kernel; u [ndir*B*L, D] and xdbl [.., R+32] are written for the backward
- * (u bit-identical to vc_mamba_dirconv_fwd). */
+ * vc_mamba_scan_fwd in one kernel; u [ndir*B*L, D] (bit-identical to vc_mamba_dirconv_fwd) and xdbl
+ * [.., R+32] are written for the backward. */
 VC_API int vc_mamba_scan_fwd_fused(int B, int L, int D, int R, int ndir, const float* xz, const int* order,
                                    const float* conv_w, const float* conv_b, const float* x_proj_w,
                                    const float* dt_w, const float* dt_b, const float* A_log, const float* Dskip,
                                    float* u, float* xdbl, float* yp, float* ckpt, hipStream_t stream);
 /* vc_mamba_scan_bwd followed, per sequence, by the dt_proj / x_proj data gradients and the conv1d + SiLU
- * backward: dxdbl complete (all R+32 columns), dpre = d(conv pre-activation) [ndir*B*L, D], ddt_lin as
- * vc_mamba_scan_bwd, conv_part [ndir*B][5D] per-sequence conv weight / bias partials (reduce with
- * vc_mamba_conv_params).  ckpt required.  The x half of dxz then comes from vc_mamba_dirconv_bwd_gather. */
+ * backward (modeling_mamba.py:433-456 backward): dxdbl complete (all R+32 columns), dpre = d(conv
+ * pre-activation) [ndir*B*L, D], ddt_lin and the scan parameter outputs as vc_mamba_scan_bwd, conv_part
+ * [ndir*B][5D] the per-sequence conv weight / bias partials (reduce with vc_mamba_conv_params).  ckpt
+ * required.  The x half of dxz then comes from vc_mamba_dirconv_bwd_gather. */
 VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                                    const int* order, const float* xz, const float* conv_w, const float* conv_b,
                                    const float* x_proj_w, const float* dt_w, const float* dt_b, const float* A_log,
@@ -257,8 +258,43 @@ VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const f
                                    hipStream_t stream);
 VC_API int vc_mamba_dirconv_bwd_gather(int B, int L, int D, int ndir, const int* inv_order, const float* conv_w,
                                        const float* dpre, float* dxz, hipStream_t stream);
+/* conv1d weight [D,1,4] / bias [D] gradients (overwritten) from vc_mamba_scan_bwd_fused's partials */
 VC_API int vc_mamba_conv_params(int B, int D, int ndir, const float* conv_part, float* dconv_w, float* dconv_b,
                                 hipStream_t stream);
+
+/* ---------------------------------------------------------------- hsiMamba row chains
+ * Two projections with a LayerNorm between them for 32-row blocks in one launch (rowchain.hip), fp32:
+ * front (Mutimodality_Mamba7.py:651-656, modeling_mamba.py:433): t = x w_embed^T + pos[row % L],
+ *   xn = LN(t) (ln_w, ln_b, eps; mean / rstd saved), out = xn w_proj^T   (K0, E, N2 <= 256, % 4 == 0);
+ * back (:694-701, modeling_mamba.py:274, :481, Mutimodality_Mamba7.py:985, :1068): ypsum / ysum as
+ *   vc_mamba_combine_fwd (bit-identical, ndir <= 10), t2 = ysum w_out^T + residual, g = LN(t2),
+ *   out = g w_proj^T + b_proj.  Each replaces 3 / 4 launches of the separate path. */
+VC_API int vc_rowchain_front(int rows, int K0, int E, int N2, const float* x, const float* w_embed, const float* pos,
+                             int L, float* t, const float* ln_w, const float* ln_b, float eps, float* xn, float* mean,
+                             float* rstd, const float* w_proj, float* out, hipStream_t stream);
+VC_API int vc_rowchain_back(int B, int L, int D, int ndir, const int* inv_order, const float* gate_logits,
+                            const float* yp, const float* xz, float* ypsum, float* ysum, int E, const float* w_out,
+                            const float* residual, float* t2, const float* ln_w, const float* ln_b, float eps,
+                            float* g, float* mean, float* rstd, int N2, const float* w_proj, const float* b_proj,
+                            float* out, hipStream_t stream);
+
+/* Backward chains (same blocking): back_bwd = change_dim's data gradient (dcd w_cd), the ln1 backward
+ * (dt = LN grad; per-block dw / db partials into ln_part), out_proj's data gradient and the SiLU(z) gate
+ * backward (dyp, the z half of dxz) -- the separate path's vc_gemm + vc_layernorm_bwd_dx + vc_gemm +
+ * vc_mamba_gate_bwd; front_bwd = in_proj's data gradient (dxz w_in), the pre_norm backward with the
+ * residual gradient (dtt = res + LN grad; partials) and dx = beta dx + dtt w_embed (dx nullable).
+ * vc_rowchain_ln_params reduces the partials (size: vc_rowchain_ln_part_floats).  Weight gradients of
+ * the projections are separate vc_gemm calls. */
+VC_API int vc_rowchain_back_bwd(int rows, int Cout, int E, int D, const float* dcd, const float* w_cd, const float* t2,
+                                const float* mean, const float* rstd, const float* ln_w, float* dt, float* ln_part,
+                                const float* w_out, const float* xz, const float* ypsum, float* dyp, float* dxz,
+                                hipStream_t stream);
+VC_API int vc_rowchain_front_bwd(int rows, int K0, int E, int Cin, const float* dxz, const float* w_in, const float* t,
+                                 const float* mean, const float* rstd, const float* ln_w, const float* res, float* dtt,
+                                 float* ln_part, const float* w_embed, float* dx, float beta, hipStream_t stream);
+VC_API int vc_rowchain_ln_params(int rows, int E, const float* ln_part, float* dw, float* db, float beta,
+                                 hipStream_t stream);
+VC_API int vc_rowchain_ln_part_floats(int rows, int E);
 
 /* ---------------------------------------------------------------- TokenLearner
  * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64).  params: S x 5 floats

@@ -122,9 +122,9 @@ def test_mamba_fused_vs_float64(L, D, E):
 
     dU, dDTL = (torch.full((rows, D), float("nan"), device=DEV) for _ in range(2))
     dXD = torch.full((rows, XW), float("nan"), device=DEV)
+    CP = torch.full((ndir * B * 5 * D,), float("nan"), device=DEV)
     dXZ = torch.full((B * L, 2 * D), float("nan"), device=DEV)
     dYP = torch.empty(B * L, D, device=DEV)
-    CP = torch.full((ndir * B * 5 * D,), float("nan"), device=DEV)
     dA, dDs, dG = torch.empty(D, N, device=DEV), torch.empty(D, device=DEV), torch.empty(ndir, device=DEV)
     lib.vc_mamba_gate_bwd(B, L, D, P(c["xz"]), P(YP), P(c["dys"]), P(dYP), P(dXZ), s)
     assert lib.vc_mamba_scan_bwd_fused(B, L, D, R, ndir, P(U), P(XD), P(c["o32"]), P(c["xz"]), P(c["cw"]), P(c["cb"]),

@@ -221,15 +221,16 @@ __device__ __forceinline__ void stage_dt(const ScanArgs& a, const SeqLds& m, int
 // ---------------------------------------------------------------- fused front end (scan_fwd<RT, true>)
 // The direction conv and x_proj of a sequence computed inside the scan block, before its scan:
 //   phase 1  u[t, c] = SiLU(conv1d_k4(xz[b, order_k(t), c]) + bias) -> LDS image UD [Lp][Dp] (the dts
-//            region, not yet in use) and U in HBM (the backward reads it).  Thread (c = i % Dp, g = i / Dp)
-//            slides the 4-tap window along tokens [g nseg, (g + 1) nseg), each gathered input loaded once;
-//            the same fma order as dirconv_fwd_run, so U is bit-identical to the unfused path.
-//   phase 2  xdbl[t, j] = sum_c u[t, c] W_x[j, c] on v_mfma_f32_16x16x4_f32 (A = UD rows, B = W_x rows from
-//            L1 / L2; 16 x 16 output tiles of (token, j), k = channel in float4 steps: step s of lane
-//            group g pairs channel 16 kc + 4 g + s on both operands) -> the dt-rank / B / C columns of the
-//            LDS image and XD in HBM.
+//            region, not yet in use) and U in HBM (read by the scan below and by the backward).  Thread
+//            (c = i % Dp, g = i / Dp) slides the 4-tap window along tokens [g nseg, (g + 1) nseg), each
+//            gathered input loaded once; dirconv_fwd_run's fma order, so U is bit-identical to it.
+//   phase 2  xdbl[t, j] = sum_c u[t, c] W_x[j, c] on v_mfma_f32_16x16x4_f32: 16 x 16 (token, j) tiles,
+//            A = UD rows, B = W_x rows (a wave's W_x fragments for every k chunk loaded at once and kept
+//            while its tiles share the column tile); step s of lane group g pairs channel 16 kc + 4 g + s
+//            on both operands -> the dt-rank / B / C columns of the LDS image and XD in HBM.
 //   phase 3  dt = softplus(W_dt xr + b) over UD (stage_dt).
 // Replaces the dirconv_fwd launch, the x_proj GEMM launch and the scan's staging of xdbl from HBM.
+constexpr int FMAX_KC = 8;   // Dp / 16 <= 8 (D <= 128)
 struct FusedFwd {
   const float* xz;       // [B*L, 2D] in_proj output (token order)
   const float* conv_w;   // [D, 4]
@@ -265,7 +266,7 @@ __device__ __forceinline__ void fused_conv_seq(const ScanArgs& a, const FusedFwd
     }
     x0 = xv[0], x1 = xv[1], x2 = xv[2];
   }
-  constexpr int CH = 8;   // gathered inputs loaded together
+  constexpr int CH = 12;   // gathered inputs loaded together (a 21-token run: two rounds)
   for (int i0 = 0; i0 < nseg; i0 += CH) {
     float xv[CH];
 #pragma unroll
@@ -301,21 +302,32 @@ __device__ __forceinline__ void fused_xproj_seq(const ScanArgs& a, const FusedFw
   const int r = lane & 15, g = lane >> 4;
   const int ntm = (Lp + 15) / 16, ntj = (XW + 15) / 16, nkc = Dp / 16;
   float* xd = f.xdbl + (long)s * L * XW;
+  f32x4 bw[FMAX_KC];
+  int cur_tj = -1;
+  // column-tile-major tile order: a wave's consecutive tiles mostly share tj (its W_x fragments)
   for (int tile = wave; tile < ntm * ntj; tile += nw) {
-    const int tm = tile / ntj, tj = tile - tm * ntj;
-    const int ar = min(16 * tm + r, Lp - 1);   // A row = token (rows past Lp: clamped, discarded)
-    const int bj = min(16 * tj + r, XW - 1);   // B column = x_proj output j (clamped, discarded)
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nkc; ++kc) {
-      const int k0 = 16 * kc + 4 * g;
-      const f32x4 av = *reinterpret_cast<const f32x4*>(UD + ar * Dp + k0);
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 bv = k0 < D ? *reinterpret_cast<const f32x4*>(f.wx + (long)bj * D + k0) : z;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+    const int tj = tile / ntm, tm = tile - tj * ntm;
+    if (tj != cur_tj) {
+      cur_tj = tj;
+      const int bj = min(16 * tj + r, XW - 1);   // B column = x_proj output j (clamped, discarded)
+#pragma unroll
+      for (int kc = 0; kc < FMAX_KC; ++kc) {
+        const int k0 = 16 * kc + 4 * g;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        bw[kc] = (kc < nkc && k0 < D) ? *reinterpret_cast<const f32x4*>(f.wx + (long)bj * D + k0) : z;
+      }
     }
+    const int ar = min(16 * tm + r, Lp - 1);   // A row = token (rows past Lp: clamped, discarded)
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < FMAX_KC; ++kc)
+      if (kc < nkc) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(UD + ar * Dp + 16 * kc + 4 * g);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bw[kc].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bw[kc].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bw[kc].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bw[kc].w, acc, 0, 0, 0);
+      }
     // C[t = 16 tm + 4 g + i][j = 16 tj + r]
     const int j = 16 * tj + r;
 #pragma unroll
@@ -470,23 +482,28 @@ __device__ __forceinline__ float reduce_scatter8_row_bm(const float (&v)[8]) {
 }
 
 // ---------------------------------------------------------------- fused tail (scan_bwd<RT, BM, true>)
-// After the reverse sweep the block holds its sequence's d(dt_lin) (over the dts region), dB / dC (over
-// Bs / Cs) in LDS, and du (the scan's part) in HBM.  The tail finishes the sequence's backward through
-// dt_proj, x_proj and the direction conv, replacing three launches (the dt_proj and x_proj data-gradient
-// GEMMs and dirconv_bwd_wgrad):
-//   (a) dxr[t, j] = sum_c ddtl[t, c] W_dt[c, j]            (v_mfma_f32_16x16x4_f32, k = channel)
-//   (b) du[t, c] += sum_j dxdbl[t, j] W_x[j, c]            (MFMA, k = j over the [Lp][XWp] image
-//                                                            dt-rank | dB | dC built over the dts region)
-//   (c) dpre = du SiLU'(pre), pre recomputed from the 4 gathered taps (dirconv_fwd_run's fma order),
-//       written over du; the conv weight / bias partials of the sequence, [nseq][5D] (c*4 + j | 4D + c),
-//       summed over tokens in a fixed order.
-// In (b) / (c) wave w owns channels 16 w .. 16 w + 15, so a channel's partials never leave its wave.
+// After the reverse sweep the block holds its sequence's du (the scan's part, over the dts region) and
+// dB / dC (over Bs / Cs) in LDS, and d(dt_lin) in HBM.  The tail finishes the sequence's backward
+// through dt_proj, x_proj and the direction conv, replacing three launches (the dt_proj and x_proj
+// data-gradient GEMMs and dirconv_bwd_wgrad) and du's HBM round trip:
+//   (a) dxr[t, j] = sum_c ddtl[t, c] W_dt[c, j]            (v_mfma_f32_16x16x4_f32, k = channel; A from
+//                                                            HBM, W_dt staged over the dead dB / dC
+//                                                            partial buffers) -> a [Lp][16] LDS image
+//   (b) du[t, c] += sum_j dxdbl[t, j] W_x[j, c]            (MFMA, k = j in three 16-wide chunks: the
+//                                                            dxr image | dB (Bs) | dC (Cs))
+//   (c) dpre = du SiLU'(pre), pre recomputed from the 4 gathered taps (dirconv_fwd_run's fma order; xz is
+//       L2-resident), written to HBM; the sequence's conv weight / bias partials [nseq][5D]
+//       (c*4 + j | 4D + c), summed over its tokens in a fixed order.
+// Global operands are issued ahead of their MFMAs (W_x fragments once per wave, the gathered taps for
+// two token tiles at a time).  In (b) / (c) wave w owns channels 16 w .. 16 w + 15, so a channel's conv
+// partials never leave its wave.  Needs R <= 16.
 struct FusedBwd {
   const float* xz;       // [B*L, 2D]
   const float* conv_w;   // [D, 4]
   const float* conv_b;   // [D]
   const float* wx;       // [R+2N, D]
   float* conv_part;      // [nseq][5D] out
+  int tail;              // 1; 0 skips the tail (VITCNN_SCAN_TAIL=0: a measurement switch, results incomplete)
 };
 
 struct ScanBwdOut {
@@ -500,106 +517,148 @@ struct ScanBwdOut {
 
 template <int RT>
 __device__ __forceinline__ void fused_bwd_tail(const ScanArgs& a, const FusedBwd& fb, const ScanBwdOut& o, int s,
-                                               int b, const SeqLds& m, const int* ord, int Lp, int Dp) {
+                                               int b, const SeqLds& m, const int* ord, float* red, int Lp,
+                                               int Dp) {
   const int R = RT ? RT : a.R, XW = R + 2 * NST, D = a.D, L = a.L;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int ntm = (Lp + 15) / 16, nkc = Dp / 16;
   const long base = (long)s * L;
-  // (a) A = ddtl rows (dts region), B[k = c][col = j] = W_dt[c, j]
-  const int ntr = (R + 15) / 16;
-  for (int tile = wave; tile < ntm * ntr; tile += nw) {
-    const int tm = tile / ntr, tr = tile - tm * ntr;
-    const int ar = min(16 * tm + r, Lp - 1);
-    const int jc = 16 * tr + r;
-    const bool jok = jc < R;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nkc; ++kc) {
-      const int k0 = 16 * kc + 4 * g;
-      const f32x4 av = *reinterpret_cast<const f32x4*>(m.dts + ar * Dp + k0);
-      float bv[4];
+  float* DX16 = red;                 // [Lp][16] dxr, columns R..15 zero
+  float* wdt_lds = red + Lp * 16;    // [D][R]
+  {   // W_dt: all of a thread's loads issued before its stores (one latency, not one per trip)
+    constexpr int WS = 8;   // D R <= 128 x 16 over >= 256 threads
+    float wv[WS];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = (jok && k0 + e < D) ? a.wdt[(long)(k0 + e) * R + jc] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[3], acc, 0, 0, 0);
+    for (int j = 0; j < WS; ++j) {
+      const int i = threadIdx.x + j * blockDim.x;
+      wv[j] = i < D * R ? a.wdt[i] : 0.f;
     }
+#pragma unroll
+    for (int j = 0; j < WS; ++j) {
+      const int i = threadIdx.x + j * blockDim.x;
+      if (i < D * R) wdt_lds[i] = wv[j];
+    }
+  }
+  __syncthreads();
+  // (a) A = ddtl rows from HBM (this block's sweep wrote them), B[k = c][col = j] = W_dt[c, j] (LDS);
+  // a wave's (at most two, ntm <= 2 nw) token tiles' A rows loaded at once
+  f32x4 avs[2][FMAX_KC];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int ta = 16 * (wave + u * nw) + r;
+    const bool tok = ta < L;
+    const float* arow = o.ddtl + (base + (tok ? ta : 0)) * D;
+#pragma unroll
+    for (int kc = 0; kc < FMAX_KC; ++kc) {
+      const int k0 = 16 * kc + 4 * g;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      avs[u][kc] = (kc < nkc && tok && k0 < D) ? *reinterpret_cast<const f32x4*>(arow + k0) : z;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int tm = wave + u * nw;
+    if (tm >= ntm) break;
+    const f32x4* av = avs[u];   // (tiles past 2 nw: none for the fused shapes, host check)
+    const bool jok = r < R;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < FMAX_KC; ++kc)
+      if (kc < nkc) {
+        const int k0 = 16 * kc + 4 * g;
+        float bv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = (jok && k0 + e < D) ? wdt_lds[(k0 + e) * R + r] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].x, bv[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].y, bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].z, bv[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].w, bv[3], acc, 0, 0, 0);
+      }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int t = 16 * tm + 4 * g + i;
-      if (t < Lp && jok) {
-        m.xr[t * R + jc] = acc[i];
-        if (t < L) o.dxdbl[(base + t) * XW + jc] = acc[i];
+      if (t < Lp) {
+        DX16[t * 16 + r] = jok ? acc[i] : 0.f;
+        if (jok && t < L) o.dxdbl[(base + t) * XW + r] = acc[i];
       }
     }
   }
-  __syncthreads();
-  // the dxdbl image [Lp][XWp] over the dts region (its d(dt_lin) consumed above)
-  const int XWp = (XW + 15) / 16 * 16;
-  float* XI = m.dts;
-  for (int idx = threadIdx.x; idx < Lp * XWp; idx += blockDim.x) {
-    const int t = idx / XWp, j = idx - t * XWp;
-    XI[idx] = j < R ? m.xr[t * R + j] : (j < R + NST ? m.Bs[t * NST + j - R] : (j < XW ? m.Cs[t * NST + j - R - NST] : 0.f));
-  }
-  __syncthreads();
-  // (b) + (c): lane channel dl = 16 wave + r; B[k = j][col = dl] = W_x[j, dl] held in registers
+  // the wave's W_x fragments for (b): B[k = j][col = dl], chunk 0 = dt-rank rows, 1 = B rows, 2 = C rows
+  // (in flight across the barrier)
   const int dl = 16 * wave + r;
   const bool dok = dl < D;
   const int dcl = dok ? dl : 0;
-  constexpr int NKX = RT ? (RT + 2 * NST + 15) / 16 : 6;   // k chunks of the image (<= 6, host check)
-  const int nkx = XWp / 16;
-  f32x4 bw[NKX];
+  f32x4 bw[3];
 #pragma unroll
-  for (int kc = 0; kc < NKX; ++kc)
+  for (int kc = 0; kc < 3; ++kc)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int j = 16 * kc + 4 * g + e;
-      bw[kc][e] = (kc < nkx && dok && j < XW) ? fb.wx[(long)j * D + dcl] : 0.f;
+      const int jj = 4 * g + e;
+      const int j = kc == 0 ? jj : R + 16 * (kc - 1) + jj;
+      bw[kc][e] = (dok && (kc > 0 || jj < R)) ? fb.wx[(long)j * D + dcl] : 0.f;
     }
+  __syncthreads();
+  // (b) + (c)
+  const unsigned lb = dok ? (unsigned)dl * 4u : 0x80000000u;   // padding channels: stores dropped
+  const auto r_dp = buf_rsrc(o.du + base * D, (unsigned)(L * D * 4));
   const float w0 = cf_ld(fb.conv_w, dcl * 4, dok), w1 = cf_ld(fb.conv_w, dcl * 4 + 1, dok),
               w2 = cf_ld(fb.conv_w, dcl * 4 + 2, dok), w3 = cf_ld(fb.conv_w, dcl * 4 + 3, dok),
               bias = cf_ld(fb.conv_b, dcl, dok);
   const float* xb = fb.xz + (long)b * L * (2 * D) + dcl;
   float cacc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int tm = 0; tm < ntm; ++tm) {
-    const int ar = min(16 * tm + r, Lp - 1);
-    const int tq = 16 * tm + 4 * g;   // this lane's 4 tokens tq .. tq + 3
-    float xv[7];                      // gathered taps tq - 3 .. tq + 3 (issued before the MFMAs)
+  constexpr int TG = 3;   // token tiles whose gathered taps are issued together (more spills the 128-VGPR budget)
+  for (int tm0 = 0; tm0 < ntm; tm0 += TG) {
+    float xv[TG][7];   // taps tq - 3 .. tq + 3 of this lane's tokens tq .. tq + 3
 #pragma unroll
-    for (int e = 0; e < 7; ++e) {
-      const int tau = tq - 3 + e;
-      xv[e] = (dok && tau >= 0 && tau < L) ? xb[ord[tau] * (2 * D)] : 0.f;
-    }
-    float dus[4];
+    for (int u = 0; u < TG; ++u) {
+      const int tq = 16 * (tm0 + u) + 4 * g;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dus[i] = (dok && tq + i < L) ? o.du[(base + tq + i) * D + dl] : 0.f;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kc = 0; kc < NKX; ++kc)
-      if (kc < nkx) {
-        const f32x4 av = *reinterpret_cast<const f32x4*>(XI + ar * XWp + 16 * kc + 4 * g);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bw[kc].x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bw[kc].y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bw[kc].z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bw[kc].w, acc, 0, 0, 0);
+      for (int e = 0; e < 7; ++e) {
+        const int tau = tq - 3 + e;
+        xv[u][e] = (dok && tau >= 0 && tau < L) ? xb[ord[tau] * (2 * D)] : 0.f;
       }
+    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = tq + i;
-      if (dok && t < L) {
-        float pre = fmaf(w0, xv[i], bias);
-        pre = fmaf(w1, xv[i + 1], pre);
-        pre = fmaf(w2, xv[i + 2], pre);
-        pre = fmaf(w3, xv[i + 3], pre);
-        const float sg = sigmoid_f(pre);
-        const float gd = (dus[i] + acc[i]) * sg * (1.f + pre * (1.f - sg));
-        o.du[(base + t) * D + dl] = gd;
-        cacc[4] += gd;
-        cacc[0] += gd * xv[i];
-        cacc[1] += gd * xv[i + 1];
-        cacc[2] += gd * xv[i + 2];
-        cacc[3] += gd * xv[i + 3];
+    for (int u = 0; u < TG; ++u) {
+      const int tm = tm0 + u;
+      if (tm >= ntm) break;
+      const int ar = min(16 * tm + r, Lp - 1);
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(DX16 + ar * 16 + 4 * g);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(m.Bs + ar * NST + 4 * g);
+      const f32x4 a2 = *reinterpret_cast<const f32x4*>(m.Cs + ar * NST + 4 * g);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bw[0].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bw[0].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bw[0].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bw[0].w, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bw[1].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bw[1].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bw[1].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bw[1].w, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a2.x, bw[2].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a2.y, bw[2].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a2.z, bw[2].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a2.w, bw[2].w, acc, 0, 0, 0);
+      // C[t = 16 tm + 4 g + i][dl]
+      const int tq = 16 * tm + 4 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (tq + i < L) {
+          float pre = fmaf(w0, xv[u][i], bias);
+          pre = fmaf(w1, xv[u][i + 1], pre);
+          pre = fmaf(w2, xv[u][i + 2], pre);
+          pre = fmaf(w3, xv[u][i + 3], pre);
+          const float sg = sigmoid_f(pre);
+          const float du = m.dts[(tq + i) * Dp + dl] + acc[i];
+          const float gd = dok ? du * sg * (1.f + pre * (1.f - sg)) : 0.f;
+          buf_st(r_dp, (unsigned)((tq + i) * D * 4) + lb, gd);
+          cacc[4] += gd;
+          cacc[0] += gd * xv[u][i];
+          cacc[1] += gd * xv[u][i + 1];
+          cacc[2] += gd * xv[u][i + 2];
+          cacc[3] += gd * xv[u][i + 3];
+        }
       }
     }
   }
@@ -626,7 +685,9 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
   const SeqLds m(smem, Lp, R, Dp);
   float* red = m.xr + Lp * R;
   const int nbuf = 2 * rbs;   // partial buffers: a combine every rbs segments, double-buffered
-  int* ord = reinterpret_cast<int*>(red + nbuf * nw * SCK * 32 + nw);   // [L] this direction's order
+  // partial buffers; the fused tail reuses them for its dxr image and W_dt ([Lp][16] + [D][R])
+  const int red_n = FUSE ? max(nbuf * nw * SCK * 32, Lp * 16 + a.D * R) : nbuf * nw * SCK * 32;
+  int* ord = reinterpret_cast<int*>(red + red_n + nw);   // [L] this direction's order
   const int s = blockIdx.x, k = s / a.B, b = s - k * a.B;
   for (int t = threadIdx.x; t < a.L; t += blockDim.x) ord[t] = a.order[k * a.L + t];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, cl = lane & 15;
@@ -745,13 +806,13 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
       const float qa = row_scatter4(Qv[0], Qv[1], Qv[2], Qv[3]);
       const float dt = m.dts[(t0 + q) * Dp + d], ut = row_select4(uc, q), dy = g * row_select4(dyr, q);
       const unsigned row = (unsigned)((t0 + q) * a.D * 4) + lane_b;
-      buf_st(r_du, row, dt * S + Dd * dy);
+      const float duv = dt * S + Dd * dy;
+      // fused tail: du stays in LDS, over this token's dt (read for the last time above, by this wave
+      // only: its channels); the tail adds x_proj's part and writes dpre
+      if (FUSE) m.dts[(t0 + q) * Dp + d] = duv;
+      else buf_st(r_du, row, duv);
       // softplus'(dt_lin) = sigmoid(dt_lin) = 1 - exp(-softplus(dt_lin))
-      const float ddl = (qa * LN2 + ut * S) * -expm1_c(-dt);
-      buf_st(r_ddtl, row, ddl);
-      // fused tail: d(dt_lin) kept in LDS over this token's dt (read for the last time above, by this
-      // wave only: its channels)
-      if (FUSE) m.dts[(t0 + q) * Dp + d] = valid ? ddl : 0.f;
+      buf_st(r_ddtl, row, (qa * LN2 + ut * S) * -expm1_c(-dt));
       dD_acc += dy * ut;   // row q's tokens; the rows are summed at the end
     }
     // one barrier per rbs segments: segment c's partials go to buffer c % (2 rbs), so the next rbs
@@ -787,7 +848,7 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
     if (q == 0) o.dd_part[(long)s * a.D + d] = dD_acc;
   }
   const float v = wave_sum(q == 0 ? dg_acc : 0.f);
-  float* rg = red + nbuf * nw * SCK * 32;
+  float* rg = red + red_n;
   if (lane == 0) rg[wave] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -795,7 +856,7 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
     for (int ww = 0; ww < nw; ++ww) sum += rg[ww];
     o.dg_part[s] = sum;
   }
-  if (FUSE) fused_bwd_tail<RT>(a, fb, o, s, b, m, ord, Lp, Dp);   // the barrier above: LDS images complete
+  if (FUSE && fb.tail) fused_bwd_tail<RT>(a, fb, o, s, b, m, ord, red, Lp, Dp);   // the barrier above: LDS images complete
 }
 
 // token-wise SiLU(z) gate of the combined output, backward:
@@ -1072,12 +1133,9 @@ static int scan_param_reduce(int B, int D, int ndir, const float* gate_logits, c
 // (null: they are recomputed into ws first).
 // ws needs (nseq*D*N + nseq*D + nseq + 2048*ceil(D*N/64)*64) floats (+ vc_mamba_scan_ckpt_floats
 // without ckpt).
-// the fused front end / tail need float4 rows of W_x (D % 4 == 0) and the [Lp][XWp] dxdbl image inside
-// the [Lp][Dp] dts region, XWp <= 96 (the model: D = 72, R = 9 -> XWp = 48 <= Dp = 80)
-static bool scan_fusable(int D, int R) {
-  const int XWp = (R + 2 * NST + 15) / 16 * 16;
-  return D % 4 == 0 && XWp <= vc_cdiv(D, 16) * 16 && XWp <= 96;
-}
+// the fused front end / tail need float4 rows of W_x / d(dt_lin) (D % 4 == 0) and R <= 16 (one 16-wide
+// chunk of dt-rank columns); the model: (D, R) = (72, 9), (128, 16)
+static bool scan_fusable(int D, int R) { return D % 4 == 0 && R <= 16; }
 
 static int scan_bwd_impl(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                          const int* order, const float* dt_w, const float* dt_b, const float* A_log,
@@ -1102,10 +1160,15 @@ static int scan_bwd_impl(int B, int L, int D, int R, int ndir, const float* u, c
   // three blocks per CU; else every segment
   const char* rbs_env = getenv("VITCNN_SCAN_RBS");
   int rbs = rbs_env ? std::max(1, std::min(4, atoi(rbs_env))) : 2;
-  auto lds_bytes = [&](int r) { return sizeof(float) * (seq_lds_floats(L, R, nw * 16) + 2 * r * nw * SCK * 32 + nw + L); };
+  const long tail_n = fb ? (long)seg_count_h(L) * SCK * 16 + (long)D * R : 0;
+  auto lds_bytes = [&](int r) {
+    return sizeof(float) * (seq_lds_floats(L, R, nw * 16) + std::max<long>(2L * r * nw * SCK * 32, tail_n) + nw + L);
+  };
   while (rbs > 1 && lds_bytes(rbs) > 160 * 1024 / 3 && lds_bytes(1) <= 160 * 1024 / 3) --rbs;
   const size_t sm = lds_bytes(rbs);
   VC_REQUIRE(sm <= 160 * 1024);
+  // the tail's (a) takes at most two token tiles per wave
+  VC_REQUIRE(!fb || (R <= 16 && (seg_count_h(L) * SCK + 15) / 16 <= 2 * nw));
   VC_REQUIRE_I32((long)nseq * L * (R + 2 * NST));
   float* p_a = ws;
   float* p_d = p_a + need_a;
@@ -1162,7 +1225,8 @@ VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const f
                                    hipStream_t stream) {
   VC_REQUIRE(xz && conv_w && conv_b && x_proj_w && conv_part);
   VC_REQUIRE_I32((long)B * L * 2 * D);
-  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part};
+  const char* tail_env = getenv("VITCNN_SCAN_TAIL");
+  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part, tail_env ? atoi(tail_env) : 1};
   return scan_bwd_impl(B, L, D, R, ndir, u, xdbl, order, dt_w, dt_b, A_log, Dskip, gate_logits, y, dyp, ckpt, dpre,
                        ddt_lin, dxdbl, dA_log, dDskip, dgate_logits, ws, ws_floats, &fb, stream);
 }
@@ -1230,6 +1294,7 @@ VC_API int vc_mamba_scan_bwd_params(int B, int D, int ndir, const float* gate_lo
   return scan_param_reduce(B, D, ndir, gate_logits, p_a, p_d, p_g, dA_log, dDskip, dgate_logits, scratch,
                            scratch_floats, stream);
 }
+
 
 // Backward of the direction gather + causal conv1d + SiLU.  dpre overwrites du in place;
 // the x half of dxz (ld 2D) is overwritten (vc_mamba_gate_bwd writes the z half); conv grads

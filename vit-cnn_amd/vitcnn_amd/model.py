@@ -56,6 +56,9 @@ N_COUNTERS = 1 << 16       # split-K tile counters per stream
 # conv1d backward into the scan backward's tail (vc_mamba_scan_fwd_fused / _bwd_fused); "0" restores the
 # separate launches (measurement switch, read per program)
 _SCAN_FUSED = os.environ.get("VITCNN_SCAN_FUSED", "1") != "0"
+# patch_embed + pre_norm + in_proj and combine + out_proj + ln1 + change_dim as one launch each
+# (vc_rowchain_front / _back); "0" restores the separate launches (measurement switch)
+_ROW_CHAIN = os.environ.get("VITCNN_ROW_CHAIN", "1") != "0"
 _LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
 _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in normal runs)
 _GROUP = os.environ.get("VITCNN_GEMM_GROUP", "1") != "0"   # grouped launches of independent fp32 GEMMs
@@ -445,6 +448,7 @@ class _Program:
         # 3x3 convs as implicit GEMMs (fp32 only, opt-in); bf16 operands use im2col + the bf16 vc_gemm
         self.implicit_conv = not self.gemm_flags and _IMPLICIT_CONV
         self.scan_fused = _SCAN_FUSED
+        self.row_chain = _ROW_CHAIN
         self.cur = 0
         self._gemm_i = 0
         self._ev_i = 0
@@ -656,11 +660,20 @@ class _Program:
         FM, e_fm = self.block_local_branch(blk, pfx, X, H)
         # --- hsiMamba global view (Mutimodality_Mamba7.py:419-701, :983-1017), on lane 0
         T = ws.f(pfx + ".T", rows * E)
-        self.mm_nt(rows, E, Cin, X, Cin, P[gv + ".patch_embed.projection.weight"], Cin, T, E,
-                   add=P[gv + ".pos_embed"], add_ld=E, add_mod=L_)
-        Xn = self.layernorm(gv + ".pre_norm", T, rows, E, pfx + ".Xn")
         XZ = ws.f(pfx + ".XZ", rows * 2 * D)
-        self.mm_nt(rows, 2 * D, E, Xn, E, P[mx + ".in_proj.weight"], E, XZ, 2 * D)
+        chain = self._chain_ok(blk)
+        if chain:
+            # patch_embed + pos_embed -> pre_norm -> in_proj in one launch (T, Xn and its statistics kept)
+            tag = pfx + ".Xn"
+            self.L.vc_rowchain_front(rows, Cin, E, 2 * D, X, P[gv + ".patch_embed.projection.weight"],
+                                     P[gv + ".pos_embed"], L_, T, P[gv + ".pre_norm.weight"], P[gv + ".pre_norm.bias"],
+                                     LN_EPS, ws.f(tag, rows * E), ws.f(tag + ".m", rows), ws.f(tag + ".r", rows),
+                                     P[mx + ".in_proj.weight"], XZ, self.s)
+        else:
+            self.mm_nt(rows, E, Cin, X, Cin, P[gv + ".patch_embed.projection.weight"], Cin, T, E,
+                       add=P[gv + ".pos_embed"], add_ld=E, add_mod=L_)
+            Xn = self.layernorm(gv + ".pre_norm", T, rows, E, pfx + ".Xn")
+            self.mm_nt(rows, 2 * D, E, Xn, E, P[mx + ".in_proj.weight"], E, XZ, 2 * D)
         U = ws.f(pfx + ".U", NDIR * rows * D)
         XD = ws.f(pfx + ".XD", NDIR * rows * XW)
         Y = ws.f(pfx + ".Y", NDIR * rows * D)
@@ -679,13 +692,22 @@ class _Program:
             self.L.vc_mamba_scan_fwd(B, L_, D, R, NDIR, U, XD, order, P[mx + ".dt_proj.weight"],
                                      P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], Y, CKP, self.s)
         YP, YS = ws.f(pfx + ".YP", rows * D), ws.f(pfx + ".YS", rows * D)
-        self.L.vc_mamba_combine_fwd(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, XZ, YP, YS, self.s)
         T2 = ws.f(pfx + ".T2", rows * E)
-        self.mm_nt(rows, E, D, YS, D, P[mx + ".out_proj.weight"], D, T2, E, add=T, add_ld=E, add_mod=rows)
-        G = self.layernorm(gv + ".ln1", T2, rows, E, pfx + ".G")
-        # --- global feature: change_dim -> TokenLearner -> ln3
         CD = ws.f(pfx + ".CD", rows * Cout)
-        self.mm_nt(rows, Cout, E, G, E, P[pfx + ".change_dim.weight"], E, CD, Cout, bias=P[pfx + ".change_dim.bias"])
+        if chain:
+            # combine -> out_proj (+ residual) -> ln1 -> change_dim in one launch
+            tag = pfx + ".G"
+            self.L.vc_rowchain_back(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, XZ, YP, YS, E,
+                                    P[mx + ".out_proj.weight"], T, T2, P[gv + ".ln1.weight"], P[gv + ".ln1.bias"],
+                                    LN_EPS, ws.f(tag, rows * E), ws.f(tag + ".m", rows), ws.f(tag + ".r", rows), Cout,
+                                    P[pfx + ".change_dim.weight"], P[pfx + ".change_dim.bias"], CD, self.s)
+        else:
+            self.L.vc_mamba_combine_fwd(B, L_, D, NDIR, inv, P[gv + ".weights"], Y, XZ, YP, YS, self.s)
+            self.mm_nt(rows, E, D, YS, D, P[mx + ".out_proj.weight"], D, T2, E, add=T, add_ld=E, add_mod=rows)
+            G = self.layernorm(gv + ".ln1", T2, rows, E, pfx + ".G")
+            # --- global feature: change_dim -> TokenLearner -> ln3
+            self.mm_nt(rows, Cout, E, G, E, P[pfx + ".change_dim.weight"], E, CD, Cout,
+                       bias=P[pfx + ".change_dim.bias"])
         Zg = self.token_learner(pfx + ".global_feature", CD, L_, Cout, S)
         Fg = self.layernorm(pfx + ".ln3", Zg, B * S, Cout, pfx + ".Fg")
         self.wait(e_fm)
@@ -982,25 +1004,37 @@ class _Program:
         CD, dCD = f(pfx + ".CD", rows * Cout), f(pfx + ".dCD", rows * Cout)
         self.token_learner_bwd(pfx + ".global_feature", CD, L_, Cout, S, dZg, dCD)
         Gm, dG = f(pfx + ".G", rows * E), f(pfx + ".dG", rows * E)
-        self.linear_bwd(pfx + ".change_dim.weight", pfx + ".change_dim.bias", dCD, rows, Cout, E, Gm, E, dG, 0.0,
-                        defer=True)
         # hsiMamba: ln1 -> out_proj -> scan/combine -> x_proj/dt_proj -> conv -> in_proj -> pre_norm -> patch_embed
         T2, dT = f(pfx + ".T2", rows * E), f(pfx + ".dT", rows * E)
-        self.ln_bwd(gv + ".ln1", pfx + ".G", dG, T2, rows, E, dT, 0.0, defer=True)
         YS, dYS = f(pfx + ".YS", rows * D), f(pfx + ".dYS", rows * D)
-        # (the pre_norm backward below writes the residual sum to dTt, so dT stays as this reads it)
-        self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0, defer=True)
         U, XD, XZ = f(pfx + ".U", NDIR * rows * D), f(pfx + ".XD", NDIR * rows * XW), f(pfx + ".XZ", rows * 2 * D)
         Y, YP = f(pfx + ".Y", NDIR * rows * D), f(pfx + ".YP", rows * D)
         dU, dDTL = f(pfx + ".dU", NDIR * rows * D), f(pfx + ".dDTL", NDIR * rows * D)
         dXD, dXZ, dYP = f(pfx + ".dXD", NDIR * rows * XW), f(pfx + ".dXZ", rows * 2 * D), f(pfx + ".dYP", rows * D)
-        # SiLU(z) gate (token-wise): dyp and the z half of dxz
-        self.L.vc_mamba_gate_bwd(B, L_, D, XZ, YP, dYS, dYP, dXZ, self.s)
+        if self._chain_ok(blk):
+            # change_dim / ln1 / out_proj data gradients + the SiLU(z) gate backward in one launch; the
+            # weight gradients and ln1's parameter reduction queued for the weight-gradient lane
+            part = f(pfx + ".ln1part", self.L.vc_rowchain_ln_part_floats(rows, E))
+            self.L.vc_rowchain_back_bwd(rows, Cout, E, D, dCD, P[pfx + ".change_dim.weight"], T2, f(pfx + ".G.m", rows),
+                                        f(pfx + ".G.r", rows), P[gv + ".ln1.weight"], dT, part,
+                                        P[mx + ".out_proj.weight"], XZ, YP, dYP, dXZ, self.s)
+            self.defer_wgrad(True, Cout, E, rows, dCD, Cout, Gm, E, G[pfx + ".change_dim.weight"], E,
+                             G[pfx + ".change_dim.bias"])
+            self._ln_params(gv + ".ln1", rows, E, part)
+            self.defer_wgrad(True, E, D, rows, dT, E, YS, D, G[mx + ".out_proj.weight"], D)
+        else:
+            self.linear_bwd(pfx + ".change_dim.weight", pfx + ".change_dim.bias", dCD, rows, Cout, E, Gm, E, dG, 0.0,
+                            defer=True)
+            self.ln_bwd(gv + ".ln1", pfx + ".G", dG, T2, rows, E, dT, 0.0, defer=True)
+            # (the pre_norm backward below writes the residual sum to dTt, so dT stays as this reads it)
+            self.linear_bwd(mx + ".out_proj.weight", None, dT, rows, E, D, YS, D, dYS, 0.0, defer=True)
+            # SiLU(z) gate (token-wise): dyp and the z half of dxz
+            self.L.vc_mamba_gate_bwd(B, L_, D, XZ, YP, dYS, dYP, dXZ, self.s)
         self.flush_wgrads()   # fusion, change_dim, out_proj: alongside the scan backward
         CKPb = f(pfx + ".CKP", self.L.vc_mamba_scan_ckpt_floats(B, L_, D, NDIR))
         if self.scan_fused:
             self._scan_bwd_fused(pfx, gv, mx, B, L_, D, R, XW, order, inv, CKPb)
-            return self._block_bwd_tail(pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch)
+            return self._block_bwd_tail(blk, pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch)
         if self._deferring(True):
             # the per-sequence dA_log / D / gate partials stay in a buffer of their own; their
             # reductions go with the next weight-gradient flush
@@ -1029,13 +1063,13 @@ class _Program:
         self.L.vc_mamba_dirconv_bwd(B, L_, D, NDIR, order, inv, XZ, P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"],
                                     dU, dXZ, G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"], self.scr_p,
                                     self.scr_n, self.s)
-        self._block_bwd_tail(pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch)
+        self._block_bwd_tail(blk, pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch)
 
     def _scan_bwd_fused(self, pfx, gv, mx, B, L_, D, R, XW, order, inv, CKPb):
         """scan backward + dt_proj / x_proj data gradients + conv1d / SiLU backward in one launch
         (vc_mamba_scan_bwd_fused), the direction gather into dxz, and the parameter gradients (dt_proj,
         x_proj, conv1d, A_log / D / gate) queued for the weight-gradient lane"""
-        ws, P, G, f = self.ws, self.P, self.G, self.ws.f
+        P, G, f = self.P, self.G, self.ws.f
         rows = B * L_
         nr, nseq = NDIR * rows, NDIR * B
         U, XD, XZ = f(pfx + ".U", nr * D), f(pfx + ".XD", nr * XW), f(pfx + ".XZ", rows * 2 * D)
@@ -1062,24 +1096,54 @@ class _Program:
         self.defer_wgrad(True, D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, G[mx + ".dt_proj.bias"])
         self.defer_wgrad(True, XW, D, nr, dXD, XW, U, D, G[mx + ".x_proj.weight"], D)
         cw, cb = G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"]
+        conv = lambda: self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s)  # noqa: E731
         if defer:
-            self.pending_wgrads.append(lambda: self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s))
+            self.pending_wgrads.append(conv)
         else:
-            self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s)
+            conv()
 
-    def _block_bwd_tail(self, pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch):
+    def _chain_ok(self, blk):
+        """the row-chain launches apply to this block's widths (rowchain.hip limits)"""
+        E = blk.embed
+        return (self.row_chain and blk.cin <= 256 and blk.cin % 4 == 0 and E <= 256 and E % 4 == 0
+                and (E // 2) % 4 == 0 and blk.cout <= 256)
+
+    def _ln_params(self, pfx, rows, E, part):
+        """a LayerNorm's weight / bias gradients from a backward chain's partials: queued for the
+        weight-gradient lane (or now, without lanes)"""
+        gw, gb = self.G[pfx + ".weight"], self.G[pfx + ".bias"]
+        fn = lambda: self.L.vc_rowchain_ln_params(rows, E, part, gw, gb, 0.0, self.s)  # noqa: E731
+        if self._deferring(True):
+            self.pending_wgrads.append(fn)
+        else:
+            fn()
+
+    def _block_bwd_tail(self, blk, pfx, gv, mx, B, L_, E, Cin, rows, X, dX, dT, e_ch):
         """in_proj -> pre_norm -> patch_embed backward of a GlobalLocal block"""
         ws, P, G, f = self.ws, self.P, self.G, self.ws.f
         D = E // 2
         dXZ = f(pfx + ".dXZ", rows * 2 * D)
         Xn, dXn = f(pfx + ".Xn", rows * E), f(pfx + ".dXn", rows * E)
-        self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0, defer=True)
-        self.flush_wgrads()   # dt_proj, x_proj, conv1d, in_proj
         T, dTt = f(pfx + ".T", rows * E), f(pfx + ".dTt", rows * E)
-        self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dTt, 0.0, res=dT, defer=True)   # dT + LN grad
-        if dX:
-            self.wait(e_ch)
-            self.mm_nn(rows, Cin, E, dTt, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
+        if self._chain_ok(blk):
+            # in_proj / pre_norm (+ the residual dT) / patch_embed data gradients in one launch, after the
+            # other branches' accumulations into dX (lane 1 is done long before lane 0 gets here)
+            self.defer_wgrad(True, 2 * D, E, rows, dXZ, 2 * D, Xn, E, G[mx + ".in_proj.weight"], E)
+            self.flush_wgrads()   # dt_proj, x_proj, conv1d, in_proj
+            if dX:
+                self.wait(e_ch)
+            part = f(pfx + ".prepart", self.L.vc_rowchain_ln_part_floats(rows, E))
+            self.L.vc_rowchain_front_bwd(rows, 2 * D, E, Cin, dXZ, P[mx + ".in_proj.weight"], T, f(pfx + ".Xn.m", rows),
+                                         f(pfx + ".Xn.r", rows), P[gv + ".pre_norm.weight"], dT, dTt, part,
+                                         P[gv + ".patch_embed.projection.weight"], dX or None, 1.0, self.s)
+            self._ln_params(gv + ".pre_norm", rows, E, part)
+        else:
+            self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0, defer=True)
+            self.flush_wgrads()   # dt_proj, x_proj, conv1d, in_proj
+            self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dTt, 0.0, res=dT, defer=True)   # dT + LN grad
+            if dX:
+                self.wait(e_ch)
+                self.mm_nn(rows, Cin, E, dTt, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
         # pos_embed and patch_embed weight gradients: off the critical path
         e = self.mark()
         with self.lane(WGRAD_LANE if _DEFER_WGRAD else 0, e):
