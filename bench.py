@@ -78,7 +78,7 @@ def time_kernel(fn, reps, stream):
     return s.elapsed_time(e) / reps * 1e-3
 
 
-PMC_PROFILES = ("r02_pmc_s4.json", "r02_pmc.json", "r01_pmc.json")   # newest first
+PMC_PROFILES = ("r03_pmc.json", "r02_pmc_s4.json", "r02_pmc.json", "r01_pmc.json")   # newest first
 
 
 def _pmc_from_profile(kernel_key):
@@ -208,14 +208,16 @@ def dominant_kernel_roofline(model, batch, reps):
     """Re-launch the step's dominant kernel on its live workspace buffers and time it with HIP events
     on the stream it is launched on.
 
-    Dominant kernel (profiles/r01_*_kernel_stats.md): the hsiMamba selective-scan backward of
-    block hsi1 (`scan_bwd<9>`, grid 640 sequences x 5 channel chunks), the longest single launch
-    of the step.  It is a sequential recurrence over 81 tokens with no matrix work, so its roofline
-    is HBM.  Algorithmic bytes per launch = compulsory reads of u, x_proj rows, yp (each
-    [10*B*L, *]), d(yp) [B*L, D] and the forward's 4-token state checkpoints
-    [10*B][ceil(L/4)][16][D] + writes of du, d(dt_lin) and the dB/dC columns (DESIGN.md
-    section 4).  The parameter-gradient outputs are passed as NULL, so the timed launch is the
-    scan_bwd kernel alone (the same kernel rocprofv3 reports in profiles/)."""
+    Dominant kernel (profiles/r03_*): the hsiMamba selective-scan backward of block hsi1 with its fused
+    tail (`scan_bwd<9, true, true>`, vc_mamba_scan_bwd_fused: grid 640 sequences x 5 channel chunks), the
+    longest single launch of the step.  A sequential recurrence over 81 tokens, then the sequence's
+    dt_proj / x_proj data gradients (MFMA) and conv1d + SiLU backward; its roofline is HBM.  Algorithmic
+    bytes per launch = compulsory reads of u, x_proj rows, yp (each [10*B*L, *]), d(yp) [B*L, D], the x
+    half of xz [B*L, D] (gathered, counted once) and the forward's 4-token state checkpoints
+    [10*B][ceil(L/4)][16][D] + writes of d(dt_lin), the full dxdbl rows, dpre and the per-sequence
+    parameter partials (A_log / D / gate, conv1d).  The parameter-gradient outputs
+    are passed as NULL, so the timed launch is the kernel alone (the same kernel rocprofv3 reports in
+    profiles/)."""
     from vitcnn_amd._lib import lib
     from vitcnn_amd.model import NDIR, _Program
     dev = model.flat_params.device
@@ -225,7 +227,7 @@ def dominant_kernel_roofline(model, batch, reps):
     E = blk.embed
     D, R, Lt = E // 2, -(-E // 16), H * H
     XW = R + 32
-    rows, nr = batch * Lt, NDIR * batch * Lt
+    rows, nr, nseq = batch * Lt, NDIR * batch * Lt, NDIR * batch
     f = prog.ws.f
     mx, gv = pfx + ".global_view.layers.0", pfx + ".global_view"
     P = prog.P
@@ -234,25 +236,31 @@ def dominant_kernel_roofline(model, batch, reps):
     stream = torch.cuda.current_stream(dev)
 
     def fn():
-        L.vc_mamba_scan_bwd(batch, Lt, D, R, NDIR, f(pfx + ".U", nr * D), f(pfx + ".XD", nr * XW), order,
-                            P[mx + ".dt_proj.weight"], P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"],
-                            P[gv + ".weights"], f(pfx + ".Y", nr * D), f(pfx + ".dYP", rows * D),
-                            f(pfx + ".CKP", ckpt),
-                            f(pfx + ".dU", nr * D), f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW),
-                            None, None, None, prog.scr_p, prog.scr_n, stream.cuda_stream)
+        L.vc_mamba_scan_bwd_fused(batch, Lt, D, R, NDIR, f(pfx + ".U", nr * D), f(pfx + ".XD", nr * XW), order,
+                                  f(pfx + ".XZ", rows * 2 * D), P[mx + ".conv1d.weight"], P[mx + ".conv1d.bias"],
+                                  P[mx + ".x_proj.weight"], P[mx + ".dt_proj.weight"], P[mx + ".dt_proj.bias"],
+                                  P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], f(pfx + ".Y", nr * D),
+                                  f(pfx + ".dYP", rows * D), f(pfx + ".CKP", ckpt), f(pfx + ".dU", nr * D),
+                                  f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW),
+                                  f(pfx + ".convpart", nseq * 5 * D), None, None, None, prog.scr_p, prog.scr_n,
+                                  stream.cuda_stream)
 
     t = time_kernel(fn, reps, stream)
-    algo = 4.0 * (nr * D * 2 + nr * XW + rows * D + ckpt + nr * D * 2 + nr * 32)
+    reads = nr * D + nr * XW + nr * D + rows * D + rows * D + ckpt
+    writes = nr * D + nr * XW + nr * D + nseq * 5 * D + nseq * (D * 16 + D + 1)
+    algo = 4.0 * (reads + writes)
     achieved = algo / t / 1e9
-    traffic = _traffic_from_profile("scan_bwd<9>")
+    key = "scan_bwd<9, true, true>"
+    traffic = _traffic_from_profile(key)
     # the same launch against its two other bounds: compulsory HBM bytes only (the 4-token state
     # checkpoints the forward writes for it excluded), and VALU issue (the committed PMC profile's
     # SQ_INSTS_VALU per launch x 4 cycles / 1024 SIMDs at 2.4 GHz = the time the instructions need
     # with every SIMD issuing every cycle)
     compulsory = algo - 4.0 * ckpt
-    pmc = _pmc_from_profile("scan_bwd<9>") or {}
+    pmc = _pmc_from_profile(key) or {}
     valu_us = pmc.get("valu_issue_bound_us")
-    return {"kernel": "scan_bwd<9> (hsi1 selective-scan backward, 640 seq x 81 tokens x 72 ch x 16 states)",
+    return {"kernel": key + " (hsi1 selective-scan backward + fused dt_proj / x_proj / conv1d data-gradient tail, "
+                            "640 seq x 81 tokens x 72 ch x 16 states)",
             "bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic, "avg_launch_us": round(t * 1e6, 2),
             "algorithmic_bytes_per_launch": algo,

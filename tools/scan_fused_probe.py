@@ -94,12 +94,14 @@ def main():
             L.vc_mamba_scan_bwd_fused(B, Lt, D, R, NDIR, U, XD, order, XZ, cw, cb, wx, wdt, bdt, alog, dsk, gl, Y, dYP,
                                       CKP, dU, dDTL, dXD, CP, None, None, None, wsp, wsn, s)
 
-        def scan_bwd_fused_notail():   # measurement only: the sweep with the tail skipped
-            os.environ["VITCNN_SCAN_TAIL"] = "0"
-            try:
-                scan_bwd_fused()
-            finally:
-                del os.environ["VITCNN_SCAN_TAIL"]
+        def tail_mask(mask):   # measurement only: parts of the tail skipped (VITCNN_SCAN_TAIL bits)
+            def fn():
+                os.environ["VITCNN_SCAN_TAIL"] = str(mask)
+                try:
+                    scan_bwd_fused()
+                finally:
+                    del os.environ["VITCNN_SCAN_TAIL"]
+            return fn
 
         def bwd_fused():
             scan_bwd_fused()
@@ -111,7 +113,8 @@ def main():
         res = {}
         for nm, fn in (("fwd_separate", fwd_sep), ("fwd_fused", fwd_fused), ("scan_bwd", scan_bwd),
                        ("bwd_separate", bwd_sep), ("scan_bwd_fused", scan_bwd_fused),
-                       ("scan_bwd_fused_notail", scan_bwd_fused_notail), ("bwd_fused", bwd_fused),
+                       ("tail_none", tail_mask(0)), ("tail_staging_only", tail_mask(1)),
+                       ("tail_a", tail_mask(3)), ("tail_bc", tail_mask(5)), ("bwd_fused", bwd_fused),
                        ("conv_params (off path)", conv_wgrad)):
             res[nm] = timed(fn, reps, st)
         print(pfx, "  ".join(f"{k} {v:.1f}" for k, v in res.items()), flush=True)

@@ -503,7 +503,8 @@ struct FusedBwd {
   const float* conv_b;   // [D]
   const float* wx;       // [R+2N, D]
   float* conv_part;      // [nseq][5D] out
-  int tail;              // 1; 0 skips the tail (VITCNN_SCAN_TAIL=0: a measurement switch, results incomplete)
+  int tail;              // 7 (all); measurement masks (VITCNN_SCAN_TAIL, results incomplete): bit 0 the
+                         // tail at all, bit 1 phase (a), bit 2 phases (b) + (c)
 };
 
 struct ScanBwdOut {
@@ -544,6 +545,7 @@ __device__ __forceinline__ void fused_bwd_tail(const ScanArgs& a, const FusedBwd
   // (a) A = ddtl rows from HBM (this block's sweep wrote them), B[k = c][col = j] = W_dt[c, j] (LDS);
   // a wave's (at most two, ntm <= 2 nw) token tiles' A rows loaded at once
   f32x4 avs[2][FMAX_KC];
+  const int nu = (fb.tail & 2) ? 2 : 0;   // measurement mask (see FusedBwd::tail)
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int ta = 16 * (wave + u * nw) + r;
@@ -557,7 +559,7 @@ __device__ __forceinline__ void fused_bwd_tail(const ScanArgs& a, const FusedBwd
     }
   }
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < nu; ++u) {
     const int tm = wave + u * nw;
     if (tm >= ntm) break;
     const f32x4* av = avs[u];   // (tiles past 2 nw: none for the fused shapes, host check)
@@ -608,7 +610,8 @@ __device__ __forceinline__ void fused_bwd_tail(const ScanArgs& a, const FusedBwd
   const float* xb = fb.xz + (long)b * L * (2 * D) + dcl;
   float cacc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   constexpr int TG = 3;   // token tiles whose gathered taps are issued together (more spills the 128-VGPR budget)
-  for (int tm0 = 0; tm0 < ntm; tm0 += TG) {
+  const int ntm_c = (fb.tail & 4) ? ntm : 0;   // measurement mask
+  for (int tm0 = 0; tm0 < ntm_c; tm0 += TG) {
     float xv[TG][7];   // taps tq - 3 .. tq + 3 of this lane's tokens tq .. tq + 3
 #pragma unroll
     for (int u = 0; u < TG; ++u) {
@@ -856,7 +859,7 @@ __global__ __launch_bounds__(512, 4) void scan_bwd(ScanArgs a, int ndir, const f
     for (int ww = 0; ww < nw; ++ww) sum += rg[ww];
     o.dg_part[s] = sum;
   }
-  if (FUSE && fb.tail) fused_bwd_tail<RT>(a, fb, o, s, b, m, ord, red, Lp, Dp);   // the barrier above: LDS images complete
+  if (FUSE && (fb.tail & 1)) fused_bwd_tail<RT>(a, fb, o, s, b, m, ord, red, Lp, Dp);   // the barrier above: LDS images complete
 }
 
 // token-wise SiLU(z) gate of the combined output, backward:
@@ -1226,7 +1229,7 @@ VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const f
   VC_REQUIRE(xz && conv_w && conv_b && x_proj_w && conv_part);
   VC_REQUIRE_I32((long)B * L * 2 * D);
   const char* tail_env = getenv("VITCNN_SCAN_TAIL");
-  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part, tail_env ? atoi(tail_env) : 1};
+  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part, tail_env ? atoi(tail_env) : 7};
   return scan_bwd_impl(B, L, D, R, ndir, u, xdbl, order, dt_w, dt_b, A_log, Dskip, gate_logits, y, dyp, ckpt, dpre,
                        ddt_lin, dxdbl, dA_log, dDskip, dgate_logits, ws, ws_floats, &fb, stream);
 }

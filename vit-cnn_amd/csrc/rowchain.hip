@@ -22,8 +22,11 @@
 
 namespace {
 
-constexpr int RC_BM = 32;       // rows per block (two 16-row MFMA tiles)
-constexpr int RC_THREADS = 512;  // 8 waves
+// rows per block BM: 32 (two 16-row MFMA tiles) when that still gives >= 160 blocks, else 16 (hsi2's 3136
+// rows: 196 blocks instead of 98 -- the products are fp32-MFMA-bound per block, so the row count per
+// block sets the per-block time and the block count the share of the 256 CUs that work)
+constexpr int RC_THREADS = 512;  // backward chains: 8 waves; forward chains: one wave per 16-column tile,
+                                 // 8..16 waves
 constexpr int RC_KC = 16;        // k chunks of 16: K <= 256
 
 struct ChainArgs {
@@ -59,35 +62,41 @@ __device__ __forceinline__ float rc_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, 
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
-// The block's 32 rows of a [rows, K] matrix (K % 4 == 0) into LDS rows of stride lda, zero past the last
+// The block's BM rows of a [rows, K] matrix (K % 4 == 0) into LDS rows of stride lda, zero past the last
 // row and in columns K..lda-1: float4 loads, all of a thread's (<= RC_STAGE) issued before any store, so
 // the phase costs one load latency instead of one per loop trip.
 constexpr int RC_STAGE = 5;   // ceil(32 rows x (256 + 4) floats / 4 / 512 threads)
+template <int BM>
 __device__ __forceinline__ void stage_rows(float* As, int lda, const float* __restrict__ src, int K, int r0, int nrow) {
   const int q = lda / 4;   // float4 per LDS row (lda % 4 == 0)
   const int kq = K / 4;
-  f32x4 v[RC_STAGE];
+  const int nt = blockDim.x;
+  for (int base = 0; base < BM * q; base += RC_STAGE * nt) {   // one trip for every shape here
+    f32x4 v[RC_STAGE];
 #pragma unroll
-  for (int j = 0; j < RC_STAGE; ++j) {
-    const int i = threadIdx.x + j * RC_THREADS;
-    const int rr = i / q, k4 = i - rr * q;
-    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    v[j] = (i < RC_BM * q && rr < nrow && k4 < kq) ? *reinterpret_cast<const f32x4*>(src + (long)(r0 + rr) * K + 4 * k4)
-                                                    : z;
-  }
+    for (int j = 0; j < RC_STAGE; ++j) {
+      const int i = base + threadIdx.x + j * nt;
+      const int rr = i / q, k4 = i - rr * q;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      v[j] = (i < BM * q && rr < nrow && k4 < kq) ? *reinterpret_cast<const f32x4*>(src + (long)(r0 + rr) * K + 4 * k4)
+                                                   : z;
+    }
 #pragma unroll
-  for (int j = 0; j < RC_STAGE; ++j) {
-    const int i = threadIdx.x + j * RC_THREADS;
-    if (i < RC_BM * q) reinterpret_cast<f32x4*>(As)[i] = v[j];
+    for (int j = 0; j < RC_STAGE; ++j) {
+      const int i = base + threadIdx.x + j * nt;
+      if (i < BM * q) reinterpret_cast<f32x4*>(As)[i] = v[j];
+    }
   }
 }
 
-// C[32 x N] = A[32 x K] (LDS, row stride lda, columns K..kpad(K)-1 zero) op(W); op(W) = W[N][K]^T
+// C[16 MT x N] = A[16 MT x K] (LDS, row stride lda, columns K..kpad(K)-1 zero) op(W); op(W) = W[N][K]^T
 // (TW = false: a projection, float4 fragment loads along k) or W[K][N] (TW = true: its data gradient,
-// four k rows per fragment).  For each output element calls epi(row, col, value) (row < 32, col < N).
-template <bool TW = false, typename Epi>
-__device__ __forceinline__ void block_gemm32(const float* A, int lda, int K, const float* __restrict__ W, int N,
-                                             Epi epi) {
+// four k rows per fragment).  For each output element calls epi(row, col, value) (col < N).  MT = 2: one
+// accumulator per 16-row tile; MT = 1: the even and the odd k chunks in two accumulators (two independent
+// MFMA chains: the 40-cycle dependent latency of v_mfma_f32_16x16x4_f32 hidden behind its 32-cycle issue).
+template <int MT, bool TW = false, typename Epi>
+__device__ __forceinline__ void block_gemm(const float* A, int lda, int K, const float* __restrict__ W, int N,
+                                           Epi epi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int nkc = kpad(K) / 16, ntn = (N + 15) / 16;
@@ -115,39 +124,53 @@ __device__ __forceinline__ void block_gemm32(const float* A, int lda, int K, con
     for (int kc = 0; kc < RC_KC; ++kc)
       if (kc < nkc) {
         const int k0 = 16 * kc + 4 * g;
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(A + r * lda + k0);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(A + (16 + r) * lda + k0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bw[kc].x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bw[kc].x, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bw[kc].y, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bw[kc].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bw[kc].z, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bw[kc].z, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bw[kc].w, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bw[kc].w, acc1, 0, 0, 0);
+        if (MT == 2) {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(A + r * lda + k0);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(A + (16 + r) * lda + k0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bw[kc].x, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bw[kc].x, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bw[kc].y, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bw[kc].y, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bw[kc].z, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bw[kc].z, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bw[kc].w, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bw[kc].w, acc1, 0, 0, 0);
+        } else {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(A + r * lda + k0);
+          f32x4& acc = (kc & 1) ? acc1 : acc0;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bw[kc].x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bw[kc].y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bw[kc].z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bw[kc].w, acc, 0, 0, 0);
+        }
       }
     if (n < N) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        epi(4 * g + i, n, acc0[i]);
-        epi(16 + 4 * g + i, n, acc1[i]);
+        if (MT == 2) {
+          epi(4 * g + i, n, acc0[i]);
+          epi(16 + 4 * g + i, n, acc1[i]);
+        } else {
+          epi(4 * g + i, n, acc0[i] + acc1[i]);
+        }
       }
     }
   }
 }
 
 // MODE 0: front chain (A = block input rows), MODE 1: back chain (A = the gated combine)
-template <int MODE>
-__global__ __launch_bounds__(RC_THREADS) void rowchain_fwd(ChainArgs c) {
+template <int MODE, int BM>
+__global__ __launch_bounds__(1024) void rowchain_fwd(ChainArgs c) {
+  constexpr int MT = BM / 16;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lda = kpad(c.K0) + 4, ldt = kpad(c.E) + 4;   // +4 floats: rows start 4 banks apart
-  float* As = sm;                    // [32][lda]
-  float* Ts = sm + RC_BM * lda;      // [32][ldt]
-  const int r0 = blockIdx.x * RC_BM;
-  const int nrow = min(RC_BM, c.rows - r0);
+  float* As = sm;                 // [BM][lda]
+  float* Ts = sm + BM * lda;      // [BM][ldt]
+  const int r0 = blockIdx.x * BM;
+  const int nrow = min(BM, c.rows - r0);
   // ---- A phase (zero rows past the end and columns past K0)
   if (MODE == 0) {
-    stage_rows(As, lda, c.A0, c.K0, r0, nrow);
+    stage_rows<BM>(As, lda, c.A0, c.K0, r0, nrow);
   } else {
     // vc_mamba_combine_fwd per element (same operation order): YP = sum_k softmax(g)_k y_k[inv_k(l)],
     // YS = YP SiLU(z).  A thread takes 4 consecutive channels of a row (float4 gathers) and issues the
@@ -158,13 +181,14 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_fwd(ChainArgs c) {
     float den = 0.f;
     for (int i = 0; i < c.ndir; ++i) den += __expf(c.glog[i] - mx);
     const float rden = 1.f / den;
-    constexpr int NI = 2;   // items per thread: 32 rows x 64 float4 / 512 threads = 4 at most, in 2 rounds
-    for (int i0 = threadIdx.x; i0 < RC_BM * q; i0 += NI * RC_THREADS) {
+    constexpr int NI = 2;   // items per thread per round (32 rows x 33 float4 / 512 threads: 3 at most)
+    const int nt = blockDim.x;
+    for (int i0 = threadIdx.x; i0 < BM * q; i0 += NI * nt) {
       int tk[NI][10];
 #pragma unroll
       for (int u = 0; u < NI; ++u) {
-        const int i = i0 + u * RC_THREADS, rr = i / q, d4 = i - rr * q;
-        const bool ok = i < RC_BM * q && rr < nrow && d4 < dq;
+        const int i = i0 + u * nt, rr = i / q, d4 = i - rr * q;
+        const bool ok = i < BM * q && rr < nrow && d4 < dq;
         const int bl = r0 + rr, l = bl % c.L;
 #pragma unroll
         for (int kk = 0; kk < 10; ++kk) tk[u][kk] = (ok && kk < c.ndir) ? c.inv[kk * c.L + l] : 0;
@@ -172,8 +196,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_fwd(ChainArgs c) {
       f32x4 yv[NI][10];
 #pragma unroll
       for (int u = 0; u < NI; ++u) {
-        const int i = i0 + u * RC_THREADS, rr = i / q, d4 = i - rr * q;
-        const bool ok = i < RC_BM * q && rr < nrow && d4 < dq;
+        const int i = i0 + u * nt, rr = i / q, d4 = i - rr * q;
+        const bool ok = i < BM * q && rr < nrow && d4 < dq;
         const int bl = r0 + rr, b = bl / c.L;
 #pragma unroll
         for (int kk = 0; kk < 10; ++kk) {
@@ -185,8 +209,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_fwd(ChainArgs c) {
       }
 #pragma unroll
       for (int u = 0; u < NI; ++u) {
-        const int i = i0 + u * RC_THREADS, rr = i / q, d4 = i - rr * q;
-        if (i >= RC_BM * q) continue;
+        const int i = i0 + u * nt, rr = i / q, d4 = i - rr * q;
+        if (i >= BM * q) continue;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (rr < nrow && d4 < dq) {
           const long bl = r0 + rr;
@@ -214,7 +238,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_fwd(ChainArgs c) {
   }
   __syncthreads();
   // ---- G1: out1 = A W1^T + addend -> HBM and Ts
-  block_gemm32(As, lda, c.K0, c.W1, c.E, [&](int rr, int n, float v) {
+  block_gemm<MT>(As, lda, c.K0, c.W1, c.E, [&](int rr, int n, float v) {
     const int row = r0 + rr;
     float o = 0.f;
     if (rr < nrow) {
@@ -224,7 +248,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_fwd(ChainArgs c) {
     Ts[rr * ldt + n] = o;
   });
   // zero the padding columns E..kpad(E)-1 (read as k by G2)
-  for (int i = threadIdx.x; i < RC_BM * (kpad(c.E) - c.E); i += blockDim.x) {
+  for (int i = threadIdx.x; i < BM * (kpad(c.E) - c.E); i += blockDim.x) {
     const int w = kpad(c.E) - c.E, rr = i / w;
     Ts[rr * ldt + c.E + (i - rr * w)] = 0.f;
   }
@@ -268,7 +292,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_fwd(ChainArgs c) {
   }
   __syncthreads();
   // ---- G2: out2 = Xn W2^T (+ bias)
-  block_gemm32(Ts, ldt, c.E, c.W2, c.N2, [&](int rr, int n, float v) {
+  block_gemm<MT>(Ts, ldt, c.E, c.W2, c.N2, [&](int rr, int n, float v) {
     if (rr < nrow) c.out2[(long)(r0 + rr) * c.N2 + n] = v + (c.b2 ? c.b2[n] : 0.f);
   });
 }
@@ -297,20 +321,21 @@ struct BwdChainArgs {
   float *dyp, *dxz;                    // back: outputs ([rows, D], z half of [rows, 2D])
 };
 
-template <int MODE>
+template <int MODE, int BM>
 __global__ __launch_bounds__(RC_THREADS) void rowchain_bwd(BwdChainArgs c) {
+  constexpr int MT = BM / 16;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lda = kpad(c.K0) + 4, ldt = kpad(c.E) + 4;
-  float* As = sm;                    // [32][lda]
-  float* Ts = sm + RC_BM * lda;      // [32][ldt]
-  float* Ps = Ts + RC_BM * ldt;      // [8 waves][2][256] LN partials
-  const int r0 = blockIdx.x * RC_BM;
-  const int nrow = min(RC_BM, c.rows - r0);
-  stage_rows(As, lda, c.dIn, c.K0, r0, nrow);
+  float* As = sm;                 // [BM][lda]
+  float* Ts = sm + BM * lda;      // [BM][ldt]
+  float* Ps = Ts + BM * ldt;      // [8 waves][2][256] LN partials
+  const int r0 = blockIdx.x * BM;
+  const int nrow = min(BM, c.rows - r0);
+  stage_rows<BM>(As, lda, c.dIn, c.K0, r0, nrow);
   __syncthreads();
   // ---- G1: dY(LN output) = dIn W1
-  block_gemm32<true>(As, lda, c.K0, c.W1, c.E, [&](int rr, int n, float v) { Ts[rr * ldt + n] = v; });
-  for (int i = threadIdx.x; i < RC_BM * (kpad(c.E) - c.E); i += blockDim.x) {
+  block_gemm<MT, true>(As, lda, c.K0, c.W1, c.E, [&](int rr, int n, float v) { Ts[rr * ldt + n] = v; });
+  for (int i = threadIdx.x; i < BM * (kpad(c.E) - c.E); i += blockDim.x) {
     const int w = kpad(c.E) - c.E, rr = i / w;
     Ts[rr * ldt + c.E + (i - rr * w)] = 0.f;
   }
@@ -321,7 +346,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_bwd(BwdChainArgs c) {
     float pw[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f};
     // the wave's rows (wave, wave + 8, ...: 4 of the 32) -- their LN inputs, statistics and residual
     // gradients loaded at once
-    constexpr int WR = RC_BM / (RC_THREADS / 64);
+    constexpr int WR = BM / (RC_THREADS / 64);
     float xr[WR][4], rsd[WR][4], mur[WR], rsr[WR], wl[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) wl[j] = lane + 64 * j < c.E ? c.lnw[lane + 64 * j] : 0.f;
@@ -395,7 +420,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_bwd(BwdChainArgs c) {
   if (MODE == 0) {
     // dYS = dT W_out, then the gate backward (vc_mamba_gate_bwd)
     const int D = c.N2;
-    block_gemm32<true>(Ts, ldt, c.E, c.W2, D, [&](int rr, int n, float v) {
+    block_gemm<MT, true>(Ts, ldt, c.E, c.W2, D, [&](int rr, int n, float v) {
       if (rr < nrow) {
         const long row = r0 + rr;
         const float z = c.xz[row * 2 * D + D + n];
@@ -405,7 +430,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_bwd(BwdChainArgs c) {
       }
     });
   } else if (c.dout) {
-    block_gemm32<true>(Ts, ldt, c.E, c.W2, c.N2, [&](int rr, int n, float v) {
+    block_gemm<MT, true>(Ts, ldt, c.E, c.W2, c.N2, [&](int rr, int n, float v) {
       if (rr < nrow) {
         float* p = c.dout + (long)(r0 + rr) * c.N2 + n;
         *p = (c.beta != 0.f ? *p * c.beta : 0.f) + v;
@@ -414,9 +439,12 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_bwd(BwdChainArgs c) {
   }
 }
 
-size_t chain_lds(int K0, int E) { return sizeof(float) * RC_BM * ((kpad(K0) + 4) + (kpad(E) + 4)); }
+int rc_bm(int rows) { return vc_cdiv(rows, 32) >= 160 ? 32 : 16; }
+size_t chain_lds(int bm, int K0, int E) { return sizeof(float) * bm * ((kpad(K0) + 4) + (kpad(E) + 4)); }
+// forward chains: a wave per 16-column tile of the wider product, 8..16 waves
+int chain_threads(int n1, int n2) { return 64 * std::min(16, std::max(8, std::max(vc_cdiv(n1, 16), vc_cdiv(n2, 16)))); }
 
-size_t bwd_chain_lds(int K0, int E) { return chain_lds(K0, E) + sizeof(float) * 16 * 256; }
+size_t bwd_chain_lds(int bm, int K0, int E) { return chain_lds(bm, K0, E) + sizeof(float) * 16 * 256; }
 
 }  // namespace
 
@@ -430,7 +458,13 @@ VC_API int vc_rowchain_front(int rows, int K0, int E, int N2, const float* x, co
   c.rows = rows, c.K0 = K0, c.E = E, c.N2 = N2, c.A0 = x, c.W1 = w_embed, c.add1 = pos, c.add_mod = L, c.out1 = t;
   c.lnw = ln_w, c.lnb = ln_b, c.eps = eps, c.xn = xn, c.mu = mean, c.rs = rstd, c.W2 = w_proj, c.b2 = nullptr;
   c.out2 = out;
-  hipLaunchKernelGGL(rowchain_fwd<0>, dim3(vc_cdiv(rows, RC_BM)), dim3(RC_THREADS), chain_lds(K0, E), stream, c);
+  const int bm = rc_bm(rows);
+  if (bm == 32)
+    hipLaunchKernelGGL((rowchain_fwd<0, 32>), dim3(vc_cdiv(rows, 32)), dim3(chain_threads(E, N2)), chain_lds(32, K0, E),
+                       stream, c);
+  else
+    hipLaunchKernelGGL((rowchain_fwd<0, 16>), dim3(vc_cdiv(rows, 16)), dim3(chain_threads(E, N2)), chain_lds(16, K0, E),
+                       stream, c);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -454,7 +488,13 @@ VC_API int vc_rowchain_back(int B, int L, int D, int ndir, const int* inv_order,
   c.out2 = out;
   c.B = B, c.L = L, c.ndir = ndir, c.inv = inv_order, c.glog = gate_logits, c.Y = y, c.xz = xz, c.yp = ypsum,
   c.ys = ysum;
-  hipLaunchKernelGGL(rowchain_fwd<1>, dim3(vc_cdiv(rows, RC_BM)), dim3(RC_THREADS), chain_lds(D, E), stream, c);
+  const int bm = rc_bm((int)rows);
+  if (bm == 32)
+    hipLaunchKernelGGL((rowchain_fwd<1, 32>), dim3(vc_cdiv(rows, 32)), dim3(chain_threads(E, N2)), chain_lds(32, D, E),
+                       stream, c);
+  else
+    hipLaunchKernelGGL((rowchain_fwd<1, 16>), dim3(vc_cdiv(rows, 16)), dim3(chain_threads(E, N2)), chain_lds(16, D, E),
+                       stream, c);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -470,7 +510,13 @@ VC_API int vc_rowchain_back_bwd(int rows, int Cout, int E, int D, const float* d
   c.rows = rows, c.K0 = Cout, c.E = E, c.N2 = D, c.dIn = dcd, c.W1 = w_cd, c.x = t2, c.mu = mean, c.rs = rstd;
   c.lnw = ln_w, c.res = nullptr, c.dln = dt, c.part = ln_part, c.W2 = w_out, c.xz = xz, c.yp = ypsum, c.dyp = dyp;
   c.dxz = dxz;
-  hipLaunchKernelGGL(rowchain_bwd<0>, dim3(vc_cdiv(rows, RC_BM)), dim3(RC_THREADS), bwd_chain_lds(Cout, E), stream, c);
+  const int bm = rc_bm(rows);
+  if (bm == 32)
+    hipLaunchKernelGGL((rowchain_bwd<0, 32>), dim3(vc_cdiv(rows, 32)), dim3(RC_THREADS), bwd_chain_lds(32, Cout, E),
+                       stream, c);
+  else
+    hipLaunchKernelGGL((rowchain_bwd<0, 16>), dim3(vc_cdiv(rows, 16)), dim3(RC_THREADS), bwd_chain_lds(16, Cout, E),
+                       stream, c);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -484,7 +530,13 @@ VC_API int vc_rowchain_front_bwd(int rows, int K0, int E, int Cin, const float* 
   BwdChainArgs c{};
   c.rows = rows, c.K0 = K0, c.E = E, c.N2 = Cin, c.dIn = dxz, c.W1 = w_in, c.x = t, c.mu = mean, c.rs = rstd;
   c.lnw = ln_w, c.res = res, c.dln = dtt, c.part = ln_part, c.W2 = w_embed, c.dout = dx, c.beta = beta;
-  hipLaunchKernelGGL(rowchain_bwd<1>, dim3(vc_cdiv(rows, RC_BM)), dim3(RC_THREADS), bwd_chain_lds(K0, E), stream, c);
+  const int bm = rc_bm(rows);
+  if (bm == 32)
+    hipLaunchKernelGGL((rowchain_bwd<1, 32>), dim3(vc_cdiv(rows, 32)), dim3(RC_THREADS), bwd_chain_lds(32, K0, E),
+                       stream, c);
+  else
+    hipLaunchKernelGGL((rowchain_bwd<1, 16>), dim3(vc_cdiv(rows, 16)), dim3(RC_THREADS), bwd_chain_lds(16, K0, E),
+                       stream, c);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -493,7 +545,7 @@ VC_API int vc_rowchain_front_bwd(int rows, int K0, int E, int Cin, const float* 
 VC_API int vc_rowchain_ln_params(int rows, int E, const float* ln_part, float* dw, float* db, float beta,
                                  hipStream_t stream) {
   VC_REQUIRE(rows > 0 && E > 0 && ln_part && dw && db);
-  const int P = vc_cdiv(rows, RC_BM);
+  const int P = vc_cdiv(rows, rc_bm(rows));
   if (db == dw + E) return launch_sum_rows(P, 2 * E, ln_part, 2L * E, 0L, dw, beta, stream);
   const int rc = launch_sum_rows(P, E, ln_part, 2L * E, 0L, dw, beta, stream);
   if (rc) return rc;
@@ -502,6 +554,6 @@ VC_API int vc_rowchain_ln_params(int rows, int E, const float* ln_part, float* d
 
 VC_API int vc_rowchain_ln_part_floats(int rows, int E) {
   if (rows <= 0 || E <= 0) return -1;
-  const long n = (long)vc_cdiv(rows, RC_BM) * 2 * E;
+  const long n = (long)vc_cdiv(rows, rc_bm(rows)) * 2 * E;
   return n < (1L << 31) ? (int)n : -1;
 }
