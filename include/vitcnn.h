@@ -282,7 +282,8 @@ VC_API int vc_rowchain_back(int B, int L, int D, int ndir, const int* inv_order,
  * (dt = LN grad; per-block dw / db partials into ln_part), out_proj's data gradient and the SiLU(z) gate
  * backward (dyp, the z half of dxz) -- the separate path's vc_gemm + vc_layernorm_bwd_dx + vc_gemm +
  * vc_mamba_gate_bwd; front_bwd = in_proj's data gradient (dxz w_in), the pre_norm backward with the
- * residual gradient (dtt = res + LN grad; partials) and dx = beta dx + dtt w_embed (dx nullable).
+ * residual gradient (dtt = res + LN grad; partials) and dx = beta dx + dtt w_embed (+ dx_add) (dx and dx_add
+ * nullable; dx_add: another branch's share of dx, e.g. computed concurrently on another stream).
  * vc_rowchain_ln_params reduces the partials (size: vc_rowchain_ln_part_floats).  Weight gradients of
  * the projections are separate vc_gemm calls. */
 VC_API int vc_rowchain_back_bwd(int rows, int Cout, int E, int D, const float* dcd, const float* w_cd, const float* t2,
@@ -291,7 +292,8 @@ VC_API int vc_rowchain_back_bwd(int rows, int Cout, int E, int D, const float* d
                                 hipStream_t stream);
 VC_API int vc_rowchain_front_bwd(int rows, int K0, int E, int Cin, const float* dxz, const float* w_in, const float* t,
                                  const float* mean, const float* rstd, const float* ln_w, const float* res, float* dtt,
-                                 float* ln_part, const float* w_embed, float* dx, float beta, hipStream_t stream);
+                                 float* ln_part, const float* w_embed, float* dx, float beta, const float* dx_add,
+                                 hipStream_t stream);
 VC_API int vc_rowchain_ln_params(int rows, int E, const float* ln_part, float* dw, float* db, float beta,
                                  hipStream_t stream);
 VC_API int vc_rowchain_ln_part_floats(int rows, int E);

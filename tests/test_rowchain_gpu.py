@@ -137,9 +137,9 @@ def test_rowchain_back_bwd(B, H, Cout, E, D):
     assert _rel(dw[:E], dw64) < 1e-4 and _rel(dw[E:], db64) < 1e-4
 
 
-@pytest.mark.parametrize("B,H,E,Cin,with_dx", [(3, 9, 144, 144, False), (5, 7, 256, 256, True),
-                                               (64, 7, 256, 256, True)])
-def test_rowchain_front_bwd(B, H, E, Cin, with_dx):
+@pytest.mark.parametrize("B,H,E,Cin,with_dx,with_add", [(3, 9, 144, 144, False, False), (5, 7, 256, 256, True, False),
+                                                        (64, 7, 256, 256, True, True), (64, 9, 144, 144, True, True)])
+def test_rowchain_front_bwd(B, H, E, Cin, with_dx, with_add):
     """in_proj / pre_norm (+ residual) / patch_embed data gradients, dX accumulated; pre_norm parameters"""
     lib = _lib()
     torch.manual_seed(4)
@@ -154,7 +154,8 @@ def test_rowchain_front_bwd(B, H, E, Cin, with_dx):
     dxn64 = dxz.double() @ win.double()
     dl64, dw64, db64, mu64, rs64 = _ln_bwd64(dxn64, t.double(), lw.double(), 1e-6)
     dtt64 = dl64 + res.double()
-    dx64 = dx0.double() + dtt64 @ wpe.double()
+    dxa = torch.randn(rows, Cin, device=DEV)
+    dx64 = dx0.double() + dtt64 @ wpe.double() + (dxa.double() if with_add else 0)
     P = lambda t_: t_.data_ptr()  # noqa: E731
     s = torch.cuda.current_stream().cuda_stream
     mu, rs = mu64.float().contiguous(), rs64.float().contiguous()
@@ -162,7 +163,8 @@ def test_rowchain_front_bwd(B, H, E, Cin, with_dx):
     dX = dx0.clone()
     part = torch.empty(lib.vc_rowchain_ln_part_floats(rows, E), device=DEV)
     assert lib.vc_rowchain_front_bwd(rows, E, E, Cin, P(dxz), P(win), P(t), P(mu), P(rs), P(lw), P(res), P(dTt),
-                                     P(part), P(wpe), P(dX) if with_dx else None, 1.0, s) == 0
+                                     P(part), P(wpe), P(dX) if with_dx else None, 1.0, P(dxa) if with_add else None,
+                                     s) == 0
     dw, db = torch.empty(E, device=DEV), torch.empty(E, device=DEV)
     assert lib.vc_rowchain_ln_params(rows, E, P(part), P(dw), P(db), 0.0, s) == 0
     torch.cuda.synchronize()

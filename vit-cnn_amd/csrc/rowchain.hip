@@ -317,6 +317,7 @@ struct BwdChainArgs {
   const float* W2;                     // [E][N2]: W_out (back: N2 = D) / W_pe (front: N2 = Cin)
   float* dout;                         // front: dX [rows, N2] (+)=, null = skip
   float beta;                          // front: 0 overwrite, 1 accumulate
+  const float* dadd;                   // front: [rows, N2] added to dX (nullable: another branch's share)
   const float *xz, *yp;                // back: gate operands ([rows, 2D], [rows, D])
   float *dyp, *dxz;                    // back: outputs ([rows, D], z half of [rows, 2D])
 };
@@ -432,8 +433,9 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_bwd(BwdChainArgs c) {
   } else if (c.dout) {
     block_gemm<MT, true>(Ts, ldt, c.E, c.W2, c.N2, [&](int rr, int n, float v) {
       if (rr < nrow) {
-        float* p = c.dout + (long)(r0 + rr) * c.N2 + n;
-        *p = (c.beta != 0.f ? *p * c.beta : 0.f) + v;
+        const long o = (long)(r0 + rr) * c.N2 + n;
+        float* p = c.dout + o;
+        *p = (c.beta != 0.f ? *p * c.beta : 0.f) + v + (c.dadd ? c.dadd[o] : 0.f);
       }
     });
   }
@@ -523,13 +525,14 @@ VC_API int vc_rowchain_back_bwd(int rows, int Cout, int E, int D, const float* d
 
 VC_API int vc_rowchain_front_bwd(int rows, int K0, int E, int Cin, const float* dxz, const float* w_in, const float* t,
                                  const float* mean, const float* rstd, const float* ln_w, const float* res, float* dtt,
-                                 float* ln_part, const float* w_embed, float* dx, float beta, hipStream_t stream) {
+                                 float* ln_part, const float* w_embed, float* dx, float beta, const float* dx_add,
+                                 hipStream_t stream) {
   VC_REQUIRE(rows > 0 && K0 > 0 && K0 <= 256 && E > 0 && E <= 256 && Cin > 0);
   VC_REQUIRE(dxz && w_in && t && mean && rstd && ln_w && dtt && ln_part && (!dx || w_embed));
   VC_REQUIRE_I32((long)rows * std::max(std::max(K0, E), Cin));
   BwdChainArgs c{};
   c.rows = rows, c.K0 = K0, c.E = E, c.N2 = Cin, c.dIn = dxz, c.W1 = w_in, c.x = t, c.mu = mean, c.rs = rstd;
-  c.lnw = ln_w, c.res = res, c.dln = dtt, c.part = ln_part, c.W2 = w_embed, c.dout = dx, c.beta = beta;
+  c.lnw = ln_w, c.res = res, c.dln = dtt, c.part = ln_part, c.W2 = w_embed, c.dout = dx, c.beta = beta, c.dadd = dx_add;
   const int bm = rc_bm(rows);
   if (bm == 32)
     hipLaunchKernelGGL((rowchain_bwd<1, 32>), dim3(vc_cdiv(rows, 32)), dim3(RC_THREADS), bwd_chain_lds(32, K0, E),

@@ -138,6 +138,17 @@ class Multimodality_Mamba(nn.Module):
         named = list(nn.Module.named_parameters(self))
         active = [(n, p) for n, p in named if not n.startswith(UNUSED_PREFIXES)]
         unused = [(n, p) for n, p in named if n.startswith(UNUSED_PREFIXES)]
+        # NonLocal phi / g: the two weights, then the two biases, adjacent (stacked [2 Ci, Cout] / [2 Ci]),
+        # so that both projections -- forward, data and weight gradient -- are one GEMM each
+        for pfx in ("hsi1", "hsi2"):
+            nl = pfx + ".FusionLayer.cross_attention."
+            group = [nl + "phi.0.weight", nl + "g.0.weight", nl + "phi.0.bias", nl + "g.0.bias"]
+            idx = {n: i for i, (n, _) in enumerate(active)}
+            if all(n in idx for n in group):
+                items = [active[idx[n]] for n in group]
+                first = min(idx[n] for n in group)
+                rest = [it for it in active if it[0] not in group]
+                active = rest[:first] + items + rest[first:]
         self._poff: Dict[str, int] = {}
         off = 0
         for n, p in active + unused:
@@ -747,9 +758,9 @@ class _Program:
         PG = ws.f(pfx + ".PG", M * 2 * Ci)
         with self.gemm_group():
             self.mm_nt(M, Ci, Cout, Fl, Cout, P[nl + ".theta.weight"], Cout, TH, Ci, bias=P[nl + ".theta.bias"])
-            self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, PG, 2 * Ci, bias=P[nl + ".phi.0.bias"])
-            self.mm_nt(M, Ci, Cout, Fc, Cout, P[nl + ".g.0.weight"], Cout, PG + F32 * Ci, 2 * Ci,
-                       bias=P[nl + ".g.0.bias"])
+            # phi | g as one product over their stacked weights / biases (_build_flat keeps them adjacent)
+            self.mm_nt(M, 2 * Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, PG, 2 * Ci,
+                       bias=P[nl + ".phi.0.bias"])
         PP = ws.f(pfx + ".PP", B * Pk * 2 * Ci)
         PA = ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr()
         self.L.vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, PG, 2 * Ci, PP, PA, self.s)
@@ -979,11 +990,10 @@ class _Program:
             dPG = f(pfx + ".dPG", M * 2 * Ci)
             self.L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dPP,
                                    ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr(), dPG, 2 * Ci, self.s)
-            self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, Ci, Cout, Fc, Cout, dFc, 1.0,
-                            lddy=2 * Ci)
-            self.linear_bwd(nl + ".g.0.weight", nl + ".g.0.bias", dPG + F32 * Ci, M, Ci, Cout, Fc, Cout, dFc, 1.0,
-                            lddy=2 * Ci)
-            self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
+            # phi | g (stacked, one weight + one data gradient) and theta: one grouped launch
+            with self.gemm_group():
+                self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, 2 * Ci, Cout, Fc, Cout, dFc, 1.0)
+                self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
             # local feature: BN -> conv3x3 -> ReLU backward (first accumulation into dX)
             self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0)
             # channel feature: ln4 -> TokenLearner -> conv1x1
@@ -1135,7 +1145,7 @@ class _Program:
             part = f(pfx + ".prepart", self.L.vc_rowchain_ln_part_floats(rows, E))
             self.L.vc_rowchain_front_bwd(rows, 2 * D, E, Cin, dXZ, P[mx + ".in_proj.weight"], T, f(pfx + ".Xn.m", rows),
                                          f(pfx + ".Xn.r", rows), P[gv + ".pre_norm.weight"], dT, dTt, part,
-                                         P[gv + ".patch_embed.projection.weight"], dX or None, 1.0, self.s)
+                                         P[gv + ".patch_embed.projection.weight"], dX or None, 1.0, None, self.s)
             self._ln_params(gv + ".pre_norm", rows, E, part)
         else:
             self.linear_bwd(mx + ".in_proj.weight", None, dXZ, rows, 2 * D, E, Xn, E, dXn, 0.0, defer=True)
