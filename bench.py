@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement) with `roofline` 
 kernel (HIP-event timed inside this process) and `cpu_baseline` (the CPU oracle, rank 0, N=1).
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -54,6 +55,9 @@ def parse():
     ap.add_argument("--no-f1", action="store_true")
     ap.add_argument("--no-train-loop", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="build the step, then only the roofline legs (for a rocprofv3 --stats run whose "
+                         "per-kernel average is the roofline leg's launch alone)")
     return ap.parse_args()
 
 
@@ -783,6 +787,11 @@ def main():
     log(f"rank {rank}/{world}: building the {args.precision} step")
     step, model, (hsi, lidar, target), holder, launch = build_step(
         dev, args.precision, world, rank, args.batch, exchange, args.warmup, not args.no_graph)
+    if args.roofline_only:
+        out = {"roofline": dominant_kernel_roofline(model, args.batch, args.kernel_reps),
+               "roofline_gemm": gemm_roofline(model, args.batch, args.kernel_reps)}
+        print(json.dumps(out), flush=True)
+        return
     log(f"timing {args.steps} steps ({launch})")
     elapsed = time_steps(step, dev, args.steps, world)
     loss_val = float(holder["loss"].item())
@@ -849,7 +858,9 @@ def main():
         cpu_legs.append(c)
     if world == 1 and not args.no_train_loop:
         log("train(): the plugin-surface loop over a PatchBatcher loader")
-        out["value_via_train_loop"] = train_loop_leg(dev, 3, 1000 + rank, elapsed / args.steps * 1e3)
+        # train() prints the reference's progress lines; stdout carries only the one JSON line
+        with contextlib.redirect_stdout(sys.stderr):
+            out["value_via_train_loop"] = train_loop_leg(dev, 3, 1000 + rank, elapsed / args.steps * 1e3)
     # the CPU baselines last: minutes of all-core CPU work that must not precede a timed GPU leg
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(f"CPU baseline: {args.cpu_warmup} + {args.cpu_steps} oracle steps on {cpu_threads()} threads")
