@@ -64,6 +64,11 @@ _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in 
 _GROUP = os.environ.get("VITCNN_GEMM_GROUP", "1") != "0"   # grouped launches of independent fp32 GEMMs
 # bf16 mode diagnostics (tools/bf16_sites.py): GEMM issue indices kept in fp32, and a log of call sites
 _BF16_EXACT: set = set()
+# bf16 mode: bf16 operands only for products with K >= this that are not weight gradients (the im2col'ed
+# 3x3 convs, K = 9 Cin): the short-K products are launch-latency-bound, where bf16 saves nothing and costs
+# the grouped launch (bf16 GEMMs launch alone), and the long-K weight gradients run slower on the bf16
+# kernel than on the fp32 split-K one; 0 = every GEMM bf16 (round 2's mode)
+_BF16_MIN_K = int(os.environ.get("VITCNN_BF16_MIN_K", "1024"))
 _GEMM_SITES = None
 _LANE_MAP = [int(v) for v in os.environ.get("VITCNN_LANE_MAP", "").split(",") if v]   # measurement switch
 _BN_TICKETS = os.environ.get("VITCNN_BN_TICKETS", "0") == "1"   # BN reductions in the last-arriving block: measured ~1% slower (every arrival is an agent-scope release = L2 writeback)
@@ -506,7 +511,8 @@ class _Program:
             f = sys._getframe(1)
             f = f.f_back if f.f_code.co_name.startswith("mm_") else f
             _GEMM_SITES.append((i, f.f_code.co_name, f.f_lineno, args[2], args[3], args[4], exact))
-        if self.gemm_flags and not exact and i not in _BF16_EXACT:
+        if self.gemm_flags and not exact and i not in _BF16_EXACT and args[4] >= _BF16_MIN_K and not (
+                _BF16_MIN_K and args[0]):
             args = args[:21] + (args[21] | self.gemm_flags,) + args[22:]
         self.L.vc_gemm_ex(*args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
 
@@ -514,7 +520,7 @@ class _Program:
     def gemm_group(self):
         """the fp32 GEMMs issued inside (on the current lane; they must be independent of each other)
         launch as one grouped grid + one grouped split-K reduce (vc_gemm_group_begin / _end)"""
-        if not _GROUP or self.gemm_flags or self._grouping:   # nested: the outer group collects
+        if not _GROUP or self._grouping:   # nested: the outer group collects (bf16 members launch alone)
             yield
             return
         self.L.vc_gemm_group_begin(self.s)
