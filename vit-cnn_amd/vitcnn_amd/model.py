@@ -59,6 +59,10 @@ _SCAN_FUSED = os.environ.get("VITCNN_SCAN_FUSED", "1") != "0"
 # patch_embed + pre_norm + in_proj and combine + out_proj + ln1 + change_dim as one launch each
 # (vc_rowchain_front / _back); "0" restores the separate launches (measurement switch)
 _ROW_CHAIN = os.environ.get("VITCNN_ROW_CHAIN", "1") != "0"
+# the local conv's data gradient as the tap-major implicit GEMM (vc_conv3x3_tap_dgrad, no dcol matrix, no
+# col2im) over the weights packed tap-major by lane 0 in the forward: opt-in, measured slower on the B=64
+# step (1.90-1.94 -> 1.99-2.01 ms: at 7x7 / 9x9 maps the row gathers cost more than dcol + col2im)
+_TAP_DGRAD = os.environ.get("VITCNN_TAP_DGRAD", "0") == "1"
 _LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
 _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in normal runs)
 _GROUP = os.environ.get("VITCNN_GEMM_GROUP", "1") != "0"   # grouped launches of independent fp32 GEMMs
@@ -675,6 +679,10 @@ class _Program:
         order, inv = self.tab[("order", H)].data_ptr(), self.tab[("inv", H)].data_ptr()
         M = B * S
         FM, e_fm = self.block_local_branch(blk, pfx, X, H)
+        if self._tap_dgrad(blk):
+            # the local conv's weight, tap-major, for its data gradient in the backward (lane 0 has slack here)
+            self.L.vc_conv3x3_pack(Cout, Cin, 0, P[pfx + ".local_feature.conv.weight"],
+                                   ws.f(pfx + ".local_feature.wt", Cout * 9 * ((Cin + 3) // 4 * 4)), 0.0, self.s)
         # --- hsiMamba global view (Mutimodality_Mamba7.py:419-701, :983-1017), on lane 0
         T = ws.f(pfx + ".T", rows * E)
         XZ = ws.f(pfx + ".XZ", rows * 2 * D)
@@ -912,7 +920,11 @@ class _Program:
         self.L.vc_cat2_bwd(M, C1, C2, dcat, 1 if C1 == C2 else 0, dX1 or None, C1, beta1, dX2 or None, C2, beta2,
                            self.s)
 
-    def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx):
+    def _tap_dgrad(self, blk):
+        return _TAP_DGRAD and self.ws_grad and not self.implicit_conv and blk.cin % 4 == 0
+
+    def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx, tap=False):
+        """tap: the data gradient by vc_conv3x3_tap_dgrad over the tap-major weight block() packed"""
         B, ws = self.B, self.ws
         S = (H - 2) * (H - 2)
         out = ws.f(pfx + ".out", B * S * Cout)
@@ -927,6 +939,12 @@ class _Program:
                                     self.s)
             self.L.vc_conv3x3_dgrad(B, H, H, Cin, Cout, 0, dpre, Cout, self.P[pfx + ".conv.weight"], 0.0, dxbn, Cin,
                                     self.scr_p, self.scr_n, self.s)
+        elif tap:
+            col = ws.f(pfx + ".col", B * S * 9 * Cin)
+            self.linear_bwd(pfx + ".conv.weight", pfx + ".conv.bias", dpre, B * S, Cout, 9 * Cin, col, 9 * Cin, 0, 0.0)
+            self.L.vc_conv3x3_tap_dgrad(B, H, H, Cin, Cout, 0, dpre, Cout,
+                                        ws.f(pfx + ".wt", Cout * 9 * ((Cin + 3) // 4 * 4)), 0.0, dxbn, Cin,
+                                        self.scr_p, self.scr_n, self.s)
         else:
             col = ws.f(pfx + ".col", B * S * 9 * Cin)
             dcol = ws.f(pfx + ".dcol", B * S * 9 * Cin)
@@ -1001,7 +1019,7 @@ class _Program:
                 self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, 2 * Ci, Cout, Fc, Cout, dFc, 1.0)
                 self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
             # local feature: BN -> conv3x3 -> ReLU backward (first accumulation into dX)
-            self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0)
+            self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0, tap=self._tap_dgrad(blk))
             # channel feature: ln4 -> TokenLearner -> conv1x1
             Zc, dZc = f(pfx + ".channel_token.Z", M * Cout), f(pfx + ".dZc", M * Cout)
             self.ln_bwd(pfx + ".ln4", pfx + ".Fc", dFc, Zc, M, Cout, dZc, 0.0)
