@@ -184,6 +184,18 @@ VC_API int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, cons
 /* gradient of vc_im2col3x3 w.r.t. its (post-BN) input, gather form: dx [B,H,W,C] overwritten */
 VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx, hipStream_t stream);
 
+/* vc_maxpool2_fwd of the phi | g map pg [B,Hs,Hs,2Ci] (row stride ldpg) followed by vc_nonlocal_attn_fwd, in
+ * one launch where the wave-per-row forward runs (training batch sizes): pooled [B,P,2Ci] and arg are still
+ * written for the backward. */
+VC_API int vc_nonlocal_attn_pool_fwd(int B, int S, int P, int Ci, int Hs, const float* theta, const float* pg,
+                                     long ldpg, float* pooled, unsigned char* arg, float* att, float* o,
+                                     hipStream_t stream);
+/* vc_nonlocal_attn_bwd followed by vc_maxpool2_bwd of the pooled phi | g map (Hs x Hs, P = (Hs/2)^2 keys), in
+ * one launch where the MFMA backward applies: dpg [B,Hs,Hs,2Ci] overwritten (dpooled is then untouched;
+ * it is the intermediate of the two-launch fallback). */
+VC_API int vc_nonlocal_attn_pool_bwd(int B, int S, int P, int Ci, int Hs, const float* theta, const float* pooled,
+                                     const float* att, const float* dout, const unsigned char* arg, float* dtheta,
+                                     float* dpooled, float* dpg, hipStream_t stream);
 /* nn.MaxPool2d(2) of the NonLocal phi/g branches (Mutimodality_Mamba7.py:94, :136-138):
  * x channels-last [B,H,W,C] with row stride ldx -> y [B,H/2,W/2,C] + winning tap (uint8). */
 VC_API int vc_maxpool2_fwd(int B, int H, int W, int C, const float* x, long ldx, float* y, unsigned char* arg,
@@ -342,6 +354,10 @@ VC_API int vc_glf_combine_fwd(long M, int C, const float* w_pre, const float* bn
 /* out = beta*out + a (+ b) over [M, C] strided rows */
 VC_API int vc_add2_2d(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
                       float beta, hipStream_t stream);
+/* out = out2 = a + b, both overwritten (GLfusionBlock :1112-1115: the concat gradient summed into the
+ * local- and channel-feature accumulators in one launch) */
+VC_API int vc_add2_2d_dup(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
+                          float* out2, long ldo2, hipStream_t stream);
 /* avgpool(f1) + avgpool(f2) -> feat [B,C]; logits = feat W^T + bias (Mutimodality_Mamba7.py:1174-1178) */
 VC_API int vc_head_fwd(int B, int S1, int S2, int C, int ncls, const float* f1, const float* f2, const float* W,
                        const float* bias, float* feat, float* logits, hipStream_t stream);

@@ -464,3 +464,69 @@ def test_nonlocal_attention_fwd_bwd(L, B, S, Pk, Ci):
     assert rel_err(o.cpu().view(B, S, Ci).numpy(), o_ref.detach().numpy()) < 1e-5
     assert rel_err(dth.cpu().view(B, S, Ci).numpy(), th.grad.numpy()) < 1e-5
     assert rel_err(dpp.cpu().view(B, Pk, 2 * Ci).numpy(), pp.grad.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("B,Hs,Ci", [(64, 9, 72), (64, 7, 128), (3, 5, 72), (2, 6, 64), (2, 9, 70)])
+def test_nonlocal_pool_bwd_matches_two_launches(L, B, Hs, Ci):
+    """vc_nonlocal_attn_pool_bwd (max-pool backward folded into the attention backward) writes exactly what
+    vc_nonlocal_attn_bwd + vc_maxpool2_bwd write: every dPG element (prefilled NaN), argmax taps from
+    vc_maxpool2_fwd, odd grids' uncovered last row/column 0.  Ci = 70 takes the two-launch fallback."""
+    S, Pk = Hs * Hs, (Hs // 2) ** 2
+    pg = rnd(B * S, 2 * Ci, seed=61).to(DEV)
+    th = rnd(B * S, Ci, seed=62).to(DEV)
+    dout = rnd(B * S, Ci, seed=63).to(DEV)
+    pp = torch.empty(B * Pk, 2 * Ci, device=DEV)
+    pa = torch.empty(B * Pk * 2 * Ci, dtype=torch.uint8, device=DEV)
+    att, o = torch.empty(B * S * Pk, device=DEV), torch.empty(B * S, Ci, device=DEV)
+    assert L.vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, P(pg), 2 * Ci, P(pp), P(pa), S_()) == 0
+    assert L.vc_nonlocal_attn_fwd(B, S, Pk, Ci, P(th), P(pp), P(att), P(o), S_()) == 0
+    dth1, dth2 = (torch.full((B * S, Ci), float("nan"), device=DEV) for _ in range(2))
+    dpp = torch.full((B * Pk, 2 * Ci), float("nan"), device=DEV)
+    dpg1, dpg2 = (torch.full((B * S, 2 * Ci), float("nan"), device=DEV) for _ in range(2))
+    assert L.vc_nonlocal_attn_bwd(B, S, Pk, Ci, P(th), P(pp), P(att), P(dout), P(dth1), P(dpp), S_()) == 0
+    assert L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, P(dpp), P(pa), P(dpg1), 2 * Ci, S_()) == 0
+    dpp2 = torch.full((B * Pk, 2 * Ci), float("nan"), device=DEV)
+    assert L.vc_nonlocal_attn_pool_bwd(B, S, Pk, Ci, Hs, P(th), P(pp), P(att), P(dout), P(pa), P(dth2), P(dpp2),
+                                       P(dpg2), S_()) == 0
+    torch.cuda.synchronize()
+    assert not torch.isnan(dpg2).any()
+    assert torch.equal(dth1, dth2) and torch.equal(dpg1, dpg2)
+
+
+@pytest.mark.parametrize("B,Hs,Ci", [(64, 9, 72), (64, 7, 128), (3, 5, 72), (2, 6, 64), (300, 7, 128)])
+def test_nonlocal_pool_fwd_matches_two_launches(L, B, Hs, Ci):
+    """vc_nonlocal_attn_pool_fwd (max pool while staging the keys) = vc_maxpool2_fwd + vc_nonlocal_attn_fwd
+    bit for bit: att, o, pooled and taps (ties and a NaN planted); B = 300 takes the two-launch MFMA path."""
+    S, Pk = Hs * Hs, (Hs // 2) ** 2
+    pg = rnd(B * S, 2 * Ci, seed=65)
+    pg[1:40:3] = pg[0]               # equal rows -> tied windows
+    pg[7, 5] = float("nan")
+    pg, th = pg.to(DEV), rnd(B * S, Ci, seed=66).to(DEV)
+    outs = []
+    for fused in (False, True):
+        pp = torch.full((B * Pk, 2 * Ci), float("nan"), device=DEV)
+        pa = torch.full((B * Pk * 2 * Ci,), 7, dtype=torch.uint8, device=DEV)
+        att = torch.full((B * S * Pk,), float("nan"), device=DEV)
+        o = torch.full((B * S, Ci), float("nan"), device=DEV)
+        if fused:
+            assert L.vc_nonlocal_attn_pool_fwd(B, S, Pk, Ci, Hs, P(th), P(pg), 2 * Ci, P(pp), P(pa), P(att), P(o),
+                                               S_()) == 0
+        else:
+            assert L.vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, P(pg), 2 * Ci, P(pp), P(pa), S_()) == 0
+            assert L.vc_nonlocal_attn_fwd(B, S, Pk, Ci, P(th), P(pp), P(att), P(o), S_()) == 0
+        outs.append((pp, pa, att, o))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a.nan_to_num(1e30), b.nan_to_num(1e30))
+    assert (outs[1][1] < 4).all()
+
+
+def test_add2_dup(L):
+    """vc_add2_2d_dup: out = out2 = a + b over strided rows (the GLfusion concat gradient)"""
+    M, C = 301, 144
+    cat = rnd(M, 2 * C, seed=64).to(DEV)
+    o1, o2 = torch.full((M, C), float("nan"), device=DEV), torch.full((M, 2 * C), float("nan"), device=DEV)
+    assert L.vc_add2_2d_dup(M, C, P(cat), 2 * C, P(cat) + 4 * C, 2 * C, P(o1), C, P(o2), 2 * C, S_()) == 0
+    torch.cuda.synchronize()
+    ref = cat[:, :C] + cat[:, C:]
+    assert torch.equal(o1, ref) and torch.equal(o2[:, :C], ref) and torch.isnan(o2[:, C:]).all()

@@ -19,15 +19,44 @@ constexpr int MAXCI = 256;
 // PT = number of pooled keys (compile-time so the per-row score array stays in registers)
 constexpr int NT = 1024, NW = NT / 64;
 
-template <int PT>
+// POOL: the 2x2 max pool of the phi | g map (Mutimodality_Mamba7.py:94) done while staging the keys --
+// pg [B][Hs][Hs] rows of 2 Ci (stride ldpg), the window max and its tap as vc_maxpool2_fwd takes them
+// (first max in scan order, NaN propagates); the y = 0 workgroup of each batch element stores pooled +
+// tap for the backward.  One launch instead of two on the GLfusion forward chain.
+template <int PT, bool POOL>
 __global__ __launch_bounds__(NT) void nl_fwd(int S, int Ci, const float* __restrict__ theta,
                                              const float* __restrict__ pooled, float* __restrict__ att,
-                                             float* __restrict__ o) {
+                                             float* __restrict__ o, int Hs, const float* __restrict__ pg, long ldpg,
+                                             float* __restrict__ pooled_out, unsigned char* __restrict__ tap_out) {
   constexpr int P = PT;
   extern __shared__ float kv[];  // [P][2*Ci]
   const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* src = pooled + (long)b * P * 2 * Ci;
-  for (int i = threadIdx.x; i < P * 2 * Ci; i += NT) kv[i] = src[i];
+  if (POOL) {
+    const int C2 = 2 * Ci, PWd = Hs >> 1;
+    const bool store = blockIdx.y == 0;
+    for (int i = threadIdx.x; i < P * C2; i += NT) {
+      const int key = i / C2, ch = i - key * C2, ph = key / PWd, pw = key - ph * PWd;
+      const float* xb = pg + ((long)(b * Hs + 2 * ph) * Hs + 2 * pw) * ldpg + ch;
+      float best = xb[0];
+      int bi = 0;
+#pragma unroll
+      for (int t = 1; t < 4; ++t) {
+        const float v = xb[((t >> 1) * Hs + (t & 1)) * ldpg];
+        if (v > best || isnan(v)) {
+          best = v;
+          bi = t;
+        }
+      }
+      kv[i] = best;
+      if (store) {
+        pooled_out[(long)b * P * C2 + i] = best;
+        tap_out[(long)b * P * C2 + i] = (unsigned char)bi;
+      }
+    }
+  } else {
+    const float* src = pooled + (long)b * P * 2 * Ci;
+    for (int i = threadIdx.x; i < P * 2 * Ci; i += NT) kv[i] = src[i];
+  }
   __syncthreads();
   {
     const int s = blockIdx.y * NW + wave;
@@ -238,10 +267,16 @@ __global__ __launch_bounds__(NLW * 64) void nl_fwd_mfma(int B, int S, int P, int
 // Pass 1 (wave = query tile): dA^T = G dO^T (MFMA), dS^T = att^T * (dA^T - rowsum), dtheta^T = phi^T dS^T;
 // dS and att go to LDS as [query][16].  Pass 2 (wave = channel chunks dc = 16 w, 16 (w + nqt), ...):
 // dphi^T = theta^T dS and dg^T = dO^T att, the query reduction walked in 16-query tiles (fixed order).
+// POOL: the gradient of the 2x2 max pool that made `pooled` (Mutimodality_Mamba7.py:94) folded in --
+// dpg [B][Hs][Hs][2 Ci] (the phi | g maps before pooling) gets each pooled gradient at its window's
+// argmax (arg, vc_maxpool2_fwd's record) and 0 elsewhere, as vc_maxpool2_bwd writes it: one launch
+// instead of two on the GLfusion backward chain.
+template <bool POOL>
 __global__ __launch_bounds__(1024) void nl_bwd_mfma(int S, int P, int Ci, const float* __restrict__ theta,
                                                     const float* __restrict__ pooled, const float* __restrict__ att,
                                                     const float* __restrict__ dout, float* __restrict__ dtheta,
-                                                    float* __restrict__ dpooled) {
+                                                    float* __restrict__ dpooled, int Hs,
+                                                    const unsigned char* __restrict__ arg) {
   extern __shared__ f32x4 nl_lds[];
   const int nqt = (S + 15) >> 4;
   float* dsL = reinterpret_cast<float*>(nl_lds);   // [nqt * 16][16]
@@ -316,14 +351,45 @@ __global__ __launch_bounds__(1024) void nl_bwd_mfma(int S, int P, int Ci, const 
     }
     const f32x4 aphi = tree_sum(aphi4), ag = tree_sum(ag4);
     if (c < P && dc + 4 * g < Ci) {
-      float* w = dpooled + ((long)b * P + c) * ldp + dc + 4 * g;
-      *reinterpret_cast<f32x4*>(w) = aphi;
-      *reinterpret_cast<f32x4*>(w + Ci) = ag;
+      if (POOL) {
+        // key c = pooled pixel (ph, pw) of a (Hs / 2)^2 grid; window pixel (2 ph + (a >> 1), 2 pw + (a & 1))
+        const int PW = Hs >> 1, ph = c / PW, pw = c - ph * PW;
+        const unsigned char* ab = arg + ((long)b * P + c) * ldp + dc + 4 * g;
+        float* db = dpooled + (long)b * Hs * Hs * ldp + dc + 4 * g;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          float* w = db + ((2 * ph + (a >> 1)) * Hs + 2 * pw + (a & 1)) * ldp;
+          f32x4 vp, vg;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            vp[r] = ab[r] == a ? aphi[r] : 0.f;
+            vg[r] = ab[r + Ci] == a ? ag[r] : 0.f;
+          }
+          *reinterpret_cast<f32x4*>(w) = vp;
+          *reinterpret_cast<f32x4*>(w + Ci) = vg;
+        }
+      } else {
+        float* w = dpooled + ((long)b * P + c) * ldp + dc + 4 * g;
+        *reinterpret_cast<f32x4*>(w) = aphi;
+        *reinterpret_cast<f32x4*>(w + Ci) = ag;
+      }
+    }
+  }
+  if (POOL && (Hs & 1)) {   // the last row and column are in no window: gradient 0
+    const int nl = 2 * Hs - 1;   // pixels (Hs - 1, *) and (*, Hs - 1)
+    float* db = dpooled + (long)b * Hs * Hs * ldp;
+    for (int i = threadIdx.x; i < nl * (int)(ldp / 4); i += blockDim.x) {
+      const int px = i / (int)(ldp / 4), c4 = i - px * (int)(ldp / 4);
+      const int pix = px < Hs ? (Hs - 1) * Hs + px : (px - Hs) * Hs + Hs - 1;
+      *reinterpret_cast<f32x4*>(db + (long)pix * ldp + 4 * c4) = z;
     }
   }
 }
 
 }  // namespace
+
+VC_API int vc_maxpool2_bwd(int B, int H, int W, int C, const float* dy, const unsigned char* arg, float* dx, long lddx,
+                           hipStream_t stream);
 
 // float4 row accesses of the MFMA forms need 16-B aligned bases (rows are 16-B multiples when Ci % 4 == 0)
 static bool aligned16(const void* a, const void* b, const void* c) {
@@ -357,8 +423,9 @@ VC_API int vc_nonlocal_attn_fwd(int B, int S, int P, int Ci, const float* theta,
     return VC_OK;
   }
   const size_t sm = sizeof(float) * (size_t)P * 2 * Ci;
-#define VC_NL_FWD(PT_) \
-  hipLaunchKernelGGL((nl_fwd<PT_>), dim3(B, vc_cdiv(S, NW)), dim3(NT), sm, stream, S, Ci, theta, pooled, att, o)
+#define VC_NL_FWD(PT_)                                                                                       \
+  hipLaunchKernelGGL((nl_fwd<PT_, false>), dim3(B, vc_cdiv(S, NW)), dim3(NT), sm, stream, S, Ci, theta, pooled, \
+                     att, o, 0, nullptr, 0L, nullptr, nullptr)
   switch (P) {  // pooled key counts of 5x5 / 7x7 / 9x9 query grids, then generic buckets
     case 4: VC_NL_FWD(4); break;
     case 9: VC_NL_FWD(9); break;
@@ -366,6 +433,39 @@ VC_API int vc_nonlocal_attn_fwd(int B, int S, int P, int Ci, const float* theta,
     default: return VC_EINVAL;
   }
 #undef VC_NL_FWD
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_maxpool2_fwd(int B, int H, int W, int C, const float* x, long ldx, float* y, unsigned char* arg,
+                           hipStream_t stream);
+
+// vc_maxpool2_fwd of the phi | g map + vc_nonlocal_attn_fwd in one launch where the wave-per-row forward
+// runs (the training batches); the two launches otherwise
+VC_API int vc_nonlocal_attn_pool_fwd(int B, int S, int P, int Ci, int Hs, const float* theta, const float* pg,
+                                     long ldpg, float* pooled, unsigned char* arg, float* att, float* o,
+                                     hipStream_t stream) {
+  VC_REQUIRE(B > 0 && S > 0 && P > 0 && P <= MAXP && Ci > 0 && Ci <= MAXCI && Hs >= 2 && (Hs / 2) * (Hs / 2) == P &&
+             ldpg >= 2 * Ci);
+  const bool legacy_p = P == 4 || P == 9 || P == 16;
+  const bool mfma = Ci % 4 == 0 && (B >= NL_MFMA_FWD_MIN_B || !legacy_p) && aligned16(theta, pooled, o) &&
+                    !nl_legacy(0);
+  if (mfma || !legacy_p) {
+    const int rc = vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, pg, ldpg, pooled, arg, stream);
+    if (rc) return rc;
+    return vc_nonlocal_attn_fwd(B, S, P, Ci, theta, pooled, att, o, stream);
+  }
+  VC_REQUIRE_I32((long)B * Hs * Hs * ldpg);
+  const size_t sm = sizeof(float) * (size_t)P * 2 * Ci;
+#define VC_NL_PFWD(PT_)                                                                                       \
+  hipLaunchKernelGGL((nl_fwd<PT_, true>), dim3(B, vc_cdiv(S, NW)), dim3(NT), sm, stream, S, Ci, theta, nullptr, \
+                     att, o, Hs, pg, ldpg, pooled, arg)
+  switch (P) {
+    case 4: VC_NL_PFWD(4); break;
+    case 9: VC_NL_PFWD(9); break;
+    default: VC_NL_PFWD(16); break;
+  }
+#undef VC_NL_PFWD
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -378,8 +478,8 @@ VC_API int vc_nonlocal_attn_bwd(int B, int S, int P, int Ci, const float* theta,
     // MFMA form: one wave per 16-query tile (at least 4 for pass 2)
     const int nqt = (S + 15) / 16;
     const int nw = std::max(nqt, 4);
-    hipLaunchKernelGGL(nl_bwd_mfma, dim3(B), dim3(nw * 64), sizeof(float) * nqt * 512, stream, S, P, Ci, theta,
-                       pooled, att, dout, dtheta, dpooled);
+    hipLaunchKernelGGL(nl_bwd_mfma<false>, dim3(B), dim3(nw * 64), sizeof(float) * nqt * 512, stream, S, P, Ci,
+                       theta, pooled, att, dout, dtheta, dpooled, 0, nullptr);
     VC_CHECK_LAUNCH();
     return VC_OK;
   }
@@ -396,4 +496,23 @@ VC_API int vc_nonlocal_attn_bwd(int B, int S, int P, int Ci, const float* theta,
 #undef VC_NL_BWD
   VC_CHECK_LAUNCH();
   return VC_OK;
+}
+
+// vc_nonlocal_attn_bwd + vc_maxpool2_bwd in one launch where the MFMA form applies (dpg [B][Hs][Hs][2 Ci],
+// overwritten; arg: vc_maxpool2_fwd's window argmax); the two launches otherwise
+VC_API int vc_nonlocal_attn_pool_bwd(int B, int S, int P, int Ci, int Hs, const float* theta, const float* pooled,
+                                     const float* att, const float* dout, const unsigned char* arg, float* dtheta,
+                                     float* dpooled, float* dpg, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && S > 0 && P > 0 && P <= MAXP && Ci > 0 && Ci <= MAXCI && Hs >= 2 && (Hs / 2) * (Hs / 2) == P);
+  if (Ci % 4 == 0 && S <= 256 && aligned16(theta, pooled, dout) && aligned16(dtheta, dpg, dpg) && !nl_legacy(1)) {
+    const int nqt = (S + 15) / 16;
+    const int nw = std::max(nqt, 4);
+    hipLaunchKernelGGL(nl_bwd_mfma<true>, dim3(B), dim3(nw * 64), sizeof(float) * nqt * 512, stream, S, P, Ci, theta,
+                       pooled, att, dout, dtheta, dpg, Hs, arg);
+    VC_CHECK_LAUNCH();
+    return VC_OK;
+  }
+  const int rc = vc_nonlocal_attn_bwd(B, S, P, Ci, theta, pooled, att, dout, dtheta, dpooled, stream);
+  if (rc) return rc;
+  return vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dpooled, arg, dpg, 2 * Ci, stream);
 }

@@ -62,7 +62,8 @@ __global__ void glf_combine_fwd(int total, FastDiv fC, const float* __restrict__
 }
 
 __global__ void add2_2d(int total, FastDiv fC, const float* __restrict__ a, long lda, const float* __restrict__ b,
-                        long ldb, float* __restrict__ out, long ldo, float beta) {
+                        long ldb, float* __restrict__ out, long ldo, float beta, float* __restrict__ out2 = nullptr,
+                        long ldo2 = 0) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   int c;
@@ -71,6 +72,7 @@ __global__ void add2_2d(int total, FastDiv fC, const float* __restrict__ a, long
   if (b) v += b[m * ldb + c];
   float* p = out + m * ldo + c;
   *p = (beta != 0.f ? beta * *p : 0.f) + v;
+  if (out2) out2[m * ldo2 + c] = v;
 }
 
 // feat[b,c] = mean_p f1[b,p,c] + mean_q f2[b,q,c];  logits = feat W^T + bias   (block per b)
@@ -356,6 +358,19 @@ VC_API int vc_add2_2d(long M, int C, const float* a, long lda, const float* b, l
   VC_REQUIRE_I32(M * C);
   hipLaunchKernelGGL(add2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C), a, lda,
                      b, ldb, out, ldo, beta);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// out = out2 = a + b (both overwritten): the GLfusion FusionLayer's concat gradient summed into the two
+// accumulators its consumers add to (Mutimodality_Mamba7.py:1112-1115), one launch instead of add + copy
+VC_API int vc_add2_2d_dup(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
+                          float* out2, long ldo2, hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && C > 0 && out2 != nullptr);
+  if (M == 0) return VC_OK;
+  VC_REQUIRE_I32(M * C);
+  hipLaunchKernelGGL(add2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C), a, lda,
+                     b, ldb, out, ldo, 0.f, out2, ldo2);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

@@ -13,6 +13,12 @@ namespace {
 
 constexpr int LN_MAXV = 8;  // C <= 512
 constexpr int NB = 8;       // rows (or partials) per lane whose loads a BatchNorm kernel issues together
+// row lanes of the BatchNorm statistics / apply blocks (64 channels x BN_RL rows per block): 16 puts the
+// ~80 rows of a B = 64 partial one batch of loads per lane (4 lanes: three dependent rounds of 8)
+#ifndef VC_BN_RL
+#define VC_BN_RL 16
+#endif
+constexpr int BN_RL = VC_BN_RL, BN_T = 64 * BN_RL;
 
 __global__ __launch_bounds__(256) void ln_fwd(int R, int C, const float* __restrict__ x, long ldx,
                                               const float* __restrict__ w, const float* __restrict__ b, float eps,
@@ -147,9 +153,9 @@ __global__ __launch_bounds__(256) void ln_bwd(int R, int C, int rows_per_block, 
 // Batch statistics as shifted sums in fp64 (torch's CPU kernels accumulate in double too): per
 // channel s1 = sum (x - k), s2 = sum (x - k)^2 with the shift k = x[0, c] (the first row: keeps
 // s2/M - (s1/M)^2 free of cancellation whatever the channel's offset), so mean = k + s1/M and the
-// biased variance = s2/M - (s1/M)^2.  A partial block (64 channels x 4 row lanes) sums rows_per
-// rows into part[p][2][C]; the reduction over the P partials runs in a fixed order (4 partial lanes
-// p = l, l+4, ..., then the 4 lanes in order), either in the last-arriving partial block of each
+// biased variance = s2/M - (s1/M)^2.  A partial block (64 channels x BN_RL row lanes) sums rows_per
+// rows into part[p][2][C]; the reduction over the P partials runs in a fixed order (BN_RL partial lanes
+// p = l, l+BN_RL, ..., then the lanes in order), either in the last-arriving partial block of each
 // 64-channel group (tickets: no second launch) or in bn_stats_final (same code, same result).
 // The elementwise BN arithmetic, spelled with explicit fmaf so that every kernel using it (separate or
 // fused final + apply) rounds identically whatever the surrounding code lets the compiler contract.
@@ -171,29 +177,29 @@ __device__ __forceinline__ void bn_dx_store(float* p, float beta_dx, float v) {
 }
 
 // The fixed-order reduction of the [P][2][C] fp64 partials of channel group cx (block = 64 channels x
-// 4 partial lanes): on return (after a barrier) tot[0][cl] / tot[1][cl] hold channel cx*64+cl's two sums,
+// BN_RL partial lanes): on return (after a barrier) tot[0][cl] / tot[1][cl] hold channel cx*64+cl's two sums,
 // visible to every thread of the block.  Every consumer (the separate final kernels and the fused
 // apply kernels) sums in this one order, so their results agree bit for bit.
 __device__ __forceinline__ void bn_part_sums(int P, int C, const double* __restrict__ part, int cx,
                                              double (*tot)[64]) {
-  __shared__ double shr[2][4][64];
+  __shared__ double shr[2][BN_RL][64];
   const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const int c = cx * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     // NB partials per lane loaded before they are summed (one round of dependent loads per batch of
     // NB instead of one per 4); the sums keep the partial order
-    for (int p0 = pl; p0 < P; p0 += 4 * NB) {
+    for (int p0 = pl; p0 < P; p0 += BN_RL * NB) {
       double a[NB], bq[NB];
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int p = p0 + 4 * i;
+        const int p = p0 + BN_RL * i;
         a[i] = p < P ? part[(long)p * 2 * C + c] : 0.0;
         bq[i] = p < P ? part[(long)p * 2 * C + C + c] : 0.0;
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        if (p0 + 4 * i < P) {
+        if (p0 + BN_RL * i < P) {
           s1 += a[i];
           s2 += bq[i];
         }
@@ -203,8 +209,14 @@ __device__ __forceinline__ void bn_part_sums(int P, int C, const double* __restr
   shr[1][pl][cl] = s2;
   __syncthreads();
   if (pl == 0) {
-    tot[0][cl] = shr[0][0][cl] + shr[0][1][cl] + shr[0][2][cl] + shr[0][3][cl];
-    tot[1][cl] = shr[1][0][cl] + shr[1][1][cl] + shr[1][2][cl] + shr[1][3][cl];
+    double t1 = shr[0][0][cl], t2 = shr[1][0][cl];
+#pragma unroll
+    for (int l = 1; l < BN_RL; ++l) {
+      t1 += shr[0][l][cl];
+      t2 += shr[1][l][cl];
+    }
+    tot[0][cl] = t1;
+    tot[1][cl] = t2;
   }
   __syncthreads();
 }
@@ -247,7 +259,7 @@ __device__ __forceinline__ void bn_stats_reduce(int P, int C, long M, const floa
 // Fused final + apply (train mode): grid (ceil(C/64), ceil(M/rows_per_block)); every block reduces
 // the channel group's partials itself (bn_part_sums), the blocks of row 0 write save_* and the running
 // statistics, and all apply y = relu?((x - mean) * invstd * w + b) to their rows.
-__global__ __launch_bounds__(256) void bn_apply_stats(int M, int C, const float* __restrict__ x, long ldx, int P,
+__global__ __launch_bounds__(BN_T) void bn_apply_stats(int M, int C, const float* __restrict__ x, long ldx, int P,
                                                       const double* __restrict__ part, float eps, float momentum,
                                                       float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                                       float* __restrict__ run_mean, float* __restrict__ run_var,
@@ -265,16 +277,16 @@ __global__ __launch_bounds__(256) void bn_apply_stats(int M, int C, const float*
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min((long)M, r0 + rows_per_block);
   const float wc = w[c];
-  for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight
+  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
     float xv[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) xv[i] = rb + 4 * i < r1 ? x[(rb + 4 * i) * ldx + c] : 0.f;
+    for (int i = 0; i < NB; ++i) xv[i] = rb + BN_RL * i < r1 ? x[(rb + BN_RL * i) * ldx + c] : 0.f;
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      if (rb + 4 * i < r1) {
+      if (rb + BN_RL * i < r1) {
         float v = bn_fwd_elem(xv[i], mf, isf, wc, bc);
         if (relu) v = fmaxf(v, 0.f);
-        y[(rb + 4 * i) * ldy + c] = v;
+        y[(rb + BN_RL * i) * ldy + c] = v;
       }
   }
 }
@@ -282,12 +294,12 @@ __global__ __launch_bounds__(256) void bn_apply_stats(int M, int C, const float*
 
 
 // grid (ceil(C/64), P); cnt (optional) = one zeroed arrival counter per 64-channel group
-__global__ __launch_bounds__(256) void bn_stats_sums(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
+__global__ __launch_bounds__(BN_T) void bn_stats_sums(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
                                                      double* __restrict__ part, unsigned int* __restrict__ cnt,
                                                      float eps, float momentum, float* __restrict__ save_mean,
                                                      float* __restrict__ save_invstd, float* __restrict__ run_mean,
                                                      float* __restrict__ run_var) {
-  __shared__ double sh[2][4][64];
+  __shared__ double sh[2][BN_RL][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per;
@@ -295,13 +307,13 @@ __global__ __launch_bounds__(256) void bn_stats_sums(int M, int C, const float* 
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const double k = x[c];
-    for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight, summed in row order
+    for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight, summed in row order
       float v[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i) v[i] = rb + 4 * i < r1 ? x[(rb + 4 * i) * ldx + c] : 0.f;
+      for (int i = 0; i < NB; ++i) v[i] = rb + BN_RL * i < r1 ? x[(rb + BN_RL * i) * ldx + c] : 0.f;
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        if (rb + 4 * i < r1) {
+        if (rb + BN_RL * i < r1) {
           const double d = (double)v[i] - k;
           s1 += d;
           s2 = fma(d, d, s2);
@@ -313,14 +325,20 @@ __global__ __launch_bounds__(256) void bn_stats_sums(int M, int C, const float* 
   __syncthreads();
   if (rl == 0 && c < C) {
     double* p = part + (long)blockIdx.y * 2 * C + c;
-    p[0] = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-    p[C] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+    double t1 = sh[0][0][cl], t2 = sh[1][0][cl];
+#pragma unroll
+    for (int l = 1; l < BN_RL; ++l) {
+      t1 += sh[0][l][cl];
+      t2 += sh[1][l][cl];
+    }
+    p[0] = t1;
+    p[C] = t2;
   }
   if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
   bn_stats_reduce(gridDim.y, C, M, x, part, blockIdx.x, eps, momentum, save_mean, save_invstd, run_mean, run_var);
 }
 
-__global__ __launch_bounds__(256) void bn_stats_final(int P, int C, long M, const float* __restrict__ x,
+__global__ __launch_bounds__(BN_T) void bn_stats_final(int P, int C, long M, const float* __restrict__ x,
                                                       const double* __restrict__ part, float eps, float momentum,
                                                       float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                                       float* __restrict__ run_mean, float* __restrict__ run_var) {
@@ -348,7 +366,7 @@ __global__ void bn_apply(int total, FastDiv fC, const float* __restrict__ x, lon
 }
 
 // BN backward sums: s1 = sum dyv, s2 = sum dyv*xhat (dyv = dy * (relu_out > 0) if relu_out) in fp64.
-// Partial blocks (64 channels x 4 row lanes) -> part[p][2][C]; the fixed-order reduction (as in
+// Partial blocks (64 channels x BN_RL row lanes) -> part[p][2][C]; the fixed-order reduction (as in
 // bn_stats_reduce) writes sums[0:C] = s1, sums[C:2C] = s2 and dw = beta_w*dw + s2, db = beta_w*db + s1,
 // in the last-arriving block of each 64-channel group (tickets) or in bn_bwd_final.
 __device__ __forceinline__ void bn_bwd_reduce(int P, int C, const double* __restrict__ part, int cx,
@@ -366,14 +384,14 @@ __device__ __forceinline__ void bn_bwd_reduce(int P, int C, const double* __rest
   if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_sums(int M, int C, const float* __restrict__ dy, long lddy,
+__global__ __launch_bounds__(BN_T) void bn_bwd_sums(int M, int C, const float* __restrict__ dy, long lddy,
                                                    const float* __restrict__ x, long ldx,
                                                    const float* __restrict__ relu_out, long ldo,
                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
                                                    int rows_per, double* __restrict__ part,
                                                    unsigned int* __restrict__ cnt, double* __restrict__ sums,
                                                    float* __restrict__ dw, float* __restrict__ db, float beta_w) {
-  __shared__ double sh[2][4][64];
+  __shared__ double sh[2][BN_RL][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per;
@@ -381,11 +399,11 @@ __global__ __launch_bounds__(256) void bn_bwd_sums(int M, int C, const float* __
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     const float mu = mean[c], is = invstd[c];
-    for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight, summed in row order
+    for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight, summed in row order
       float dv[NB], xv[NB], ov[NB];
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const long r = rb + 4 * i;
+        const long r = rb + BN_RL * i;
         const bool ok = r < r1;
         dv[i] = ok ? dy[r * lddy + c] : 0.f;
         xv[i] = ok ? x[r * ldx + c] : 0.f;
@@ -393,7 +411,7 @@ __global__ __launch_bounds__(256) void bn_bwd_sums(int M, int C, const float* __
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        if (rb + 4 * i < r1) {
+        if (rb + BN_RL * i < r1) {
           float d = dv[i];
           if (relu_out && !(ov[i] > 0.f)) d = 0.f;
           s1 += d;
@@ -406,14 +424,20 @@ __global__ __launch_bounds__(256) void bn_bwd_sums(int M, int C, const float* __
   __syncthreads();
   if (rl == 0 && c < C) {
     double* p = part + (long)blockIdx.y * 2 * C + c;
-    p[0] = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-    p[C] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+    double t1 = sh[0][0][cl], t2 = sh[1][0][cl];
+#pragma unroll
+    for (int l = 1; l < BN_RL; ++l) {
+      t1 += sh[0][l][cl];
+      t2 += sh[1][l][cl];
+    }
+    p[0] = t1;
+    p[C] = t2;
   }
   if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
   bn_bwd_reduce(gridDim.y, C, part, blockIdx.x, sums, dw, db, beta_w);
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_final(int P, int C, const double* __restrict__ part,
+__global__ __launch_bounds__(BN_T) void bn_bwd_final(int P, int C, const double* __restrict__ part,
                                                     double* __restrict__ sums, float* __restrict__ dw,
                                                     float* __restrict__ db, float beta_w) {
   bn_bwd_reduce(P, C, part, blockIdx.x, sums, dw, db, beta_w);
@@ -423,7 +447,7 @@ __global__ __launch_bounds__(256) void bn_bwd_final(int P, int C, const double* 
 // reduces the channel group's partials itself (bn_part_sums), the blocks of row 0 write dw / db, and
 // all write dx = beta_dx*dx + w*invstd*(dyv - s1/M - xhat*s2/M) (train) or w*invstd*dyv (eval) for
 // their rows -- the same arithmetic as bn_bwd_final + bn_bwd_apply.
-__global__ __launch_bounds__(256) void bn_bwd_apply_sums(int train, int M, int C, const float* __restrict__ dy,
+__global__ __launch_bounds__(BN_T) void bn_bwd_apply_sums(int train, int M, int C, const float* __restrict__ dy,
                                                          long lddy, const float* __restrict__ x, long ldx,
                                                          const float* __restrict__ relu_out, long ldo,
                                                          const float* __restrict__ mean,
@@ -446,11 +470,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_sums(int train, int M, int C
   const float invM = 1.f / (float)M;
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min((long)M, r0 + rows_per_block);
-  for (long rb = r0 + rl; rb < r1; rb += 4 * NB) {   // NB rows' loads in flight
+  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
     float dv[NB], xv[NB], ov[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const long r = rb + 4 * i;
+      const long r = rb + BN_RL * i;
       const bool ok = r < r1;
       dv[i] = ok ? dy[r * lddy + c] : 0.f;
       xv[i] = ok && train ? x[r * ldx + c] : 0.f;
@@ -458,13 +482,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_sums(int train, int M, int C
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      if (rb + 4 * i < r1) {
+      if (rb + BN_RL * i < r1) {
         float d = dv[i];
         if (relu_out && !(ov[i] > 0.f)) d = 0.f;
         float v;
         if (train) v = bn_bwd_elem(d, xv[i], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
         else v = (wc * is) * d;
-        bn_dx_store(dx + (rb + 4 * i) * lddx + c, beta_dx, v);
+        bn_dx_store(dx + (rb + BN_RL * i) * lddx + c, beta_dx, v);
       }
   }
 }
@@ -614,11 +638,11 @@ VC_EXPORT int vc_bn_stats_ex(int train, long M, int C, const float* x, long ldx,
   const int P = vc_cdiv(M, rows_per);
   VC_REQUIRE((long)P * C * 2 <= ws_doubles && P <= 65535);
   unsigned int* cnt = (counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;
-  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
+  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
                      cnt, eps, momentum, save_mean, save_invstd, run_mean, run_var);
   VC_CHECK_LAUNCH();
   if (!cnt) {
-    hipLaunchKernelGGL(bn_stats_final, dim3(vc_cdiv(C, 64)), dim3(256), 0, stream, P, C, M, x, wsd, eps, momentum,
+    hipLaunchKernelGGL(bn_stats_final, dim3(vc_cdiv(C, 64)), dim3(BN_T), 0, stream, P, C, M, x, wsd, eps, momentum,
                        save_mean, save_invstd, run_mean, run_var);
     VC_CHECK_LAUNCH();
   }
@@ -652,11 +676,11 @@ VC_EXPORT int vc_bn_forward(int train, long M, int C, const float* x, long ldx, 
   const int rows_per = bn_rows_per(M, C, ws_doubles, 0);
   const int P = vc_cdiv(M, rows_per);
   VC_REQUIRE((long)P * C * 2 <= ws_doubles && P <= 65535);
-  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
+  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
                      (unsigned int*)nullptr, eps, momentum, save_mean, save_invstd, run_mean, run_var);
   VC_CHECK_LAUNCH();
   const int rpb = BN_APPLY_ROWS;
-  hipLaunchKernelGGL(bn_apply_stats, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(256), 0, stream, (int)M, C, x, ldx,
+  hipLaunchKernelGGL(bn_apply_stats, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, (int)M, C, x, ldx,
                      P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy, rpb);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -690,19 +714,19 @@ VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy,
   VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_doubles && P <= 65535);
   double* sums = wsd + (long)P * C * 2;
   unsigned int* cnt = (counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;
-  hipLaunchKernelGGL(bn_bwd_sums, dim3(vc_cdiv(C, 64), P), dim3(256), 0, stream, (int)M, C, dy, lddy, x, ldx,
+  hipLaunchKernelGGL(bn_bwd_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
                      relu_out, ldo, mean, invstd, rows_per, wsd, cnt, sums, dw, db, beta_w);
   VC_CHECK_LAUNCH();
   if (!cnt && dx) {   // the channel-tiled apply reduces the partials itself: one launch fewer
     const int rpb = BN_APPLY_ROWS;
-    hipLaunchKernelGGL(bn_bwd_apply_sums, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(256), 0, stream, train,
+    hipLaunchKernelGGL(bn_bwd_apply_sums, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, train,
                        (int)M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, w, P, wsd, dx, lddx, beta_dx, dw,
                        db, beta_w, rpb);
     VC_CHECK_LAUNCH();
     return VC_OK;
   }
   if (!cnt) {
-    hipLaunchKernelGGL(bn_bwd_final, dim3(vc_cdiv(C, 64)), dim3(256), 0, stream, P, C, wsd, sums, dw, db, beta_w);
+    hipLaunchKernelGGL(bn_bwd_final, dim3(vc_cdiv(C, 64)), dim3(BN_T), 0, stream, P, C, wsd, sums, dw, db, beta_w);
     VC_CHECK_LAUNCH();
   }
   if (dx) {

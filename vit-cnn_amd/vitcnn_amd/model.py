@@ -59,6 +59,10 @@ _SCAN_FUSED = os.environ.get("VITCNN_SCAN_FUSED", "1") != "0"
 # patch_embed + pre_norm + in_proj and combine + out_proj + ln1 + change_dim as one launch each
 # (vc_rowchain_front / _back); "0" restores the separate launches (measurement switch)
 _ROW_CHAIN = os.environ.get("VITCNN_ROW_CHAIN", "1") != "0"
+# GLfusion: the phi | g max pool inside the non-local attention forward and its backward inside the
+# attention backward, the concat gradient's add + copy as one launch (vc_nonlocal_attn_pool_fwd / _bwd,
+# vc_add2_2d_dup); "0" restores the separate launches (measurement switch)
+_GLF_FUSED = os.environ.get("VITCNN_GLF_FUSED", "1") != "0"
 # the local conv's data gradient as the tap-major implicit GEMM (vc_conv3x3_tap_dgrad, no dcol matrix, no
 # col2im) over the weights packed tap-major by lane 0 in the forward: opt-in, measured slower on the B=64
 # step (1.90-1.94 -> 1.99-2.01 ms: at 7x7 / 9x9 maps the row gathers cost more than dcol + col2im)
@@ -777,9 +781,12 @@ class _Program:
                        bias=P[nl + ".phi.0.bias"])
         PP = ws.f(pfx + ".PP", B * Pk * 2 * Ci)
         PA = ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr()
-        self.L.vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, PG, 2 * Ci, PP, PA, self.s)
         ATT, O = ws.f(pfx + ".ATT", M * Pk), ws.f(pfx + ".O", M * Ci)
-        self.L.vc_nonlocal_attn_fwd(B, S, Pk, Ci, TH, PP, ATT, O, self.s)
+        if _GLF_FUSED:   # 2x2 max pool folded into the attention forward (pooled + taps kept for the backward)
+            self.L.vc_nonlocal_attn_pool_fwd(B, S, Pk, Ci, Hs, TH, PG, 2 * Ci, PP, PA, ATT, O, self.s)
+        else:
+            self.L.vc_maxpool2_fwd(B, Hs, Hs, 2 * Ci, PG, 2 * Ci, PP, PA, self.s)
+            self.L.vc_nonlocal_attn_fwd(B, S, Pk, Ci, TH, PP, ATT, O, self.s)
         WP = ws.f(pfx + ".WP", M * Cout)
         # the W projection stays fp32 in the bf16 mode: the train-mode BatchNorm after it sees a batch
         # spread small against the mean, so bf16 operands here alone move the logits by 3.3e-2 of their
@@ -1001,8 +1008,12 @@ class _Program:
             CAT1, dCAT1 = f(pfx + ".CAT1", M * 2 * Cout), f(pfx + ".dCAT1", M * 2 * Cout)
             self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout, dFM, dCAT1, 0.0)
             dFc, dFl = f(pfx + ".dFc", M * Cout), f(pfx + ".dFl", M * Cout)
-            self.L.vc_add2_2d(M, Cout, dCAT1, 2 * Cout, dCAT1 + F32 * Cout, 2 * Cout, dFc, Cout, 0.0, self.s)
-            self.L.vc_add2_2d(M, Cout, dFc, Cout, 0, 0, dFl, Cout, 0.0, self.s)
+            if _GLF_FUSED:
+                self.L.vc_add2_2d_dup(M, Cout, dCAT1, 2 * Cout, dCAT1 + F32 * Cout, 2 * Cout, dFc, Cout, dFl, Cout,
+                                      self.s)
+            else:
+                self.L.vc_add2_2d(M, Cout, dCAT1, 2 * Cout, dCAT1 + F32 * Cout, 2 * Cout, dFc, Cout, 0.0, self.s)
+                self.L.vc_add2_2d(M, Cout, dFc, Cout, 0, 0, dFl, Cout, 0.0, self.s)
             # localf = BN(W o) + Fc + Fl  ->  non-local branch
             WP, dWP = f(pfx + ".WP", M * Cout), f(pfx + ".dWP", M * Cout)
             self.bn_bwd(nl + ".W.1", pfx + ".W1", dCAT1, 2 * Cout, WP, Cout, 0, M, Cout, dWP, Cout, 0.0)
@@ -1010,10 +1021,13 @@ class _Program:
             self.linear_bwd(nl + ".W.0.weight", nl + ".W.0.bias", dWP, M, Cout, Ci, O, Ci, dO, 0.0)
             TH, PP, ATT = f(pfx + ".TH", M * Ci), f(pfx + ".PP", B * Pk * 2 * Ci), f(pfx + ".ATT", M * Pk)
             dTH, dPP = f(pfx + ".dTH", M * Ci), f(pfx + ".dPP", B * Pk * 2 * Ci)
-            self.L.vc_nonlocal_attn_bwd(B, S, Pk, Ci, TH, PP, ATT, dO, dTH, dPP, self.s)
             dPG = f(pfx + ".dPG", M * 2 * Ci)
-            self.L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dPP,
-                                   ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr(), dPG, 2 * Ci, self.s)
+            PA = ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr()
+            if _GLF_FUSED:   # attention backward with the 2x2 max-pool backward folded in (dPP: fallback only)
+                self.L.vc_nonlocal_attn_pool_bwd(B, S, Pk, Ci, Hs, TH, PP, ATT, dO, PA, dTH, dPP, dPG, self.s)
+            else:
+                self.L.vc_nonlocal_attn_bwd(B, S, Pk, Ci, TH, PP, ATT, dO, dTH, dPP, self.s)
+                self.L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dPP, PA, dPG, 2 * Ci, self.s)
             # phi | g (stacked, one weight + one data gradient) and theta: one grouped launch
             with self.gemm_group():
                 self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, 2 * Ci, Cout, Fc, Cout, dFc, 1.0)
