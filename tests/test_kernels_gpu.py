@@ -187,7 +187,7 @@ def test_layernorm_bwd_residual_is_bit_identical(L, ws, R, C):
     for a_, b_ in zip(*outs):
         assert torch.equal(a_, b_)
     # the split form (dx now, the parameter reduction later from a buffer of its own) is the same
-    part_n = 256 * 2 * C
+    part_n = 1024 * 2 * C
     part = torch.full((part_n,), float("nan"), device=DEV)
     dx = torch.full((R, C), float("nan"), device=DEV)
     dw, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), -0.5, device=DEV)
@@ -530,3 +530,33 @@ def test_add2_dup(L):
     torch.cuda.synchronize()
     ref = cat[:, :C] + cat[:, C:]
     assert torch.equal(o1, ref) and torch.equal(o2[:, :C], ref) and torch.isnan(o2[:, C:]).all()
+
+
+@pytest.mark.parametrize("B,H,C", [(64, 9, 144), (64, 7, 256), (3, 11, 64), (2, 5, 70), (1, 33, 16)])
+def test_im2col_col2im_lds_forms(L, B, H, C, monkeypatch):
+    """vc_im2col3x3 (BN affine folded) / vc_col2im3x3: the LDS-staged forms (chunks of <= 32 channels per
+    block) equal the per-thread forms (VITCNN_C2I_LDS=0) bit for bit and torch's unfold / fold; H = 33
+    exceeds the LDS budget and keeps the per-thread kernels."""
+    import torch.nn.functional as F
+    OH = H - 2
+    x = rnd(B * H * H, C, seed=71).to(DEV)
+    mean, inv = rnd(C, seed=72).to(DEV), (rnd(C, seed=73).abs() + 0.5).to(DEV)
+    w, b = rnd(C, seed=74).to(DEV), rnd(C, seed=75).to(DEV)
+    dcol = rnd(B * OH * OH, 9 * C, seed=76).to(DEV)
+    outs = []
+    for lds in ("1", "0"):
+        monkeypatch.setenv("VITCNN_C2I_LDS", lds)
+        col = torch.full((B * OH * OH, 9 * C), float("nan"), device=DEV)
+        dx = torch.full((B * H * H, C), float("nan"), device=DEV)
+        assert L.vc_im2col3x3(B, H, H, C, P(x), P(mean), P(inv), P(w), P(b), P(col), S()) == 0
+        assert L.vc_col2im3x3(B, H, H, C, P(dcol), P(dx), S()) == 0
+        torch.cuda.synchronize()
+        outs.append((col, dx))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    sc = inv * w
+    xn = (x.double() * sc.double() + (b - mean * sc).double()).view(B, H, H, C).permute(0, 3, 1, 2)
+    ref_col = F.unfold(xn, 3).permute(0, 2, 1).reshape(B * OH * OH, 9 * C)
+    assert rel_err(outs[0][0].cpu().numpy(), ref_col.cpu().numpy()) < 1e-6
+    ref_dx = F.fold(dcol.double().view(B, OH * OH, 9 * C).permute(0, 2, 1), (H, H), 3)
+    ref_dx = ref_dx.permute(0, 2, 3, 1).reshape(B * H * H, C)
+    assert rel_err(outs[0][1].cpu().numpy(), ref_dx.cpu().numpy()) < 1e-6

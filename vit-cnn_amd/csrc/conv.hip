@@ -80,6 +80,125 @@ __global__ void col2im3x3(int total, FastDiv fC, FastDiv fW, FastDiv fH, const f
   dx[idx] = s;
 }
 
+// LDS-staged forms of im2col3x3 / col2im3x3 for one batch element and a chunk of CC channels per block.
+// The per-thread forms above touch col rows with a 36-byte lane stride (9 taps per channel); here every
+// global access is a run of consecutive floats -- the image chunk [H*W][CC] and the col segments
+// [S][9*CC] (S = OH*OW) go through LDS, where the stride-9 channel reads are bank-conflict free (9 odd).
+// Same arithmetic and summation order as the per-thread kernels (bit-identical).
+constexpr int C2I_T = 512, C2I_W = C2I_T / 64, C2I_CC = 32, C2I_JK = (9 * C2I_CC + 63) / 64;
+
+__global__ __launch_bounds__(C2I_T) void im2col3x3_lds(int nchunk, int H, int W, int C,
+                                                      const float* __restrict__ x, const float* __restrict__ mean,
+                                                      const float* __restrict__ invstd, const float* __restrict__ w,
+                                                      const float* __restrict__ b, float* __restrict__ col) {
+  extern __shared__ float img[];   // [H*W][C2I_CC]
+  const int bb = blockIdx.x / nchunk, c0 = (blockIdx.x - bb * nchunk) * C2I_CC, nc = min(C2I_CC, C - c0);
+  const int OW = W - 2, S = (H - 2) * OW, HW = H * W;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  {   // stage the chunk: thread -> (pixel i >> 5, channel i & 31), every load of a pass issued together
+    const int c = threadIdx.x & (C2I_CC - 1);
+    float sc = 1.f, sh = 0.f;
+    if (mean && c < nc) {
+      sc = invstd[c0 + c] * w[c0 + c];
+      sh = b[c0 + c] - mean[c0 + c] * sc;
+    }
+    const float* xb = x + (long)bb * HW * C + c0 + c;
+    constexpr int PP = C2I_T / C2I_CC, NBP = 8;   // pixels per pass, passes batched
+    for (int p0 = threadIdx.x / C2I_CC; p0 < HW; p0 += PP * NBP) {
+      float v[NBP];
+#pragma unroll
+      for (int k = 0; k < NBP; ++k) {
+        const int p = p0 + k * PP;
+        v[k] = (p < HW && c < nc) ? xb[(long)p * C] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < NBP; ++k) {
+        const int p = p0 + k * PP;
+        if (p < HW) img[p * C2I_CC + c] = v[k] * sc + sh;
+      }
+    }
+  }
+  __syncthreads();
+  // write: a wave per col row m, lane -> the row segment's floats j = lane + 64 k (fixed per lane, so
+  // their (channel, tap) offsets into the staged image are computed once)
+  const int seg = 9 * nc;
+  int off[C2I_JK];
+#pragma unroll
+  for (int k = 0; k < C2I_JK; ++k) {
+    const int j = lane + 64 * k, c = j / 9, t = j - 9 * c, kh = t / 3, kw = t - 3 * kh;
+    off[k] = j < seg ? (kh * W + kw) * C2I_CC + c : -1;
+  }
+  float* cb = col + (long)bb * S * 9 * C + 9 * c0;
+  for (int m = wave; m < S; m += C2I_W) {
+    const int oh = m / OW, ow = m - oh * OW, base = (oh * W + ow) * C2I_CC;
+    float* row = cb + (long)m * 9 * C;
+#pragma unroll
+    for (int k = 0; k < C2I_JK; ++k)
+      if (off[k] >= 0) row[lane + 64 * k] = img[base + off[k]];
+  }
+}
+
+__global__ __launch_bounds__(C2I_T) void col2im3x3_lds(int nchunk, int H, int W, int C,
+                                                      const float* __restrict__ dcol, float* __restrict__ dx) {
+  extern __shared__ float seg_lds[];   // [S][9*C2I_CC]
+  constexpr int LD = 9 * C2I_CC, RB = 3;   // rows per wave whose loads are issued together
+  const int bb = blockIdx.x / nchunk, c0 = (blockIdx.x - bb * nchunk) * C2I_CC, nc = min(C2I_CC, C - c0);
+  const int OH = H - 2, OW = W - 2, S = OH * OW, HW = H * W, seg = 9 * nc;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* db = dcol + (long)bb * S * 9 * C + 9 * c0;
+  for (int m0 = wave; m0 < S; m0 += C2I_W * RB) {
+    float v[RB][C2I_JK];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int m = m0 + r * C2I_W;
+#pragma unroll
+      for (int k = 0; k < C2I_JK; ++k) {
+        const int j = lane + 64 * k;
+        v[r][k] = (m < S && j < seg) ? db[(long)m * 9 * C + j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int m = m0 + r * C2I_W;
+#pragma unroll
+      for (int k = 0; k < C2I_JK; ++k) {
+        const int j = lane + 64 * k;
+        if (m < S && j < seg) seg_lds[m * LD + j] = v[r][k];
+      }
+    }
+  }
+  __syncthreads();
+  // gather: thread -> (pixel, channel lane & 31), two pixels per wave
+  const int c = lane & (C2I_CC - 1);
+  float* xo = dx + (long)bb * HW * C + c0 + c;
+  if (c < nc)
+    for (int p = wave * 2 + (lane >> 5); p < HW; p += 2 * C2I_W) {
+      const int ih = p / W, iw = p - ih * W;
+      float s = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int oh = ih - kh;
+        if (oh < 0 || oh >= OH) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ow = iw - kw;
+          if (ow < 0 || ow >= OW) continue;
+          s += seg_lds[(oh * OW + ow) * LD + 9 * c + kh * 3 + kw];
+        }
+      }
+      xo[(long)p * C] = s;
+    }
+}
+
+// channels per block of the LDS forms (0: the per-thread kernels): the col chunk S x 9 x 32 floats in at
+// most 64 KB of LDS (patches up to 11 x 11); VITCNN_C2I_LDS=0 keeps the per-thread kernels (measurement switch)
+static int c2i_chunk(int H, int W, int C) {
+  const char* e = getenv("VITCNN_C2I_LDS");   // read per call (tests compare both forms in one process)
+  if (e && atoi(e) == 0) return 0;
+  const long S = (long)(H - 2) * (W - 2);
+  return S * 9 * C2I_CC * 4 <= 65536 ? C2I_CC : 0;
+}
+
 // 2x2 / stride 2 floor max-pool over a channels-last [B, H, W, C] (row stride ldx);
 // arg = which of the 4 taps won (first max in (kh, kw) scan order, as torch).
 __global__ void maxpool2(int total, FastDiv fC, FastDiv fPW, FastDiv fPH, int H, int W, const float* __restrict__ x,
@@ -140,6 +259,14 @@ VC_API int vc_im2col3x3(int B, int H, int W, int C, const float* x, const float*
   long total = (long)B * (H - 2) * (W - 2) * C;
   if (total == 0) return VC_OK;
   VC_REQUIRE_I32(total * 9);
+  if (const int cc = c2i_chunk(H, W, C)) {
+    const int nchunk = vc_cdiv(C, cc);
+    VC_REQUIRE_I32((long)B * nchunk);
+    hipLaunchKernelGGL(im2col3x3_lds, dim3(B * nchunk), dim3(C2I_T), sizeof(float) * H * W * cc, stream, nchunk, H, W,
+                       C, x, bn_mean, bn_invstd, bn_w, bn_b, col);
+    VC_CHECK_LAUNCH();
+    return VC_OK;
+  }
   hipLaunchKernelGGL(im2col3x3, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
                      make_fastdiv(W - 2), make_fastdiv(H - 2), H, W, x, bn_mean, bn_invstd, bn_w, bn_b, col);
   VC_CHECK_LAUNCH();
@@ -151,6 +278,14 @@ VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx
   long total = (long)B * H * W * C;
   if (total == 0) return VC_OK;
   VC_REQUIRE_I32(total * 9);
+  if (const int cc = c2i_chunk(H, W, C)) {
+    const int nchunk = vc_cdiv(C, cc);
+    VC_REQUIRE_I32((long)B * nchunk);
+    hipLaunchKernelGGL(col2im3x3_lds, dim3(B * nchunk), dim3(C2I_T), sizeof(float) * (H - 2) * (W - 2) * 9 * cc,
+                       stream, nchunk, H, W, C, dcol, dx);
+    VC_CHECK_LAUNCH();
+    return VC_OK;
+  }
   hipLaunchKernelGGL(col2im3x3, dim3(vc_cdiv(total, 256)), dim3(256), 0, stream, (int)total, make_fastdiv(C),
                      make_fastdiv(W), make_fastdiv(H), dcol, dx);
   VC_CHECK_LAUNCH();

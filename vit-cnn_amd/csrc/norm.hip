@@ -539,8 +539,12 @@ VC_EXPORT int vc_layernorm_fwd(int R, int C, const float* x, long ldx, const flo
 }
 
 // rows per ln_bwd block (P = ceil(R / rows_per) partial rows of 2C floats)
+// (8 rows = one two-row iteration per wave: the B = 64 steps' 5184-row LayerNorms as 648 blocks)
 static int ln_partial_rows(int R, int C, long part_floats) {
-  int rows_per = std::max(16, vc_cdiv(R, 256));
+#ifndef VC_LN_MIN_ROWS
+#define VC_LN_MIN_ROWS 8
+#endif
+  int rows_per = std::max(VC_LN_MIN_ROWS, vc_cdiv(R, 1024));
   while ((long)vc_cdiv(R, rows_per) * 2 * C > part_floats) rows_per *= 2;
   return rows_per;
 }

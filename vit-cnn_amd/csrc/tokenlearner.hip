@@ -77,6 +77,29 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return r;
 }
 
+// K independent block sums in one pass (one pair of barriers instead of K); each value is summed in
+// block_sum's order, so the results are bit-identical to K block_sum calls
+template <int K>
+__device__ __forceinline__ void block_sums(double (&v)[K], double* red) {
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[k * (TLT / 64) + w] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < TLT / 64; ++i) r += red[k * (TLT / 64) + i];
+    v[k] = r;
+  }
+  __syncthreads();
+}
+
 // the token's 2->1 conv output for pixel i, in fp64: BN(1) normalises values with a tiny spread
 // around a large mean, so the fp32 rounding of the conv would be amplified by 1/std
 __device__ __forceinline__ double tl_fv(float m, float v, float w0, float w1, float bc) {
@@ -175,7 +198,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, FastD
                                                 const float* __restrict__ avg, const float* __restrict__ par,
                                                 const double* __restrict__ stats, const float* __restrict__ da,
                                                 float* __restrict__ df, float* __restrict__ gpar) {
-  __shared__ double red[TLT / 64];
+  __shared__ double red[3 * (TLT / 64)];
   const int s = blockIdx.x;
   const float* p = par + (long)s * TPAR;
   const float w0 = p[0], w1 = p[1], bc = p[2], gam = p[3], bet = p[4];
@@ -215,8 +238,12 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, FastD
     s1 += g1;
     s2 += g1 * xh;
   });
-  s1 = block_sum(s1, red);
-  s2 = block_sum(s2, red);
+  {
+    double v2[2] = {s1, s2};
+    block_sums(v2, red);
+    s1 = v2[0];
+    s2 = v2[1];
+  }
   double gw0 = 0.0, gw1 = 0.0, gb = 0.0;
   pass([&](long i, float m, float v, float dav) {
     double xh;
@@ -232,9 +259,13 @@ __global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, FastD
     gw1 += d * v;
     gb += d;
   });
-  gw0 = block_sum(gw0, red);
-  gw1 = block_sum(gw1, red);
-  gb = block_sum(gb, red);
+  {
+    double v3[3] = {gw0, gw1, gb};
+    block_sums(v3, red);
+    gw0 = v3[0];
+    gw1 = v3[1];
+    gb = v3[2];
+  }
   if (threadIdx.x == 0) {
     float* g = gpar + (long)s * TPAR;
     g[0] = (float)gw0;

@@ -851,7 +851,7 @@ class _Program:
         lane (its partials kept in a buffer of their own)"""
         ws = self.ws
         if self._deferring(defer):
-            part_n = 256 * 2 * C   # >= the kernel's partial rows, so the same split as vc_layernorm_bwd
+            part_n = 1024 * 2 * C   # >= the kernel's partial rows, so the same split as vc_layernorm_bwd
             part = ws.f(tag + ".lnpart", part_n)
             self.L.vc_layernorm_bwd_dx(R, C, dY, C, X, C, self.P[pfx + ".weight"], ws.f(tag + ".m", R),
                                        ws.f(tag + ".r", R), res or None, C, dX, C, beta_dx, part, part_n, self.s)
