@@ -183,7 +183,10 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
 // Backward on MFMA, same tile scheme as the forward.  dS = P * (dP - rowsum(dO*O)), P recomputed
 // from lse.  Pass 1: a wave owns 16 queries and walks 16-key tiles: S^T = K Q^T, dP^T = V dO^T,
 // dQ^T += K^T dS^T.  Pass 2: the wave owns 16 keys and walks 16-query tiles: S = Q K^T, dP = dO V^T,
-// dV^T += dO^T P, dK^T += Q^T dS (P / dS taken from the accumulators as B operands).
+// dV^T += dO^T P, dK^T += Q^T dS (P / dS taken from the accumulators as B operands).  The two passes run
+// in two blocks per head (blockIdx.y), each staging the head: 2 x B*H blocks of T/16 waves keep twice
+// the waves per SIMD of one block doing both passes; the accumulations alternate between two
+// accumulators per output tile (even / odd tiles) so consecutive tiles' MFMA chains overlap.
 __device__ __forceinline__ f32x4 mfma4(f32x4 a, f32x4 b, f32x4 c) {
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
@@ -234,12 +237,12 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   if (r0 >= T) return;
   const int c = lane & 15, g = lane >> 4;
   const int ri = min(r0 + c, T - 1);
-  {  // pass 1: dq of queries r0 .. r0 + 15 (query c of this lane)
+  if (blockIdx.y == 0) {  // pass 1: dq of queries r0 .. r0 + 15 (query c of this lane)
     const f32x4 qv = Qs[ri * 4 + g], gv = dOs[ri * 4 + g];
     const float scale2 = scale * ATT_LOG2E;
     const float lq = Ls[ri], dq_ = Ds[ri];
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};  // dQ^T[d = 4g + r][q = c]
-    for (int k0 = 0; k0 < T; k0 += 16) {
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;  // dQ^T[d = 4g + r][q = c], even / odd tiles
+    auto tile = [&](int k0, f32x4& acc) {
       const int key = min(k0 + c, T - 1);
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       const f32x4 st = mfma4(Ks[key * 4 + g], qv, z);   // S^T[key = k0 + 4g + r][q = c]
@@ -256,14 +259,20 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
         const int kk = min(k0 + 4 * g + s2, T - 1);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Kf[kk * 16 + c], ds[s2], acc, 0, 0, 0);
       }
+    };
+    int k0 = 0;
+    for (; k0 + 16 < T; k0 += 32) {
+      tile(k0, acc0);
+      tile(k0 + 16, acc1);
     }
-    if (r0 + c < T) *(f32x4*)(dqkv + ((long)b * T + r0 + c) * ld + h * 16 + g * 4) = acc * scale;
-  }
-  {  // pass 2: dk, dv of keys r0 .. r0 + 15 (key c of this lane)
+    if (k0 < T) tile(k0, acc0);
+    if (r0 + c < T) *(f32x4*)(dqkv + ((long)b * T + r0 + c) * ld + h * 16 + g * 4) = (acc0 + acc1) * scale;
+  } else {  // pass 2: dk, dv of keys r0 .. r0 + 15 (key c of this lane)
     const f32x4 kv = Ks[ri * 4 + g], vv = Vs[ri * 4 + g];
     const float scale2 = scale * ATT_LOG2E;
-    f32x4 adk = {0.f, 0.f, 0.f, 0.f}, adv = {0.f, 0.f, 0.f, 0.f};  // dK^T / dV^T [d = 4g + r][key = c]
-    for (int q0 = 0; q0 < T; q0 += 16) {
+    // dK^T / dV^T [d = 4g + r][key = c], even / odd query tiles
+    f32x4 adk0 = {0.f, 0.f, 0.f, 0.f}, adk1 = adk0, adv0 = adk0, adv1 = adk0;
+    auto tile = [&](int q0, f32x4& adk, f32x4& adv) {
       const int qq = min(q0 + c, T - 1);
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       const f32x4 sm = mfma4(Qs[qq * 4 + g], kv, z);    // S[q = q0 + 4g + r][key = c]
@@ -284,11 +293,17 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
         adv = __builtin_amdgcn_mfma_f32_16x16x4f32(dOf[qk * 16 + c], pr[s2], adv, 0, 0, 0);
         adk = __builtin_amdgcn_mfma_f32_16x16x4f32(Qf[qk * 16 + c], ds[s2], adk, 0, 0, 0);
       }
+    };
+    int q0 = 0;
+    for (; q0 + 16 < T; q0 += 32) {
+      tile(q0, adk0, adv0);
+      tile(q0 + 16, adk1, adv1);
     }
+    if (q0 < T) tile(q0, adk0, adv0);
     if (r0 + c < T) {
       float* w = dqkv + ((long)b * T + r0 + c) * ld + h * 16 + g * 4;
-      *(f32x4*)(w + H * 16) = adk * scale;
-      *(f32x4*)(w + 2 * H * 16) = adv;
+      *(f32x4*)(w + H * 16) = (adk0 + adk1) * scale;
+      *(f32x4*)(w + 2 * H * 16) = adv0 + adv1;
     }
   }
 }
@@ -436,7 +451,7 @@ VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale,
 VC_API int vc_s2eft_attn_bwd(int B, int T, int H, const float* qkv, const float* out, const float* dout,
                              const float* lse, float scale, float* dqkv, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_bwd, dim3(B * H), dim3(64 * ((T + 15) / 16)), 4 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
+  hipLaunchKernelGGL(attn_bwd, dim3(B * H, 2), dim3(64 * ((T + 15) / 16)), 4 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
                      dout, lse, scale, dqkv);
   VC_CHECK_LAUNCH();
   return VC_OK;
