@@ -181,6 +181,12 @@ VC_API int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, cons
 VC_API int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,
                                 const float* wt, float beta, float* dx, long lddx, float* ws, long ws_floats,
                                 hipStream_t stream);
+/* train-mode BatchNorm(x) (statistics as vc_bn_stats_ex: save_* and running stats written) followed by
+ * vc_im2col3x3 of the normalised x, the statistics' final reduction done inside the im2col launch
+ * (ms_conv_bn_relu's BN -> conv3x3, Mutimodality_Mamba7.py:1035-1048); bit-identical to the two calls. */
+VC_API int vc_bn_im2col3x3(int B, int H, int W, int C, const float* x, float eps, float momentum, float* save_mean,
+                           float* save_invstd, float* run_mean, float* run_var, const float* bn_w, const float* bn_b,
+                           float* col, float* ws, long ws_floats, hipStream_t stream);
 /* gradient of vc_im2col3x3 w.r.t. its (post-BN) input, gather form: dx [B,H,W,C] overwritten */
 VC_API int vc_col2im3x3(int B, int H, int W, int C, const float* dcol, float* dx, hipStream_t stream);
 

@@ -560,3 +560,32 @@ def test_im2col_col2im_lds_forms(L, B, H, C, monkeypatch):
     ref_dx = F.fold(dcol.double().view(B, OH * OH, 9 * C).permute(0, 2, 1), (H, H), 3)
     ref_dx = ref_dx.permute(0, 2, 3, 1).reshape(B * H * H, C)
     assert rel_err(outs[0][1].cpu().numpy(), ref_dx.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("B,H,C", [(64, 9, 144), (64, 7, 256), (3, 11, 64), (2, 5, 70), (1, 33, 16)])
+def test_bn_im2col_matches_stats_then_im2col(L, B, H, C):
+    """vc_bn_im2col3x3 (the BatchNorm statistics' final reduction inside the im2col launch) = train-mode
+    vc_bn_stats_ex + vc_im2col3x3 bit for bit: save_mean / save_invstd, the running statistics and the
+    col matrix; H = 33 exceeds the LDS budget and takes the three launches."""
+    OH = H - 2
+    x = (rnd(B * H * H, C, seed=81, scale=2.0) + 3.0).to(DEV)
+    w, b = rnd(C, seed=82).to(DEV), rnd(C, seed=83).to(DEV)
+    outs = []
+    for fused in (True, False):
+        sm, si = torch.full((C,), float("nan"), device=DEV), torch.full((C,), float("nan"), device=DEV)
+        rm, rv = torch.full((C,), 0.25, device=DEV), torch.full((C,), 1.5, device=DEV)
+        col = torch.full((B * OH * OH, 9 * C), float("nan"), device=DEV)
+        ws = torch.empty(1 << 22, device=DEV)
+        if fused:
+            assert L.vc_bn_im2col3x3(B, H, H, C, P(x), 1e-5, 0.1, P(sm), P(si), P(rm), P(rv), P(w), P(b), P(col),
+                                     P(ws), ws.numel(), S()) == 0
+        else:
+            assert L.vc_bn_stats_ex(1, B * H * H, C, P(x), C, 1e-5, 0.1, P(sm), P(si), P(rm), P(rv), P(ws),
+                                    ws.numel(), None, 0, S()) == 0
+            assert L.vc_im2col3x3(B, H, H, C, P(x), P(sm), P(si), P(w), P(b), P(col), S()) == 0
+        torch.cuda.synchronize()
+        outs.append((sm, si, rm, rv, col))
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+    xd = x.double()
+    assert rel_err(outs[0][0].cpu().numpy(), xd.mean(0).cpu().numpy()) < 1e-6

@@ -527,6 +527,105 @@ int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
   return rows_per;
 }
 
+
+// Train-mode BatchNorm in front of a 3x3 valid conv, its statistics finished inside the im2col that
+// applies it (the bn_stats_final launch folded in): block = (sample, 32-channel chunk) as im2col3x3_lds
+// in conv.hip.  Each block reduces its channels' [P][2][C] partials in bn_part_sums' order (lane l sums
+// p = l, l + BN_RL, ... in increasing p, then the lanes in order: the same fp64 operations, so mean /
+// invstd are bit-identical to vc_bn_stats'), the sample-0 blocks write save_* and the running stats,
+// and the chunk is staged BN-applied in LDS and written as col rows.
+constexpr int IBS_CC = 32, IBS_T = 64 * BN_RL / 2, IBS_W = IBS_T / 64, IBS_JK = (9 * IBS_CC + 63) / 64;
+static_assert(IBS_T == IBS_CC * BN_RL, "one thread per (channel, partial lane)");
+
+__global__ __launch_bounds__(IBS_T) void im2col3x3_bnstats(int nchunk, int H, int W, int C, long M, int P,
+                                                          const double* __restrict__ part, float eps,
+                                                          float momentum, float* __restrict__ save_mean,
+                                                          float* __restrict__ save_invstd,
+                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                          const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ b, float* __restrict__ col) {
+  extern __shared__ float img[];   // [H*W][IBS_CC]
+  __shared__ double shr[2][BN_RL][IBS_CC];
+  __shared__ float scs[IBS_CC], shs[IBS_CC];
+  const int bb = blockIdx.x / nchunk, c0 = (blockIdx.x - bb * nchunk) * IBS_CC, nc = min(IBS_CC, C - c0);
+  const int OW = W - 2, S = (H - 2) * OW, HW = H * W;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = threadIdx.x & (IBS_CC - 1), pl = threadIdx.x / IBS_CC;
+  {
+    double s1 = 0.0, s2 = 0.0;
+    if (c < nc) {
+      const int cg = c0 + c;
+      for (int p0 = pl; p0 < P; p0 += BN_RL * NB) {
+        double a[NB], bq[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int p = p0 + BN_RL * i;
+          a[i] = p < P ? part[(long)p * 2 * C + cg] : 0.0;
+          bq[i] = p < P ? part[(long)p * 2 * C + C + cg] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          if (p0 + BN_RL * i < P) {
+            s1 += a[i];
+            s2 += bq[i];
+          }
+      }
+    }
+    shr[0][pl][c] = s1;
+    shr[1][pl][c] = s2;
+  }
+  __syncthreads();
+  if (pl == 0 && c < nc) {
+    double t1 = shr[0][0][c], t2 = shr[1][0][c];
+#pragma unroll
+    for (int l = 1; l < BN_RL; ++l) {
+      t1 += shr[0][l][c];
+      t2 += shr[1][l][c];
+    }
+    float mf, isf;
+    bn_stats_from_sums(t1, t2, c0 + c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean, run_var,
+                       bb == 0);
+    const float sc = isf * w[c0 + c];
+    scs[c] = sc;
+    shs[c] = b[c0 + c] - mf * sc;
+  }
+  __syncthreads();
+  {   // stage the chunk BN-applied: thread -> (pixel, channel c)
+    const float sc = c < nc ? scs[c] : 1.f, sh = c < nc ? shs[c] : 0.f;
+    const float* xb = x + (long)bb * HW * C + c0 + c;
+    constexpr int PP = IBS_T / IBS_CC, NBP = 8;
+    for (int p0 = pl; p0 < HW; p0 += PP * NBP) {
+      float v[NBP];
+#pragma unroll
+      for (int k = 0; k < NBP; ++k) {
+        const int p = p0 + k * PP;
+        v[k] = (p < HW && c < nc) ? xb[(long)p * C] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < NBP; ++k) {
+        const int p = p0 + k * PP;
+        if (p < HW) img[p * IBS_CC + c] = v[k] * sc + sh;
+      }
+    }
+  }
+  __syncthreads();
+  const int seg = 9 * nc;
+  int off[IBS_JK];
+#pragma unroll
+  for (int k = 0; k < IBS_JK; ++k) {
+    const int j = lane + 64 * k, cc = j / 9, t = j - 9 * cc, kh = t / 3, kw = t - 3 * kh;
+    off[k] = j < seg ? (kh * W + kw) * IBS_CC + cc : -1;
+  }
+  float* cb = col + (long)bb * S * 9 * C + 9 * c0;
+  for (int m = wave; m < S; m += IBS_W) {
+    const int oh = m / OW, ow = m - oh * OW, base = (oh * W + ow) * IBS_CC;
+    float* row = cb + (long)m * 9 * C;
+#pragma unroll
+    for (int k = 0; k < IBS_JK; ++k)
+      if (off[k] >= 0) row[lane + 64 * k] = img[base + off[k]];
+  }
+}
+
 }  // namespace
 
 VC_EXPORT int vc_layernorm_fwd(int R, int C, const float* x, long ldx, const float* w, const float* b, float eps,
@@ -749,4 +848,38 @@ VC_EXPORT int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, co
                         long ws_floats, hipStream_t stream) {
   return vc_bn_bwd_ex(train, M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, w, dx, lddx, beta_dx, dw, db,
                       beta_w, ws, ws_floats, nullptr, 0, stream);
+}
+
+// Train-mode BatchNorm(x) -> im2col for a 3x3 valid conv, the statistics' final reduction inside the
+// im2col launch: vc_bn_stats_ex (train) + vc_im2col3x3 with the same save_* / running-stat / col
+// results, bit for bit, in two launches instead of three.  Falls back to the three launches where the
+// chunk does not fit the LDS budget.
+VC_EXPORT int vc_bn_im2col3x3(int B, int H, int W, int C, const float* x, float eps, float momentum, float* save_mean,
+                              float* save_invstd, float* run_mean, float* run_var, const float* bn_w,
+                              const float* bn_b, float* col, float* ws, long ws_floats, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && H >= 3 && W >= 3 && C > 0 && ((uintptr_t)ws & 7) == 0);
+  const long M = (long)B * H * W;
+  VC_REQUIRE(M < (1L << 31));
+  VC_REQUIRE_I32((long)B * (H - 2) * (W - 2) * C * 9);
+  const long S = (long)(H - 2) * (W - 2);
+  const char* e = getenv("VITCNN_BN_IM2COL");   // "0": the three launches (measurement switch, read per call)
+  if (S * 9 * IBS_CC * 4 > 65536 || (e && atoi(e) == 0)) {
+    int rc = vc_bn_stats_ex(1, M, C, x, C, eps, momentum, save_mean, save_invstd, run_mean, run_var, ws, ws_floats,
+                            nullptr, 0, stream);
+    if (rc) return rc;
+    return vc_im2col3x3(B, H, W, C, x, save_mean, save_invstd, bn_w, bn_b, col, stream);
+  }
+  double* wsd = reinterpret_cast<double*>(ws);
+  const int rows_per = bn_rows_per(M, C, ws_floats / 2, 0);
+  const int P = vc_cdiv(M, rows_per);
+  VC_REQUIRE((long)P * C * 2 <= ws_floats / 2 && P <= 65535);
+  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, (long)C, rows_per,
+                     wsd, (unsigned int*)nullptr, eps, momentum, save_mean, save_invstd, run_mean, run_var);
+  VC_CHECK_LAUNCH();
+  const int nchunk = vc_cdiv(C, IBS_CC);
+  VC_REQUIRE_I32((long)B * nchunk);
+  hipLaunchKernelGGL(im2col3x3_bnstats, dim3(B * nchunk), dim3(IBS_T), sizeof(float) * H * W * IBS_CC, stream, nchunk,
+                     H, W, C, M, P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, x, bn_w, bn_b, col);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
 }

@@ -624,6 +624,17 @@ class _Program:
         """ms_conv_bn_relu: BN(X) -> conv3x3 valid (+bias) -> ReLU: vc_im2col3x3 (BN affine fused) +
         vc_gemm, or the implicit GEMM vc_conv3x3_fwd (VITCNN_IMPLICIT_CONV=1, fp32)."""
         B, S = self.B, (H - 2) * (H - 2)
+        if self.train and not self.implicit_conv:
+            # statistics partials + (final reduction, BN apply, im2col) in one launch: vc_bn_im2col3x3
+            tag, ws = pfx + ".bn", self.ws
+            col = ws.f(pfx + ".col", B * S * 9 * Cin)
+            self.L.vc_bn_im2col3x3(B, H, H, Cin, X, BN_EPS, BN_MOM, ws.f(tag + ".bm", Cin), ws.f(tag + ".bi", Cin),
+                                   self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"],
+                                   self.P[tag + ".weight"], self.P[tag + ".bias"], col, self.scr_p, self.scr_n, self.s)
+            out = ws.f(pfx + ".out", B * S * Cout)
+            self.mm_nt(B * S, Cout, 9 * Cin, col, 9 * Cin, self.P[pfx + ".conv.weight"], 9 * Cin, out, Cout,
+                       bias=self.P[pfx + ".conv.bias"], relu=1)
+            return out
         mean, inv = self.bn_stats(pfx + ".bn", X, Cin, B * H * H, Cin, pfx + ".bn")
         if self.implicit_conv:
             out = self.ws.f(pfx + ".out", B * S * Cout)
