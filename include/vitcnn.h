@@ -357,6 +357,12 @@ VC_API int vc_cat2_bwd(long M, int C1, int C2, const float* dout, int exchange, 
 VC_API int vc_glf_combine_fwd(long M, int C, const float* w_pre, const float* bn_mean, const float* bn_invstd,
                               const float* bn_w, const float* bn_b, const float* fc, const float* fl, float* out,
                               hipStream_t stream);
+/* train-mode BatchNorm statistics of w_pre (as vc_bn_stats_ex: save_* and running stats written) +
+ * vc_glf_combine_fwd, the statistics' final reduction inside the combine launch */
+VC_API int vc_bn_glf_combine(long M, int C, const float* w_pre, float eps, float momentum, float* save_mean,
+                             float* save_invstd, float* run_mean, float* run_var, const float* bn_w, const float* bn_b,
+                             const float* fc, const float* fl, float* out, float* ws, long ws_floats,
+                             hipStream_t stream);
 /* out = beta*out + a (+ b) over [M, C] strided rows */
 VC_API int vc_add2_2d(long M, int C, const float* a, long lda, const float* b, long ldb, float* out, long ldo,
                       float beta, hipStream_t stream);

@@ -589,3 +589,29 @@ def test_bn_im2col_matches_stats_then_im2col(L, B, H, C):
         assert torch.equal(a_, b_)
     xd = x.double()
     assert rel_err(outs[0][0].cpu().numpy(), xd.mean(0).cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("M,C", [(5184, 128), (3136, 128), (100, 72)])
+def test_bn_glf_combine_matches_stats_then_combine(L, M, C):
+    """vc_bn_glf_combine (BN(W y) statistics finished inside the GLfusion combine) = train-mode
+    vc_bn_stats_ex + vc_glf_combine_fwd bit for bit (save_*, running statistics, the [M, 2C] output)."""
+    wp = (rnd(M, C, seed=91, scale=0.5) + 1.0).to(DEV)
+    fc, fl = rnd(M, C, seed=92).to(DEV), rnd(M, C, seed=93).to(DEV)
+    g, bt = rnd(C, seed=94).to(DEV), rnd(C, seed=95).to(DEV)
+    outs = []
+    for fused in (True, False):
+        sm, si = torch.full((C,), float("nan"), device=DEV), torch.full((C,), float("nan"), device=DEV)
+        rm, rv = torch.full((C,), 0.25, device=DEV), torch.full((C,), 1.5, device=DEV)
+        out = torch.full((M, 2 * C), float("nan"), device=DEV)
+        ws = torch.empty(1 << 22, device=DEV)
+        if fused:
+            assert L.vc_bn_glf_combine(M, C, P(wp), 1e-5, 0.1, P(sm), P(si), P(rm), P(rv), P(g), P(bt), P(fc), P(fl),
+                                       P(out), P(ws), ws.numel(), S()) == 0
+        else:
+            assert L.vc_bn_stats_ex(1, M, C, P(wp), C, 1e-5, 0.1, P(sm), P(si), P(rm), P(rv), P(ws), ws.numel(),
+                                    None, 0, S()) == 0
+            assert L.vc_glf_combine_fwd(M, C, P(wp), P(sm), P(si), P(g), P(bt), P(fc), P(fl), P(out), S()) == 0
+        torch.cuda.synchronize()
+        outs.append((sm, si, rm, rv, out))
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)

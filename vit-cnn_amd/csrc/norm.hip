@@ -528,6 +528,50 @@ int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
 }
 
 
+// GLfusionBlock's NonLocal output BN(W y) combined with the two branches (vc_glf_combine_fwd's
+// arithmetic, Mutimodality_Mamba7.py:154-156, :1112-1115), the BN statistics' final reduction inside the
+// launch as in bn_apply_stats: out [M, 2C] = [ (BN(w_pre) + fc) + fl | fl + fc ].
+__global__ __launch_bounds__(BN_T) void glf_combine_stats(int M, int C, const float* __restrict__ wpre, int P,
+                                                         const double* __restrict__ part, float eps, float momentum,
+                                                         float* __restrict__ save_mean,
+                                                         float* __restrict__ save_invstd,
+                                                         float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                         const float* __restrict__ gam, const float* __restrict__ bet,
+                                                         const float* __restrict__ fc, const float* __restrict__ fl,
+                                                         float* __restrict__ out, int rows_per_block) {
+  __shared__ double tot[2][64];
+  bn_part_sums(P, C, part, blockIdx.x, tot);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  if (c >= C) return;
+  float mf, isf;
+  bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, wpre, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
+                     run_var, blockIdx.y == 0 && rl == 0);
+  const float g = gam[c], bt = bet[c];
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min((long)M, r0 + rows_per_block);
+  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {
+    float wv[NB], zv[NB], xv[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const long r = rb + BN_RL * i;
+      const bool ok = r < r1;
+      wv[i] = ok ? wpre[r * C + c] : 0.f;
+      zv[i] = ok ? fc[r * C + c] : 0.f;
+      xv[i] = ok ? fl[r * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const long r = rb + BN_RL * i;
+      if (r < r1) {
+        const float wy = (wv[i] - mf) * isf * g + bt;
+        out[r * 2 * C + c] = (wy + zv[i]) + xv[i];
+        out[r * 2 * C + C + c] = xv[i] + zv[i];
+      }
+    }
+  }
+}
+
 // Train-mode BatchNorm in front of a 3x3 valid conv, its statistics finished inside the im2col that
 // applies it (the bn_stats_final launch folded in): block = (sample, 32-channel chunk) as im2col3x3_lds
 // in conv.hip.  Each block reduces its channels' [P][2][C] partials in bn_part_sums' order (lane l sums
@@ -880,6 +924,35 @@ VC_EXPORT int vc_bn_im2col3x3(int B, int H, int W, int C, const float* x, float 
   VC_REQUIRE_I32((long)B * nchunk);
   hipLaunchKernelGGL(im2col3x3_bnstats, dim3(B * nchunk), dim3(IBS_T), sizeof(float) * H * W * IBS_CC, stream, nchunk,
                      H, W, C, M, P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, x, bn_w, bn_b, col);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// train-mode vc_bn_stats_ex of w_pre + vc_glf_combine_fwd in two launches instead of three (the
+// statistics' final reduction inside the combine); save_* / running stats as vc_bn_stats_ex writes them
+VC_EXPORT int vc_bn_glf_combine(long M, int C, const float* w_pre, float eps, float momentum, float* save_mean,
+                                float* save_invstd, float* run_mean, float* run_var, const float* bn_w,
+                                const float* bn_b, const float* fc, const float* fl, float* out, float* ws,
+                                long ws_floats, hipStream_t stream) {
+  VC_REQUIRE(M > 0 && M < (1L << 31) && C > 0 && ((uintptr_t)ws & 7) == 0);
+  VC_REQUIRE_I32(M * 2 * C);
+  const char* e = getenv("VITCNN_BN_GLF");   // "0": the three launches (measurement switch, read per call)
+  if (e && atoi(e) == 0) {
+    int rc = vc_bn_stats_ex(1, M, C, w_pre, C, eps, momentum, save_mean, save_invstd, run_mean, run_var, ws,
+                            ws_floats, nullptr, 0, stream);
+    if (rc) return rc;
+    return vc_glf_combine_fwd(M, C, w_pre, save_mean, save_invstd, bn_w, bn_b, fc, fl, out, stream);
+  }
+  double* wsd = reinterpret_cast<double*>(ws);
+  const int rows_per = bn_rows_per(M, C, ws_floats / 2, 0);
+  const int P = vc_cdiv(M, rows_per);
+  VC_REQUIRE((long)P * C * 2 <= ws_floats / 2 && P <= 65535);
+  hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, w_pre, (long)C, rows_per,
+                     wsd, (unsigned int*)nullptr, eps, momentum, save_mean, save_invstd, run_mean, run_var);
+  VC_CHECK_LAUNCH();
+  const int rpb = BN_APPLY_ROWS;
+  hipLaunchKernelGGL(glf_combine_stats, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, (int)M, C, w_pre,
+                     P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, bn_w, bn_b, fc, fl, out, rpb);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

@@ -803,10 +803,17 @@ class _Program:
         # spread small against the mean, so bf16 operands here alone move the logits by 3.3e-2 of their
         # scale (tools/bf16_sites.py: 5.8e-2 -> 2.5e-2 deviation, argmax 61/64 -> 64/64); a K = 128 GEMM
         self.mm_nt(M, Cout, Ci, O, Ci, P[nl + ".W.0.weight"], Ci, WP, Cout, bias=P[nl + ".W.0.bias"], exact=True)
-        wm, wi = self.bn_stats(nl + ".W.1", WP, Cout, M, Cout, pfx + ".W1")
         CAT1 = ws.f(pfx + ".CAT1", M * 2 * Cout)
-        self.L.vc_glf_combine_fwd(M, Cout, WP, wm, wi, P[nl + ".W.1.weight"], P[nl + ".W.1.bias"], Fc, Fl, CAT1,
-                                  self.s)
+        if self.train:   # BN(W y) statistics finished inside the combine launch
+            tag = pfx + ".W1"
+            self.L.vc_bn_glf_combine(M, Cout, WP, BN_EPS, BN_MOM, ws.f(tag + ".bm", Cout), ws.f(tag + ".bi", Cout),
+                                     self.BUF[nl + ".W.1.running_mean"], self.BUF[nl + ".W.1.running_var"],
+                                     P[nl + ".W.1.weight"], P[nl + ".W.1.bias"], Fc, Fl, CAT1, self.scr_p, self.scr_n,
+                                     self.s)
+        else:
+            wm, wi = self.bn_stats(nl + ".W.1", WP, Cout, M, Cout, pfx + ".W1")
+            self.L.vc_glf_combine_fwd(M, Cout, WP, wm, wi, P[nl + ".W.1.weight"], P[nl + ".W.1.bias"], Fc, Fl, CAT1,
+                                      self.s)
         return self.conv1x1_bn_relu(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout)
 
     def forward(self, hsi, lidar):
