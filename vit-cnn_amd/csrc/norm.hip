@@ -522,7 +522,11 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
 constexpr int BN_APPLY_ROWS = 64;   // rows per block of the fused (partials-reducing) apply kernels
 
 int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
-  int rows_per = std::max<long>(32, (M + 63) / 64);
+  static const int pcap = [] {   // VITCNN_BN_PCAP: most partials per channel (measurement switch)
+    const char* e = getenv("VITCNN_BN_PCAP");
+    return e ? std::max(16, std::min(1024, atoi(e))) : 64;
+  }();
+  int rows_per = std::max<long>(32, (M + pcap - 1) / pcap);
   while ((long)vc_cdiv(M, rows_per) * 2 * C + reserve_doubles > ws_doubles && rows_per < (1 << 29)) rows_per *= 2;
   return rows_per;
 }
