@@ -63,18 +63,29 @@ VC_API int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha, 
 
 /* Measurement hook: force the tile (bm, bn in {64, 128}), split-K slice count, prefetch depth
  * (pf in {1, 2}) and combine path (combine: 1 in-launch, 0 separate reduce kernel) of the following
- * vc_gemm / vc_gemm_ex calls; 0 (-1 for combine) restores the automatic choice.  Process-global
- * state for tuning tools (tools/gemm_sweep.py), not for concurrent use. */
+ * vc_gemm / vc_gemm_ex calls; 0 (-1 for combine) restores the automatic choice.  Only the probe
+ * library (libvitcnn_probe.so, `make probe`; tools/gemm_sweep.py) keeps this state; the product
+ * library keeps none and accepts only the automatic configuration (0, 0, 0, 0, -1). */
 VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
 
-/* Grouped launches: the fp32 (k-major kernel) GEMMs issued through vc_gemm / vc_gemm_ex on `stream`
- * between vc_gemm_group_begin and vc_gemm_group_end are recorded and launched together as one grid
- * (up to 8 per launch) plus one grouped split-K reduce -- a horizontal fusion for independent
- * products (a layer's weight and data gradients, parallel branches).  The problems of a group must
- * not depend on each other; each takes its own slice of the workspace and arrival counters passed
- * to it.  Other GEMMs (bf16, long-K) and other streams launch at once.  Host-thread state. */
-VC_API int vc_gemm_group_begin(hipStream_t stream);
-VC_API int vc_gemm_group_end(void);
+/* Grouped launches: a horizontal fusion of independent products (a layer's weight and data
+ * gradients, parallel branches).  `group` is caller-owned host memory of VC_GEMM_GROUP_BYTES bytes
+ * (8-byte aligned) holding the group's state -- the library keeps none, so distinct groups (one per
+ * stream / thread) are independent and every entry point stays reentrant.  vc_gemm_group_begin
+ * opens it for `stream`; vc_gemm_group_add takes vc_gemm_ex's arguments (minus the stream): the fp32
+ * k-major problems are recorded, anything else (bf16 operands, long K) launches at once on the
+ * group's stream; vc_gemm_group_end launches the recorded problems as one grid (up to 8 per launch)
+ * plus one grouped split-K reduce.  The problems must not depend on each other; each takes its own
+ * slice of the workspace and arrival counters passed to it.  Misuse (add / end on a group that is
+ * not open) returns 1. */
+#define VC_GEMM_GROUP_BYTES 16384
+VC_API int vc_gemm_group_begin(void* group, hipStream_t stream);
+VC_API int vc_gemm_group_add(void* group, int transA, int transB, int M, int N, int K, float alpha,
+                             const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                             float beta, float* C, long ldc, long strideC, int batch, const float* bias,
+                             const float* addend, long add_ld, int add_mod, int flags, float* bias_grad,
+                             float* ws, long ws_floats, unsigned int* tile_counters, int n_counters);
+VC_API int vc_gemm_group_end(void* group);
 
 /* out[c] = beta*out[c] + sum_r X[r*ldx + c]  (bias gradients; fixed-order two-stage) */
 VC_API int vc_colsum(int R, int C, const float* X, long ldx, float* out, float beta,

@@ -2,6 +2,8 @@
 
 fp32 kernels, tolerance 1e-4 relative to the output's max |value| unless stated.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -19,6 +21,19 @@ def L():
         pytest.skip("no GPU")
     from vitcnn_amd._lib import lib
     return lib()
+
+
+@pytest.fixture(scope="module")
+def probe():
+    """libvitcnn_probe.so: the same kernels with the measurement knobs read from VITCNN_* (tests that
+    compare two bit-identical forms in one process); the product library reads no environment"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vitcnn_amd._lib import probe_lib
+    return probe_lib()
+
+
+GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES
 
 
 @pytest.fixture(scope="module")
@@ -343,20 +358,25 @@ def test_gemm_group_is_bit_identical(L, ws, n):
         A = (rnd(batch, K, M, seed=50 + i) if ta else rnd(batch, M, K, seed=50 + i)).to(DEV)
         B = (rnd(batch, N, K, seed=70 + i) if tb else rnd(batch, K, N, seed=70 + i)).to(DEV)
         ins.append((A, B))
+    grp = ctypes.create_string_buffer(GROUP_BYTES)
     for grouped in (False, True, True):
         res = []
         if grouped:
-            L.vc_gemm_group_begin(S())
+            L.vc_gemm_group_begin(ctypes.addressof(grp), S())
         for i, (ta, tb, M, N, K, batch, bg, beta) in enumerate(probs):
             A, B = ins[i]
             C = rnd(batch, M, N, seed=90 + i).to(DEV)
             bgr = torch.full((M,), 0.25, device=DEV) if bg else None
-            L.vc_gemm_ex(ta, tb, M, N, K, 1.0, P(A), M if ta else K, A[0].numel(), P(B), K if tb else N, B[0].numel(),
-                         beta, P(C), N, C[0].numel(), batch, None, None, 0, 0, F_LEGACY, P(bgr), P(ws), ws.numel(),
-                         P(cnt), cnt.numel(), S())
+            args = (ta, tb, M, N, K, 1.0, P(A), M if ta else K, A[0].numel(), P(B), K if tb else N, B[0].numel(),
+                    beta, P(C), N, C[0].numel(), batch, None, None, 0, 0, F_LEGACY, P(bgr), P(ws), ws.numel(),
+                    P(cnt), cnt.numel())
+            if grouped:
+                L.vc_gemm_group_add(ctypes.addressof(grp), *args)
+            else:
+                L.vc_gemm_ex(*args, S())
             res.append((C, bgr))
         if grouped:
-            L.vc_gemm_group_end()
+            L.vc_gemm_group_end(ctypes.addressof(grp))
         torch.cuda.synchronize()
         outs.append([(c.cpu(), b.cpu() if b is not None else None) for c, b in res])
         assert int(cnt.abs().sum()) == 0
@@ -373,12 +393,21 @@ def test_gemm_group_is_bit_identical(L, ws, n):
 
 
 def test_gemm_group_misuse_raises(L):
-    L.vc_gemm_group_begin(S())
+    """the group state is the caller's: ending / adding to a group that is not open is an error, and two
+    groups are independent (no library state)"""
+    g1, g2 = ctypes.create_string_buffer(GROUP_BYTES), ctypes.create_string_buffer(GROUP_BYTES)
+    a1, a2 = ctypes.addressof(g1), ctypes.addressof(g2)
     with pytest.raises(RuntimeError):
-        L.vc_gemm_group_begin(S())
-    L.vc_gemm_group_end()
+        L.vc_gemm_group_end(a1)
+    L.vc_gemm_group_begin(a1, S())
+    L.vc_gemm_group_begin(a2, S())
+    L.vc_gemm_group_end(a2)
+    L.vc_gemm_group_end(a1)
     with pytest.raises(RuntimeError):
-        L.vc_gemm_group_end()
+        L.vc_gemm_group_end(a1)
+    with pytest.raises(RuntimeError):
+        L.vc_gemm_group_add(a1, 0, 0, 4, 4, 4, 1.0, None, 4, 0, None, 4, 0, 0.0, None, 4, 0, 1, None, None, 0, 0, 0,
+                            None, None, 0, None, 0)
 
 
 @pytest.mark.parametrize("kern", KERNELS)
@@ -533,7 +562,7 @@ def test_add2_dup(L):
 
 
 @pytest.mark.parametrize("B,H,C", [(64, 9, 144), (64, 7, 256), (3, 11, 64), (2, 5, 70), (1, 33, 16)])
-def test_im2col_col2im_lds_forms(L, B, H, C, monkeypatch):
+def test_im2col_col2im_lds_forms(probe, B, H, C, monkeypatch):
     """vc_im2col3x3 (BN affine folded) / vc_col2im3x3: the LDS-staged forms (chunks of <= 32 channels per
     block) equal the per-thread forms (VITCNN_C2I_LDS=0) bit for bit and torch's unfold / fold; H = 33
     exceeds the LDS budget and keeps the per-thread kernels."""
@@ -548,8 +577,8 @@ def test_im2col_col2im_lds_forms(L, B, H, C, monkeypatch):
         monkeypatch.setenv("VITCNN_C2I_LDS", lds)
         col = torch.full((B * OH * OH, 9 * C), float("nan"), device=DEV)
         dx = torch.full((B * H * H, C), float("nan"), device=DEV)
-        assert L.vc_im2col3x3(B, H, H, C, P(x), P(mean), P(inv), P(w), P(b), P(col), S()) == 0
-        assert L.vc_col2im3x3(B, H, H, C, P(dcol), P(dx), S()) == 0
+        assert probe.vc_im2col3x3(B, H, H, C, P(x), P(mean), P(inv), P(w), P(b), P(col), S()) == 0
+        assert probe.vc_col2im3x3(B, H, H, C, P(dcol), P(dx), S()) == 0
         torch.cuda.synchronize()
         outs.append((col, dx))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

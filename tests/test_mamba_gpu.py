@@ -218,12 +218,13 @@ def test_mamba_kernels_vs_float64(L, D, E, use_ckpt):
         lib.vc_mamba_scan_bwd_params(B, D, ndir, P(gate_d), P(sp), P(dA2), P(dD2), P(dG2), P(ws), ws.numel(), s)
         torch.cuda.synchronize()
         assert torch.equal(dA2.cpu(), dA.cpu()) and torch.equal(dD2.cpu(), dDs.cpu()) and torch.equal(dG2.cpu(), dG.cpu())
-        # the dB / dC reduce-scatter's two forms (bank-masked DPP adds, default; selects + DPP,
-        # VITCNN_SCAN_SELECT_RS=1) pair the same lanes in the same order: bit-identical outputs
+        # the dB / dC reduce-scatter's two forms (bank-masked DPP adds, default; selects + DPP, knob
+        # SCAN_SELECT_RS=1 of the probe library) pair the same lanes in the same order: bit-identical outputs
         outs = [t.clone() for t in (dU, dDTL, dXD)]
+        from vitcnn_amd._lib import probe_lib
         os.environ["VITCNN_SCAN_SELECT_RS"] = "1"
         try:
-            lib.vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
+            probe_lib().vc_mamba_scan_bwd(B, L, D, R, ndir, P(U), P(XD), P(o32), P(wdt_d), P(bdt_d), P(alog_d), P(dsk_d),
                                   P(gate_d), P(Y), P(dYP), P(CKP), P(dU), P(dDTL), P(dXD), None, None, None, P(sp),
                                   spn, s)
             torch.cuda.synchronize()

@@ -2,6 +2,7 @@
 # A/B of an environment switch on one box: the captured B=64 training step (tools/prof_step.py, K graph
 # replays) with VAR=value for each value in turn, ROUNDS times interleaved.
 # usage: bash tools/ab_env.sh K ROUNDS VAR v1 v2 ...
+export VITCNN_LIB=${VITCNN_LIB:-$(pwd)/vit-cnn_amd/vitcnn_amd/libvitcnn_probe.so}  # measurement knobs: the probe library
 K=$1; ROUNDS=$2; VAR=$3; shift 3
 for r in $(seq 1 $ROUNDS); do
   for v in "$@"; do

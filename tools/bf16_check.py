@@ -12,6 +12,7 @@ import torch  # noqa: E402
 
 from helpers import golden_batch, hash_state_dict, load_npz  # noqa: E402
 from oracle import vitcnn_oracle as O  # noqa: E402
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 from vitcnn_amd import AdamW, CrossEntropyLoss, Multimodality_Mamba, fused_train_step  # noqa: E402
 
 

@@ -11,6 +11,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from helpers import golden_batch, hash_state_dict, load_npz  # noqa: E402
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 from vitcnn_amd import Multimodality_Mamba  # noqa: E402
 import vitcnn_amd.model as M  # noqa: E402
 

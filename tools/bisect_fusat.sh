@@ -3,6 +3,7 @@
 set -o pipefail
 timeout -k 10 300 python -u -m pytest -q --timeout 150 --timeout-method thread tests/test_conv_tap_gpu.py > gpurun_out/tap_bisect.log 2>&1
 echo "tap tests rc=$?"; tail -5 gpurun_out/tap_bisect.log
+export VITCNN_LIB=${VITCNN_LIB:-$(pwd)/vit-cnn_amd/vitcnn_amd/libvitcnn_probe.so}  # measurement knobs: the probe library
 for cfg in "VITCNN_FUSAT_IM2COL=1 VITCNN_FUSAT_SCRATCH_LOG2=26" "VITCNN_TAP_NOSPLIT=1 VITCNN_FUSAT_SCRATCH_LOG2=22" \
            "VITCNN_FUSAT_SCRATCH_LOG2=22" "VITCNN_FUSAT_SCRATCH_LOG2=23"; do
   echo "=== $cfg"

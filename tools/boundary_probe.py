@@ -13,6 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "vit-cnn_amd"))
 import torch  # noqa: E402
 
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 from vitcnn_amd._lib import lib  # noqa: E402
 
 

@@ -11,6 +11,7 @@ import torch  # noqa: E402
 
 from helpers import golden_batch, hash_state_dict  # noqa: E402
 from oracle import vitcnn_oracle as O  # noqa: E402
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 from vitcnn_amd import CrossEntropyLoss, Multimodality_Mamba  # noqa: E402
 
 HOOK = ["hsi_mamba", "token_learner", "bn_conv3_relu", "conv_bn_relu_1x1", "non_local", "layernorm", "fusion"]

@@ -11,6 +11,7 @@ import torch  # noqa: E402
 
 from helpers import golden_batch, hash_state_dict, masked_oracle_step, relu_masks_from_workspace  # noqa: E402
 from oracle import vitcnn_oracle as O  # noqa: E402
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 from vitcnn_amd import CrossEntropyLoss, Multimodality_Mamba  # noqa: E402
 
 

@@ -3,6 +3,7 @@ sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/vit-cnn_amd"); 
 import torch
 from helpers import golden_batch, hash_state_dict
 from oracle import vitcnn_oracle as O
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 from vitcnn_amd import Multimodality_Mamba, CrossEntropyLoss
 sd = hash_state_dict()
 hsi, lidar, target = golden_batch("golden.b4", 4)

@@ -10,6 +10,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "vit-cnn_amd"))
 import torch  # noqa: E402
 
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
+knobs.use_probe()   # vc_gemm_tune: the probe library
 from vitcnn_amd._lib import lib  # noqa: E402
 from vitcnn_amd.fusatnet import FusAtNet  # noqa: E402
 from vitcnn_amd.losses import CrossEntropyLoss  # noqa: E402

@@ -1,4 +1,5 @@
 """GPU probe: which multi-stream capture pattern breaks hipGraph capture end?"""
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 import faulthandler
 import os
 import sys

@@ -5,6 +5,7 @@ import sys
 sys.path.insert(0, "tests"); sys.path.insert(0, "vit-cnn_amd"); sys.path.insert(0, ".")
 import torch
 import test_model_gpu as T
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 from vitcnn_amd._lib import lib
 
 b4 = T.b4._get_wrapped_function()()

@@ -395,12 +395,9 @@ VC_API int vc_maxpool2_bwd(int B, int H, int W, int C, const float* dy, const un
 static bool aligned16(const void* a, const void* b, const void* c) {
   return (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15) == 0;
 }
-// VITCNN_NL_LEGACY (read per call; bit 0 forward, bit 1 backward): the wave-per-row kernels even where
+// knob NL_LEGACY (probe library only; bit 0 forward, bit 1 backward): the wave-per-row kernels even where
 // the MFMA form applies
-static bool nl_legacy(int bit) {
-  const char* e = getenv("VITCNN_NL_LEGACY");
-  return e && ((atoi(e) >> bit) & 1);
-}
+static bool nl_legacy(int bit) { return (vc_knob("VITCNN_NL_LEGACY", 0) >> bit) & 1; }
 
 VC_API int vc_nonlocal_attn_fwd(int B, int S, int P, int Ci, const float* theta, const float* pooled, float* att,
                                 float* o, hipStream_t stream) {

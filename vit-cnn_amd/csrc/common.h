@@ -9,6 +9,22 @@
 
 #define VC_EXPORT extern "C" __attribute__((visibility("default")))
 
+// Measurement knobs: the A/B switches the tools/ probes flip (kernel variants, split policies, phase
+// masks).  The product library (libvitcnn_hip.so, no VC_PROBE) reads no environment and keeps no
+// state between calls: every knob is its compile-time default below, so an entry point's result
+// depends on its arguments only.  `make probe` builds libvitcnn_probe.so with -DVC_PROBE, where
+// vc_knob reads VITCNN_<name> on every call (tests that compare two bit-identical forms in one
+// process, and the tools, load it explicitly).
+#ifdef VC_PROBE
+#include <cstdlib>
+static inline long vc_knob(const char* env, long dflt) {
+  const char* e = getenv(env);
+  return e ? atol(e) : dflt;
+}
+#else
+static inline long vc_knob(const char*, long dflt) { return dflt; }
+#endif
+
 #define VC_OK 0
 #define VC_EINVAL 1  // hipErrorInvalidValue
 

@@ -191,10 +191,10 @@ __global__ __launch_bounds__(C2I_T) void col2im3x3_lds(int nchunk, int H, int W,
 }
 
 // channels per block of the LDS forms (0: the per-thread kernels): the col chunk S x 9 x 32 floats in at
-// most 64 KB of LDS (patches up to 11 x 11); VITCNN_C2I_LDS=0 keeps the per-thread kernels (measurement switch)
+// most 64 KB of LDS (patches up to 11 x 11); knob C2I_LDS=0 keeps the per-thread kernels (probe library:
+// tests compare both forms in one process)
 static int c2i_chunk(int H, int W, int C) {
-  const char* e = getenv("VITCNN_C2I_LDS");   // read per call (tests compare both forms in one process)
-  if (e && atoi(e) == 0) return 0;
+  if (vc_knob("VITCNN_C2I_LDS", 1) == 0) return 0;
   const long S = (long)(H - 2) * (W - 2);
   return S * 9 * C2I_CC * 4 <= 65536 ? C2I_CC : 0;
 }

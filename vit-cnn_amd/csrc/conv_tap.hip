@@ -304,8 +304,7 @@ int launch_tap(TapArgs& a, int grid_n, int grid_m, float* ws, long ws_floats, hi
   // without a ragged second round; slices of >= 4 k-tiles; the slabs must fit the workspace
   const long tiles = (long)grid_n * grid_m;
   int nsplit = 1;
-  static const char* no_split = getenv("VITCNN_TAP_NOSPLIT");
-  if (no_split && atoi(no_split)) ws = nullptr;
+  if (vc_knob("VITCNN_TAP_NOSPLIT", 0)) ws = nullptr;
   if (ws && tiles < 768 && a.nk >= 8) {
     nsplit = (int)std::max<long>(1, std::min<long>(768 / tiles, a.nk / 4));
     while (nsplit > 1 && (long)nsplit * a.M * a.N > ws_floats) --nsplit;

@@ -856,36 +856,31 @@ __global__ __launch_bounds__(256) void splitk_reduce4(GemmArgs g, long nelem, in
 struct G2Tune {
   int bm, bn, nsplit, pf, combine;
 };
+#ifdef VC_PROBE
 static G2Tune g_tune = {0, 0, 0, 0, -1};
+#else
+static constexpr G2Tune g_tune = {0, 0, 0, 0, -1};   // the product library keeps no tuning state
+#endif
 
 VC_EXPORT int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine) {
   VC_REQUIRE((bm == 0 || bm == 64 || bm == 128) && (bn == 0 || bn == 64 || bn == 128));
   VC_REQUIRE(nsplit >= 0 && nsplit <= 4096 && pf >= 0 && pf <= 2 && combine >= -1 && combine <= 1);
+#ifdef VC_PROBE
   g_tune = G2Tune{bm, bn, nsplit, pf, combine};
+#else
+  // product library: only the automatic configuration (the forced ones exist in libvitcnn_probe.so)
+  VC_REQUIRE(bm == 0 && bn == 0 && nsplit == 0 && pf == 0 && combine == -1);
+#endif
   return VC_OK;
 }
 
 // largest per-tile slab volume (bytes) combined in-launch by the last-arriving slice (else a separate
-// reduce kernel); VITCNN_SPLITK_COMBINE overrides it for measurements
-static long g2_combine_limit() {
-  static long v = -1;
-  if (v < 0) {
-    const char* e = getenv("VITCNN_SPLITK_COMBINE");
-    v = e ? atol(e) : 4096;
-  }
-  return v;
-}
+// reduce kernel); knob SPLITK_COMBINE (probe library)
+static long g2_combine_limit() { return vc_knob("VITCNN_SPLITK_COMBINE", 4096); }
 
 // largest per-tile slab volume (bytes) the k-major kernel's last-arriving slice combines in-launch;
-// VITCNN_LEGACY_COMBINE overrides it for measurements
-static long legacy_combine_limit() {
-  static long v = -1;
-  if (v < 0) {
-    const char* e = getenv("VITCNN_LEGACY_COMBINE");
-    v = e ? atol(e) : 4096;
-  }
-  return v;
-}
+// knob LEGACY_COMBINE (probe library)
+static long legacy_combine_limit() { return vc_knob("VITCNN_LEGACY_COMBINE", 4096); }
 
 // the k-major fp32 kernel (LDS [k][row], 16x16x4 f32): launch configuration of one problem
 struct LegacyPlan {
@@ -948,15 +943,8 @@ static LegacyPlan plan_legacy(int transA, int transB, int M, int N, int K, float
 // register sets of staged k-tiles in the k-major kernel: 1.  Deeper sets (bit-identical results) measured
 // slower on the whole step -- PD 1 / 2 / 3 / 4: 2.148 / 2.19 / 2.19 / 2.245 ms (round 3,
 // tools/ab_env.sh, profiles/r03_ab_gemm_pd.log): the extra VGPRs cost more occupancy than the earlier
-// loads save latency.  VITCNN_GEMM_PD=2 selects the two-set build for measurements.
-static int legacy_pd() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("VITCNN_GEMM_PD");
-    v = e ? std::max(1, std::min(2, atoi(e))) : 1;
-  }
-  return v;
-}
+// loads save latency.  Knob GEMM_PD=2 (probe library) selects the two-set build for measurements.
+static int legacy_pd() { return (int)std::max(1L, std::min(2L, vc_knob("VITCNN_GEMM_PD", 1))); }
 
 template <int PD>
 static int launch_plan_pd(const LegacyPlan& pl, hipStream_t stream) {
@@ -988,22 +976,23 @@ static int launch_plan(const LegacyPlan& pl, hipStream_t stream) {
   return legacy_pd() == 2 ? launch_plan_pd<2>(pl, stream) : launch_plan_pd<1>(pl, stream);
 }
 
-// ---- grouped launches (vc_gemm_group_begin / _end): the fp32 k-major problems issued in between
-// on the group's stream are recorded and launched as one gemm_f32_group grid (plus one grouped
-// split-K reduce); each takes its own slice of the workspace and of the arrival counters.
+// ---- grouped launches: the fp32 k-major problems added to a group (vc_gemm_group_add) launch at
+// vc_gemm_group_end as one gemm_f32_group grid (plus one grouped split-K reduce); each takes its own slice
+// of the workspace and of the arrival counters.  The group state lives in caller-owned host memory
+// (VC_GEMM_GROUP_BYTES), so the library keeps none and distinct groups are independent.
 struct GroupState {
-  bool active = false;
-  hipStream_t stream = nullptr;
-  int n = 0;
+  unsigned magic;          // GROUP_MAGIC between begin and end
+  hipStream_t stream;
+  int n;
   LegacyPlan plans[GROUP_MAX];
-  long ws_used = 0;
-  int cnt_used = 0;
-  int err = 0;
+  long ws_used;
+  int cnt_used;
+  int err;
 };
-static thread_local GroupState g_group;
+constexpr unsigned GROUP_MAGIC = 0x56434747u;   // "VCGG"
+static_assert(sizeof(GroupState) <= VC_GEMM_GROUP_BYTES, "VC_GEMM_GROUP_BYTES too small");
 
-static int group_flush() {
-  GroupState& st = g_group;
+static int group_flush(GroupState& st) {
   const int n = st.n;
   st.n = 0;
   st.ws_used = 0;
@@ -1043,22 +1032,29 @@ static int group_flush() {
   return VC_OK;
 }
 
-VC_EXPORT int vc_gemm_group_begin(hipStream_t stream) {
-  VC_REQUIRE(!g_group.active);
-  g_group.active = true;
-  g_group.stream = stream;
-  g_group.n = 0;
-  g_group.ws_used = 0;
-  g_group.cnt_used = 0;
-  g_group.err = 0;
+static GroupState* group_of(void* group) {
+  if (!group || ((uintptr_t)group % alignof(GroupState)) != 0) return nullptr;
+  return reinterpret_cast<GroupState*>(group);
+}
+
+VC_EXPORT int vc_gemm_group_begin(void* group, hipStream_t stream) {
+  GroupState* st = group_of(group);
+  VC_REQUIRE(st);
+  st->magic = GROUP_MAGIC;
+  st->stream = stream;
+  st->n = 0;
+  st->ws_used = 0;
+  st->cnt_used = 0;
+  st->err = 0;
   return VC_OK;
 }
 
-VC_EXPORT int vc_gemm_group_end(void) {
-  VC_REQUIRE(g_group.active);
-  g_group.active = false;
-  const int err = g_group.err;
-  const int rc = group_flush();
+VC_EXPORT int vc_gemm_group_end(void* group) {
+  GroupState* st = group_of(group);
+  VC_REQUIRE(st && st->magic == GROUP_MAGIC);
+  st->magic = 0;
+  const int err = st->err;
+  const int rc = group_flush(*st);
   return err ? err : rc;
 }
 
@@ -1067,28 +1063,51 @@ static int launch_legacy(int transA, int transB, int M, int N, int K, float alph
                          float beta, float* C, long ldc, long strideC, int batch,
                          const float* bias, const float* addend, long add_ld, int add_mod, int flags,
                          float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
-                         int n_counters, hipStream_t stream) {
-  GroupState& st = g_group;
-  if (!st.active || stream != st.stream)
+                         int n_counters, hipStream_t stream, GroupState* st) {
+  if (!st)
     return launch_plan(plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc,
                                    strideC, batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats,
                                    tile_counters, n_counters),
                        stream);
-  if (st.n == GROUP_MAX) {
-    const int rc = group_flush();
+  if (st->n == GROUP_MAX) {
+    const int rc = group_flush(*st);
     if (rc) return rc;
   }
   // this problem's slices of the workspace and the counters follow the earlier problems' slices
-  float* wsp = ws ? ws + st.ws_used : nullptr;
-  const long wsn = ws ? ws_floats - st.ws_used : 0;
-  unsigned int* cp = tile_counters ? tile_counters + st.cnt_used : nullptr;
-  const int cn = tile_counters ? n_counters - st.cnt_used : 0;
+  float* wsp = ws ? ws + st->ws_used : nullptr;
+  const long wsn = ws ? ws_floats - st->ws_used : 0;
+  unsigned int* cp = tile_counters ? tile_counters + st->cnt_used : nullptr;
+  const int cn = tile_counters ? n_counters - st->cnt_used : 0;
   LegacyPlan pl = plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
                               batch, bias, addend, add_ld, add_mod, flags, bias_grad, wsp, wsn, cp, cn);
-  st.ws_used += (pl.ws_floats + 63) / 64 * 64;
-  st.cnt_used += pl.counters;
-  st.plans[st.n++] = pl;
+  st->ws_used += (pl.ws_floats + 63) / 64 * 64;
+  st->cnt_used += pl.counters;
+  st->plans[st->n++] = pl;
   return VC_OK;
+}
+
+static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
+                     const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                     float beta, float* C, long ldc, long strideC, int batch,
+                     const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                     float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                     int n_counters, hipStream_t stream, GroupState* group);
+
+// a problem of the group: the fp32 k-major ones wait for vc_gemm_group_end; any other (bf16 operands,
+// K >= 4096) launches at once on the group's stream
+VC_EXPORT int vc_gemm_group_add(void* group, int transA, int transB, int M, int N, int K, float alpha,
+                                const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                                float beta, float* C, long ldc, long strideC, int batch,
+                                const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                                float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                                int n_counters) {
+  GroupState* st = group_of(group);
+  VC_REQUIRE(st && st->magic == GROUP_MAGIC);
+  const int rc = gemm_impl(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
+                           batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
+                           n_counters, st->stream, st);
+  if (rc && !st->err) st->err = rc;
+  return rc;
 }
 
 VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha,
@@ -1097,6 +1116,17 @@ VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alph
                          const float* bias, const float* addend, long add_ld, int add_mod, int flags,
                          float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
                          int n_counters, hipStream_t stream) {
+  return gemm_impl(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC, batch,
+                   bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters, n_counters, stream,
+                   nullptr);
+}
+
+static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
+                     const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                     float beta, float* C, long ldc, long strideC, int batch,
+                     const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                     float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                     int n_counters, hipStream_t stream, GroupState* group) {
   VC_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1);
   VC_REQUIRE(!bias_grad || batch == 1);
   if (M == 0 || N == 0) return VC_OK;
@@ -1109,7 +1139,7 @@ VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alph
   if (legacy)
     return launch_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
                          batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
-                         n_counters, stream);
+                         n_counters, stream, group);
   Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, flags};
   const int Ne = N + (bias_grad ? 1 : 0);
   const int KT = bf ? 64 : 32;

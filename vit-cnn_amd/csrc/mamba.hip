@@ -1159,10 +1159,9 @@ static int scan_bwd_impl(int B, int L, int D, int R, int ndir, const float* u, c
   VC_REQUIRE(need_a + need_d + need_g + need_ck <= ws_floats);
   const int nw = vc_cdiv(D, 16);
   VC_REQUIRE(nw <= 8);
-  // dB / dC partial combine every rbs segments (VITCNN_SCAN_RBS, default 2), when the LDS still holds
-  // three blocks per CU; else every segment
-  const char* rbs_env = getenv("VITCNN_SCAN_RBS");
-  int rbs = rbs_env ? std::max(1, std::min(4, atoi(rbs_env))) : 2;
+  // dB / dC partial combine every rbs segments (2; knob SCAN_RBS in the probe library), when the LDS still
+  // holds three blocks per CU; else every segment
+  int rbs = (int)std::max(1L, std::min(4L, vc_knob("VITCNN_SCAN_RBS", 2)));
   const long tail_n = fb ? (long)seg_count_h(L) * SCK * 16 + (long)D * R : 0;
   auto lds_bytes = [&](int r) {
     return sizeof(float) * (seq_lds_floats(L, R, nw * 16) + std::max<long>(2L * r * nw * SCK * 32, tail_n) + nw + L);
@@ -1190,10 +1189,9 @@ static int scan_bwd_impl(int B, int L, int D, int R, int ndir, const float* u, c
     ckpt = p_ck;
   }
   ScanBwdOut o{du, ddt_lin, dxdbl, p_a, p_d, p_g};
-  // dB / dC reduce-scatter: bank-masked DPP adds (default) or the select-based form
-  // (VITCNN_SCAN_SELECT_RS=1, read per call; bit-identical, kept for the A/B measurement and its test)
-  const char* sel_env = getenv("VITCNN_SCAN_SELECT_RS");
-  const bool bm = !(sel_env && atoi(sel_env));
+  // dB / dC reduce-scatter: bank-masked DPP adds (default) or the select-based form (knob SCAN_SELECT_RS=1,
+  // probe library; bit-identical, kept for the A/B measurement and its test)
+  const bool bm = vc_knob("VITCNN_SCAN_SELECT_RS", 0) == 0;
 #define VC_SCAN_BWD(RV)                                                                                     \
   do {                                                                                                      \
     if (fb) hipLaunchKernelGGL((scan_bwd<RV, true, true>), grid, block, sm, stream, a, ndir, gate_logits, y, dyp, ckpt, o, rbs, *fb); \
@@ -1228,8 +1226,8 @@ VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const f
                                    hipStream_t stream) {
   VC_REQUIRE(xz && conv_w && conv_b && x_proj_w && conv_part);
   VC_REQUIRE_I32((long)B * L * 2 * D);
-  const char* tail_env = getenv("VITCNN_SCAN_TAIL");
-  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part, tail_env ? atoi(tail_env) : 7};
+  // tail phase mask: 7 = every phase (the product); the probe library's knob SCAN_TAIL times phases alone
+  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part, (int)vc_knob("VITCNN_SCAN_TAIL", 7)};
   return scan_bwd_impl(B, L, D, R, ndir, u, xdbl, order, dt_w, dt_b, A_log, Dskip, gate_logits, y, dyp, ckpt, dpre,
                        ddt_lin, dxdbl, dA_log, dDskip, dgate_logits, ws, ws_floats, &fb, stream);
 }

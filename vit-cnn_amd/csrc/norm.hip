@@ -522,10 +522,8 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
 constexpr int BN_APPLY_ROWS = 64;   // rows per block of the fused (partials-reducing) apply kernels
 
 int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
-  static const int pcap = [] {   // VITCNN_BN_PCAP: most partials per channel (measurement switch)
-    const char* e = getenv("VITCNN_BN_PCAP");
-    return e ? std::max(16, std::min(1024, atoi(e))) : 64;
-  }();
+  // most partials per channel (knob BN_PCAP, probe library)
+  const int pcap = (int)std::max(16L, std::min(1024L, vc_knob("VITCNN_BN_PCAP", 64)));
   int rows_per = std::max<long>(32, (M + pcap - 1) / pcap);
   while ((long)vc_cdiv(M, rows_per) * 2 * C + reserve_doubles > ws_doubles && rows_per < (1 << 29)) rows_per *= 2;
   return rows_per;
@@ -910,8 +908,8 @@ VC_EXPORT int vc_bn_im2col3x3(int B, int H, int W, int C, const float* x, float 
   VC_REQUIRE(M < (1L << 31));
   VC_REQUIRE_I32((long)B * (H - 2) * (W - 2) * C * 9);
   const long S = (long)(H - 2) * (W - 2);
-  const char* e = getenv("VITCNN_BN_IM2COL");   // "0": the three launches (measurement switch, read per call)
-  if (S * 9 * IBS_CC * 4 > 65536 || (e && atoi(e) == 0)) {
+  // knob BN_IM2COL=0 (probe library): the three launches
+  if (S * 9 * IBS_CC * 4 > 65536 || vc_knob("VITCNN_BN_IM2COL", 1) == 0) {
     int rc = vc_bn_stats_ex(1, M, C, x, C, eps, momentum, save_mean, save_invstd, run_mean, run_var, ws, ws_floats,
                             nullptr, 0, stream);
     if (rc) return rc;
@@ -940,8 +938,7 @@ VC_EXPORT int vc_bn_glf_combine(long M, int C, const float* w_pre, float eps, fl
                                 long ws_floats, hipStream_t stream) {
   VC_REQUIRE(M > 0 && M < (1L << 31) && C > 0 && ((uintptr_t)ws & 7) == 0);
   VC_REQUIRE_I32(M * 2 * C);
-  const char* e = getenv("VITCNN_BN_GLF");   // "0": the three launches (measurement switch, read per call)
-  if (e && atoi(e) == 0) {
+  if (vc_knob("VITCNN_BN_GLF", 1) == 0) {   // knob BN_GLF=0 (probe library): the three launches
     int rc = vc_bn_stats_ex(1, M, C, w_pre, C, eps, momentum, save_mean, save_invstd, run_mean, run_var, ws,
                             ws_floats, nullptr, 0, stream);
     if (rc) return rc;

@@ -11,7 +11,7 @@ import os
 import re
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("VITCNN_LIB", os.path.join(_PKG, "libvitcnn_hip.so"))
+LIB_PATH = os.path.join(_PKG, "libvitcnn_hip.so")   # the product library (VITCNN_LIB: a tool's override)
 _HEADER_CANDIDATES = [
     os.path.join(_PKG, "..", "..", "include", "vitcnn.h"),
     os.path.join(_PKG, "vitcnn.h"),
@@ -58,13 +58,18 @@ def parse_header(path: str | None = None):
     return out
 
 
+PROBE_PATH = os.path.join(_PKG, "libvitcnn_probe.so")
+
+
 class _Lib:
-    def __init__(self):
-        if not os.path.exists(LIB_PATH):
+    def __init__(self, path=None):
+        path = path or os.environ.get("VITCNN_LIB", LIB_PATH)
+        if not os.path.exists(path):
             raise RuntimeError(
-                f"HIP extension not built: {LIB_PATH} is missing (run `make -C vit-cnn_amd/csrc` "
+                f"HIP extension not built: {path} is missing (run `make -C vit-cnn_amd/csrc` "
                 "or __graft_entry__.build()); there is no CPU fallback")
-        self.handle = ctypes.CDLL(LIB_PATH)
+        self.path = path
+        self.handle = ctypes.CDLL(path)
         self.sigs = parse_header()
         self.raw = {}
         for name, types in self.sigs.items():
@@ -107,3 +112,16 @@ def lib() -> _Lib:
     if _LIB is None:
         _LIB = _Lib()
     return _LIB
+
+
+_PROBE = None
+
+
+def probe_lib() -> _Lib:
+    """libvitcnn_probe.so (`make -C vit-cnn_amd/csrc probe`): the same sources built with -DVC_PROBE, whose
+    measurement knobs read VITCNN_* environment variables per call (tools/, and tests comparing two
+    bit-identical kernel forms in one process).  The product path never loads it."""
+    global _PROBE
+    if _PROBE is None:
+        _PROBE = _Lib(PROBE_PATH)
+    return _PROBE

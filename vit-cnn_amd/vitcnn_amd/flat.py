@@ -17,12 +17,23 @@ import torch.nn as nn
 F32 = 4
 
 
+def _last_active_name(model, names):
+    """the last parameter (in flat order) that receives gradients: the views fast path checks it, not
+    names[-1] (ViT-CNN's tail holds the never-used parameters, whose .grad stays None by design)"""
+    last = getattr(model, "_vc_last_active", None)   # the flat layout is fixed at construction
+    if last is None:
+        last = max((n for n in names if model._poff[n] < model._n_active), key=lambda n: model._poff[n])
+        object.__setattr__(model, "_vc_last_active", last)
+    return last
+
+
 def expose_grad_views(model):
     """Point every parameter's .grad at its slice of the flat gradient (`flat_params.grad`), so torch
     optimizers (e.g. the reference's torch.optim.Adam(model.parameters()), model_utils.py:109-118),
     gradient clipping or inspection see the gradient the hand-written backward wrote.  A no-op when
-    the views are current, or when the model is trained by vitcnn_amd.optim.AdamW (which reads the
-    flat gradient and clears `_grad_views`: ~1000 views per ViT-CNN step would cost milliseconds)."""
+    the views are current, or while the model is being stepped by vitcnn_amd.optim.AdamW (which reads
+    the flat gradient and clears `_grad_views` when it steps: ~1000 views per ViT-CNN step would cost
+    milliseconds); a torch optimizer stepping the model turns them back on (optim._torch_step_pre_hook)."""
     if not getattr(model, "_grad_views", True):
         return
     g = model._flat_store.grad
@@ -30,10 +41,11 @@ def expose_grad_views(model):
         return
     base = g.data_ptr()
     names = model._pnames if hasattr(model, "_pnames") else list(model._pmods)
-    first, last = model._pmods[names[0]], model._pmods[names[-1]]
+    lastn = _last_active_name(model, names)
+    first, last = model._pmods[names[0]], model._pmods[lastn]
     p0, p1 = first[0]._parameters[first[1]], last[0]._parameters[last[1]]
     if p0.grad is not None and p1.grad is not None and p0.grad.data_ptr() == base + F32 * model._poff[names[0]] \
-            and p1.grad.data_ptr() == base + F32 * model._poff[names[-1]]:
+            and p1.grad.data_ptr() == base + F32 * model._poff[lastn]:
         return
     n_active = model._n_active
     for n in names:

@@ -3,22 +3,22 @@
 Reference: `model/compare_method/FusAtNet.py` (`FusAtNet` :168-186), built by `model_utils.py:109-118`
 (patch 11, Adam lr 1e-3).  The module keeps the reference's parameter tree and state_dict names.
 Forward (train-mode BatchNorm with running-stat updates, or eval-mode) is a program of HIP kernels
-over channels-last [B, H, W, C] rows: every 3x3 conv is `vc_im2col3x3_pad` + `vc_gemm` (bias fused; or
-the implicit GEMM `vc_conv3x3_fwd` with VITCNN_IMPLICIT_CONV=1),
-BatchNorm `vc_bn_stats` + `vc_bn_apply` (ReLU fused), residual adds `vc_add2_2d`, pools
+over channels-last [B, H, W, C] rows: every 3x3 conv is the tap-major implicit GEMM
+`vc_conv3x3_tap_fwd` (conv_tap.hip: operand rows gathered from the channels-last map as float4 runs,
+k = tap * C + c, weights repacked tap-major once per step by `vc_conv3x3_pack`, bias fused; no im2col
+matrix), BatchNorm `vc_bn_stats` + `vc_bn_apply` (ReLU fused), residual adds `vc_add2_2d`, pools
 `vc_maxpool2_fwd` / `vc_pool_scale`, products `vc_mul2_2d`, the concatenation is written in place.
+(The module constant `_TAP_CONV = False` restores the rounds 1-2 formulation, `vc_im2col3x3_pad` +
+`vc_gemm`, for measurements.)
 
 Backward: the reference's own autograd raises (the in-place `x += identity` on a saved ReLU output,
 :44, :61).  This path defines the out-of-place semantics (`b = relu(bn2(conv2(a)))
-+ a`) and runs a hand-written backward over a tape of the forward's ops (conv: wgrad GEMM with the
-bias gradient fused, dgrad GEMM + `vc_col2im3x3_pad` (or `vc_conv3x3_wgrad` / `_dgrad`); `vc_bn_bwd`
-with the ReLU mask; maxpool,
-pooled-scale and product backwards); the parameter gradients land in one flat gradient
++ a`) and runs a hand-written backward over a tape of the forward's ops (conv: `vc_conv3x3_tap_wgrad`
+with the bias gradient, `vc_conv3x3_tap_dgrad` over the tap-major weights; `vc_bn_bwd` with the ReLU
+mask; maxpool, pooled-scale and product backwards); the parameter gradients land in one flat gradient
 (`flat_params.grad`) for the fused Adam (vitcnn_amd.optim.AdamW, weight_decay 0).
 """
 from __future__ import annotations
-
-import os
 
 import torch
 import torch.nn as nn
@@ -27,9 +27,9 @@ from ._lib import lib
 from .flat import F32, FlatParams
 from .model import _IMPLICIT_CONV, N_COUNTERS
 
-# 3x3 convs: the tap-major implicit GEMM (vc_conv3x3_tap_*, conv_tap.hip) by default; VITCNN_FUSAT_IM2COL=1
-# restores the im2col + vc_gemm formulation of rounds 1-2 (measurements)
-_TAP_CONV = os.environ.get("VITCNN_FUSAT_IM2COL", "0") != "1"
+# 3x3 convs: the tap-major implicit GEMM (vc_conv3x3_tap_*, conv_tap.hip); False restores the im2col +
+# vc_gemm formulation of rounds 1-2 (a module constant: tools/knobs.py sets it from VITCNN_FUSAT_IM2COL=1)
+_TAP_CONV = True
 
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
 _COUNTER_BUFS = {}
@@ -200,15 +200,22 @@ class _FusAtNetFunction(torch.autograd.Function):
 
 
 class _Program:
-    # floats: split-K slabs of the tap-major conv GEMMs (up to ~50 MB at B = 64)
-    SCRATCH = 1 << int(os.environ.get("VITCNN_FUSAT_SCRATCH_LOG2", "26"))
+    # split-K slabs of the tap-major conv GEMMs: ~50 MB at B = 64 (sized from the batch, not a
+    # fixed 256 MiB), cached per (device, batch) on the model so a forward allocates nothing
+    SCRATCH_PER_SAMPLE = 1 << 18      # floats (1 MiB) per sample: 64 MiB at B = 64
 
     def __init__(self, m: FusAtNet, x1, x2, grad: bool):
         self.m, self.L, self.dev = m, lib(), x1.device
         self.s = torch.cuda.current_stream(self.dev).cuda_stream
         self.B, self.P = x1.shape[0], x1.shape[2]
         self.x1, self.x2 = x1, x2
-        self.scr = torch.empty(self.SCRATCH, dtype=torch.float32, device=self.dev)
+        self.SCRATCH = max(1 << 22, self.B * self.SCRATCH_PER_SAMPLE)
+        key = (str(self.dev), self.SCRATCH)
+        cache = m.__dict__.setdefault("_vc_scratch", {})
+        if key not in cache:
+            cache.clear()
+            cache[key] = torch.empty(self.SCRATCH, dtype=torch.float32, device=self.dev)
+        self.scr = cache[key]
         self.cnt = _counters(self.dev, self.s)
         self.train = m.training
         self.grad = grad

@@ -19,8 +19,8 @@ MI355X-first design:
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import math
-import os
 import sys
 import weakref
 from typing import Dict
@@ -40,46 +40,53 @@ BN_MOM = 0.1
 NDIR = 10
 N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
 WGRAD_LANE = 2             # backward: lane 0's deferred weight gradients (lane 2 is idle after the forward)
+# Program switches.  Module constants -- the product reads no environment: each selects between two
+# forms the tests hold to the same parity (or bit-identity), and the measurement tools set them from
+# VITCNN_<NAME> variables through tools/knobs.py (tools/ab_env.sh A/B runs).  The defaults are the
+# measured-fastest forms.
+#
 # 3x3 convs of ViT-CNN: im2col + vc_gemm by default; VITCNN_IMPLICIT_CONV=1 selects the implicit GEMM
 # (vc_conv3x3_*), measured slower on this step (2.39 -> 2.55 ms: the per-element gather with the fused
 # BN affine costs more VALU than the small im2col matrices cost bandwidth); FusAtNet, whose col
 # matrices reach 611 MB, always uses the implicit GEMM
-_IMPLICIT_CONV = os.environ.get("VITCNN_IMPLICIT_CONV", "0") == "1"
+_IMPLICIT_CONV = False
 # lane-0 weight gradients are batched and issued on the weight-gradient lane at a few flush points
 # (one fork each); forking each one separately measured slower (2.39 -> 2.63 ms: every cross-lane
-# graph edge costs more than one GEMM's overlap gains)
-_DEFER_WGRAD = os.environ.get("VITCNN_DEFER_WGRAD", "1") == "1"
+# graph edge costs more than one GEMM's overlap gains); False: every weight gradient in place
+_DEFER_WGRAD = True
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
+GEMM_GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES (include/vitcnn.h)
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 # the Mamba direction conv + x_proj folded into the scan launch and the dt_proj / x_proj data gradients +
-# conv1d backward into the scan backward's tail (vc_mamba_scan_fwd_fused / _bwd_fused); "0" restores the
-# separate launches (measurement switch, read per program)
-_SCAN_FUSED = os.environ.get("VITCNN_SCAN_FUSED", "1") != "0"
+# conv1d backward into the scan backward's tail (vc_mamba_scan_fwd_fused / _bwd_fused); False restores the
+# separate launches
+_SCAN_FUSED = True
 # patch_embed + pre_norm + in_proj and combine + out_proj + ln1 + change_dim as one launch each
-# (vc_rowchain_front / _back); "0" restores the separate launches (measurement switch)
-_ROW_CHAIN = os.environ.get("VITCNN_ROW_CHAIN", "1") != "0"
+# (vc_rowchain_front / _back); False restores the separate launches
+_ROW_CHAIN = True
 # GLfusion: the phi | g max pool inside the non-local attention forward and its backward inside the
 # attention backward, the concat gradient's add + copy as one launch (vc_nonlocal_attn_pool_fwd / _bwd,
-# vc_add2_2d_dup); "0" restores the separate launches (measurement switch)
-_GLF_FUSED = os.environ.get("VITCNN_GLF_FUSED", "1") != "0"
+# vc_add2_2d_dup); False restores the separate launches
+_GLF_FUSED = True
 # the local conv's data gradient as the tap-major implicit GEMM (vc_conv3x3_tap_dgrad, no dcol matrix, no
 # col2im) over the weights packed tap-major by lane 0 in the forward: opt-in, measured slower on the B=64
 # step (1.90-1.94 -> 1.99-2.01 ms: at 7x7 / 9x9 maps the row gathers cost more than dcol + col2im)
-_TAP_DGRAD = os.environ.get("VITCNN_TAP_DGRAD", "0") == "1"
-_LANES = os.environ.get("VITCNN_LANES", "1") != "0"   # branch-level stream concurrency (debug switch)
+_TAP_DGRAD = False
+_LANES = True        # branch-level stream concurrency (False: every lane on the caller's stream)
+_LANES_BWD = True    # the same for the backward alone
 _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in normal runs)
-_GROUP = os.environ.get("VITCNN_GEMM_GROUP", "1") != "0"   # grouped launches of independent fp32 GEMMs
+_GROUP = True        # grouped launches of independent fp32 GEMMs
 # bf16 mode diagnostics (tools/bf16_sites.py): GEMM issue indices kept in fp32, and a log of call sites
 _BF16_EXACT: set = set()
 # bf16 mode: bf16 operands only for products with K >= this that are not weight gradients (the im2col'ed
 # 3x3 convs, K = 9 Cin): the short-K products are launch-latency-bound, where bf16 saves nothing and costs
 # the grouped launch (bf16 GEMMs launch alone), and the long-K weight gradients run slower on the bf16
 # kernel than on the fp32 split-K one; 0 = every GEMM bf16 (round 2's mode)
-_BF16_MIN_K = int(os.environ.get("VITCNN_BF16_MIN_K", "1024"))
+_BF16_MIN_K = 1024
 _GEMM_SITES = None
-_LANE_MAP = [int(v) for v in os.environ.get("VITCNN_LANE_MAP", "").split(",") if v]   # measurement switch
-_BN_TICKETS = os.environ.get("VITCNN_BN_TICKETS", "0") == "1"   # BN reductions in the last-arriving block: measured ~1% slower (every arrival is an agent-scope release = L2 writeback)
+_LANE_MAP = []       # logical lane -> stream index (empty: lane i on stream i)
+_BN_TICKETS = False  # BN reductions in the last-arriving block: measured ~1% slower (every arrival is an agent-scope release = L2 writeback)
 
 UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
                    "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
@@ -387,6 +394,15 @@ class Multimodality_Mamba(nn.Module):
             tab["lanes"] = lanes
         return lanes
 
+    def _gemm_group_buf(self, device, lane):
+        """host memory of one grouped-GEMM state per lane (vc_gemm_group_*: the library keeps none)"""
+        tab = self._device_tables(device)
+        bufs = tab.get("gemm_groups")
+        if bufs is None:
+            bufs = [ctypes.create_string_buffer(GEMM_GROUP_BYTES) for _ in range(N_SIDE + 1)]
+            tab["gemm_groups"] = bufs
+        return ctypes.addressof(bufs[lane])
+
     def _tile_counters(self, device):
         """one zeroed split-K arrival-counter array per lane (vc_gemm_ex; kernels leave them zero)"""
         tab = self._device_tables(device)
@@ -480,7 +496,8 @@ class _Program:
         self.lanes_on = _LANES
         self.wgrad_tail = None
         self.pending_wgrads = []
-        self._grouping = False
+        self._grouping = None      # the open GEMM group's state (host address) while gemm_group() collects
+        self._group_lane = 0
         _, self.P, self.BUF, self.I64 = model._ptrs()
         self.device = device
 
@@ -522,22 +539,27 @@ class _Program:
         if self.gemm_flags and not exact and i not in _BF16_EXACT and args[4] >= _BF16_MIN_K and not (
                 _BF16_MIN_K and args[0]):
             args = args[:21] + (args[21] | self.gemm_flags,) + args[22:]
-        self.L.vc_gemm_ex(*args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
+        if self._grouping is not None and self._group_lane == self.cur:
+            self.L.vc_gemm_group_add(self._grouping, *args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS)
+        else:
+            self.L.vc_gemm_ex(*args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
 
     @contextlib.contextmanager
     def gemm_group(self):
         """the fp32 GEMMs issued inside (on the current lane; they must be independent of each other)
-        launch as one grouped grid + one grouped split-K reduce (vc_gemm_group_begin / _end)"""
-        if not _GROUP or self._grouping:   # nested: the outer group collects (bf16 members launch alone)
+        launch as one grouped grid + one grouped split-K reduce (vc_gemm_group_begin / _add / _end over
+        the lane's caller-owned group state)"""
+        if not _GROUP or self._grouping is not None:   # nested: the outer group collects
             yield
             return
-        self.L.vc_gemm_group_begin(self.s)
-        self._grouping = True
+        grp = self.m._gemm_group_buf(self.device, self.cur)
+        self.L.vc_gemm_group_begin(grp, self.s)
+        self._grouping, self._group_lane = grp, self.cur
         try:
             yield
         finally:
-            self._grouping = False
-            self.L.vc_gemm_group_end()
+            self._grouping = None
+            self.L.vc_gemm_group_end(grp)
 
     def mark(self):
         """event recorded on the current lane"""
@@ -1231,7 +1253,7 @@ class _Program:
         """bucket_hook(name, events): called as each gradient bucket of parallel.GradExchange.BUCKETS
         ("tail": LiDAR + fusion + classifier, "hsi2", "hsi1" — head side first) is complete."""
         m, B, ws = self.m, self.B, self.ws
-        self.lanes_on = lanes and _LANES and os.environ.get("VITCNN_LANES_BWD", "1") != "0"
+        self.lanes_on = lanes and _LANES and _LANES_BWD
         grad = out if out is not None else torch.empty(m._n_params, dtype=torch.float32, device=self.device)
         if m._n_params > m._n_active:  # parameters the reference forward never uses get no gradient
             # (off lane 0's chain: nothing reads this range before the final join)

@@ -19,7 +19,7 @@ Data parallelism: when a torch.distributed process grou
 one rank is initialised, `train` starts every replica from rank 0's parameters, all-reduces the
 gradient after every backward (RCCL) and folds the 1/world average into the fused AdamW update;
 each rank iterates its own shard of the batches (a loader that is not already sharded is wrapped in
-`parallel.ShardedLoader`).
+`parallel.ShardedLoader`, which shards a torch DataLoader at its sampler).
 
 Precision (BASELINE.json config 2): `get_model(..., precision="bf16")` builds ViT-CNN with bf16
 GEMM operands and fp32 accumulation (`Multimodality_Mamba.set_precision`); the default "fp32" is
@@ -189,7 +189,9 @@ def train(savename, run, bands, net, optimizer, criterion, data_loader, epoch, s
 
     Data parallel (a process group with more than one rank): replicas start from rank 0's parameters,
     a loader that is not already sharded is wrapped in `parallel.ShardedLoader` (every rank the same
-    number of batches: one gradient exchange per batch on every rank), and the per-epoch metric that
+    number of batches: one gradient exchange per batch on every rank; a torch DataLoader is sharded at
+    its sampler, so each rank assembles only its own batches), a loader that shards itself
+    (PatchBatcher(rank=, world=)) is checked against the group, and the per-epoch metric that
     decides the best-state branch -- whose buffer broadcast is a collective -- is the mean over the
     ranks (validation: accuracy over the union of the ranks' validation batches), so every rank takes
     the same branch.  `train.last_stats` holds per-epoch wall times and batch counts."""
@@ -202,6 +204,7 @@ def train(savename, run, bands, net, optimizer, criterion, data_loader, epoch, s
     distributed = parallel.is_distributed()
     if distributed:
         parallel.broadcast_parameters(net)       # replicas start identical (rank 0's values)
+        parallel.check_loader_shard(data_loader)  # a self-sharding loader (PatchBatcher) agrees with the group
         if not parallel.is_sharded(data_loader):
             data_loader = parallel.ShardedLoader(data_loader, parallel.rank(), parallel.world())
     stepper = _stepper(net, optimizer, criterion)

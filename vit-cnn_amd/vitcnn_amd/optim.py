@@ -28,9 +28,6 @@ class AdamW(torch.optim.Optimizer):
         self.grad_scale = 1.0   # data-parallel: 1/world_size folded into the update
         self._dev = None
         self._hyper_vals = None
-        # the model need not expose per-parameter .grad views of its flat gradient (torch optimizers
-        # need them; this one reads the flat gradient)
-        owner()._grad_views = False
 
     def sync_hyper(self):
         """Copy lr / betas / eps / weight decay / grad_scale to the device tensor the kernel reads, if
@@ -66,6 +63,10 @@ class AdamW(torch.optim.Optimizer):
         if g is None:
             return loss
         st = self.sync_hyper()
+        # this optimizer reads the flat gradient: the model need not rebuild ~1000 per-parameter .grad views
+        # after every backward while it is the one stepping (a torch optimizer stepping the same model turns
+        # them back on: _torch_step_pre_hook)
+        model._grad_views = False
         s = torch.cuda.current_stream(flat.device).cuda_stream
         lib().vc_adamw(model._n_active, flat.data_ptr(), g.data_ptr(), st["m"].data_ptr(), st["v"].data_ptr(),
                        st["hyper"].data_ptr(), st["step"].data_ptr(), s)
@@ -74,3 +75,33 @@ class AdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True):
         super().zero_grad(set_to_none=set_to_none)
         self._owner().zero_grad(set_to_none=set_to_none)
+
+
+def _torch_step_pre_hook(opt, args, kwargs):
+    """Global step pre-hook of every torch optimizer: a torch optimizer (e.g. the reference pattern
+    torch.optim.Adam(model.parameters())) stepping a flat-buffer vitcnn_amd model needs the per-parameter
+    .grad views; if the fused AdamW stepped that model before (and switched them off), they are turned
+    back on and built now, before this step reads them."""
+    if isinstance(opt, AdamW):
+        return
+    owners = getattr(opt, "_vc_owners", None)
+    if owners is None or owners[0] != len(opt.param_groups):
+        found = {}
+        for grp in opt.param_groups:
+            for p in grp["params"]:
+                o = getattr(p, "_vc_owner", None)
+                if o is not None:
+                    found[id(o)] = o
+        owners = (len(opt.param_groups), list(found.values()))
+        opt._vc_owners = owners
+    for o in owners[1]:
+        m = o()
+        if m is not None and not getattr(m, "_grad_views", True):
+            from .flat import expose_grad_views
+            m._grad_views = True
+            expose_grad_views(m)
+
+
+from torch.optim.optimizer import register_optimizer_step_pre_hook  # noqa: E402
+
+register_optimizer_step_pre_hook(_torch_step_pre_hook)

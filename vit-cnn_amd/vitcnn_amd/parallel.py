@@ -277,37 +277,94 @@ def shard_indices(n: int, rank_: int, world_: int, seed: int = 0, epoch: int = 0
     return idx[rank_:total:world_]
 
 
-class ShardedLoader:
-    """Wrap a reference-style DataLoader (batches of (data, data2, target)) so each rank iterates a
-    disjoint shard of its batches: batch b goes to rank b % world, and the batch list is padded by
-    wrapping (as `shard_indices` / DistributedSampler pad their index lists) to ceil(n / world) * world,
-    so EVERY rank iterates the same number of batches -- train() issues one gradient all-reduce per
-    batch, and ranks with different batch counts would pair their collectives across epochs (or block
-    forever in the last one).  The wrapped batches are the first ones of the same pass (kept from it,
-    not re-drawn).  Used by train() when a process group is up and the loader is not already sharded
-    (a loader whose sampler is a DistributedSampler, or whose dataset carries `rank`/`world`
-    attributes, is)."""
+def rank_batches(n: int, rank_: int, world_: int):
+    """Batch positions rank `rank_` trains on out of a pass of `n` batches: b = rank_, rank_ + world_, ...
+    over the pass padded by wrapping to ceil(n / world_) * world_ (as `shard_indices` / DistributedSampler
+    pad their index lists), so EVERY rank gets the same number of batches -- train() issues one gradient
+    all-reduce per batch, and ranks with different batch counts would pair their collectives across
+    epochs (or block forever in the last one).  Padded position j repeats batch j % n."""
+    if n <= 0:
+        return []
+    total = -(-n // world_) * world_
+    return [j % n for j in range(rank_, total, world_)]
 
-    def __init__(self, loader, rank_: int, world_: int):
-        self.loader, self.rank, self.world = loader, rank_, world_
-        self.dataset = loader.dataset
+
+def _broadcast_order(order, group=None):
+    """rank 0's sample order, on every rank (one broadcast of its length, one of the indices)"""
+    dev = _scalar_device(group)
+    n = torch.tensor([len(order) if rank() == 0 else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src=0, group=group)
+    t = torch.tensor(order if rank() == 0 else [0] * int(n.item()), dtype=torch.int64, device=dev)
+    dist.broadcast(t, src=0, group=group)
+    return t.cpu().tolist()
+
+
+class ShardedLoader:
+    """Wrap a reference-style loader (batches of (data, data2, target)) so each rank iterates a disjoint
+    shard of the pass's batches -- batch b goes to rank b % world, every rank the same number of batches
+    (`rank_batches`) -- and materialises ONLY its own batches:
+
+    * a torch DataLoader (main.py:434-440: MultiModalX, shuffle=True, num_workers=0): sharded at the
+      sampler level.  Each pass, rank 0 draws the loader's own sample order (its RandomSampler, i.e. the
+      draw a single-process epoch would make) and broadcasts it; every rank cuts that shared order into
+      the loader's batches and builds a DataLoader over its own batch list (same dataset, collate_fn,
+      workers).  The shards are disjoint by construction, whatever each rank's torch seed is;
+    * an indexable loader (a list of batches): rank r takes its batch positions directly;
+    * any other iterable: the pass is iterated and the other ranks' batches are discarded (the only form
+      that assembles every batch on every rank; documented fallback).
+
+    Used by train() when a process group is up and the loader is not already sharded (a loader whose
+    sampler is a DistributedSampler, or which carries `rank`/`world` attributes -- PatchBatcher -- is)."""
+
+    def __init__(self, loader, rank_, world_, group=None):
+        self.loader, self.rank, self.world, self.group = loader, rank_, world_, group
+        self.dataset = getattr(loader, "dataset", None)
+        DL = torch.utils.data.DataLoader
+        if isinstance(loader, DL) and loader.batch_size is not None and \
+                not isinstance(loader.dataset, torch.utils.data.IterableDataset):
+            self.mode = "sampler"
+        elif hasattr(loader, "__getitem__") and hasattr(loader, "__len__"):
+            self.mode = "indexed"
+        else:
+            self.mode = "iterate"
 
     def __len__(self):
         n = len(self.loader)
         return -(-n // self.world) if n > 0 else 0
 
     def __iter__(self):
-        n = len(self.loader)
-        total = len(self) * self.world
-        # padded position n + j repeats batch j % n; this rank owns at most one of them (pad < world)
-        need = [j % n for j in range(total - n) if (n + j) % self.world == self.rank]
+        if self.mode == "sampler":
+            yield from self._iter_sampler()
+        elif self.mode == "indexed":
+            for b in rank_batches(len(self.loader), self.rank, self.world):
+                yield self.loader[b]
+        else:
+            yield from self._iter_discard()
+
+    def _iter_sampler(self):
+        ld = self.loader
+        if is_distributed():
+            order = _broadcast_order(list(iter(ld.sampler)) if rank() == 0 else [], self.group)
+        else:
+            order = list(iter(ld.sampler))
+        bs = ld.batch_size
+        batches = [order[i:i + bs] for i in range(0, len(order), bs)]
+        if ld.drop_last and batches and len(batches[-1]) < bs:
+            batches.pop()
+        mine = [batches[b] for b in rank_batches(len(batches), self.rank, self.world)]
+        sub = torch.utils.data.DataLoader(ld.dataset, batch_sampler=mine, num_workers=ld.num_workers,
+                                          collate_fn=ld.collate_fn, pin_memory=ld.pin_memory,
+                                          worker_init_fn=ld.worker_init_fn)
+        yield from sub
+
+    def _iter_discard(self):
+        want = rank_batches(len(self.loader), self.rank, self.world)
+        need = set(want)
         kept = {}
         for b, item in enumerate(self.loader):
             if b in need:
                 kept[b] = item
-            if b % self.world == self.rank:
-                yield item
-        for b in need:
+        for b in want:
             yield kept[b]
 
 
@@ -319,3 +376,28 @@ def is_sharded(loader) -> bool:
         return True
     ds = getattr(loader, "dataset", None)
     return getattr(ds, "world", 1) > 1 or getattr(loader, "world", 1) > 1
+
+
+def check_loader_shard(loader, group=None):
+    """A loader that shards itself (PatchBatcher: `rank` / `world` / `seed`) must agree with the process
+    group: its rank and world are this process's, and every rank built it from the same seed (the
+    shuffled order the shards are cut from is then the same permutation on every rank).  Raises
+    RuntimeError otherwise -- nothing else would notice overlapping or missing shards."""
+    if not is_distributed() or getattr(loader, "world", None) is None:
+        return
+    if int(loader.world) != world() or int(loader.rank) != rank():
+        raise RuntimeError(f"loader shard (rank {loader.rank} of {loader.world}) does not match the process group "
+                           f"(rank {rank()} of {world()})")
+    seed = getattr(loader, "seed", None)
+    if seed is not None:
+        s = int(seed) & ((1 << 62) - 1)
+        t = torch.tensor([s, -s], dtype=torch.int64, device=_scalar_device(group))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        if int(t[0].item()) != -int(t[1].item()):
+            raise RuntimeError("the ranks' loaders were built from different seeds: their shards would overlap")
+
+
+def capturable(group=None) -> bool:
+    """Can the gradient exchange be captured into a hipGraph?  RCCL ("nccl") collectives can; gloo's
+    host-side collectives cannot, so a gloo-backed data-parallel step runs eagerly."""
+    return not is_distributed() or dist.get_backend(group) == "nccl"

@@ -104,6 +104,10 @@ class TrainStepper:
         if self.fused and parallel.is_distributed():
             self.exchange = parallel.GradExchange(net)
             optimizer.grad_scale = 1.0 / parallel.world()
+            if self.use_graph and not parallel.capturable():
+                # gloo's host-side collectives cannot be captured: the same fused step, eagerly
+                self.use_graph = False
+                self.launch = "eager (the gloo exchange is not graph-capturable)"
 
     def _check_binding(self):
         """captured graphs hold the parameter / buffer / optimizer-state addresses of their capture:

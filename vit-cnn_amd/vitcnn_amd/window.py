@@ -80,8 +80,11 @@ class PatchBatcher:
     """Training batches of MultiModalX patches assembled on the device.
 
     Iterating yields (hsi [B,C1,P,P], lidar [B,C2,P,P], target [B] int64) on `device`, in the
-    order of the shuffled `indices` (DataLoader(shuffle=False) over the dataset, as main.py builds
-    it).  `rank`/`world` select a disjoint shard for data parallelism.
+    order of the shuffled `indices` (DataLoader(shuffle=False) over the dataset; the reference's train
+    loader reshuffles every epoch, main.py:434-440, this one keeps its construction-time order).
+    `rank`/`world` select a disjoint shard for data parallelism: every rank builds the batcher with the
+    same `seed` and takes every world-th centre of the padded shuffled list (equal batch counts on every
+    rank; `parallel.is_sharded` sees the attributes, so train() does not shard it again).
 
     Augmentations of MultiModalX.__getitem__ (datasets.py:559-568), per sample in the reference's
     order and with its probabilities, the decisions drawn from one host RandomState in the reference's
@@ -91,10 +94,16 @@ class PatchBatcher:
     pixels, :534-545) on the HSI patch by `vc_patch_noise`.  The per-element normal fields and the
     per-pixel same-class choices (the reference's np.random.normal(size=patch) / np.random.choice) are
     drawn on the device from a counter-based hash, so the host stream differs from the reference's
-    after the first noisy sample (same distributions).  The mixture's source
-    pixel reproduces the reference's pairing of its UNshuffled label list with its shuffled index list
-    (datasets.py:505-506, :540-543): for class v the candidates are indices[j] over the positions j
-    with labels[j] == v."""
+    after the first noisy sample (same distributions).
+
+    Mixture noise is a deliberate divergence whose parity is UNPINNED: in the reference,
+    datasets.py:540 evaluates `np.nonzero(self.labels == value)` with `self.labels` a Python list, so
+    the comparison is a scalar False, np.random.choice receives an empty array and raises -- the
+    reference's --mixture_augmentation never completes.  This path implements the evident intent,
+    pairing the UNshuffled label list with the shuffled index list as the surrounding code does
+    (:505-506, :540-543: for class v the candidates are indices[j] over the positions j with
+    labels[j] == v), and is checked only against its own CPU restatement
+    (oracle/patch_noise_oracle.py)."""
 
     def __init__(self, img1, img2, gt, patch_size: int, ignored_labels=(0,), batch_size: int = 64,
                  flip_augmentation: bool = False, device="cuda", seed: int = 0, rank: int = 0, world: int = 1,
@@ -120,7 +129,18 @@ class PatchBatcher:
         self.W, self.H = int(self.c1.shape[0]), int(self.c1.shape[1])
         if self.mixture:
             self._mixture_tables(gt, idx, labels_unshuffled)
-        idx = idx[rank::world] if world > 1 else idx
+        self.rank, self.world = int(rank), int(world)
+        if self.world > 1:
+            # data-parallel shard: the shuffled list padded by wrapping to ceil(N / world) * world, then every
+            # world-th centre from `rank` -- disjoint shards of equal length (equal batch counts: train()
+            # exchanges one gradient per batch on every rank); parallel.check_loader_shard verifies that
+            # every rank built its batcher from the same seed, i.e. cut its shard from the same permutation
+            per = -(-len(idx) // self.world)
+            idx = np.resize(idx, (per * self.world, 2))[self.rank::self.world] if len(idx) else idx
+            if self.rank > 0:
+                # augmentation draws of their own on every rank (rank 0 keeps the single-process stream)
+                self.rng = np.random.RandomState((int(seed) + 7919 * self.rank) % (1 << 32))
+        self.noise_seed = (self.seed ^ (0x9E3779B97F4A7C15 * self.rank)) & ((1 << 63) - 1)
         self.centers = idx
         self.labels = torch.as_tensor(gt[idx[:, 0], idx[:, 1]].astype(np.int64)).to(self.device)
         corners = (idx - p).astype(np.int32)
@@ -216,6 +236,6 @@ class PatchBatcher:
                               lab.data_ptr(), stream)
             off, pix, nlab = self.mix_off.data_ptr(), self.mix_pix.data_ptr(), self.nlab
         L.vc_patch_noise(n, C1, P, self.H, x1.data_ptr(), lab.data_ptr() if lab is not None else None,
-                         rad_d.data_ptr(), mix_d.data_ptr(), off, pix, nlab, self.c1.data_ptr(), self.seed, self.gid,
+                         rad_d.data_ptr(), mix_d.data_ptr(), off, pix, nlab, self.c1.data_ptr(), self.noise_seed, self.gid,
                          stream)
         self._last_noise = (rad_d, mix_d, lab)   # keep the uploads alive until the kernel has run
