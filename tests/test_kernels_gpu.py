@@ -57,10 +57,10 @@ def rnd(*shape, seed=0, scale=1.0):
     return (torch.rand(*shape, generator=g) * 2 - 1) * scale
 
 
-# vc_gemm flags: bit 0 ReLU, bit 1 bf16 operands (fp32 accumulate), bit 2 / bit 3 force the k-major /
-# the K-contiguous fp32 kernel (default: chosen by shape)
-F_BF16, F_LEGACY, F_V2 = 2, 4, 8
-KERNELS = [0, F_LEGACY, F_V2, F_BF16]
+# vc_gemm flags: bit 0 ReLU, bit 1 bf16 operands (fp32 accumulate), bit 2 / bit 3 / bit 4 force the k-major /
+# the K-contiguous / the LDS-DMA pipelined fp32 kernel (default: chosen by shape)
+F_BF16, F_LEGACY, F_V2, F_PIPE = 2, 4, 8, 16
+KERNELS = [0, F_LEGACY, F_V2, F_PIPE, F_BF16]
 
 
 def bf16_round(t):

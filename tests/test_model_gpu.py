@@ -351,3 +351,57 @@ def test_trained_eval_mode_class_indices():
             assert sel.sum() >= 56, (key, int(sel.sum()))
             assert np.array_equal(got.argmax(1)[sel], ref.argmax(1)[sel]), key
     assert len(set(z["eval_argmax"].tolist())) >= 10
+
+
+def _schedule_grad(sd, batch, crit, captured, lanes_bwd=True, lane_map=(), ch_lane=1, ch_ordered=True):
+    """(loss, flat gradient) of one fused training step under a given lane schedule, eager or replayed
+    from a hipGraph capture"""
+    import vitcnn_amd.model as VM
+    from vitcnn_amd import fused_train_step
+    saved = (VM._LANES_BWD, VM._LANE_MAP, VM._CH_LANE, VM._CH_ORDERED)
+    VM._LANES_BWD, VM._LANE_MAP, VM._CH_LANE, VM._CH_ORDERED = lanes_bwd, list(lane_map), ch_lane, ch_ordered
+    try:
+        hsi, lidar, target = batch
+        m = _product(sd).train()
+        if not captured:
+            loss = fused_train_step(m, crit, hsi, lidar, target)
+            torch.cuda.synchronize()
+            return float(loss), m.flat_params.grad.detach().clone()
+        holder = {}
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fused_train_step(m, crit, hsi, lidar, target)     # warm-up: workspaces, events, streams
+        torch.cuda.current_stream().wait_stream(s)
+        m.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            holder["l"] = fused_train_step(m, crit, hsi, lidar, target)
+        m.load_state_dict(sd)       # the warm-up step updated the BN running statistics
+        g.replay()
+        torch.cuda.synchronize()
+        return float(holder["l"]), m.flat_params.grad.detach().clone()
+    finally:
+        VM._LANES_BWD, VM._LANE_MAP, VM._CH_LANE, VM._CH_ORDERED = saved
+
+
+@pytest.mark.parametrize("lane_map,lanes_bwd,ch_lane", [((), True, 1), ((), False, 1), ((0, 0, 0, 0), True, 1),
+                                                        ((0, 1, 1, 1), True, 1), ((0, 1, 2, 1), True, 1),
+                                                        ((), True, 3)])
+def test_lane_schedules_are_bit_identical(lane_map, lanes_bwd, ch_lane):
+    """the step's result does not depend on its schedule.  The default four-lane step
+    (eager) is the reference; every other lane map (logical lanes folded onto fewer streams), the
+    single-stream backward, and the channel chain on a lane of its own (its dX accumulation ordered after
+    the local chain's) -- each eager AND replayed from a hipGraph capture -- give the same loss and the
+    same flat gradient bit for bit.  (A cross-lane accumulation without a fixed order -- the round-3
+    channel-lane experiment -- makes the sum depend on the schedule: DESIGN.md section 11.)"""
+    _need_gpu()
+    from vitcnn_amd import CrossEntropyLoss
+    sd = hash_state_dict()
+    batch = tuple(t.to(DEV) for t in golden_batch("golden.b64", 64))
+    crit = CrossEntropyLoss(weight=O.ce_class_weights(16).to(DEV))
+    ref_loss, ref = _schedule_grad(sd, batch, crit, False)
+    for captured in (False, True):
+        loss, g = _schedule_grad(sd, batch, crit, captured, lanes_bwd, lane_map, ch_lane)
+        assert loss == ref_loss, (captured, loss, ref_loss)
+        assert torch.equal(g, ref), (captured, float((g - ref).abs().max()))

@@ -17,7 +17,7 @@ namespace {
 constexpr int BM = 64, BN = 64;
 constexpr int LDS_STRIDE = 81;  // 64 + 17: conflict-free fragment reads, <=2-way stores
 
-enum { F_RELU = 1, F_BF16 = 2, F_LEGACY = 4, F_V2 = 8 };
+enum { F_RELU = 1, F_BF16 = 2, F_LEGACY = 4, F_V2 = 8, F_PIPE = 16, F_NOPIPE = 32 };
 
 struct Epi {
   float alpha, beta;
@@ -849,6 +849,213 @@ __global__ __launch_bounds__(256) void splitk_reduce4(GemmArgs g, long nelem, in
 
 }  // namespace g2
 
+// ------------------------------------------------------------------------------------------------
+// gemm_pipe: the fp32 GEMM of the step's mid shapes (M 1600-5184, N 72-1296, K 128-3136; the 3x3
+// convs, the fusion / non-local 1x1 convs and their data / weight gradients), k-pipelined.
+//
+// The k-major kernel above stages one k-tile in registers and waits for it behind ~1000 cycles of
+// MFMAs per wave: these shapes run at 1-2 blocks per CU, so the L2 / Infinity-Cache latency of every
+// k-tile is exposed (the largest conv at 0.30 of the fp32 peak, MFMA busy 0.155).  Here the
+// operand tiles go HBM/L2 -> LDS by LDS-DMA (buffer_load ... lds, 16 B per lane: no VGPRs, no
+// ds_write pass), into a ring of NS stages, so NS - 1 k-tiles of loads are in flight behind the MFMAs;
+// one raw s_barrier per k-tile with a COUNTED vmcnt wait (the stage being read has landed, the later
+// ones stay in flight).  The buffer descriptors' range checks zero-fill everything past the operand
+// (rows >= M / N, k >= K) and a per-lane out-of-range offset masks k past a split-K slice.
+//
+// LDS images (the same layouts and fragment reads as g2::Stage, fp32):
+//  * K-contiguous operand ([row][k]: A of C = A W^T, W of a 1x1 conv): 128-B rows, chunk c of row r at
+//    slot c ^ ((r >> 1) & 7); one DMA wave-instruction fills 8 rows (lane -> row lane>>3, slot lane&7,
+//    the source address pre-swizzled);
+//  * row-contiguous operand ([k][row]: dY / X of a weight gradient, W of a data gradient): ROWS floats
+//    per k-row, 16-column blocks XOR-swizzled by (k >> 2) & 1; one DMA wave-instruction fills
+//    256 / ROWS k-rows.
+// Wave tile (BM/2) x (BN/2) of 16x16 v_mfma_f32_16x16x4_f32 tiles (2 x 2 waves), one accumulator chain
+// per output tile; MT * NT >= 4 independent chains keep the 32-cycle issue rate.
+namespace gp {
+
+constexpr int KT = 32;   // k per stage (fp32: 128-B LDS rows)
+constexpr unsigned OOB = 0x80000000u;   // a voffset past every operand: the DMA writes zeros
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// One 16-B-per-lane LDS-DMA wave-instruction: lane i's 16 source bytes (buffer offset voff) land at LDS
+// byte lds + 16 i.  Written as asm on purpose: for the builtin form hipcc's wait-count pass cannot tell
+// which ring slot a DMA writes, so it drains every outstanding DMA (vmcnt(0)) before each ds_read of any
+// slot -- no k-tile would stay in flight.  Here the kernel counts them itself (vm_wait before the barrier
+// that precedes the reads).  M0 is compiler-reserved: saved and restored inside the statement
+// (cdna_hip_programming.md section 5.7); `lds` must be wave-uniform.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const char* lds, unsigned voff) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(const lds_void*)lds);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(dst), "s"(r)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// one operand's share of a stage: ROWS rows of the operand (r in [row0, row0 + ROWS)), k in
+// [k0, k0 + KT) masked at kend; T = row-contiguous source (element (r, k) at k * ld + r) else
+// K-contiguous (r * ld + k).  Wave w issues the wave-instructions w, w + 4, ... (ROWS / 32 each).
+template <bool T, int ROWS>
+__device__ __forceinline__ void fill(__amdgpu_buffer_rsrc_t r, char* img, int row0, int k0, int kend, long ld,
+                                     int wave, int lane) {
+#pragma unroll
+  for (int q = 0; q < ROWS / 32; ++q) {
+    const int i = wave + 4 * q;   // wave-instruction: 1 KB of the image
+    unsigned voff;
+    if constexpr (!T) {
+      const int row = 8 * i + (lane >> 3), slot = lane & 7;
+      const int k = k0 + 4 * (slot ^ ((row >> 1) & 7));
+      voff = k < kend ? (unsigned)(((long)(row0 + row) * ld + k) * 4) : OOB;
+    } else {
+      constexpr int KR = 256 / ROWS;          // k-rows per wave-instruction
+      constexpr int SL = ROWS / 4;            // 16-B slots per k-row
+      const int kr = KR * i + lane / SL, sq = lane % SL;
+      const int col = ((((sq >> 2) ^ ((kr >> 2) & 1))) << 4) + ((sq & 3) << 2);
+      const int k = k0 + kr;
+      voff = k < kend ? (unsigned)(((long)k * ld + row0 + col) * 4) : OOB;
+    }
+    dma16(r, img + i * 1024, voff);
+  }
+}
+
+template <int BM, int BN, bool TA, bool TB, int NS>
+__global__ __launch_bounds__(256) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G, int zfast) {
+  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int SA_B = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int LOADS = BM / 32 + BN / 32;   // DMA wave-instructions per wave and stage
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const unsigned bid = blockIdx.x, q8 = total >> 3, r8 = total & 7, x8 = bid & 7;
+  const unsigned lin = x8 * q8 + min(x8, r8) + (bid >> 3);
+  int zs, xn, ym, zb;
+  if (zfast) {
+    zs = (int)(lin % (unsigned)g.nsplit);
+    const unsigned t1 = lin / (unsigned)g.nsplit;
+    xn = (int)(t1 % (unsigned)tn);
+    const unsigned t2 = t1 / (unsigned)tn;
+    ym = (int)(t2 % (unsigned)tm);
+    zb = (int)(t2 / (unsigned)tm);
+  } else {
+    xn = (int)(lin % (unsigned)tn);
+    const unsigned t1 = lin / (unsigned)tn;
+    ym = (int)(t1 % (unsigned)tm);
+    const unsigned t2 = t1 / (unsigned)tm;
+    zs = (int)(t2 % (unsigned)g.nsplit);
+    zb = (int)(t2 / (unsigned)g.nsplit);
+  }
+  const int z = zb * g.nsplit + zs;
+  const int m0 = ym * BM, n0 = xn * BN;
+  const int kbeg = zs * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const bool ones = g.Ne > g.N;
+  // operand descriptors (wave-uniform): the batch's whole operand, so the range check covers its edges
+  const unsigned a_bytes = (unsigned)((TA ? (long)g.K * g.lda : (long)g.M * g.lda) * 4);
+  const unsigned b_bytes = (unsigned)((TB ? (long)g.N * g.ldb : (long)g.K * g.ldb) * 4);
+  const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.A + (long)zb * g.sA), (short)0,
+                                                    (int)a_bytes, 0x00020000);
+  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.B + (long)zb * g.sB), (short)0,
+                                                    (int)b_bytes, 0x00020000);
+  typedef g2::Stage<false, TA, BM, false> SA;
+  typedef g2::Stage<false, !TB, BN, true> SB;
+  f32x4 acc[1][MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[0][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kend > kbeg ? (kend - kbeg + KT - 1) / KT : 0;
+  auto issue = [&](int t) {
+    char* st = smem + (t % NS) * STAGE;
+    const int k0 = kbeg + t * KT;
+    fill<TA, BM>(ra, st, m0, k0, kend, g.lda, wave, lane);
+    fill<!TB, BN>(rb, st + SA_B, n0, k0, kend, g.ldb, wave, lane);
+  };
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) issue(p);
+  // the implicit ones column of op(B) (bias gradient, B row-contiguous only): column N of the tile
+  const int ones_col = (ones && g.N >= n0 && g.N < n0 + BN) ? g.N - n0 : -1;
+  for (int t = 0; t < nk; ++t) {
+    // stage t has landed once at most the later stages' DMAs are outstanding
+    const int later = min(NS - 2, nk - 1 - t);
+    if (NS >= 4 && later >= 2) vm_wait<2 * LOADS>();
+    else if (NS >= 3 && later >= 1) vm_wait<LOADS>();
+    else vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the slot refilled below
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");                          // no LDS read moves above the barrier
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    const char* cur = smem + (t % NS) * STAGE;
+    if (ones_col >= 0) {
+      if (tid < KT) {
+        const int k = kbeg + t * KT + tid;
+        *reinterpret_cast<float*>(const_cast<char*>(cur) + SA_B + SB::rc_off(tid, ones_col)) = k < kend ? 1.f : 0.f;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * (BM / 2), wn * (BN / 2), lane, acc);
+  }
+
+  // C/D map of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (BM / 2) + mi * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * (BN / 2) + ni * 16 + (lane & 15);
+        if (m < g.M && n < g.Ne) {
+          if (g.nsplit > 1) g.part[((long)z * g.M + m) * g.Ne + n] = acc[0][mi][ni][r];
+          else store_out(g, zb, m, n, acc[0][mi][ni][r]);
+        }
+      }
+  if (g.nsplit == 1 || !g.cnt) return;
+  // in-launch split-K combine (as g2::gemm_mfma; flag through the idle ring)
+  int* last = reinterpret_cast<int*>(smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int tile = (zb * tm + ym) * tn + xn;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = __hip_atomic_fetch_add(&g.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = (tk == (unsigned)(g.nsplit - 1));
+  }
+  __syncthreads();
+  if (!*last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const long slab = (long)g.M * g.Ne;
+  const float* pz = g.part + (long)zb * g.nsplit * slab;
+  for (int e = tid; e < BM * BN; e += 256) {
+    const int m = m0 + e / BN, n = n0 + e % BN;
+    if (m >= g.M || n >= g.Ne) continue;
+    store_out(g, zb, m, n, g2::slab_sum(pz + (long)m * g.Ne + n, slab, g.nsplit, G));
+  }
+  if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace gp
+
 
 // C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b] (+ bias[n]) (+ addend[(m % add_mod), n]) (relu);
 // bias_grad (optional): bias_grad[m] = alpha * sum_k op(A)(m,k) + beta * bias_grad[m]
@@ -1064,23 +1271,22 @@ static int launch_legacy(int transA, int transB, int M, int N, int K, float alph
                          const float* bias, const float* addend, long add_ld, int add_mod, int flags,
                          float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
                          int n_counters, hipStream_t stream, GroupState* st) {
-  if (!st)
-    return launch_plan(plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc,
-                                   strideC, batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats,
-                                   tile_counters, n_counters),
-                       stream);
-  if (st->n == GROUP_MAX) {
-    const int rc = group_flush(*st);
+  // the plan (split-K slices, combine path) depends on the problem and the caller's whole workspace /
+  // counter arrays only -- never on what a group has used of them -- so a GEMM gives the same bits
+  // grouped or alone, whatever its neighbours (tests/test_model_gpu.py::test_lane_schedules_*)
+  LegacyPlan pl = plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
+                              batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
+                              n_counters);
+  if (!st) return launch_plan(pl, stream);
+  const long need = (pl.ws_floats + 63) / 64 * 64;
+  if (st->n == GROUP_MAX || st->ws_used + need > ws_floats || st->cnt_used + pl.counters > n_counters) {
+    const int rc = group_flush(*st);   // launch what is recorded; this problem starts a new group
     if (rc) return rc;
   }
   // this problem's slices of the workspace and the counters follow the earlier problems' slices
-  float* wsp = ws ? ws + st->ws_used : nullptr;
-  const long wsn = ws ? ws_floats - st->ws_used : 0;
-  unsigned int* cp = tile_counters ? tile_counters + st->cnt_used : nullptr;
-  const int cn = tile_counters ? n_counters - st->cnt_used : 0;
-  LegacyPlan pl = plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
-                              batch, bias, addend, add_ld, add_mod, flags, bias_grad, wsp, wsn, cp, cn);
-  st->ws_used += (pl.ws_floats + 63) / 64 * 64;
+  if (pl.g.nsplit > 1) pl.g.part = ws + st->ws_used;
+  if (pl.g.cnt) pl.g.cnt = tile_counters + st->cnt_used;
+  st->ws_used += need;
   st->cnt_used += pl.counters;
   st->plans[st->n++] = pl;
   return VC_OK;
@@ -1121,6 +1327,106 @@ VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alph
                    nullptr);
 }
 
+// ---- gemm_pipe launch configuration
+// Can the pipelined kernel take this problem?  fp32, one batch, 16-B aligned operands with leading
+// dimensions divisible by 4 and K % 4 == 0 (whole 16-B chunks along k), operands < 2 GB (32-bit buffer
+// offsets), the bias-gradient ones column only on a row-contiguous B.
+static bool pipe_fits(int transA, int transB, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                      int batch, const float* bias_grad) {
+  if (batch != 1 || K % 4 || lda % 4 || ldb % 4 || ((uintptr_t)A % 16) || ((uintptr_t)B % 16)) return false;
+  if (bias_grad && transB) return false;
+  const long ab = (transA ? (long)K * lda : (long)M * lda) * 4, bb = (transB ? (long)N * ldb : (long)K * ldb) * 4;
+  return ab < (1L << 31) && bb < (1L << 31);
+}
+
+// the shapes it pays on (tools/gemm_census.py): enough work per launch that the pipeline fills
+static bool pipe_wanted(int M, int N, int K) {
+  return vc_knob("VITCNN_GEMM_PIPE", 0) && (long)M * N * K >= (1L << 24) && K >= 128 && M >= 128 && N >= 64;
+}
+
+struct PipePlan {
+  int bm, bn, ns, nsplit, k_chunk, tn, tm;
+};
+
+static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws) {
+  PipePlan p;
+  p.bm = M >= 512 ? 128 : 64;
+  p.bn = Ne >= 192 ? 128 : 64;
+  if (g_tune.bm) p.bm = g_tune.bm;
+  if (g_tune.bn) p.bn = g_tune.bn;
+  p.ns = vc_knob("VITCNN_PIPE_NS", 4) == 2 ? 2 : 4;   // ring depth (knob: probe library)
+  p.tn = vc_cdiv(Ne, p.bn);
+  p.tm = vc_cdiv(M, p.bm);
+  const long tiles = (long)p.tn * p.tm;
+  // blocks per CU the LDS ring allows (128 KB for 128 x 128 at NS 4: one; 64 x 64: two)
+  const int per_cu = std::min(8, (160 * 1024) / ((p.bm + p.bn) * 128 * p.ns));
+  const long target = 256L * std::max(1, per_cu);
+  int nsplit = 1;
+  if (have_ws && tiles < target) {
+    const long want = (target + tiles - 1) / tiles;
+    const long by_k = std::max(1, K / (4 * gp::KT));   // slices of >= 4 k-tiles
+    nsplit = (int)std::min<long>(std::min(want, by_k), 64);
+  }
+  if (g_tune.nsplit) nsplit = std::min(g_tune.nsplit, std::max(1, K / gp::KT));
+  while (nsplit > 1 && (long)nsplit * M * Ne > ws_floats) --nsplit;
+  p.k_chunk = vc_cdiv(K, gp::KT) * gp::KT;
+  if (nsplit > 1) {
+    p.k_chunk = vc_cdiv(vc_cdiv(K, nsplit), gp::KT) * gp::KT;
+    nsplit = vc_cdiv(K, p.k_chunk);
+  }
+  p.nsplit = nsplit;
+  return p;
+}
+
+static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha, const float* A, long lda,
+                       const float* B, long ldb, float beta, float* C, long ldc, const float* bias,
+                       const float* addend, long add_ld, int add_mod, int flags, float* bias_grad, float* ws,
+                       long ws_floats, unsigned int* tile_counters, int n_counters, hipStream_t stream) {
+  Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, flags};
+  const int Ne = N + (bias_grad ? 1 : 0);
+  const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr);
+  const long tiles = (long)p.tn * p.tm;
+  const long slab_bytes = (long)p.nsplit * std::min(p.bm, M) * std::min(p.bn, Ne) * 4;
+  bool inl = slab_bytes <= g2_combine_limit();
+  if (g_tune.combine >= 0) inl = g_tune.combine == 1;
+  unsigned int* cnt = (p.nsplit > 1 && tile_counters && tiles <= n_counters && inl) ? tile_counters : nullptr;
+  GemmArgs g{M, N, K, Ne, p.k_chunk, p.nsplit, A, lda, 0, B, ldb, 0, C, ldc, 0, bias_grad, ws, cnt, epi};
+  const long total = tiles * p.nsplit;
+  VC_REQUIRE(total < (1L << 31));
+  const int G = g2::slab_groups(p.nsplit);
+  const int zfast = cnt ? 1 : 0;
+  dim3 grid((unsigned)total), block(256);
+#define VC_GP(BM_, BN_, NS_)                                                                                     \
+  do {                                                                                                           \
+    if (transA && transB)                                                                                        \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, true, true, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);   \
+    else if (transA)                                                                                             \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, true, false, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+    else if (transB)                                                                                             \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, false, true, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+    else                                                                                                         \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, false, false, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast); \
+  } while (0)
+#define VC_GP_T(NS_)                                    \
+  do {                                                  \
+    if (p.bm == 128 && p.bn == 128) VC_GP(128, 128, NS_); \
+    else if (p.bm == 128) VC_GP(128, 64, NS_);          \
+    else if (p.bn == 128) VC_GP(64, 128, NS_);          \
+    else VC_GP(64, 64, NS_);                            \
+  } while (0)
+  if (p.ns == 2) VC_GP_T(2);
+  else VC_GP_T(4);
+#undef VC_GP_T
+#undef VC_GP
+  VC_CHECK_LAUNCH();
+  if (p.nsplit > 1 && !cnt) {
+    const long nelem = (long)M * Ne;
+    hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, g, nelem, G);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
 static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
                      const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
                      float beta, float* C, long ldc, long strideC, int batch,
@@ -1131,6 +1437,14 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
   VC_REQUIRE(!bias_grad || batch == 1);
   if (M == 0 || N == 0) return VC_OK;
   const bool bf = (flags & F_BF16) != 0;
+  // fp32 mid shapes: the LDS-DMA pipelined kernel (F_PIPE forces it where it fits, F_NOPIPE keeps the
+  // older kernels: tests, census).  The choice depends on the problem only: a grouped problem that
+  // takes it launches at once on the group's stream
+  if (!bf && !(flags & (F_LEGACY | F_V2 | F_NOPIPE)) &&
+      pipe_fits(transA, transB, M, N, K, A, lda, B, ldb, batch, bias_grad) &&
+      ((flags & F_PIPE) || pipe_wanted(M, N, K)))
+    return launch_pipe(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, addend, add_ld, add_mod,
+                       flags & ~(F_PIPE | F_NOPIPE), bias_grad, ws, ws_floats, tile_counters, n_counters, stream);
   // fp32: the k-major kernel (faster on every shape of the ViT-CNN step, tools/gemm_census.py) except
   // long contractions (K >= 4096, e.g. FusAtNet's 3x3 convs over 1024-2193 channels), where the
   // K-contiguous kernel's two accumulator chains and <= 2048-long slices keep the fp32 rounding at

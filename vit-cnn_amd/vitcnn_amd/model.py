@@ -86,6 +86,13 @@ _BF16_EXACT: set = set()
 _BF16_MIN_K = 1024
 _GEMM_SITES = None
 _LANE_MAP = []       # logical lane -> stream index (empty: lane i on stream i)
+# the channel-feature backward chain's lane: 1 = after the local-conv chain on lane 1 (default); 3 = on
+# lane 3 beside it (measured slower, round 3: 2.01 -> 2.23 ms).  Both chains accumulate into the block's
+# input gradient dX; with _CH_ORDERED the side lane waits for the local chain before its accumulation,
+# so the sum is formed in the same order under every schedule (without that wait
+# the two read-modify-write GEMM epilogues race, and the result depends on the schedule)
+_CH_LANE = 1
+_CH_ORDERED = True
 _BN_TICKETS = False  # BN reductions in the last-arriving block: measured ~1% slower (every arrival is an agent-scope release = L2 writeback)
 
 UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
@@ -1072,20 +1079,27 @@ class _Program:
             with self.gemm_group():
                 self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, 2 * Ci, Cout, Fc, Cout, dFc, 1.0)
                 self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
+            side = self.lanes_on and _CH_LANE != 1
+            e_pg = self.mark() if side else None
             # local feature: BN -> conv3x3 -> ReLU backward (first accumulation into dX)
             self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0, tap=self._tap_dgrad(blk))
-            # channel feature: ln4 -> TokenLearner -> conv1x1
+            e_loc = self.mark() if side else None
+        # channel feature: ln4 -> TokenLearner -> conv1x1, after the local chain on lane 1 (or, measurement
+        # switch _CH_LANE, on a lane of its own beside it: see _CH_ORDERED)
+        with (self.lane(_CH_LANE, e0, e_pg) if side else self.lane(1)):
             Zc, dZc = f(pfx + ".channel_token.Z", M * Cout), f(pfx + ".dZc", M * Cout)
             self.ln_bwd(pfx + ".ln4", pfx + ".Fc", dFc, Zc, M, Cout, dZc, 0.0)
             CF, dCF = f(pfx + ".CF", rows * Cout), f(pfx + ".dCF", rows * Cout)
             self.token_learner_bwd(pfx + ".channel_token", CF, L_, Cout, S, dZc, dCF)
+            if side and dX and _CH_ORDERED:
+                self.wait(e_loc)   # the dX accumulations in program order: local, then channel
             with self.gemm_group():
                 self.linear_bwd(pfx + ".channel_feature.weight", pfx + ".channel_feature.bias", dCF, rows, Cout,
                                 Cin, X, Cin, 0, 0.0)
                 if dX:
                     self.mm_nn(rows, Cin, Cout, dCF, Cout, self.P[pfx + ".channel_feature.weight"], Cin, dX, Cin,
                                beta=1.0)
-            e_ch = self.mark()
+            e_ch = (self.mark(), e_loc) if side else (self.mark(),)
         # global feature: ln3 -> TokenLearner -> change_dim
         Zg, dZg = f(pfx + ".global_feature.Z", M * Cout), f(pfx + ".dZg", M * Cout)
         self.ln_bwd(pfx + ".ln3", pfx + ".Fg", dFg, Zg, M, Cout, dZg, 0.0, defer=True)
@@ -1219,7 +1233,7 @@ class _Program:
             self.defer_wgrad(True, 2 * D, E, rows, dXZ, 2 * D, Xn, E, G[mx + ".in_proj.weight"], E)
             self.flush_wgrads()   # dt_proj, x_proj, conv1d, in_proj
             if dX:
-                self.wait(e_ch)
+                self.wait(*e_ch)
             part = f(pfx + ".prepart", self.L.vc_rowchain_ln_part_floats(rows, E))
             self.L.vc_rowchain_front_bwd(rows, 2 * D, E, Cin, dXZ, P[mx + ".in_proj.weight"], T, f(pfx + ".Xn.m", rows),
                                          f(pfx + ".Xn.r", rows), P[gv + ".pre_norm.weight"], dT, dTt, part,
@@ -1230,7 +1244,7 @@ class _Program:
             self.flush_wgrads()   # dt_proj, x_proj, conv1d, in_proj
             self.ln_bwd(gv + ".pre_norm", pfx + ".Xn", dXn, T, rows, E, dTt, 0.0, res=dT, defer=True)   # dT + LN grad
             if dX:
-                self.wait(e_ch)
+                self.wait(*e_ch)
                 self.mm_nn(rows, Cin, E, dTt, E, P[gv + ".patch_embed.projection.weight"], Cin, dX, Cin, beta=1.0)
         # pos_embed and patch_embed weight gradients: off the critical path
         e = self.mark()
