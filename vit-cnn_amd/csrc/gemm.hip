@@ -905,13 +905,14 @@ __device__ __forceinline__ void vm_wait() {
 
 // one operand's share of a stage: ROWS rows of the operand (r in [row0, row0 + ROWS)), k in
 // [k0, k0 + KT) masked at kend; T = row-contiguous source (element (r, k) at k * ld + r) else
-// K-contiguous (r * ld + k).  Wave w issues the wave-instructions w, w + 4, ... (ROWS / 32 each).
-template <bool T, int ROWS>
+// K-contiguous (r * ld + k).  Wave w of NW issues the wave-instructions w, w + NW, ... (ROWS / 8 / NW each).
+template <bool T, int ROWS, int NW>
 __device__ __forceinline__ void fill(__amdgpu_buffer_rsrc_t r, char* img, int row0, int k0, int kend, long ld,
                                      int wave, int lane) {
+  static_assert((ROWS / 8) % NW == 0, "the waves split the stage's wave-instructions evenly");
 #pragma unroll
-  for (int q = 0; q < ROWS / 32; ++q) {
-    const int i = wave + 4 * q;   // wave-instruction: 1 KB of the image
+  for (int q = 0; q < ROWS / 8 / NW; ++q) {
+    const int i = wave + NW * q;   // wave-instruction: 1 KB of the image
     unsigned voff;
     if constexpr (!T) {
       const int row = 8 * i + (lane >> 3), slot = lane & 7;
@@ -929,15 +930,17 @@ __device__ __forceinline__ void fill(__amdgpu_buffer_rsrc_t r, char* img, int ro
   }
 }
 
-template <int BM, int BN, bool TA, bool TB, int NS>
-__global__ __launch_bounds__(256) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G, int zfast) {
-  constexpr int MT = BM / 32, NT = BN / 32;
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G, int zfast) {
+  constexpr int NW = WM * WN, NTH = 64 * NW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
+  constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int SA_B = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int LOADS = BM / 32 + BN / 32;   // DMA wave-instructions per wave and stage
+  constexpr int LOADS = (BM / 8 + BN / 8) / NW;   // DMA wave-instructions per wave and stage
   static_assert(NS >= 2 && NS <= 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const unsigned bid = blockIdx.x, q8 = total >> 3, r8 = total & 7, x8 = bid & 7;
   const unsigned lin = x8 * q8 + min(x8, r8) + (bid >> 3);
   int zs, xn, ym, zb;
@@ -980,8 +983,8 @@ __global__ __launch_bounds__(256) void gemm_pipe(GemmArgs g, int tn, int tm, uns
   auto issue = [&](int t) {
     char* st = smem + (t % NS) * STAGE;
     const int k0 = kbeg + t * KT;
-    fill<TA, BM>(ra, st, m0, k0, kend, g.lda, wave, lane);
-    fill<!TB, BN>(rb, st + SA_B, n0, k0, kend, g.ldb, wave, lane);
+    fill<TA, BM, NW>(ra, st, m0, k0, kend, g.lda, wave, lane);
+    fill<!TB, BN, NW>(rb, st + SA_B, n0, k0, kend, g.ldb, wave, lane);
   };
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
@@ -1008,7 +1011,7 @@ __global__ __launch_bounds__(256) void gemm_pipe(GemmArgs g, int tn, int tm, uns
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * (BM / 2), wn * (BN / 2), lane, acc);
+    g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
   }
 
   // C/D map of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
@@ -1018,8 +1021,8 @@ __global__ __launch_bounds__(256) void gemm_pipe(GemmArgs g, int tn, int tm, uns
     for (int ni = 0; ni < NT; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / 2) + mi * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wn * (BN / 2) + ni * 16 + (lane & 15);
+        const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * WTN + ni * 16 + (lane & 15);
         if (m < g.M && n < g.Ne) {
           if (g.nsplit > 1) g.part[((long)z * g.M + m) * g.Ne + n] = acc[0][mi][ni][r];
           else store_out(g, zb, m, n, acc[0][mi][ni][r]);
@@ -1046,7 +1049,7 @@ __global__ __launch_bounds__(256) void gemm_pipe(GemmArgs g, int tn, int tm, uns
   __syncthreads();
   const long slab = (long)g.M * g.Ne;
   const float* pz = g.part + (long)zb * g.nsplit * slab;
-  for (int e = tid; e < BM * BN; e += 256) {
+  for (int e = tid; e < BM * BN; e += NTH) {
     const int m = m0 + e / BN, n = n0 + e % BN;
     if (m >= g.M || n >= g.Ne) continue;
     store_out(g, zb, m, n, g2::slab_sum(pz + (long)m * g.Ne + n, slab, g.nsplit, G));
@@ -1341,35 +1344,35 @@ static bool pipe_fits(int transA, int transB, int M, int N, int K, const float* 
 
 // the shapes it pays on (tools/gemm_census.py): enough work per launch that the pipeline fills
 static bool pipe_wanted(int M, int N, int K) {
-  return vc_knob("VITCNN_GEMM_PIPE", 0) && (long)M * N * K >= (1L << 24) && K >= 128 && M >= 128 && N >= 64;
+  return vc_knob("VITCNN_GEMM_PIPE", 1) && (long)M * N * K >= (1L << 24) && K >= 128 && M >= 128 && N >= 64;
 }
 
 struct PipePlan {
   int bm, bn, ns, nsplit, k_chunk, tn, tm;
 };
 
+// Launch plan (tools/gemm_lab.hip sweep over the step's 21 critical-path shapes, profiles/r04_gemm_lab.log):
+// 64 x 64 tiles on 4 waves with a 2-stage ring (32 KB: up to 5 blocks per CU) won or tied on nearly every
+// shape; a grid of >= 128 tiles runs unsplit (the split-K slab reduce costs more than the extra blocks
+// gain), a smaller one splits K towards ~512 blocks in slices of >= 4 k-tiles (the weight gradients,
+// K = 1600-5184 rows over a 2 x 5 ... 4 x 21 tile grid).
 static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws) {
   PipePlan p;
-  p.bm = M >= 512 ? 128 : 64;
-  p.bn = Ne >= 192 ? 128 : 64;
+  p.bm = 64;
+  p.bn = 64;
   if (g_tune.bm) p.bm = g_tune.bm;
   if (g_tune.bn) p.bn = g_tune.bn;
-  p.ns = vc_knob("VITCNN_PIPE_NS", 4) == 2 ? 2 : 4;   // ring depth (knob: probe library)
+  p.ns = vc_knob("VITCNN_PIPE_NS", 2) == 4 ? 4 : 2;   // ring depth (knob: probe library)
   p.tn = vc_cdiv(Ne, p.bn);
   p.tm = vc_cdiv(M, p.bm);
   const long tiles = (long)p.tn * p.tm;
-  // blocks per CU the LDS ring allows (128 KB for 128 x 128 at NS 4: one; 64 x 64: two)
-  const int per_cu = std::min(8, (160 * 1024) / ((p.bm + p.bn) * 128 * p.ns));
-  const long target = 256L * std::max(1, per_cu);
+  const int kt = vc_cdiv(K, gp::KT);
   int nsplit = 1;
-  if (have_ws && tiles < target) {
-    const long want = (target + tiles - 1) / tiles;
-    const long by_k = std::max(1, K / (4 * gp::KT));   // slices of >= 4 k-tiles
-    nsplit = (int)std::min<long>(std::min(want, by_k), 64);
-  }
-  if (g_tune.nsplit) nsplit = std::min(g_tune.nsplit, std::max(1, K / gp::KT));
+  if (have_ws && tiles < 128)
+    nsplit = (int)std::max<long>(1, std::min<long>(std::min<long>((512 + tiles - 1) / tiles, kt / 4), 64));
+  if (g_tune.nsplit) nsplit = std::min(g_tune.nsplit, std::max(1, kt));
   while (nsplit > 1 && (long)nsplit * M * Ne > ws_floats) --nsplit;
-  p.k_chunk = vc_cdiv(K, gp::KT) * gp::KT;
+  p.k_chunk = kt * gp::KT;
   if (nsplit > 1) {
     p.k_chunk = vc_cdiv(vc_cdiv(K, nsplit), gp::KT) * gp::KT;
     nsplit = vc_cdiv(K, p.k_chunk);
@@ -1394,28 +1397,29 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
   const long total = tiles * p.nsplit;
   VC_REQUIRE(total < (1L << 31));
   const int G = g2::slab_groups(p.nsplit);
-  const int zfast = cnt ? 1 : 0;
-  dim3 grid((unsigned)total), block(256);
-#define VC_GP(BM_, BN_, NS_)                                                                                     \
+  // split slice fastest in the block order: a tile's K slices run side by side on one XCD (measured
+  // faster for every split shape of the step, tools/gemm_lab.hip; the in-launch combine reads its slabs there)
+  const int zfast = 1;
+  dim3 grid((unsigned)total);
+#define VC_GP(BM_, BN_, WM_, WN_, NS_)                                                                          \
   do {                                                                                                           \
     if (transA && transB)                                                                                        \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, true, true, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);   \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, true, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);   \
     else if (transA)                                                                                             \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, true, false, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, false, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
     else if (transB)                                                                                             \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, false, true, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, true, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
     else                                                                                                         \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, false, false, NS_>), grid, block, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast); \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, false, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast); \
   } while (0)
-#define VC_GP_T(NS_)                                    \
-  do {                                                  \
-    if (p.bm == 128 && p.bn == 128) VC_GP(128, 128, NS_); \
-    else if (p.bm == 128) VC_GP(128, 64, NS_);          \
-    else if (p.bn == 128) VC_GP(64, 128, NS_);          \
-    else VC_GP(64, 64, NS_);                            \
+#define VC_GP_T(NS_)                                                \
+  do {                                                              \
+    if (p.bm == 128 && p.bn == 64) VC_GP(128, 64, 4, 2, NS_);        \
+    else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_);   \
+    else VC_GP(64, 64, 2, 2, NS_);                                  \
   } while (0)
-  if (p.ns == 2) VC_GP_T(2);
-  else VC_GP_T(4);
+  if (p.ns == 4) VC_GP_T(4);
+  else VC_GP_T(2);
 #undef VC_GP_T
 #undef VC_GP
   VC_CHECK_LAUNCH();
