@@ -401,6 +401,8 @@ VC_API int vc_index_add_i64(int n, const int* idx, long long* ptr, long long val
 /* dx = dy * (y > 0)  (nn.ReLU backward from the saved output) */
 VC_API int vc_relu_bwd(long n, const float* dy, const float* y, float* dx, hipStream_t stream);
 VC_API int vc_fill(long n, float* ptr, float value, hipStream_t stream);
+/* ptr[idx[i]] = value  (the alignment gaps of the flat gradient: parameters start 16-B aligned) */
+VC_API int vc_fill_index(int n, const int* idx, float* ptr, float value, hipStream_t stream);
 
 /* ---------------------------------------------------------------- patch windows (callers of the step)
  * The reference cuts patches on the host: MultiModalX.__getitem__ (datasets.py:550-593) for

@@ -80,7 +80,15 @@ def test_get_model_defaults_and_unknown_name():
     w = kw["weights"]
     assert w[0] == 0 and float(w[1:].sum()) == 15
     assert sum(p.numel() for p in model.parameters()) == 1661260
-    assert model.n_active_params == 1661260 - 1170
+    # 1,660,090 of them receive gradients; in the flat buffer every parameter starts 16-B aligned, so the
+    # active section [0, n_active) also holds zero-filled alignment gaps (fewer than 4 floats each)
+    from vitcnn_amd.model import UNUSED_PREFIXES
+    named = dict(model.named_parameters())
+    active = [n for n in named if not n.startswith(UNUSED_PREFIXES)]
+    assert sum(named[n].numel() for n in active) == 1661260 - 1170
+    assert all(model._poff[n] % 4 == 0 for n in named)
+    assert model.n_active_params % 4 == 0 and 0 <= model.n_active_params - 1660090 < 4 * len(active)
+    assert len(model._gaps) == model.n_active_params - 1660090
 
 
 def test_state_dict_contract():

@@ -241,7 +241,16 @@ def test_bucketed_exchange_world4_equals_mean_of_shards():
     finally:
         torch.set_num_threads(nt)
     ranges = out[0][2]
-    assert ranges == {"tail": (1595080, 1660090), "hsi2": (873324, 1595080), "hsi1": (0, 873324)}
+    # the buckets tile [0, n_active): hsi1 first in the layout, then hsi2, then the tail (LiDAR, fusion,
+    # classifier), each holding exactly its block's parameters (plus alignment gaps)
+    assert ranges["hsi1"][0] == 0 and ranges["hsi1"][1] == ranges["hsi2"][0]
+    assert ranges["hsi2"][1] == ranges["tail"][0] and ranges["tail"][1] == m.n_active_params
+    named = dict(m.named_parameters())
+    for n, o in m._poff.items():
+        if o >= m.n_active_params:
+            continue
+        b = "hsi1" if n.startswith("hsi1.") else "hsi2" if n.startswith("hsi2.") else "tail"
+        assert ranges[b][0] <= o and o + named[n].numel() <= ranges[b][1], n
     for r in range(world):
         g, scale, _ = out[r]
         assert scale == 1.0 / world

@@ -196,8 +196,11 @@ def test_flat_model_exposes_per_parameter_grad_views():
     before = v.flat_params.detach().clone()
     torch.optim.SGD(v.parameters(), lr=0.5).step()
     assert named["classifier.weight"].grad is not None
-    moved = (before - v.flat_params.detach())[: v.n_active_params]
-    assert torch.allclose(moved, torch.full_like(moved, 0.5))
+    moved = before - v.flat_params.detach()
+    for n, o in v._poff.items():
+        k = named[n].numel()
+        want = 0.5 if o < v.n_active_params else 0.0          # the never-used parameters have no gradient
+        assert torch.allclose(moved[o:o + k], torch.full((k,), want)), n
     # the views fast path keys on the last ACTIVE parameter (the unused tail keeps grad None)
     from vitcnn_amd.flat import _last_active_name
     last = _last_active_name(v, v._pnames)

@@ -313,6 +313,11 @@ __global__ void fill_f32(long n, float* __restrict__ p, float v) {
   if (i < n) p[i] = v;
 }
 
+__global__ void fill_index_f32(int n, const int* __restrict__ idx, float* __restrict__ p, float v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[idx[i]] = v;
+}
+
 }  // namespace
 
 VC_API int vc_cat2_fwd(long M, int C1, int C2, const float* x1, long ld1, const float* x2, long ld2, int exchange,
@@ -440,6 +445,14 @@ VC_API int vc_relu_bwd(long n, const float* dy, const float* y, float* dx, hipSt
   VC_REQUIRE(n >= 0);
   if (n == 0) return VC_OK;
   hipLaunchKernelGGL(relu_bwd, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, dy, y, dx);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_fill_index(int n, const int* idx, float* ptr, float value, hipStream_t stream) {
+  VC_REQUIRE(n >= 0);
+  if (n == 0) return VC_OK;
+  hipLaunchKernelGGL(fill_index_f32, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, idx, ptr, value);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

@@ -55,6 +55,7 @@ _IMPLICIT_CONV = False
 # graph edge costs more than one GEMM's overlap gains); False: every weight gradient in place
 _DEFER_WGRAD = True
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
+PARAM_ALIGN = 4            # floats: flat-buffer alignment of every parameter (16 B)
 GEMM_GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES (include/vitcnn.h)
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
@@ -176,15 +177,37 @@ class Multimodality_Mamba(nn.Module):
                 first = min(idx[n] for n in group)
                 rest = [it for it in active if it[0] not in group]
                 active = rest[:first] + items + rest[first:]
+        # every parameter starts 16-B aligned (PARAM_ALIGN floats): the GEMM kernels stage weights by
+        # 16-B LDS-DMA / float4 loads, which an arbitrary float offset would rule out.  The gaps hold
+        # zeros in the parameters and in every gradient (the backward zeroes them: vc_fill_index)
         self._poff: Dict[str, int] = {}
         off = 0
-        for n, p in active + unused:
+        for n, p in active:
+            off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
             self._poff[n] = off
             off += p.numel()
-        self._n_active = sum(p.numel() for _, p in active)
+        self._n_active = -(-off // PARAM_ALIGN) * PARAM_ALIGN
+        off = self._n_active
+        for n, p in unused:
+            off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
+            self._poff[n] = off
+            off += p.numel()
         self._n_params = off
+        self._n_elems = sum(p.numel() for _, p in named)
+        covered = torch.zeros(self._n_active, dtype=torch.bool)
+        for n, p in active:
+            covered[self._poff[n]:self._poff[n] + p.numel()] = True
+        self._gaps = (~covered).nonzero().flatten().to(torch.int32).tolist()
+        for pfx in ("hsi1", "hsi2"):   # the stacked phi | g projection needs its four tensors adjacent
+            nl = pfx + ".FusionLayer.cross_attention."
+            w, g_, b, gb = (self._poff.get(nl + k) for k in ("phi.0.weight", "g.0.weight", "phi.0.bias", "g.0.bias"))
+            if w is not None:
+                ci = dict(named)[nl + "phi.0.bias"].numel()
+                cout = dict(named)[nl + "phi.0.weight"].numel() // ci
+                if not (g_ == w + ci * cout and b == g_ + ci * cout and gb == b + ci):
+                    raise RuntimeError(f"{nl}phi / g are not adjacent in the flat layout")
         device = named[0][1].device
-        flat = torch.empty(off, dtype=torch.float32, device=device)
+        flat = torch.zeros(off, dtype=torch.float32, device=device)
         for n, p in named:
             flat[self._poff[n]:self._poff[n] + p.numel()].copy_(p.detach().reshape(-1))
         self._pnames = [n for n, _ in active + unused]
@@ -263,7 +286,7 @@ class Multimodality_Mamba(nn.Module):
     def _ensure_flat(self):
         if not self._flat_intact():  # e.g. parameters replaced by user code: re-flatten current values
             dev = self._flat_store.device
-            flat = torch.empty(self._n_params, dtype=torch.float32, device=dev)
+            flat = torch.zeros(self._n_params, dtype=torch.float32, device=dev)
             for n in self._pnames:
                 m, pn = self._pmods[n]
                 o = self._poff[n]
@@ -367,6 +390,7 @@ class Multimodality_Mamba(nn.Module):
                 t[("order", H)] = torch.tensor(orders, dtype=torch.int32, device=device).contiguous()
                 t[("inv", H)] = torch.tensor(inv, dtype=torch.int32, device=device).contiguous()
             t["tracked"] = torch.tensor(self._tracked, dtype=torch.int32, device=device)
+            t["gaps"] = torch.tensor(self._gaps, dtype=torch.int32, device=device)
             self._dev_cache[key] = t
         return t
 
@@ -1269,10 +1293,13 @@ class _Program:
         m, B, ws = self.m, self.B, self.ws
         self.lanes_on = lanes and _LANES and _LANES_BWD
         grad = out if out is not None else torch.empty(m._n_params, dtype=torch.float32, device=self.device)
-        if m._n_params > m._n_active:  # parameters the reference forward never uses get no gradient
-            # (off lane 0's chain: nothing reads this range before the final join)
+        if m._n_params > m._n_active or m._gaps:
+            # parameters the reference forward never uses get no gradient, and the alignment gaps stay zero
+            # (off lane 0's chain: nothing reads these entries before the final join)
             with self.lane(3, self.mark()):
                 self.L.vc_fill(m._n_params - m._n_active, grad.data_ptr() + F32 * m._n_active, 0.0, self.s)
+                gaps = self.tab["gaps"]
+                self.L.vc_fill_index(gaps.numel(), gaps.data_ptr(), grad.data_ptr(), 0.0, self.s)
         gb = grad.data_ptr()
         self.G = {n: gb + F32 * o for n, o in m._poff.items()}
         Pp = m.patch

@@ -22,7 +22,8 @@ class AdamW(torch.optim.Optimizer):
         if owner is None or len(owners) != 1:
             raise ValueError("vitcnn_amd.optim.AdamW expects the parameters of one vitcnn_amd model")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        if sum(p.numel() for g in self.param_groups for p in g["params"]) != owner()._n_params:
+        if sum(p.numel() for g in self.param_groups for p in g["params"]) != getattr(owner(), "_n_elems",
+                                                                                      owner()._n_params):
             raise ValueError("vitcnn_amd.optim.AdamW must be given all parameters of the model")
         self._owner = owner
         self.grad_scale = 1.0   # data-parallel: 1/world_size folded into the update

@@ -131,20 +131,26 @@ BUCKETS = (("tail", ("lidar1.", "lidar2.", "fusion1.", "fusion2.", "classifier."
 
 def bucket_ranges(model):
     """{bucket: (lo, hi)} over the model's flat parameter layout; the buckets are contiguous,
-    disjoint and together cover exactly the active parameters [0, n_active)."""
+    disjoint and together cover exactly the active parameters [0, n_active).  Parameters start 16-B
+    aligned (model.PARAM_ALIGN), so a bucket may hold alignment gaps (< 4 floats each, zero in every
+    gradient); each bucket runs up to the next bucket's first parameter."""
     named = dict(model.named_parameters())
-    out = {}
+    spans = {}
     for name, prefixes in BUCKETS:
-        offs = [(o, o + named[n].numel()) for n, o in model._poff.items()
-                if n.startswith(prefixes) and o < model.n_active_params]
-        lo, hi = min(a for a, _ in offs), max(b for _, b in offs)
-        if sum(b - a for a, b in offs) != hi - lo:
+        offs = sorted((o, o + named[n].numel()) for n, o in model._poff.items()
+                      if n.startswith(prefixes) and o < model.n_active_params)
+        if any(b[0] - a[1] >= 4 or b[0] < a[1] for a, b in zip(offs, offs[1:])):
             raise RuntimeError(f"gradient bucket {name} is not contiguous in the flat layout")
-        out[name] = (lo, hi)
-    spans = sorted(out.values())
-    if spans[0][0] != 0 or spans[-1][1] != model.n_active_params or \
-            any(a[1] != b[0] for a, b in zip(spans, spans[1:])):
+        spans[name] = (offs[0][0], offs[-1][1])
+    order = sorted(spans, key=lambda k: spans[k][0])
+    if spans[order[0]][0] != 0 or spans[order[-1]][1] > model.n_active_params:
         raise RuntimeError("gradient buckets do not tile the active parameters")
+    out = {}
+    for i, name in enumerate(order):
+        hi = spans[order[i + 1]][0] if i + 1 < len(order) else model.n_active_params
+        if hi - spans[name][1] >= 4 or hi < spans[name][1]:
+            raise RuntimeError("gradient buckets do not tile the active parameters")
+        out[name] = (spans[name][0], hi)
     return out
 
 
