@@ -38,7 +38,10 @@
  * op(A)(m,k) = transA ? A[k*lda+m] : A[m*lda+k];  op(B)(k,n) = transB ? B[n*ldb+k] : B[k*ldb+n].
  * fp32 in / fp32 accumulate on v_mfma_f32_16x16x4_f32, or, with flags&2, bf16 operands (rounded
  * RNE as they are staged) with fp32 accumulation on v_mfma_f32_16x16x32_bf16 (the config-2 mode);
- * flags&4 / flags&8 force the k-major / K-contiguous fp32 kernel (default: chosen by shape).
+ * flags&4 / flags&8 force the k-major / K-contiguous fp32 kernel, flags&16 / flags&32 take / skip the
+ * pipelined LDS-DMA fp32 kernel (default: chosen by shape).  flags&64 turns the addend into a mask:
+ * the result (after alpha, beta, bias) is kept where addend[(m % add_mod)*add_ld + n] > 0 and zeroed
+ * elsewhere -- a ReLU backward through that layer output, fused into the GEMM producing the gradient.
  * Split-K (fixed-order, deterministic) when the output grid is small and ws is given.  bias_grad (batch 1 only, may be null) additionally receives
  * alpha * sum_k op(A)(m,k) (+ beta * bias_grad[m]) through an implicit ones column of op(B): the
  * bias gradient of a layer rides along its weight-gradient GEMM.  Replaces nn.Conv2d 1x1 /
@@ -73,9 +76,11 @@ VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
  * (8-byte aligned) holding the group's state -- the library keeps none, so distinct groups (one per
  * stream / thread) are independent and every entry point stays reentrant.  vc_gemm_group_begin
  * opens it for `stream`; vc_gemm_group_add takes vc_gemm_ex's arguments (minus the stream): the fp32
- * k-major problems are recorded, anything else (bf16 operands, long K) launches at once on the
- * group's stream; vc_gemm_group_end launches the recorded problems as one grid (up to 8 per launch)
- * plus one grouped split-K reduce.  The problems must not depend on each other; each takes its own
+ * problems of the k-major and of the pipelined kernel are recorded, anything else (bf16 operands,
+ * long K) launches at once on the group's stream; vc_gemm_group_end launches the recorded problems as
+ * one grid per kernel (up to 8 problems each) plus one grouped split-K reduce.  A problem's plan
+ * depends on its shape and the workspace / counters passed to it only, so its result is bit-identical
+ * grouped or alone.  The problems must not depend on each other; each takes its own
  * slice of the workspace and arrival counters passed to it.  Misuse (add / end on a group that is
  * not open) returns 1. */
 #define VC_GEMM_GROUP_BYTES 16384

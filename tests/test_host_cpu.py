@@ -86,7 +86,7 @@ def test_get_model_defaults_and_unknown_name():
     named = dict(model.named_parameters())
     active = [n for n in named if not n.startswith(UNUSED_PREFIXES)]
     assert sum(named[n].numel() for n in active) == 1661260 - 1170
-    assert all(model._poff[n] % 4 == 0 for n in named)
+    assert all(model._poff[n] % 4 == 0 for n in named if named[n].numel() >= 64)
     assert model.n_active_params % 4 == 0 and 0 <= model.n_active_params - 1660090 < 4 * len(active)
     assert len(model._gaps) == model.n_active_params - 1660090
 

@@ -347,11 +347,24 @@ GROUP_PROBLEMS = [
 ]
 
 
-@pytest.mark.parametrize("n", [2, 3, 9])
-def test_gemm_group_is_bit_identical(L, ws, n):
-    """vc_gemm_group_begin / _end (one grouped grid + one grouped split-K reduce, 8 problems per launch)
-    == the same GEMMs launched one by one, bit for bit, including the in-launch combine's counters"""
-    probs = GROUP_PROBLEMS[:n]
+# problems the automatic choice sends to the pipelined LDS-DMA kernel (a weight gradient with its bias
+# column and K split, a data gradient, a 1x1-conv forward) beside k-major ones
+GROUP_PROBLEMS_PIPE = [
+    (1, 0, 256, 1296, 3136, 1, True, 0.0),
+    (0, 0, 3136, 512, 256, 1, False, 1.0),
+    (0, 1, 3136, 256, 512, 1, False, 0.0),
+    (1, 0, 72, 9, 5000, 1, True, 0.0),
+    (1, 0, 144, 288, 1600, 1, True, 1.0),
+]
+
+
+@pytest.mark.parametrize("n,auto", [(2, False), (3, False), (9, False), (5, True), (14, True)])
+def test_gemm_group_is_bit_identical(L, ws, n, auto):
+    """vc_gemm_group_begin / _add / _end (one grouped k-major grid, one grouped pipelined grid, one grouped
+    split-K reduce, 8 problems of each kind per launch) == the same GEMMs launched one by one, bit for
+    bit, including the in-launch combine's counters; `auto`: the automatic kernel choice (pipelined
+    problems mixed in), else the k-major kernel forced"""
+    probs = (GROUP_PROBLEMS_PIPE + GROUP_PROBLEMS)[:n] if auto else GROUP_PROBLEMS[:n]
     cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
     ins, outs = [], []
     for i, (ta, tb, M, N, K, batch, bg, beta) in enumerate(probs):
@@ -368,8 +381,8 @@ def test_gemm_group_is_bit_identical(L, ws, n):
             C = rnd(batch, M, N, seed=90 + i).to(DEV)
             bgr = torch.full((M,), 0.25, device=DEV) if bg else None
             args = (ta, tb, M, N, K, 1.0, P(A), M if ta else K, A[0].numel(), P(B), K if tb else N, B[0].numel(),
-                    beta, P(C), N, C[0].numel(), batch, None, None, 0, 0, F_LEGACY, P(bgr), P(ws), ws.numel(),
-                    P(cnt), cnt.numel())
+                    beta, P(C), N, C[0].numel(), batch, None, None, 0, 0, 0 if auto else F_LEGACY, P(bgr), P(ws),
+                    ws.numel(), P(cnt), cnt.numel())
             if grouped:
                 L.vc_gemm_group_add(ctypes.addressof(grp), *args)
             else:

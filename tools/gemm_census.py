@@ -1,4 +1,4 @@
-"""GPU tool: every vc_gemm_ex call of one training step (B=64), re-timed in isolation with HIP events.
+"""GPU tool: every vc_gemm_ex / vc_gemm_group_add problem of one training step (B=64), re-timed in isolation with HIP events.
 Prints shape, layout and time per call for the first-round fp32 kernel (legacy), the current fp32
 kernel and the bf16-operand kernel, sorted by the current fp32 time.
 usage: python tools/gemm_census.py [reps]"""
@@ -25,16 +25,20 @@ def main():
     torch.cuda.synchronize()
     L = lib()
     calls = []
-    orig = L.vc_gemm_ex
+    orig, orig_add = L.vc_gemm_ex, L.vc_gemm_group_add
 
     def spy(*a):
         calls.append(a)
         return orig(*a)
 
-    L.vc_gemm_ex = spy
+    def spy_add(group, *a):   # grouped problems: vc_gemm_ex's arguments without the stream
+        calls.append(a + (None,))
+        return orig_add(group, *a)
+
+    L.vc_gemm_ex, L.vc_gemm_group_add = spy, spy_add
     fused_train_step(m, crit, hsi, lidar, tgt)
     torch.cuda.synchronize()
-    L.vc_gemm_ex = orig
+    L.vc_gemm_ex, L.vc_gemm_group_add = orig, orig_add
     raw = L.raw["vc_gemm_ex"]
     st = torch.cuda.Stream(dev)
     def time_call(a, extra_flags):
@@ -56,15 +60,15 @@ def main():
         batch = a[16]
         base = a[21] & ~(2 | 4 | 8 | 16 | 32)
         a = a[:21] + (base,) + a[22:]
-        t_auto, t_leg, t_v2, t_bf = time_call(a, 0), time_call(a, 4), time_call(a, 8), time_call(a, 2)
+        t_auto, t_leg, t_v2, t_bf = time_call(a, 0), time_call(a, 4), time_call(a, 16), time_call(a, 2)
         fl = 2.0 * M * N * K * batch
         rows.append((t_auto, t_leg, t_v2, t_bf, ta, tb, M, N, K, batch, a[22] is not None,
                      fl / min(t_leg, t_v2) * 1e-6, fl / t_bf * 1e-6))
     rows.sort(reverse=True)
     tots = [sum(r[i] for r in rows) for i in range(4)]
-    print(f"{len(rows)} GEMMs, isolated sums (us): auto {tots[0]:.1f}  legacy {tots[1]:.1f}  v2 {tots[2]:.1f}  "
+    print(f"{len(rows)} GEMMs, isolated sums (us): auto {tots[0]:.1f}  legacy {tots[1]:.1f}  pipe {tots[2]:.1f}  "
           f"bf16 {tots[3]:.1f}")
-    print("  auto legacy     v2   bf16  tA tB      M      N      K  batch bgrad TF(fp32) TF(bf16)")
+    print("  auto legacy   pipe   bf16  tA tB      M      N      K  batch bgrad TF(fp32) TF(bf16)")
     for r in rows:
         print("%6.1f %6.1f %6.1f %6.1f  %d  %d %6d %6d %6d %5d %5s %8.1f %8.1f" % r)
 

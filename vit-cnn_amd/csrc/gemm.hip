@@ -17,12 +17,12 @@ namespace {
 constexpr int BM = 64, BN = 64;
 constexpr int LDS_STRIDE = 81;  // 64 + 17: conflict-free fragment reads, <=2-way stores
 
-enum { F_RELU = 1, F_BF16 = 2, F_LEGACY = 4, F_V2 = 8, F_PIPE = 16, F_NOPIPE = 32 };
+enum { F_RELU = 1, F_BF16 = 2, F_LEGACY = 4, F_V2 = 8, F_PIPE = 16, F_NOPIPE = 32, F_MASK = 64 };
 
 struct Epi {
   float alpha, beta;
   const float* bias;     // [N] or null
-  const float* addend;   // addend[(m % add_mod) * add_ld + n] or null
+  const float* addend;   // addend[(m % add_mod) * add_ld + n] or null; with F_MASK a ReLU output mask
   long add_ld;
   int add_mod;
   int flags;
@@ -32,7 +32,11 @@ __device__ __forceinline__ float epilogue(const Epi& e, float acc, const float* 
   float v = e.alpha * acc;
   if (e.beta != 0.f) v += e.beta * (*cptr);
   if (e.bias) v += e.bias[n];
-  if (e.addend) v += e.addend[(long)(m % e.add_mod) * e.add_ld + n];
+  if (e.addend) {
+    const float a = e.addend[(long)(m % e.add_mod) * e.add_ld + n];
+    if (e.flags & F_MASK) v = a > 0.f ? v : 0.f;   // ReLU backward through the layer output `a`
+    else v += a;
+  }
   if (e.flags & F_RELU) v = fmaxf(v, 0.f);
   return v;
 }
@@ -81,6 +85,32 @@ __device__ __forceinline__ void tile_idx(int tid, int e, int& r, int& k) {
     if (T) { r = tid & 63; k = (tid >> 6) + 4 * e; }
     else   { k = tid & 31; r = (tid >> 5) + 8 * e; }
   }
+}
+
+// The fixed summation order of split-K slices (every combine path of every kernel): G interleaved partial sums
+// s_g = sum over z = g, g+G, ... (ascending), then s_0 + s_1 + ... + s_{G-1} left to right.  G (a
+// power of two <= 16) depends on nsplit only (slab_groups), so the in-launch and the separate
+// combine give bit-identical results.
+__host__ __device__ inline int slab_groups(int nsplit) {
+  int g = 1;
+  while (g < 16 && 4 * (2 * g) <= nsplit) g *= 2;
+  return g;
+}
+
+__device__ __forceinline__ float slab_sum(const float* p, long slab, int nsplit, int G) {
+  float s[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) s[g] = 0.f;
+  for (int z0 = 0; z0 < nsplit; z0 += G) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+      if (g < G && z0 + g < nsplit) s[g] += p[(z0 + g) * slab];
+  }
+  float t = s[0];
+#pragma unroll
+  for (int g = 1; g < 16; ++g)
+    if (g < G) t += s[g];
+  return t;
 }
 
 // One 64x64 output tile (bx, by) of K slice / batch bz; tn x tm tiles per slice (the arrival-counter
@@ -227,8 +257,8 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
 
   // In-launch split-K combine (cdna_hip_programming.md, "In-launch split-K reduction"): every
   // slice publishes its slab (stores drained, barrier, one agent-scope release), takes a ticket;
-  // the tile's last arriver acquires and sums all slices in fixed z order — the same order as
-  // splitk_reduce, so results do not depend on which slice arrives last — then re-zeroes the
+  // the tile's last arriver acquires and sums all slices in slab_sum's fixed order — the same order
+  // as the separate reduce, so results do not depend on which slice arrives last — then re-zeroes the
   // counter for the next launch on this stream.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -251,11 +281,7 @@ __device__ __forceinline__ void gemm_f32_tile(const GemmArgs& g, int bx, int by,
   for (int e = tid; e < BM * BN; e += 256) {
     const int m = m0 + (e >> 6), n = n0 + (e & 63);
     if (m >= g.M || n >= g.Ne) continue;
-    const float* p = pz + (long)m * g.Ne + n;
-    float sum = 0.f;
-#pragma unroll 8
-    for (int z = 0; z < g.nsplit; ++z) sum += p[z * slab];
-    store_out(g, zb, m, n, sum);
+    store_out(g, zb, m, n, slab_sum(pz + (long)m * g.Ne + n, slab, g.nsplit, slab_groups(g.nsplit)));
   }
   if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -332,38 +358,6 @@ __global__ __launch_bounds__(256) void gemm_f32_group(GemmGroup G) {
     default: break;
   }
 #undef VC_TILE
-}
-
-// grouped split-K reduce: block b of problem p covers 64 output columns of one row (as splitk_reduce)
-__global__ __launch_bounds__(64) void splitk_reduce_group(GemmGroup G) {
-  const int b = blockIdx.x;
-  const GroupSel sel = group_select(G, b);
-  const GemmArgs& g = sel.g;
-  const int local = b - sel.start;
-  const int nx = (g.Ne + 63) / 64;
-  const int n = (local % nx) * 64 + threadIdx.x;
-  if (n >= g.Ne) return;
-  const int m = (local / nx) % g.M, bb = local / (nx * g.M);
-  const long slab = (long)g.M * g.Ne;
-  const float* pp = g.part + (long)bb * g.nsplit * slab + (long)m * g.Ne + n;
-  float s = 0.f;
-#pragma unroll 8
-  for (int z = 0; z < g.nsplit; ++z) s += pp[z * slab];
-  store_out(g, bb, m, n, s);
-}
-
-// grid (ceil(Ne/64), M, batch): one thread per output element, no index division; the
-// nsplit slab reads are independent (unrolled) and summed in fixed z order (deterministic)
-__global__ __launch_bounds__(64) void splitk_reduce(GemmArgs g) {
-  const int n = blockIdx.x * 64 + threadIdx.x;
-  if (n >= g.Ne) return;
-  const int m = blockIdx.y, b = blockIdx.z;
-  const long slab = (long)g.M * g.Ne;
-  const float* p = g.part + (long)b * g.nsplit * slab + (long)m * g.Ne + n;
-  float s = 0.f;
-#pragma unroll 8
-  for (int z = 0; z < g.nsplit; ++z) s += p[z * slab];
-  store_out(g, b, m, n, s);
 }
 
 // Column sums: block (cx, ry) sums rows [ry*rows_per, ...) of 64 columns (4 row lanes, combined in
@@ -629,31 +623,8 @@ __device__ __forceinline__ void mma_ktile(const char* As, const char* Bs, int ar
   }
 }
 
-// The fixed summation order of split-K slices (both combine paths): G interleaved partial sums
-// s_g = sum over z = g, g+G, ... (ascending), then s_0 + s_1 + ... + s_{G-1} left to right.  G (a
-// power of two <= 16) depends on nsplit only (slab_groups), so the in-launch and the separate
-// combine give bit-identical results.
-static inline int slab_groups(int nsplit) {
-  int g = 1;
-  while (g < 16 && 4 * (2 * g) <= nsplit) g *= 2;
-  return g;
-}
-
-__device__ __forceinline__ float slab_sum(const float* p, long slab, int nsplit, int G) {
-  float s[16];
-#pragma unroll
-  for (int g = 0; g < 16; ++g) s[g] = 0.f;
-  for (int z0 = 0; z0 < nsplit; z0 += G) {
-#pragma unroll
-    for (int g = 0; g < 16; ++g)
-      if (g < G && z0 + g < nsplit) s[g] += p[(z0 + g) * slab];
-  }
-  float t = s[0];
-#pragma unroll
-  for (int g = 1; g < 16; ++g)
-    if (g < G) t += s[g];
-  return t;
-}
+using ::slab_groups;
+using ::slab_sum;
 
 // Block = 4 waves (2 x 2) over a BM x BN output tile, each wave (BM/2) x (BN/2).  1-D grid of
 // nsplit * tn * tm * batch blocks in XCD-aware order: the hardware deals block i to XCD i % 8, and
@@ -815,36 +786,45 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g, int tn, int tm, uns
 // Separate split-K combine for large slab volumes: a block covers 256/G lanes x 4 consecutive output
 // elements (row-major over [batch][M][Ne], so rows wrap) x G z-groups (z = g, g+G, ...); the G
 // partial sums meet in LDS and are added in slab_sum's order (bit-identical to the in-launch path).
-__global__ __launch_bounds__(256) void splitk_reduce4(GemmArgs g, long nelem, int G) {
-  __shared__ float sh[1024];
+// block `blk` of the reduce over nelem = batch * M * Ne elements
+__device__ __forceinline__ void reduce4_block(const GemmArgs& g, long nelem, int G, long blk, float* sh) {
   const int lanes = 256 / G;
   const int lane = threadIdx.x % lanes, zg = threadIdx.x / lanes;
   const int per_block = 4 * lanes;
-  const long e0 = (long)blockIdx.x * per_block + 4 * lane;
-  const long slab = (long)g.M * g.Ne;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  const int e0 = (int)(blk * per_block) + 4 * lane;   // nelem < 2^31 (host check)
+  const int slab = g.M * g.Ne;
+  const long zs = slab;
+  // the 4 elements' slab columns first, then z outer / element inner: 4 x 8 independent loads in
+  // flight per thread while each element's adds stay in ascending z
+  const float* p[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const long e = e0 + i;
-    if (e < nelem) {
-      const long b = e / slab, w = e - b * slab;
-      const float* p = g.part + b * g.nsplit * slab + w;
-      float a = 0.f;
-      for (int z = zg; z < g.nsplit; z += G) a += p[z * slab];
-      s[i] = a;
-    }
+    const int e = min(e0 + i, (int)nelem - 1);
+    const int b = e / slab, w = e - b * slab;
+    p[i] = g.part + (long)b * g.nsplit * zs + w;
+  }
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int z = zg; z < g.nsplit; z += G) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] += p[i][z * zs];
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) sh[zg * per_block + 4 * lane + i] = s[i];
   __syncthreads();
   for (int t = threadIdx.x; t < per_block; t += 256) {
-    const long e = (long)blockIdx.x * per_block + t;
+    const long e = blk * per_block + t;
     if (e >= nelem) break;
     float v = sh[t];
     for (int q = 1; q < G; ++q) v += sh[q * per_block + t];
-    const long b = e / slab, w = e - b * slab;
-    store_out(g, (int)b, (int)(w / g.Ne), (int)(w % g.Ne), v);
+    const int b = (int)e / slab, w = (int)e - b * slab;
+    store_out(g, b, w / g.Ne, w % g.Ne, v);
   }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce4(GemmArgs g, long nelem, int G) {
+  __shared__ float sh[1024];
+  reduce4_block(g, nelem, G, blockIdx.x, sh);
 }
 
 }  // namespace g2
@@ -930,35 +910,23 @@ __device__ __forceinline__ void fill(__amdgpu_buffer_rsrc_t r, char* img, int ro
   }
 }
 
+template <int BM, int BN, int NS>
+constexpr int ring_bytes() { return NS * (BM + BN) * 128; }
+
+// The block's output tile: (xn, ym) of K slice zs / batch zb, tn x tm tiles per slice (the arrival
+// counter's index of the in-launch combine, g.cnt; null = slabs for a separate reduce).  `smem` is the
+// block's LDS ring (ring_bytes), shared by the single-problem and the grouped kernel.
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G, int zfast) {
+__device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int xn, int ym, int tn, int tm, int G,
+                                          char* smem) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int SA_B = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int LOADS = (BM / 8 + BN / 8) / NW;   // DMA wave-instructions per wave and stage
   static_assert(NS >= 2 && NS <= 4, "ring depth");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const unsigned bid = blockIdx.x, q8 = total >> 3, r8 = total & 7, x8 = bid & 7;
-  const unsigned lin = x8 * q8 + min(x8, r8) + (bid >> 3);
-  int zs, xn, ym, zb;
-  if (zfast) {
-    zs = (int)(lin % (unsigned)g.nsplit);
-    const unsigned t1 = lin / (unsigned)g.nsplit;
-    xn = (int)(t1 % (unsigned)tn);
-    const unsigned t2 = t1 / (unsigned)tn;
-    ym = (int)(t2 % (unsigned)tm);
-    zb = (int)(t2 / (unsigned)tm);
-  } else {
-    xn = (int)(lin % (unsigned)tn);
-    const unsigned t1 = lin / (unsigned)tn;
-    ym = (int)(t1 % (unsigned)tm);
-    const unsigned t2 = t1 / (unsigned)tm;
-    zs = (int)(t2 % (unsigned)g.nsplit);
-    zb = (int)(t2 / (unsigned)g.nsplit);
-  }
   const int z = zb * g.nsplit + zs;
   const int m0 = ym * BM, n0 = xn * BN;
   const int kbeg = zs * g.k_chunk;
@@ -1057,6 +1025,113 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe(GemmArgs g, int tn, in
   if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 1-D grid in XCD-aware order (g2::gemm_mfma): block i runs on XCD i % 8, each XCD gets a contiguous
+// run of logical blocks -- with zfast the K slices of a tile side by side
+__device__ __forceinline__ unsigned xcd_linear(unsigned bid, unsigned total) {
+  const unsigned q8 = total >> 3, r8 = total & 7, x8 = bid & 7;
+  return x8 * q8 + min(x8, r8) + (bid >> 3);
+}
+
+__device__ __forceinline__ void tile_coords(unsigned lin, int nsplit, int tn, int tm, int zfast, int& zs, int& xn,
+                                            int& ym, int& zb) {
+  if (zfast) {
+    zs = (int)(lin % (unsigned)nsplit);
+    const unsigned t1 = lin / (unsigned)nsplit;
+    xn = (int)(t1 % (unsigned)tn);
+    const unsigned t2 = t1 / (unsigned)tn;
+    ym = (int)(t2 % (unsigned)tm);
+    zb = (int)(t2 / (unsigned)tm);
+  } else {
+    xn = (int)(lin % (unsigned)tn);
+    const unsigned t1 = lin / (unsigned)tn;
+    ym = (int)(t1 % (unsigned)tm);
+    const unsigned t2 = t1 / (unsigned)tm;
+    zs = (int)(t2 % (unsigned)nsplit);
+    zb = (int)(t2 / (unsigned)nsplit);
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G, int zfast) {
+  __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS>()];
+  int zs, xn, ym, zb;
+  tile_coords(xcd_linear(blockIdx.x, total), g.nsplit, tn, tm, zfast, zs, xn, ym, zb);
+  pipe_tile<BM, BN, WM, WN, TA, TB, NS>(g, zb, zs, xn, ym, tn, tm, G, smem);
+}
+
+// Grouped launch: up to GROUP_MAX independent problems (any of the four layouts, a runtime switch) in one
+// grid; problem p owns the logical blocks [start[p], start[p + 1]) of the XCD-ordered grid (slices of a
+// tile fastest); no in-launch combine (the group's split-K slabs go to one grouped reduce).
+struct PipeGroup {
+  int n;
+  int start[GROUP_MAX + 1];
+  int tn[GROUP_MAX], tm[GROUP_MAX], variant[GROUP_MAX];   // variant = 2 TA + TB
+  GemmArgs g[GROUP_MAX];
+};
+
+template <int BM, int BN, int WM, int WN, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_group(PipeGroup P, unsigned total) {
+  __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS>()];
+  const unsigned lin = xcd_linear(blockIdx.x, total);
+  int p = 0;
+#pragma unroll
+  for (int k = 1; k < GROUP_MAX; ++k)
+    if (k < P.n && (int)lin >= P.start[k]) p = k;
+  // the selected problem's descriptor by constant indices only (scalar loads from the argument segment)
+  GemmArgs g = P.g[0];
+  int tn = P.tn[0], tm = P.tm[0], variant = P.variant[0], start = P.start[0];
+#pragma unroll
+  for (int k = 1; k < GROUP_MAX; ++k)
+    if (k == p) {
+      g = P.g[k];
+      tn = P.tn[k];
+      tm = P.tm[k];
+      variant = P.variant[k];
+      start = P.start[k];
+    }
+  int zs, xn, ym, zb;
+  tile_coords(lin - (unsigned)start, g.nsplit, tn, tm, 1, zs, xn, ym, zb);
+  switch (variant) {
+    case 0: pipe_tile<BM, BN, WM, WN, false, false, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 1: pipe_tile<BM, BN, WM, WN, false, true, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 2: pipe_tile<BM, BN, WM, WN, true, false, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    default: pipe_tile<BM, BN, WM, WN, true, true, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+  }
+}
+
+// Grouped split-K reduce: g2::splitk_reduce4's blocks (G z-groups per element, combined in slab_sum's
+// order) of up to RGROUP_MAX problems in one grid, so
+// a GEMM gives the same bits grouped or alone
+constexpr int RGROUP_MAX = 2 * GROUP_MAX;   // a group's k-major and pipelined problems
+struct ReduceGroup {
+  int n;
+  int start[RGROUP_MAX + 1];
+  int G[RGROUP_MAX];
+  long nelem[RGROUP_MAX];
+  GemmArgs g[RGROUP_MAX];
+};
+
+__global__ __launch_bounds__(256) void splitk_reduce_sum_group(ReduceGroup R) {
+  __shared__ float sh[1024];
+  const int b = blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int k = 1; k < RGROUP_MAX; ++k)
+    if (k < R.n && b >= R.start[k]) p = k;
+  GemmArgs g = R.g[0];
+  int G = R.G[0], start = R.start[0];
+  long nelem = R.nelem[0];
+#pragma unroll
+  for (int k = 1; k < RGROUP_MAX; ++k)
+    if (k == p) {
+      g = R.g[k];
+      G = R.G[k];
+      start = R.start[k];
+      nelem = R.nelem[k];
+    }
+  g2::reduce4_block(g, nelem, G, b - start, sh);
+}
+
 }  // namespace gp
 
 
@@ -1113,7 +1188,7 @@ static LegacyPlan plan_legacy(int transA, int transB, int M, int N, int K, float
   const long tiles = (long)tn * tm * batch;
   // Split K when the output grid leaves the chip short of ~3 blocks per CU (768 blocks): each
   // K slice keeps >= 128 of K (4 BK steps), the slabs must fit the workspace, and the slices are
-  // summed in fixed order (splitk_reduce) so results do not depend on the split's scheduling.
+  // summed in fixed order (slab_sum) so results do not depend on the split's scheduling.
   int nsplit = 1;
   constexpr long kTargetBlocks = 768;
   if (ws && K >= 256 && tiles < kTargetBlocks / 2) {
@@ -1176,7 +1251,10 @@ static int launch_plan_pd(const LegacyPlan& pl, hipStream_t stream) {
 #undef VC_L
   VC_CHECK_LAUNCH();
   if (pl.reduce) {
-    hipLaunchKernelGGL(splitk_reduce, dim3(vc_cdiv(g.Ne, 64), g.M, pl.nz / g.nsplit), dim3(64), 0, stream, g);
+    const long nelem = (long)(pl.nz / g.nsplit) * g.M * g.Ne;
+    const int G = g2::slab_groups(g.nsplit);
+    VC_REQUIRE(nelem < (1L << 31));
+    hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, g, nelem, G);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;
@@ -1184,150 +1262,6 @@ static int launch_plan_pd(const LegacyPlan& pl, hipStream_t stream) {
 
 static int launch_plan(const LegacyPlan& pl, hipStream_t stream) {
   return legacy_pd() == 2 ? launch_plan_pd<2>(pl, stream) : launch_plan_pd<1>(pl, stream);
-}
-
-// ---- grouped launches: the fp32 k-major problems added to a group (vc_gemm_group_add) launch at
-// vc_gemm_group_end as one gemm_f32_group grid (plus one grouped split-K reduce); each takes its own slice
-// of the workspace and of the arrival counters.  The group state lives in caller-owned host memory
-// (VC_GEMM_GROUP_BYTES), so the library keeps none and distinct groups are independent.
-struct GroupState {
-  unsigned magic;          // GROUP_MAGIC between begin and end
-  hipStream_t stream;
-  int n;
-  LegacyPlan plans[GROUP_MAX];
-  long ws_used;
-  int cnt_used;
-  int err;
-};
-constexpr unsigned GROUP_MAGIC = 0x56434747u;   // "VCGG"
-static_assert(sizeof(GroupState) <= VC_GEMM_GROUP_BYTES, "VC_GEMM_GROUP_BYTES too small");
-
-static int group_flush(GroupState& st) {
-  const int n = st.n;
-  st.n = 0;
-  st.ws_used = 0;
-  st.cnt_used = 0;
-  if (n == 0) return VC_OK;
-  if (n == 1) return launch_plan(st.plans[0], st.stream);
-  GemmGroup G, R;
-  G.n = n;
-  R.n = 0;
-  long total = 0, rtotal = 0;
-  for (int p = 0; p < n; ++p) {
-    const LegacyPlan& pl = st.plans[p];
-    G.start[p] = (int)total;
-    G.tn[p] = pl.tn;
-    G.tm[p] = pl.tm;
-    G.variant[p] = pl.variant;
-    G.g[p] = pl.g;
-    total += (long)pl.tn * pl.tm * pl.nz;
-    if (pl.reduce) {
-      R.start[R.n] = (int)rtotal;
-      R.g[R.n] = pl.g;
-      R.tn[R.n] = R.tm[R.n] = R.variant[R.n] = 0;
-      ++R.n;
-      rtotal += (long)vc_cdiv(pl.g.Ne, 64) * pl.g.M * (pl.nz / pl.g.nsplit);
-    }
-  }
-  G.start[n] = (int)total;
-  VC_REQUIRE(total < (1L << 31) && rtotal < (1L << 31));
-  if (legacy_pd() == 2) hipLaunchKernelGGL(gemm_f32_group<2>, dim3((unsigned)total), dim3(256), 0, st.stream, G);
-  else hipLaunchKernelGGL(gemm_f32_group<1>, dim3((unsigned)total), dim3(256), 0, st.stream, G);
-  VC_CHECK_LAUNCH();
-  if (R.n) {
-    R.start[R.n] = (int)rtotal;
-    hipLaunchKernelGGL(splitk_reduce_group, dim3((unsigned)rtotal), dim3(64), 0, st.stream, R);
-    VC_CHECK_LAUNCH();
-  }
-  return VC_OK;
-}
-
-static GroupState* group_of(void* group) {
-  if (!group || ((uintptr_t)group % alignof(GroupState)) != 0) return nullptr;
-  return reinterpret_cast<GroupState*>(group);
-}
-
-VC_EXPORT int vc_gemm_group_begin(void* group, hipStream_t stream) {
-  GroupState* st = group_of(group);
-  VC_REQUIRE(st);
-  st->magic = GROUP_MAGIC;
-  st->stream = stream;
-  st->n = 0;
-  st->ws_used = 0;
-  st->cnt_used = 0;
-  st->err = 0;
-  return VC_OK;
-}
-
-VC_EXPORT int vc_gemm_group_end(void* group) {
-  GroupState* st = group_of(group);
-  VC_REQUIRE(st && st->magic == GROUP_MAGIC);
-  st->magic = 0;
-  const int err = st->err;
-  const int rc = group_flush(*st);
-  return err ? err : rc;
-}
-
-static int launch_legacy(int transA, int transB, int M, int N, int K, float alpha,
-                         const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
-                         float beta, float* C, long ldc, long strideC, int batch,
-                         const float* bias, const float* addend, long add_ld, int add_mod, int flags,
-                         float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
-                         int n_counters, hipStream_t stream, GroupState* st) {
-  // the plan (split-K slices, combine path) depends on the problem and the caller's whole workspace /
-  // counter arrays only -- never on what a group has used of them -- so a GEMM gives the same bits
-  // grouped or alone, whatever its neighbours (tests/test_model_gpu.py::test_lane_schedules_*)
-  LegacyPlan pl = plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
-                              batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
-                              n_counters);
-  if (!st) return launch_plan(pl, stream);
-  const long need = (pl.ws_floats + 63) / 64 * 64;
-  if (st->n == GROUP_MAX || st->ws_used + need > ws_floats || st->cnt_used + pl.counters > n_counters) {
-    const int rc = group_flush(*st);   // launch what is recorded; this problem starts a new group
-    if (rc) return rc;
-  }
-  // this problem's slices of the workspace and the counters follow the earlier problems' slices
-  if (pl.g.nsplit > 1) pl.g.part = ws + st->ws_used;
-  if (pl.g.cnt) pl.g.cnt = tile_counters + st->cnt_used;
-  st->ws_used += need;
-  st->cnt_used += pl.counters;
-  st->plans[st->n++] = pl;
-  return VC_OK;
-}
-
-static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
-                     const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
-                     float beta, float* C, long ldc, long strideC, int batch,
-                     const float* bias, const float* addend, long add_ld, int add_mod, int flags,
-                     float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
-                     int n_counters, hipStream_t stream, GroupState* group);
-
-// a problem of the group: the fp32 k-major ones wait for vc_gemm_group_end; any other (bf16 operands,
-// K >= 4096) launches at once on the group's stream
-VC_EXPORT int vc_gemm_group_add(void* group, int transA, int transB, int M, int N, int K, float alpha,
-                                const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
-                                float beta, float* C, long ldc, long strideC, int batch,
-                                const float* bias, const float* addend, long add_ld, int add_mod, int flags,
-                                float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
-                                int n_counters) {
-  GroupState* st = group_of(group);
-  VC_REQUIRE(st && st->magic == GROUP_MAGIC);
-  const int rc = gemm_impl(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
-                           batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
-                           n_counters, st->stream, st);
-  if (rc && !st->err) st->err = rc;
-  return rc;
-}
-
-VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha,
-                         const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
-                         float beta, float* C, long ldc, long strideC, int batch,
-                         const float* bias, const float* addend, long add_ld, int add_mod, int flags,
-                         float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
-                         int n_counters, hipStream_t stream) {
-  return gemm_impl(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC, batch,
-                   bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters, n_counters, stream,
-                   nullptr);
 }
 
 // ---- gemm_pipe launch configuration
@@ -1425,10 +1359,203 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
   VC_CHECK_LAUNCH();
   if (p.nsplit > 1 && !cnt) {
     const long nelem = (long)M * Ne;
+    VC_REQUIRE(nelem < (1L << 31));
     hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, g, nelem, G);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;
+}
+
+// ---- grouped launches: the problems added to a group (vc_gemm_group_add) launch at vc_gemm_group_end as
+// one gemm_f32_group grid (the k-major problems), one gemm_pipe_group grid (the pipelined ones) and ONE
+// grouped split-K reduce over both (each problem's slabs summed in the order its ungrouped launch uses, so
+// a GEMM gives the same bits grouped or alone); each problem takes its own slice of the workspace and of
+// the arrival counters.  The group state lives in caller-owned host memory (VC_GEMM_GROUP_BYTES), so the
+// library keeps none and distinct groups are independent.
+struct PipeRec {
+  GemmArgs g;
+  int tn, tm, variant;   // variant = 2 transA + transB
+};
+
+struct GroupState {
+  unsigned magic;          // GROUP_MAGIC between begin and end
+  hipStream_t stream;
+  int n, np;
+  LegacyPlan plans[GROUP_MAX];
+  PipeRec pipes[GROUP_MAX];
+  long ws_used;
+  int cnt_used;
+  int err;
+};
+constexpr unsigned GROUP_MAGIC = 0x56434747u;   // "VCGG"
+static_assert(sizeof(GroupState) <= VC_GEMM_GROUP_BYTES, "VC_GEMM_GROUP_BYTES too small");
+
+struct ReduceItems {
+  gp::ReduceGroup R;
+  long total = 0;
+  void add(const GemmArgs& g, int G, int batch) {
+    R.start[R.n] = (int)total;
+    R.g[R.n] = g;
+    R.G[R.n] = G;
+    R.nelem[R.n] = (long)batch * g.M * g.Ne;
+    ++R.n;
+    total += (R.nelem[R.n - 1] + 1024 / G - 1) / (1024 / G);
+  }
+};
+
+static int group_flush(GroupState& st) {
+  const int n = st.n, np = st.np;
+  st.n = st.np = 0;
+  st.ws_used = 0;
+  st.cnt_used = 0;
+  if (n + np == 0) return VC_OK;
+  if (n == 1 && np == 0) return launch_plan(st.plans[0], st.stream);
+  ReduceItems red;
+  red.R.n = 0;
+  if (n == 1) {
+    // one k-major problem: its own launch, its reduce (if any) joins the grouped one
+    LegacyPlan pl = st.plans[0];
+    const bool reduce = pl.reduce;
+    pl.reduce = false;
+    const int rc = launch_plan(pl, st.stream);
+    if (rc) return rc;
+    if (reduce) red.add(pl.g, g2::slab_groups(pl.g.nsplit), pl.nz / pl.g.nsplit);
+  } else if (n > 1) {
+    GemmGroup G;
+    G.n = n;
+    long total = 0;
+    for (int p = 0; p < n; ++p) {
+      const LegacyPlan& pl = st.plans[p];
+      G.start[p] = (int)total;
+      G.tn[p] = pl.tn;
+      G.tm[p] = pl.tm;
+      G.variant[p] = pl.variant;
+      G.g[p] = pl.g;
+      total += (long)pl.tn * pl.tm * pl.nz;
+      if (pl.reduce) red.add(pl.g, g2::slab_groups(pl.g.nsplit), pl.nz / pl.g.nsplit);
+    }
+    G.start[n] = (int)total;
+    VC_REQUIRE(total < (1L << 31));
+    if (legacy_pd() == 2) hipLaunchKernelGGL(gemm_f32_group<2>, dim3((unsigned)total), dim3(256), 0, st.stream, G);
+    else hipLaunchKernelGGL(gemm_f32_group<1>, dim3((unsigned)total), dim3(256), 0, st.stream, G);
+    VC_CHECK_LAUNCH();
+  }
+  if (np > 0) {
+    gp::PipeGroup P;
+    P.n = np;
+    long total = 0;
+    for (int p = 0; p < np; ++p) {
+      const PipeRec& pr = st.pipes[p];
+      P.start[p] = (int)total;
+      P.tn[p] = pr.tn;
+      P.tm[p] = pr.tm;
+      P.variant[p] = pr.variant;
+      P.g[p] = pr.g;
+      total += (long)pr.tn * pr.tm * pr.g.nsplit;
+      if (pr.g.nsplit > 1) red.add(pr.g, g2::slab_groups(pr.g.nsplit), 1);
+    }
+    P.start[np] = (int)total;
+    VC_REQUIRE(total < (1L << 31));
+    hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0, st.stream, P,
+                       (unsigned)total);
+    VC_CHECK_LAUNCH();
+  }
+  if (red.R.n) {
+    red.R.start[red.R.n] = (int)red.total;
+    for (int p = 0; p < red.R.n; ++p) VC_REQUIRE(red.R.nelem[p] < (1L << 31));
+    VC_REQUIRE(red.total < (1L << 31));
+    hipLaunchKernelGGL(gp::splitk_reduce_sum_group, dim3((unsigned)red.total), dim3(256), 0, st.stream, red.R);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
+static GroupState* group_of(void* group) {
+  if (!group || ((uintptr_t)group % alignof(GroupState)) != 0) return nullptr;
+  return reinterpret_cast<GroupState*>(group);
+}
+
+VC_EXPORT int vc_gemm_group_begin(void* group, hipStream_t stream) {
+  GroupState* st = group_of(group);
+  VC_REQUIRE(st);
+  st->magic = GROUP_MAGIC;
+  st->stream = stream;
+  st->n = st->np = 0;
+  st->ws_used = 0;
+  st->cnt_used = 0;
+  st->err = 0;
+  return VC_OK;
+}
+
+VC_EXPORT int vc_gemm_group_end(void* group) {
+  GroupState* st = group_of(group);
+  VC_REQUIRE(st && st->magic == GROUP_MAGIC);
+  st->magic = 0;
+  const int err = st->err;
+  const int rc = group_flush(*st);
+  return err ? err : rc;
+}
+
+static int launch_legacy(int transA, int transB, int M, int N, int K, float alpha,
+                         const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                         float beta, float* C, long ldc, long strideC, int batch,
+                         const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                         float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                         int n_counters, hipStream_t stream, GroupState* st) {
+  // the plan (split-K slices, combine path) depends on the problem and the caller's whole workspace /
+  // counter arrays only -- never on what a group has used of them -- so a GEMM gives the same bits
+  // grouped or alone, whatever its neighbours (tests/test_model_gpu.py::test_lane_schedules_*)
+  LegacyPlan pl = plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
+                              batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
+                              n_counters);
+  if (!st) return launch_plan(pl, stream);
+  const long need = (pl.ws_floats + 63) / 64 * 64;
+  if (st->n == GROUP_MAX || st->ws_used + need > ws_floats || st->cnt_used + pl.counters > n_counters) {
+    const int rc = group_flush(*st);   // launch what is recorded; this problem starts a new group
+    if (rc) return rc;
+  }
+  // this problem's slices of the workspace and the counters follow the earlier problems' slices
+  if (pl.g.nsplit > 1) pl.g.part = ws + st->ws_used;
+  if (pl.g.cnt) pl.g.cnt = tile_counters + st->cnt_used;
+  st->ws_used += need;
+  st->cnt_used += pl.counters;
+  st->plans[st->n++] = pl;
+  return VC_OK;
+}
+
+static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
+                     const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                     float beta, float* C, long ldc, long strideC, int batch,
+                     const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                     float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                     int n_counters, hipStream_t stream, GroupState* group);
+
+// a problem of the group: the fp32 k-major ones wait for vc_gemm_group_end; any other (bf16 operands,
+// K >= 4096) launches at once on the group's stream
+VC_EXPORT int vc_gemm_group_add(void* group, int transA, int transB, int M, int N, int K, float alpha,
+                                const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                                float beta, float* C, long ldc, long strideC, int batch,
+                                const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                                float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                                int n_counters) {
+  GroupState* st = group_of(group);
+  VC_REQUIRE(st && st->magic == GROUP_MAGIC);
+  const int rc = gemm_impl(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
+                           batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
+                           n_counters, st->stream, st);
+  if (rc && !st->err) st->err = rc;
+  return rc;
+}
+
+VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha,
+                         const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
+                         float beta, float* C, long ldc, long strideC, int batch,
+                         const float* bias, const float* addend, long add_ld, int add_mod, int flags,
+                         float* bias_grad, float* ws, long ws_floats, unsigned int* tile_counters,
+                         int n_counters, hipStream_t stream) {
+  return gemm_impl(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC, batch,
+                   bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters, n_counters, stream,
+                   nullptr);
 }
 
 static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
@@ -1446,9 +1573,32 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
   // takes it launches at once on the group's stream
   if (!bf && !(flags & (F_LEGACY | F_V2 | F_NOPIPE)) &&
       pipe_fits(transA, transB, M, N, K, A, lda, B, ldb, batch, bias_grad) &&
-      ((flags & F_PIPE) || pipe_wanted(M, N, K)))
+      ((flags & F_PIPE) || pipe_wanted(M, N, K))) {
+    const int fl = flags & ~(F_PIPE | F_NOPIPE);
+    if (group) {
+      const int Ne = N + (bias_grad ? 1 : 0);
+      const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr);
+      if (p.bm == 64 && p.bn == 64 && p.ns == 2) {   // the grouped kernel's configuration
+        const long need = p.nsplit > 1 ? ((long)p.nsplit * M * Ne + 63) / 64 * 64 : 0;
+        GroupState& st = *group;
+        if (st.np == GROUP_MAX || st.ws_used + need > ws_floats) {
+          const int rc = group_flush(st);
+          if (rc) return rc;
+        }
+        Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, fl};
+        PipeRec& pr = st.pipes[st.np++];
+        pr.g = GemmArgs{M, N, K, Ne, p.k_chunk, p.nsplit, A, lda, 0, B, ldb, 0, C, ldc, 0, bias_grad,
+                        p.nsplit > 1 ? ws + st.ws_used : ws, nullptr, epi};
+        pr.tn = p.tn;
+        pr.tm = p.tm;
+        pr.variant = (transA ? 2 : 0) | (transB ? 1 : 0);
+        st.ws_used += need;
+        return VC_OK;
+      }
+    }
     return launch_pipe(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, addend, add_ld, add_mod,
-                       flags & ~(F_PIPE | F_NOPIPE), bias_grad, ws, ws_floats, tile_counters, n_counters, stream);
+                       fl, bias_grad, ws, ws_floats, tile_counters, n_counters, stream);
+  }
   // fp32: the k-major kernel (faster on every shape of the ViT-CNN step, tools/gemm_census.py) except
   // long contractions (K >= 4096, e.g. FusAtNet's 3x3 convs over 1024-2193 channels), where the
   // K-contiguous kernel's two accumulator chains and <= 2048-long slices keep the fp32 rounding at
@@ -1538,6 +1688,7 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
   VC_CHECK_LAUNCH();
   if (nsplit > 1 && !cnt) {
     const long nelem = (long)batch * M * Ne;
+    VC_REQUIRE(nelem < (1L << 31));
     hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, g, nelem, G);
     VC_CHECK_LAUNCH();
   }

@@ -55,8 +55,10 @@ _IMPLICIT_CONV = False
 # graph edge costs more than one GEMM's overlap gains); False: every weight gradient in place
 _DEFER_WGRAD = True
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
-PARAM_ALIGN = 4            # floats: flat-buffer alignment of every parameter (16 B)
+PARAM_ALIGN = 4            # floats: flat-buffer alignment (16 B) of every parameter of >= ALIGN_MIN elements
+ALIGN_MIN = 64
 GEMM_GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES (include/vitcnn.h)
+GEMM_MASK = 64             # vc_gemm flags: the addend is a ReLU mask (include/vitcnn.h)
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 # the Mamba direction conv + x_proj folded into the scan launch and the dt_proj / x_proj data gradients +
@@ -177,21 +179,25 @@ class Multimodality_Mamba(nn.Module):
                 first = min(idx[n] for n in group)
                 rest = [it for it in active if it[0] not in group]
                 active = rest[:first] + items + rest[first:]
-        # every parameter starts 16-B aligned (PARAM_ALIGN floats): the GEMM kernels stage weights by
-        # 16-B LDS-DMA / float4 loads, which an arbitrary float offset would rule out.  The gaps hold
-        # zeros in the parameters and in every gradient (the backward zeroes them: vc_fill_index)
+        # every parameter of >= ALIGN_MIN elements starts 16-B aligned (PARAM_ALIGN floats): the GEMM
+        # kernels stage weights by 16-B LDS-DMA / float4 loads, which an arbitrary float offset would rule
+        # out.  Smaller ones stay packed (the TokenLearner kernels address a block's S tokenizers'
+        # 2 + 1 + 1 + 1 parameters as one run).  The gaps hold zeros in the parameters and in every
+        # gradient (the backward zeroes them: vc_fill_index)
+        def place(n, p, off):
+            if p.numel() >= ALIGN_MIN:
+                off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
+            self._poff[n] = off
+            return off + p.numel()
+
         self._poff: Dict[str, int] = {}
         off = 0
         for n, p in active:
-            off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
-            self._poff[n] = off
-            off += p.numel()
+            off = place(n, p, off)
         self._n_active = -(-off // PARAM_ALIGN) * PARAM_ALIGN
         off = self._n_active
         for n, p in unused:
-            off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
-            self._poff[n] = off
-            off += p.numel()
+            off = place(n, p, off)
         self._n_params = off
         self._n_elems = sum(p.numel() for _, p in named)
         covered = torch.zeros(self._n_active, dtype=torch.bool)
@@ -643,10 +649,11 @@ class _Program:
         self.gemm(0, 1, M, N, K, alpha, A, lda, 0, W, ldw, 0, beta, C, ldc, 0, 1, bias or None, add or None,
                   add_ld, add_mod, relu, None, exact=exact)
 
-    def mm_nn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0):
-        """C[M,N] = alpha * A[M,K] B[K,N] + beta*C"""
-        self.gemm(0, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
-                       None)
+    def mm_nn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0, relu_mask=0):
+        """C[M,N] = alpha * A[M,K] B[K,N] + beta*C; relu_mask (a [M,N] layer output, ld N): the result
+        is zeroed where relu_mask <= 0 (the ReLU backward through that output, in the GEMM epilogue)"""
+        self.gemm(0, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, relu_mask or None,
+                  N if relu_mask else 0, 0, GEMM_MASK if relu_mask else 0, None)
 
     def mm_tn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0, bias_grad=0):
         """C[M,N] = alpha * A^T B, A stored [K, M] (weight gradients: M,N small, K = rows);
@@ -939,8 +946,9 @@ class _Program:
                                 dX, C, beta_dx, self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p,
                                 self.scr_n, self.s)
 
-    def linear_bwd(self, wname, bname, dY, M, N, K, X, ldx, dX, beta_dx, lddy=None, defer=False):
-        """Y[M,N] = X[M,K] W[N,K]^T + b:  dW = dY^T X, db = colsum(dY), dX (+)= dY W.
+    def linear_bwd(self, wname, bname, dY, M, N, K, X, ldx, dX, beta_dx, lddy=None, defer=False, relu_mask=0):
+        """Y[M,N] = X[M,K] W[N,K]^T + b:  dW = dY^T X, db = colsum(dY), dX (+)= dY W (then masked by
+        relu_mask > 0 if given: see mm_nn).
 
         defer (lane 0 only): the weight gradient is queued (self.defer_wgrad) and issued on the
         weight-gradient lane at the next flush_wgrads(), so the data gradient -- the only part the rest
@@ -951,7 +959,7 @@ class _Program:
         with self.gemm_group():
             self.defer_wgrad(defer, N, K, M, dY, lddy, X, ldx, self.G[wname], K, self.G[bname] if bname else 0)
             if dX:
-                self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx)
+                self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx, relu_mask=relu_mask)
 
     def _deferring(self, defer):
         return defer and _DEFER_WGRAD and self.lanes_on and self.cur == 0
@@ -1001,13 +1009,17 @@ class _Program:
     def _tap_dgrad(self, blk):
         return _TAP_DGRAD and self.ws_grad and not self.implicit_conv and blk.cin % 4 == 0
 
-    def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx, tap=False):
-        """tap: the data gradient by vc_conv3x3_tap_dgrad over the tap-major weight block() packed"""
+    def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx, tap=False, masked=False):
+        """tap: the data gradient by vc_conv3x3_tap_dgrad over the tap-major weight block() packed;
+        masked: dOut has been through the ReLU backward already (its producer's GEMM epilogue)"""
         B, ws = self.B, self.ws
         S = (H - 2) * (H - 2)
-        out = ws.f(pfx + ".out", B * S * Cout)
-        dpre = ws.f(pfx + ".dpre", B * S * Cout)
-        self.L.vc_relu_bwd(B * S * Cout, dOut, out, dpre, self.s)
+        if masked:
+            dpre = dOut
+        else:
+            out = ws.f(pfx + ".out", B * S * Cout)
+            dpre = ws.f(pfx + ".dpre", B * S * Cout)
+            self.L.vc_relu_bwd(B * S * Cout, dOut, out, dpre, self.s)
         dxbn = ws.f(pfx + ".dxbn", B * H * H * Cin)
         if self.implicit_conv:
             tag = pfx + ".bn"
@@ -1102,11 +1114,14 @@ class _Program:
             # phi | g (stacked, one weight + one data gradient) and theta: one grouped launch
             with self.gemm_group():
                 self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, 2 * Ci, Cout, Fc, Cout, dFc, 1.0)
-                self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0)
+                # dFl's last contribution; its epilogue applies the local conv's ReLU backward (mask Fl)
+                self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0,
+                                relu_mask=Fl)
             side = self.lanes_on and _CH_LANE != 1
             e_pg = self.mark() if side else None
             # local feature: BN -> conv3x3 -> ReLU backward (first accumulation into dX)
-            self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0, tap=self._tap_dgrad(blk))
+            self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0, tap=self._tap_dgrad(blk),
+                                   masked=True)
             e_loc = self.mark() if side else None
         # channel feature: ln4 -> TokenLearner -> conv1x1, after the local chain on lane 1 (or, measurement
         # switch _CH_LANE, on a lane of its own beside it: see _CH_ORDERED)
