@@ -141,8 +141,16 @@ VC_API int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, const
                      const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
                      float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w,
                      float* ws, long ws_floats, hipStream_t stream);
-/* The same with >= ceil(C/64) zeroed arrival counters (left zero; per stream, as vc_gemm_ex's):
- * the per-channel reduction runs in the last-arriving partial block, one launch fewer. */
+/* The same with zeroed arrival counters (left zero; per stream, as vc_gemm_ex's).  With >= 2*ceil(C/64)
+ * of them vc_bn_forward_ex (train) and vc_bn_bwd_ex (train, dx given) run as ONE launch: the partial
+ * blocks of each 64-channel group meet at a group barrier, reduce the partials and apply in place
+ * (grids up to 1024 blocks; larger ones take the two-launch path) -- bit-identical to the two-launch
+ * kernels.  Otherwise vc_bn_stats_ex and vc_bn_bwd_ex without dx (>= ceil(C/64) counters) reduce per
+ * channel in the last-arriving partial block, one launch fewer than without counters. */
+VC_API int vc_bn_forward_ex(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                            float* save_mean, float* save_invstd, float* run_mean, float* run_var, const float* w,
+                            const float* b, int relu, float* y, long ldy, float* ws, long ws_floats,
+                            unsigned int* counters, int n_counters, hipStream_t stream);
 VC_API int vc_bn_stats_ex(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
                           float* save_mean, float* save_invstd, float* run_mean, float* run_var,
                           float* ws, long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream);

@@ -58,9 +58,10 @@ def rnd(*shape, seed=0, scale=1.0):
 
 
 # vc_gemm flags: bit 0 ReLU, bit 1 bf16 operands (fp32 accumulate), bit 2 / bit 3 / bit 4 force the k-major /
-# the K-contiguous / the LDS-DMA pipelined fp32 kernel (default: chosen by shape)
-F_BF16, F_LEGACY, F_V2, F_PIPE = 2, 4, 8, 16
-KERNELS = [0, F_LEGACY, F_V2, F_PIPE, F_BF16]
+# the K-contiguous / the LDS-DMA pipelined kernel, bit 5 keeps the older kernels (default: chosen by shape);
+# bf16: the pipelined kernel's bf16 MFMAs (F_BF16 | F_PIPE) and the K-contiguous kernel's (F_BF16 | F_NOPIPE)
+F_BF16, F_LEGACY, F_V2, F_PIPE, F_NOPIPE = 2, 4, 8, 16, 32
+KERNELS = [0, F_LEGACY, F_V2, F_PIPE, F_BF16, F_BF16 | F_PIPE, F_BF16 | F_NOPIPE]
 
 
 def bf16_round(t):
@@ -275,16 +276,21 @@ def test_batchnorm_train_fwd_bwd(L, ws, M, C, relu):
 @pytest.mark.parametrize("train", [1, 0])
 @pytest.mark.parametrize("M,C,relu", [(5184, 144, 0), (3136, 256, 1), (1600, 16, 1), (37, 200, 1)])
 def test_bn_forward_fused_is_bit_identical(L, ws, train, M, C, relu):
-    """vc_bn_forward (partials + a channel-tiled apply that reduces them itself) == vc_bn_stats +
+    """vc_bn_forward (partials + a channel-tiled apply that reduces them itself) and vc_bn_forward_ex
+    with counters (one launch, group barrier; twice: the counters are left zero) == vc_bn_stats +
     vc_bn_apply: y, save_mean / save_invstd and the running statistics, bit for bit"""
     x = (rnd(M, C, seed=61, scale=2.0) + 3.0).to(DEV)
     w, b = (rnd(C, seed=62) + 1.0).to(DEV), rnd(C, seed=63).to(DEV)
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
     outs = []
-    for fused in (False, True):
+    for mode in ("split", "two", "one", "one"):
         rm, rv = (rnd(C, seed=64) * 0.1).to(DEV), (rnd(C, seed=65).abs() + 0.5).to(DEV)
         mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
         y = torch.full((M, C), float("nan"), device=DEV)
-        if fused:
+        if mode == "one":
+            L.vc_bn_forward_ex(train, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(w), P(b), relu, P(y),
+                               C, P(ws), ws.numel(), P(cnt), cnt.numel(), S())
+        elif mode == "two":
             L.vc_bn_forward(train, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(w), P(b), relu, P(y), C,
                             P(ws), ws.numel(), S())
         else:
@@ -292,15 +298,17 @@ def test_bn_forward_fused_is_bit_identical(L, ws, train, M, C, relu):
             L.vc_bn_apply(M, C, P(x), C, P(mean), P(inv), P(w), P(b), relu, P(y), C, S())
         torch.cuda.synchronize()
         outs.append([t.cpu() for t in (y, mean, inv, rm, rv)])
-    for a_, b_ in zip(*outs):
-        assert torch.equal(a_, b_)
+        assert int(cnt.abs().sum()) == 0
+    for o in outs[1:]:
+        for a_, b_ in zip(outs[0], o):
+            assert torch.equal(a_, b_)
 
 
 @pytest.mark.parametrize("M,C,relu", [(5184, 144, 0), (3136, 512, 1), (5184, 1, 0), (1600, 16, 1), (37, 200, 1)])
 def test_batchnorm_ticketed_reduction_is_bit_identical(L, ws, M, C, relu):
-    """vc_bn_stats_ex / vc_bn_bwd_ex (the last-arriving partial block of each channel group reduces)
-    == vc_bn_stats / vc_bn_bwd (separate reduction launch), bit for bit, twice in a row (the arrival
-    counters are left zero)"""
+    """vc_bn_stats_ex (the last-arriving partial block of each channel group reduces) / vc_bn_bwd_ex
+    (one launch: group barrier) == vc_bn_stats / vc_bn_bwd (separate launches), bit for bit, twice in a
+    row (the arrival counters are left zero)"""
     x = (rnd(M, C, seed=41, scale=3.0) + 5.0).to(DEV)
     w, dy = (rnd(C, seed=42) + 1.0).to(DEV), rnd(M, C, seed=43).to(DEV)
     relu_out = torch.relu(rnd(M, C, seed=44)).to(DEV) if relu else None

@@ -61,16 +61,17 @@ def main():
         base = a[21] & ~(2 | 4 | 8 | 16 | 32)
         a = a[:21] + (base,) + a[22:]
         t_auto, t_leg, t_v2, t_bf = time_call(a, 0), time_call(a, 4), time_call(a, 16), time_call(a, 2)
+        t_bfk = time_call(a, 2 | 32)   # bf16 on the K-contiguous kernel (no pipelined kernel)
         fl = 2.0 * M * N * K * batch
-        rows.append((t_auto, t_leg, t_v2, t_bf, ta, tb, M, N, K, batch, a[22] is not None,
+        rows.append((t_auto, t_leg, t_v2, t_bf, t_bfk, ta, tb, M, N, K, batch, a[22] is not None,
                      fl / min(t_leg, t_v2) * 1e-6, fl / t_bf * 1e-6))
     rows.sort(reverse=True)
-    tots = [sum(r[i] for r in rows) for i in range(4)]
+    tots = [sum(r[i] for r in rows) for i in range(5)]
     print(f"{len(rows)} GEMMs, isolated sums (us): auto {tots[0]:.1f}  legacy {tots[1]:.1f}  pipe {tots[2]:.1f}  "
-          f"bf16 {tots[3]:.1f}")
-    print("  auto legacy   pipe   bf16  tA tB      M      N      K  batch bgrad TF(fp32) TF(bf16)")
+          f"bf16 {tots[3]:.1f}  bf16 (K-contiguous kernel) {tots[4]:.1f}")
+    print("  auto legacy   pipe   bf16 bf16-k  tA tB      M      N      K  batch bgrad TF(fp32) TF(bf16)")
     for r in rows:
-        print("%6.1f %6.1f %6.1f %6.1f  %d  %d %6d %6d %6d %5d %5s %8.1f %8.1f" % r)
+        print("%6.1f %6.1f %6.1f %6.1f %6.1f  %d  %d %6d %6d %6d %5d %5s %8.1f %8.1f" % r)
 
 
 if __name__ == "__main__":

@@ -913,10 +913,42 @@ __device__ __forceinline__ void fill(__amdgpu_buffer_rsrc_t r, char* img, int ro
 template <int BM, int BN, int NS>
 constexpr int ring_bytes() { return NS * (BM + BN) * 128; }
 
+// bf16 operands (config 2) over the same fp32 stage: a lane's two fp32 fragments of the k-tile (sub-steps
+// 0 and 1, k = 4g + j and 16 + 4g + j) rounded RNE to bf16 (v_cvt_pk_bf16_f32, g2's staging rounding) and
+// fed to ONE v_mfma_f32_16x16x32_bf16 per output tile -- the MFMA's k order is a permutation applied to
+// both operands alike, so the products are the k-tile's.  Same LDS reads as the fp32 path, 1/8 of the MFMAs.
+template <int MT, int NT, class SA, class SB>
+__device__ __forceinline__ void mma_ktile_bf(const char* As, const char* Bs, int arow, int brow, int lane,
+                                             f32x4 (&acc)[MT][NT]) {
+  uint4 a[MT], b[NT];
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const uint4 f0 = SA::frag(As, arow + 16 * mi, 0, lane), f1 = SA::frag(As, arow + 16 * mi, 1, lane);
+    a[mi] = uint4{g2::pk_bf16(__uint_as_float(f0.x), __uint_as_float(f0.y)),
+                  g2::pk_bf16(__uint_as_float(f0.z), __uint_as_float(f0.w)),
+                  g2::pk_bf16(__uint_as_float(f1.x), __uint_as_float(f1.y)),
+                  g2::pk_bf16(__uint_as_float(f1.z), __uint_as_float(f1.w))};
+  }
+#pragma unroll
+  for (int ni = 0; ni < NT; ++ni) {
+    const uint4 f0 = SB::frag(Bs, brow + 16 * ni, 0, lane), f1 = SB::frag(Bs, brow + 16 * ni, 1, lane);
+    b[ni] = uint4{g2::pk_bf16(__uint_as_float(f0.x), __uint_as_float(f0.y)),
+                  g2::pk_bf16(__uint_as_float(f0.z), __uint_as_float(f0.w)),
+                  g2::pk_bf16(__uint_as_float(f1.x), __uint_as_float(f1.y)),
+                  g2::pk_bf16(__uint_as_float(f1.z), __uint_as_float(f1.w))};
+  }
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+      acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(g2::bf16x8, a[mi]),
+                                                            __builtin_bit_cast(g2::bf16x8, b[ni]), acc[mi][ni], 0, 0, 0);
+}
+
 // The block's output tile: (xn, ym) of K slice zs / batch zb, tn x tm tiles per slice (the arrival
 // counter's index of the in-launch combine, g.cnt; null = slabs for a separate reduce).  `smem` is the
 // block's LDS ring (ring_bytes), shared by the single-problem and the grouped kernel.
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS>
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false>
 __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int xn, int ym, int tn, int tm, int G,
                                           char* smem) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
@@ -979,7 +1011,8 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
+    if constexpr (BF) mma_ktile_bf<MT, NT, SA, SB>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc[0]);
+    else g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
   }
 
   // C/D map of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
@@ -1051,12 +1084,12 @@ __device__ __forceinline__ void tile_coords(unsigned lin, int nsplit, int tn, in
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS>
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G, int zfast) {
   __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS>()];
   int zs, xn, ym, zb;
   tile_coords(xcd_linear(blockIdx.x, total), g.nsplit, tn, tm, zfast, zs, xn, ym, zb);
-  pipe_tile<BM, BN, WM, WN, TA, TB, NS>(g, zb, zs, xn, ym, tn, tm, G, smem);
+  pipe_tile<BM, BN, WM, WN, TA, TB, NS, BF>(g, zb, zs, xn, ym, tn, tm, G, smem);
 }
 
 // Grouped launch: up to GROUP_MAX independent problems (any of the four layouts, a runtime switch) in one
@@ -1065,7 +1098,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe(GemmArgs g, int tn, in
 struct PipeGroup {
   int n;
   int start[GROUP_MAX + 1];
-  int tn[GROUP_MAX], tm[GROUP_MAX], variant[GROUP_MAX];   // variant = 2 TA + TB
+  int tn[GROUP_MAX], tm[GROUP_MAX], variant[GROUP_MAX];   // variant = 4 BF + 2 TA + TB
   GemmArgs g[GROUP_MAX];
 };
 
@@ -1091,11 +1124,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_group(PipeGroup P, uns
     }
   int zs, xn, ym, zb;
   tile_coords(lin - (unsigned)start, g.nsplit, tn, tm, 1, zs, xn, ym, zb);
-  switch (variant) {
+  switch (variant) {   // 4 BF + 2 TA + TB
     case 0: pipe_tile<BM, BN, WM, WN, false, false, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
     case 1: pipe_tile<BM, BN, WM, WN, false, true, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
     case 2: pipe_tile<BM, BN, WM, WN, true, false, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    default: pipe_tile<BM, BN, WM, WN, true, true, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 3: pipe_tile<BM, BN, WM, WN, true, true, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 4: pipe_tile<BM, BN, WM, WN, false, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 5: pipe_tile<BM, BN, WM, WN, false, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 6: pipe_tile<BM, BN, WM, WN, true, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    default: pipe_tile<BM, BN, WM, WN, true, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
   }
 }
 
@@ -1290,13 +1327,16 @@ struct PipePlan {
 // shape; a grid of >= 128 tiles runs unsplit (the split-K slab reduce costs more than the extra blocks
 // gain), a smaller one splits K towards ~512 blocks in slices of >= 4 k-tiles (the weight gradients,
 // K = 1600-5184 rows over a 2 x 5 ... 4 x 21 tile grid).
-static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws) {
+static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws, bool bf = false) {
   PipePlan p;
   p.bm = 64;
   p.bn = 64;
-  if (g_tune.bm) p.bm = g_tune.bm;
-  if (g_tune.bn) p.bn = g_tune.bn;
-  p.ns = vc_knob("VITCNN_PIPE_NS", 2) == 4 ? 4 : 2;   // ring depth (knob: probe library)
+  p.ns = 2;
+  if (!bf) {   // bf16 operands: the 64 x 64, 2-stage kernel only
+    if (g_tune.bm) p.bm = g_tune.bm;
+    if (g_tune.bn) p.bn = g_tune.bn;
+    p.ns = vc_knob("VITCNN_PIPE_NS", 2) == 4 ? 4 : 2;   // ring depth (knob: probe library)
+  }
   p.tn = vc_cdiv(Ne, p.bn);
   p.tm = vc_cdiv(M, p.bm);
   const long tiles = (long)p.tn * p.tm;
@@ -1321,7 +1361,8 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
                        long ws_floats, unsigned int* tile_counters, int n_counters, hipStream_t stream) {
   Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, flags};
   const int Ne = N + (bias_grad ? 1 : 0);
-  const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr);
+  const bool bf = (flags & F_BF16) != 0;
+  const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr, bf);
   const long tiles = (long)p.tn * p.tm;
   const long slab_bytes = (long)p.nsplit * std::min(p.bm, M) * std::min(p.bn, Ne) * 4;
   bool inl = slab_bytes <= g2_combine_limit();
@@ -1352,8 +1393,16 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
     else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_);   \
     else VC_GP(64, 64, 2, 2, NS_);                                  \
   } while (0)
-  if (p.ns == 4) VC_GP_T(4);
+#define VC_GPB(TA_, TB_) \
+  hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, TA_, TB_, 2, true>), grid, dim3(256), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
+  if (bf) {
+    if (transA && transB) VC_GPB(true, true);
+    else if (transA) VC_GPB(true, false);
+    else if (transB) VC_GPB(false, true);
+    else VC_GPB(false, false);
+  } else if (p.ns == 4) VC_GP_T(4);
   else VC_GP_T(2);
+#undef VC_GPB
 #undef VC_GP_T
 #undef VC_GP
   VC_CHECK_LAUNCH();
@@ -1568,16 +1617,16 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
   VC_REQUIRE(!bias_grad || batch == 1);
   if (M == 0 || N == 0) return VC_OK;
   const bool bf = (flags & F_BF16) != 0;
-  // fp32 mid shapes: the LDS-DMA pipelined kernel (F_PIPE forces it where it fits, F_NOPIPE keeps the
-  // older kernels: tests, census).  The choice depends on the problem only: a grouped problem that
+  // mid shapes: the LDS-DMA pipelined kernel, fp32 or (F_BF16) bf16 MFMAs over the same fp32 stages
+  // (F_PIPE forces it where it fits, F_NOPIPE keeps the older kernels: tests, census).  The choice depends on the problem only: a grouped problem that
   // takes it launches at once on the group's stream
-  if (!bf && !(flags & (F_LEGACY | F_V2 | F_NOPIPE)) &&
+  if (!(flags & (F_LEGACY | F_V2 | F_NOPIPE)) &&
       pipe_fits(transA, transB, M, N, K, A, lda, B, ldb, batch, bias_grad) &&
       ((flags & F_PIPE) || pipe_wanted(M, N, K))) {
     const int fl = flags & ~(F_PIPE | F_NOPIPE);
     if (group) {
       const int Ne = N + (bias_grad ? 1 : 0);
-      const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr);
+      const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr, bf);
       if (p.bm == 64 && p.bn == 64 && p.ns == 2) {   // the grouped kernel's configuration
         const long need = p.nsplit > 1 ? ((long)p.nsplit * M * Ne + 63) / 64 * 64 : 0;
         GroupState& st = *group;
@@ -1591,7 +1640,7 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
                         p.nsplit > 1 ? ws + st.ws_used : ws, nullptr, epi};
         pr.tn = p.tn;
         pr.tm = p.tm;
-        pr.variant = (transA ? 2 : 0) | (transB ? 1 : 0);
+        pr.variant = (bf ? 4 : 0) | (transA ? 2 : 0) | (transB ? 1 : 0);
         st.ws_used += need;
         return VC_OK;
       }

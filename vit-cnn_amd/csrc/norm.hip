@@ -256,6 +256,24 @@ __device__ __forceinline__ void bn_stats_reduce(int P, int C, long M, const floa
                      run_var, true);
 }
 
+// y = relu?((x - mean) * invstd * w + b) over rows [r0, r1) of channel c (row lane rl)
+__device__ __forceinline__ void bn_apply_rows(const float* __restrict__ x, long ldx, float mf, float isf, float wc,
+                                              float bc, int relu, float* __restrict__ y, long ldy, long r0, long r1,
+                                              int c, int rl) {
+  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
+    float xv[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) xv[i] = rb + BN_RL * i < r1 ? x[(rb + BN_RL * i) * ldx + c] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (rb + BN_RL * i < r1) {
+        float v = bn_fwd_elem(xv[i], mf, isf, wc, bc);
+        if (relu) v = fmaxf(v, 0.f);
+        y[(rb + BN_RL * i) * ldy + c] = v;
+      }
+  }
+}
+
 // Fused final + apply (train mode): grid (ceil(C/64), ceil(M/rows_per_block)); every block reduces
 // the channel group's partials itself (bn_part_sums), the blocks of row 0 write save_* and the running
 // statistics, and all apply y = relu?((x - mean) * invstd * w + b) to their rows.
@@ -273,32 +291,14 @@ __global__ __launch_bounds__(BN_T) void bn_apply_stats(int M, int C, const float
   float mf, isf;
   bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
                      run_var, blockIdx.y == 0 && rl == 0);
-  const float bc = b[c];
   const long r0 = (long)blockIdx.y * rows_per_block;
-  const long r1 = min((long)M, r0 + rows_per_block);
-  const float wc = w[c];
-  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
-    float xv[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) xv[i] = rb + BN_RL * i < r1 ? x[(rb + BN_RL * i) * ldx + c] : 0.f;
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-      if (rb + BN_RL * i < r1) {
-        float v = bn_fwd_elem(xv[i], mf, isf, wc, bc);
-        if (relu) v = fmaxf(v, 0.f);
-        y[(rb + BN_RL * i) * ldy + c] = v;
-      }
-  }
+  bn_apply_rows(x, ldx, mf, isf, w[c], b[c], relu, y, ldy, r0, min((long)M, r0 + rows_per_block), c, rl);
 }
 
-
-
-// grid (ceil(C/64), P); cnt (optional) = one zeroed arrival counter per 64-channel group
-__global__ __launch_bounds__(BN_T) void bn_stats_sums(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
-                                                     double* __restrict__ part, unsigned int* __restrict__ cnt,
-                                                     float eps, float momentum, float* __restrict__ save_mean,
-                                                     float* __restrict__ save_invstd, float* __restrict__ run_mean,
-                                                     float* __restrict__ run_var) {
+// partial block (channel group blockIdx.x, rows [blockIdx.y * rows_per, ...)) of the statistics:
+// part[blockIdx.y][0 / 1][c] = its shifted sums
+__device__ __forceinline__ void bn_stats_partial(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
+                                                 double* __restrict__ part) {
   __shared__ double sh[2][BN_RL][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -334,8 +334,44 @@ __global__ __launch_bounds__(BN_T) void bn_stats_sums(int M, int C, const float*
     p[0] = t1;
     p[C] = t2;
   }
+}
+
+// grid (ceil(C/64), P); cnt (optional) = one zeroed arrival counter per 64-channel group
+__global__ __launch_bounds__(BN_T) void bn_stats_sums(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
+                                                     double* __restrict__ part, unsigned int* __restrict__ cnt,
+                                                     float eps, float momentum, float* __restrict__ save_mean,
+                                                     float* __restrict__ save_invstd, float* __restrict__ run_mean,
+                                                     float* __restrict__ run_var) {
+  bn_stats_partial(M, C, x, ldx, rows_per, part);
   if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
   bn_stats_reduce(gridDim.y, C, M, x, part, blockIdx.x, eps, momentum, save_mean, save_invstd, run_mean, run_var);
+}
+
+// The whole train-mode forward in one launch: grid (ceil(C/64), P) partial blocks; the P blocks of a
+// channel group meet at a group barrier (cnt[2 * blockIdx.x], zeroed, left zero), then each reduces the
+// group's partials (bn_part_sums: the same order as bn_stats_final / bn_apply_stats) and applies the
+// normalisation to its own rows (re-read from L2).  Bit-identical to bn_stats_sums + bn_apply_stats.
+__global__ __launch_bounds__(BN_T) void bn_forward_fused(int M, int C, const float* __restrict__ x, long ldx,
+                                                        int rows_per, double* __restrict__ part,
+                                                        unsigned int* __restrict__ cnt, float eps, float momentum,
+                                                        float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                        float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        int relu, float* __restrict__ y, long ldy) {
+  __shared__ double tot[2][64];
+  bn_stats_partial(M, C, x, ldx, rows_per, part);
+  unsigned int* gc = cnt + 2 * blockIdx.x;
+  block_group_sync(gc, gridDim.y);
+  bn_part_sums(gridDim.y, C, part, blockIdx.x, tot);
+  block_group_leave(gc, gc + 1, gridDim.y);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  if (c >= C) return;
+  float mf, isf;
+  bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
+                     run_var, blockIdx.y == 0 && rl == 0);
+  const long r0 = (long)blockIdx.y * rows_per;
+  bn_apply_rows(x, ldx, mf, isf, w[c], b[c], relu, y, ldy, r0, min((long)M, r0 + rows_per), c, rl);
 }
 
 __global__ __launch_bounds__(BN_T) void bn_stats_final(int P, int C, long M, const float* __restrict__ x,
@@ -384,13 +420,12 @@ __device__ __forceinline__ void bn_bwd_reduce(int P, int C, const double* __rest
   if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
 }
 
-__global__ __launch_bounds__(BN_T) void bn_bwd_sums(int M, int C, const float* __restrict__ dy, long lddy,
-                                                   const float* __restrict__ x, long ldx,
-                                                   const float* __restrict__ relu_out, long ldo,
-                                                   const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                   int rows_per, double* __restrict__ part,
-                                                   unsigned int* __restrict__ cnt, double* __restrict__ sums,
-                                                   float* __restrict__ dw, float* __restrict__ db, float beta_w) {
+// partial block of the backward sums: part[blockIdx.y][0 / 1][c] = sum dyv, sum dyv * xhat over its rows
+__device__ __forceinline__ void bn_bwd_partial(int M, int C, const float* __restrict__ dy, long lddy,
+                                               const float* __restrict__ x, long ldx,
+                                               const float* __restrict__ relu_out, long ldo,
+                                               const float* __restrict__ mean, const float* __restrict__ invstd,
+                                               int rows_per, double* __restrict__ part) {
   __shared__ double sh[2][BN_RL][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -433,6 +468,16 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_sums(int M, int C, const float* _
     p[0] = t1;
     p[C] = t2;
   }
+}
+
+__global__ __launch_bounds__(BN_T) void bn_bwd_sums(int M, int C, const float* __restrict__ dy, long lddy,
+                                                   const float* __restrict__ x, long ldx,
+                                                   const float* __restrict__ relu_out, long ldo,
+                                                   const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                   int rows_per, double* __restrict__ part,
+                                                   unsigned int* __restrict__ cnt, double* __restrict__ sums,
+                                                   float* __restrict__ dw, float* __restrict__ db, float beta_w) {
+  bn_bwd_partial(M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, rows_per, part);
   if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
   bn_bwd_reduce(gridDim.y, C, part, blockIdx.x, sums, dw, db, beta_w);
 }
@@ -441,6 +486,36 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_final(int P, int C, const double*
                                                     double* __restrict__ sums, float* __restrict__ dw,
                                                     float* __restrict__ db, float beta_w) {
   bn_bwd_reduce(P, C, part, blockIdx.x, sums, dw, db, beta_w);
+}
+
+// dx rows [r0, r1) of channel c (row lane rl) from the channel's sums s1, s2 (train) -- or w*invstd*dyv (eval)
+__device__ __forceinline__ void bn_bwd_apply_rows(int train, int M, const float* __restrict__ dy, long lddy,
+                                                  const float* __restrict__ x, long ldx,
+                                                  const float* __restrict__ relu_out, long ldo, float mu, float is,
+                                                  float wc, double s1, double s2, float* __restrict__ dx, long lddx,
+                                                  float beta_dx, long r0, long r1, int c, int rl) {
+  const float invM = 1.f / (float)M;
+  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
+    float dv[NB], xv[NB], ov[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const long r = rb + BN_RL * i;
+      const bool ok = r < r1;
+      dv[i] = ok ? dy[r * lddy + c] : 0.f;
+      xv[i] = ok && train ? x[r * ldx + c] : 0.f;
+      ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (rb + BN_RL * i < r1) {
+        float d = dv[i];
+        if (relu_out && !(ov[i] > 0.f)) d = 0.f;
+        float v;
+        if (train) v = bn_bwd_elem(d, xv[i], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
+        else v = (wc * is) * d;
+        bn_dx_store(dx + (rb + BN_RL * i) * lddx + c, beta_dx, v);
+      }
+  }
 }
 
 // Fused final + apply of the BN backward: grid (ceil(C/64), ceil(M/rows_per_block)); every block
@@ -466,31 +541,40 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_sums(int train, int M, int 
     if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)s2;
     if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
   }
-  const float is = invstd[c], mu = mean[c], wc = w[c];
-  const float invM = 1.f / (float)M;
   const long r0 = (long)blockIdx.y * rows_per_block;
-  const long r1 = min((long)M, r0 + rows_per_block);
-  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
-    float dv[NB], xv[NB], ov[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const long r = rb + BN_RL * i;
-      const bool ok = r < r1;
-      dv[i] = ok ? dy[r * lddy + c] : 0.f;
-      xv[i] = ok && train ? x[r * ldx + c] : 0.f;
-      ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-      if (rb + BN_RL * i < r1) {
-        float d = dv[i];
-        if (relu_out && !(ov[i] > 0.f)) d = 0.f;
-        float v;
-        if (train) v = bn_bwd_elem(d, xv[i], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
-        else v = (wc * is) * d;
-        bn_dx_store(dx + (rb + BN_RL * i) * lddx + c, beta_dx, v);
-      }
+  bn_bwd_apply_rows(train, M, dy, lddy, x, ldx, relu_out, ldo, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
+                    min((long)M, r0 + rows_per_block), c, rl);
+}
+
+// The whole train-mode backward in one launch: grid (ceil(C/64), P) partial blocks meet at their
+// channel group's barrier (cnt[2 * blockIdx.x], zeroed, left zero), reduce the partials in
+// bn_part_sums' order and write dx for their own rows (re-read from L2).  Bit-identical to
+// bn_bwd_sums + bn_bwd_apply_sums.
+__global__ __launch_bounds__(BN_T) void bn_bwd_fused(int M, int C, const float* __restrict__ dy, long lddy,
+                                                    const float* __restrict__ x, long ldx,
+                                                    const float* __restrict__ relu_out, long ldo,
+                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                    const float* __restrict__ w, int rows_per,
+                                                    double* __restrict__ part, unsigned int* __restrict__ cnt,
+                                                    float* __restrict__ dx, long lddx, float beta_dx,
+                                                    float* __restrict__ dw, float* __restrict__ db, float beta_w) {
+  __shared__ double tot[2][64];
+  bn_bwd_partial(M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, rows_per, part);
+  unsigned int* gc = cnt + 2 * blockIdx.x;
+  block_group_sync(gc, gridDim.y);
+  bn_part_sums(gridDim.y, C, part, blockIdx.x, tot);
+  block_group_leave(gc, gc + 1, gridDim.y);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  if (c >= C) return;
+  const double s1 = tot[0][cl], s2 = tot[1][cl];
+  if (blockIdx.y == 0 && rl == 0) {
+    if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)s2;
+    if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
   }
+  const long r0 = (long)blockIdx.y * rows_per;
+  bn_bwd_apply_rows(1, M, dy, lddy, x, ldx, relu_out, ldo, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
+                    min((long)M, r0 + rows_per), c, rl);
 }
 
 // train: dx = w*invstd*(dyv - s1/M - xhat*s2/M);  eval (sums == null): dx = w*invstd*dyv
@@ -520,6 +604,13 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
 // rows per partial block: at most 64 partials per 64-channel group (the fixed-order reduction reads
 // P/4 of them per thread), at least 32 rows each, fewer partials if the fp64 workspace is short
 constexpr int BN_APPLY_ROWS = 64;   // rows per block of the fused (partials-reducing) apply kernels
+
+// the single-launch (group barrier) kernels: two zeroed counters per 64-channel group, and a grid small
+// enough that all its blocks are resident together (256 CUs x >= 4 blocks of BN_T threads)
+static bool bn_fused_fits(int C, int P, const unsigned int* counters, int n_counters) {
+  const long groups = vc_cdiv(C, 64);
+  return counters && n_counters >= 2 * groups && groups * P <= 1024 && vc_knob("VITCNN_BN_FUSED", 0);
+}
 
 int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
   // most partials per channel (knob BN_PCAP, probe library)
@@ -812,6 +903,14 @@ VC_EXPORT int vc_bn_forward(int train, long M, int C, const float* x, long ldx, 
                             float* save_mean, float* save_invstd, float* run_mean, float* run_var, const float* w,
                             const float* b, int relu, float* y, long ldy, float* ws, long ws_floats,
                             hipStream_t stream) {
+  return vc_bn_forward_ex(train, M, C, x, ldx, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y,
+                          ldy, ws, ws_floats, nullptr, 0, stream);
+}
+
+VC_EXPORT int vc_bn_forward_ex(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
+                               float* save_mean, float* save_invstd, float* run_mean, float* run_var, const float* w,
+                               const float* b, int relu, float* y, long ldy, float* ws, long ws_floats,
+                               unsigned int* counters, int n_counters, hipStream_t stream) {
   VC_REQUIRE(C > 0 && M >= 0);
   if (!train || M == 0) {
     int rc = vc_bn_stats(train, M, C, x, ldx, eps, momentum, save_mean, save_invstd, run_mean, run_var, ws, ws_floats,
@@ -825,6 +924,12 @@ VC_EXPORT int vc_bn_forward(int train, long M, int C, const float* x, long ldx, 
   const int rows_per = bn_rows_per(M, C, ws_doubles, 0);
   const int P = vc_cdiv(M, rows_per);
   VC_REQUIRE((long)P * C * 2 <= ws_doubles && P <= 65535);
+  if (bn_fused_fits(C, P, counters, n_counters)) {   // one launch: group barrier
+    hipLaunchKernelGGL(bn_forward_fused, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, ldx, rows_per,
+                       wsd, counters, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy);
+    VC_CHECK_LAUNCH();
+    return VC_OK;
+  }
   hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
                      (unsigned int*)nullptr, eps, momentum, save_mean, save_invstd, run_mean, run_var);
   VC_CHECK_LAUNCH();
@@ -862,7 +967,15 @@ VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy,
   const int P = vc_cdiv(M, rows_per);
   VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_doubles && P <= 65535);
   double* sums = wsd + (long)P * C * 2;
-  unsigned int* cnt = (counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;
+  if (train && dx && bn_fused_fits(C, P, counters, n_counters)) {   // one launch: group barrier
+    hipLaunchKernelGGL(bn_bwd_fused, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
+                       relu_out, ldo, mean, invstd, w, rows_per, wsd, counters, dx, lddx, beta_dx, dw, db, beta_w);
+    VC_CHECK_LAUNCH();
+    return VC_OK;
+  }
+  // tickets (the last-arriving partial block reduces) only without dx: with dx the channel-tiled apply
+  // reduces the partials itself
+  unsigned int* cnt = (!(train && dx) && counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;
   hipLaunchKernelGGL(bn_bwd_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
                      relu_out, ldo, mean, invstd, rows_per, wsd, cnt, sums, dw, db, beta_w);
   VC_CHECK_LAUNCH();

@@ -96,7 +96,8 @@ _LANE_MAP = []       # logical lane -> stream index (empty: lane i on stream i)
 # the two read-modify-write GEMM epilogues race, and the result depends on the schedule)
 _CH_LANE = 1
 _CH_ORDERED = True
-_BN_TICKETS = False  # BN reductions in the last-arriving block: measured ~1% slower (every arrival is an agent-scope release = L2 writeback)
+_BN_TICKETS = False  # BN reductions without dx in the last-arriving block: measured ~1% slower (every arrival is an
+#                     agent-scope release = L2 writeback); with dx the counters select the one-launch kernels
 
 UNUSED_PREFIXES = ("hsi1.global_view.tokenlearner.", "hsi1.global_view.ln3.",
                    "hsi2.global_view.tokenlearner.", "hsi2.global_view.ln3.")
@@ -717,9 +718,11 @@ class _Program:
         tag, ws = seq + ".1", self.ws
         mean, inv = ws.f(tag + ".bm", Cout), ws.f(tag + ".bi", Cout)
         out = ws.f(seq + ".out", M * Cout)
-        self.L.vc_bn_forward(self.train, M, Cout, pre, Cout, BN_EPS, BN_MOM, mean, inv,
-                             self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"], self.P[tag + ".weight"],
-                             self.P[tag + ".bias"], 1, out, Cout, self.scr_p, self.scr_n, self.s)
+        # one launch (group barrier over the lane's zeroed counters), include/vitcnn.h vc_bn_forward_ex
+        self.L.vc_bn_forward_ex(self.train, M, Cout, pre, Cout, BN_EPS, BN_MOM, mean, inv,
+                                self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"],
+                                self.P[tag + ".weight"], self.P[tag + ".bias"], 1, out, Cout, self.scr_p, self.scr_n,
+                                self._cnt[self.cur], N_COUNTERS, self.s)
         return out
 
     def fusion(self, pfx, X1, C1, X2, C2, M, Cout):
@@ -921,7 +924,7 @@ class _Program:
         self.L.vc_bn_bwd_ex(self.train, M, C, dY, lddy, X, ldx, relu_out or None, C, ws.f(tag + ".bm", C),
                             ws.f(tag + ".bi", C), self.P[pfx + ".weight"], dX or None, lddx, beta_dx,
                             self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n,
-                            self._cnt[self.cur] if _BN_TICKETS else None, N_COUNTERS, self.s)
+                            self._cnt[self.cur] if (dX or _BN_TICKETS) else None, N_COUNTERS, self.s)
 
     def ln_bwd(self, pfx, tag, dY, X, R, C, dX, beta_dx, res=0, defer=False):
         """dX = beta_dx * dX + LN grad, or res + LN grad (res: a residual gradient in another buffer).
