@@ -198,6 +198,10 @@ VC_API int vc_conv3x3_dgrad(int B, int H, int W, int C, int O, int pad, const fl
  *   dgrad: dx (ld lddx) = beta dx + the conv's input gradient for dy
  * ws: split-K slabs when the tile grid is small (fixed-order sums; may be null: no split). */
 VC_API int vc_conv3x3_pack(int O, int C, int mode, const float* src, float* dst, float beta, hipStream_t stream);
+/* mode-0 packs of n convs in one launch per 48: shapes = host array {O0, C0, O1, C1, ...}, src / dst = host
+ * arrays of n device pointers (torch-layout weights / Wt buffers); bit-identical to n vc_conv3x3_pack calls */
+VC_API int vc_conv3x3_pack_many(int n, const int* shapes, const float* const* src, float* const* dst,
+                                hipStream_t stream);
 VC_API int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* wt,
                               const float* bias, float* y, long ldy, float* ws, long ws_floats, hipStream_t stream);
 VC_API int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* dy,
@@ -205,6 +209,11 @@ VC_API int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, cons
 VC_API int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,
                                 const float* wt, float beta, float* dx, long lddx, float* ws, long ws_floats,
                                 hipStream_t stream);
+/* wgrad written straight into the torch layout dw [O][C][3][3] (overwritten): vc_conv3x3_tap_wgrad +
+ * vc_conv3x3_pack mode 2 with beta 0 in one call, bit-identical (the same sums, stored transposed). */
+VC_API int vc_conv3x3_tap_wgrad_oihw(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
+                                     const float* dy, long lddy, float* dw, float* ws, long ws_floats,
+                                     hipStream_t stream);
 /* train-mode BatchNorm(x) (statistics as vc_bn_stats_ex: save_* and running stats written) followed by
  * vc_im2col3x3 of the normalised x, the statistics' final reduction done inside the im2col launch
  * (ms_conv_bn_relu's BN -> conv3x3, Mutimodality_Mamba7.py:1035-1048); bit-identical to the two calls. */

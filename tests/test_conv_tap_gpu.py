@@ -105,3 +105,36 @@ def test_conv_tap_fwd_wgrad_dgrad(B, H, C, O, pad, ldx, ws_log2):
     # norm-relative: fp32 accumulation over K <= 20k terms stays ~1e-6 of the norm
     assert max(errs[3:]) < 3e-6, errs
     assert torch.isnan(dx[:, C:]).all()          # the row padding is never written
+    # the weight gradient stored straight into the torch layout: bit-identical to wgrad + pack mode 2
+    dw2 = torch.full((O, C, 3, 3), 7.0, device=DEV)
+    L.vc_conv3x3_tap_wgrad_oihw(B, H, H, C, O, pad, xd.data_ptr(), ldx, dyd.data_ptr(), O, dw2.data_ptr(), wsp,
+                                wsn, s)
+    torch.cuda.synchronize()
+    assert torch.equal(dw2, dw)
+
+
+@pytest.mark.gpu
+def test_conv_pack_many_matches_single_packs():
+    """vc_conv3x3_pack_many (one launch per 48 convs) == one vc_conv3x3_pack (mode 0) per conv, bit for bit,
+    padding columns written 0; 50 convs so the second launch of the batch runs too"""
+    _need_gpu()
+    import ctypes
+    from vitcnn_amd._lib import lib
+    L = lib()
+    g = torch.Generator().manual_seed(7)
+    shapes = [(1 + (7 * i) % 37, 1 + (13 * i) % 29) for i in range(50)] + [(256, 2193), (16, 1)]
+    ws = [torch.randn(O, C, 3, 3, generator=g).to(DEV) for O, C in shapes]
+    sizes = [O * 9 * ((C + 3) // 4 * 4) for O, C in shapes]
+    one = [torch.full((k,), 5.0, device=DEV) for k in sizes]
+    many = [torch.full((k,), 5.0, device=DEV) for k in sizes]
+    s = torch.cuda.current_stream().cuda_stream
+    for (O, C), w, d in zip(shapes, ws, one):
+        L.vc_conv3x3_pack(O, C, 0, w.data_ptr(), d.data_ptr(), 0.0, s)
+    n = len(shapes)
+    sh = (ctypes.c_int * (2 * n))(*[v for O, C in shapes for v in (O, C)])
+    src = (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws])
+    dst = (ctypes.c_void_p * n)(*[d.data_ptr() for d in many])
+    L.vc_conv3x3_pack_many(n, ctypes.addressof(sh), ctypes.addressof(src), ctypes.addressof(dst), s)
+    torch.cuda.synchronize()
+    for a, b in zip(one, many):
+        assert torch.equal(a, b)

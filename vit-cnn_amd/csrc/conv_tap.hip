@@ -26,6 +26,8 @@
 // operand-bandwidth-bound at ~50 TF/s).
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int TM = 128, TN = 128, TK = 32;
@@ -51,6 +53,7 @@ struct TapArgs {
   float* out; long ldo;          // fwd: y [M][ldo]; wgrad: dWt [O][9C] (ldo = 9C); dgrad: dx [M][ldo]
   float beta;                    // dgrad: dx = beta dx + ...
   float* part;                   // split-K slabs [nsplit][M][N]
+  int oihw;                      // wgrad: out is the torch layout [O][C][3][3] (else dWt [O][9C])
   int vx, vdy, vw;               // float4 loads allowed (16-B aligned base, ld % 4 == 0)
   FastDiv fOW, fOHW, fW, fHW;
 };
@@ -246,6 +249,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
         const float v = acc[mi][ni][r];
         if (split) {
           a.part[((long)blockIdx.z * a.M + row) * a.N + col] = v;
+        } else if (MODE == WGRAD && a.oihw) {
+          a.out[((long)row * a.C + cl) * 9 + ntap] = v;
         } else {
           float* o = a.out + (long)row * a.ldo + col;
           if (MODE == FWD) *o = v + (a.bias ? a.bias[col] : 0.f);
@@ -264,7 +269,13 @@ __global__ __launch_bounds__(256) void conv_tap_reduce(TapArgs a, int nsplit) {
   const int row = (int)(e / a.N), col = (int)(e - (long)row * a.N);
   const long slab = (long)a.M * a.N;
   float s = 0.f;
-  for (int z = 0; z < nsplit; ++z) s += a.part[z * slab + e];
+#pragma unroll 8
+  for (int z = 0; z < nsplit; ++z) s += a.part[z * slab + e];   // 8 slab loads in flight, summed in z order
+  if (MODE == WGRAD && a.oihw) {   // torch layout [O][C][3][3]: col = tap * C + c
+    const int tap = col / a.C, c = col - tap * a.C;
+    a.out[((long)row * a.C + c) * 9 + tap] = s;
+    return;
+  }
   float* o = a.out + (long)row * a.ldo + col;
   if (MODE == FWD) *o = s + (a.bias ? a.bias[col] : 0.f);
   else if (MODE == DGRAD) *o = (a.beta != 0.f ? a.beta * *o : 0.f) + s;
@@ -294,6 +305,31 @@ __global__ __launch_bounds__(256) void conv_pack(int O, int C, int mode, const f
   const int c = (int)(oc_ % C), o = (int)(oc_ / C);
   if (mode == 1) dst[((long)tap * O + o) * C + c] = src[e];
   else dst[e] = (beta != 0.f ? beta * dst[e] : 0.f) + src[((long)o * 9 + tap) * C + c];
+}
+
+// mode-0 packs of up to PACK_MAX convs in one launch: conv i owns blocks [start[i], start[i + 1]) of the
+// 1-D grid (256 elements of its Wt [O][9][Cw] each), the same element map as conv_pack mode 0
+constexpr int PACK_MAX = 48;
+struct PackMany {
+  int n;
+  int start[PACK_MAX + 1];
+  int O[PACK_MAX], C[PACK_MAX];
+  const float* src[PACK_MAX];
+  float* dst[PACK_MAX];
+};
+
+__global__ __launch_bounds__(256) void conv_pack_many(PackMany P) {
+  const int b = blockIdx.x;
+  int i = 0;
+  for (int k = 1; k < P.n; ++k)
+    if (b >= P.start[k]) i = k;
+  const int O = P.O[i], C = P.C[i], Cw = (C + 3) & ~3;
+  const long e = (long)(b - P.start[i]) * 256 + threadIdx.x;
+  if (e >= (long)O * 9 * Cw) return;
+  const int c = (int)(e % Cw);
+  const long ot = e / Cw;
+  const int tap = (int)(ot % 9), o = (int)(ot / 9);
+  P.dst[i][e] = c < C ? P.src[i][((long)o * C + c) * 9 + tap] : 0.f;
 }
 
 bool vec_ok(const float* p, long ld) { return p && ((uintptr_t)p % 16 == 0) && (ld % 4 == 0); }
@@ -345,6 +381,31 @@ VC_EXPORT int vc_conv3x3_pack(int O, int C, int mode, const float* src, float* d
   return VC_OK;
 }
 
+VC_EXPORT int vc_conv3x3_pack_many(int n, const int* shapes, const float* const* src, float* const* dst,
+                                   hipStream_t stream) {
+  VC_REQUIRE(n >= 0 && (n == 0 || (shapes && src && dst)));
+  for (int i0 = 0; i0 < n; i0 += PACK_MAX) {   // PACK_MAX convs per launch
+    PackMany P;
+    P.n = std::min(PACK_MAX, n - i0);
+    long total = 0;
+    for (int k = 0; k < P.n; ++k) {
+      const int O = shapes[2 * (i0 + k)], C = shapes[2 * (i0 + k) + 1];
+      VC_REQUIRE(O > 0 && C > 0 && src[i0 + k] && dst[i0 + k]);
+      P.O[k] = O;
+      P.C[k] = C;
+      P.src[k] = src[i0 + k];
+      P.dst[k] = dst[i0 + k];
+      P.start[k] = (int)total;
+      total += vc_cdiv((long)O * 9 * ((C + 3) & ~3), 256);
+      VC_REQUIRE(total < (1L << 31));
+    }
+    P.start[P.n] = (int)total;
+    hipLaunchKernelGGL(conv_pack_many, dim3((unsigned)total), dim3(256), 0, stream, P);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
 VC_EXPORT int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* wt,
                                  const float* bias, float* y, long ldy, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad && C > 0 && O > 0 && (pad == 0 || pad == 1));
@@ -361,9 +422,8 @@ VC_EXPORT int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, con
   return launch_tap<FWD>(a, vc_cdiv(O, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
 }
 
-VC_EXPORT int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
-                                   const float* dy, long lddy, float* dwt, float* ws, long ws_floats,
-                                   hipStream_t stream) {
+static int tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* dy, long lddy,
+                     float* dwt, int oihw, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad && C > 0 && O > 0 && (pad == 0 || pad == 1));
   VC_REQUIRE(x && dy && dwt && ldx >= C && lddy >= O);
   TapArgs a = geo(B, H, W, C, O, pad);
@@ -375,8 +435,21 @@ VC_EXPORT int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, c
   a.tpt = vc_cdiv(C, TN);
   a.nk = vc_cdiv(a.P, TK);
   a.x = x; a.ldx = ldx; a.dy = dy; a.lddy = lddy; a.out = dwt; a.ldo = 9L * C;
+  a.oihw = oihw;
   a.vx = vec_ok(x, ldx); a.vdy = vec_ok(dy, lddy);
   return launch_tap<WGRAD>(a, 9 * a.tpt, vc_cdiv(O, TM), ws, ws_floats, stream);
+}
+
+VC_EXPORT int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
+                                   const float* dy, long lddy, float* dwt, float* ws, long ws_floats,
+                                   hipStream_t stream) {
+  return tap_wgrad(B, H, W, C, O, pad, x, ldx, dy, lddy, dwt, 0, ws, ws_floats, stream);
+}
+
+VC_EXPORT int vc_conv3x3_tap_wgrad_oihw(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
+                                        const float* dy, long lddy, float* dw, float* ws, long ws_floats,
+                                        hipStream_t stream) {
+  return tap_wgrad(B, H, W, C, O, pad, x, ldx, dy, lddy, dw, 1, ws, ws_floats, stream);
 }
 
 VC_EXPORT int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,

@@ -20,6 +20,8 @@ mask; maxpool, pooled-scale and product backwards); the parameter gradients land
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -220,7 +222,8 @@ class _Program:
         self.train = m.training
         self.grad = grad
         self.tape = []        # backward closures, run in reverse
-        self.g = {}           # id(activation) -> gradient buffer (zero-initialised on first use)
+        self.g = {}           # id(activation) -> gradient buffer (grad_of: zero-filled on creation;
+                              # acc: left to its first writer, which writes it whole with beta 0)
         self.keep = {}        # id -> activation (keeps ids unique while the tape lives)
         self.no_grad_ids = set()
 
@@ -235,14 +238,29 @@ class _Program:
             self.g[k] = buf
         return self.g[k]
 
+    def acc(self, t):
+        """(gradient buffer of t, beta) for a writer that covers all of t's gradient: beta 0 on the first
+        write (no zero fill), 1 once the buffer holds a contribution"""
+        k = id(t)
+        if k in self.g:
+            return self.g[k], 1.0
+        buf = self.new(t.numel())
+        self.g[k] = buf
+        return buf, 0.0
+
     def record(self, fn, *acts):
         if self.grad:
             for a in acts:
                 self.keep[id(a)] = a
             self.tape.append(fn)
 
-    def add_into(self, dst, src, M, C, ld_dst=None):
-        self.L.vc_add2_2d(M, C, src.data_ptr(), C, None, 0, dst.data_ptr(), ld_dst or C, 1.0, self.s)
+    def add_into(self, dst, src, M, C, ld_dst=None, beta=1.0):
+        self.L.vc_add2_2d(M, C, src.data_ptr(), C, None, 0, dst.data_ptr(), ld_dst or C, beta, self.s)
+
+    def acc_into(self, t, src, M, C):
+        """t's gradient (+)= src (dense M x C)"""
+        g, beta = self.acc(t)
+        self.add_into(g, src, M, C, beta=beta)
 
     def nhwc(self, x):
         B, C, H, W = x.shape
@@ -271,8 +289,10 @@ class _Program:
         y = self.new(B, OH, OH, O)
         wt = None
         if _TAP_CONV:
-            wt = self.new(O * 9 * ((C + 3) // 4 * 4))   # tap-major weight (rows padded to 4), read again by dgrad
-            L.vc_conv3x3_pack(O, C, 0, conv.weight.data_ptr(), wt.data_ptr(), 0.0, self.s)
+            wt = self.wts.get(id(conv))   # tap-major weight (rows padded to 4), read again by dgrad
+            if wt is None:
+                wt = self.new(O * 9 * ((C + 3) // 4 * 4))
+                L.vc_conv3x3_pack(O, C, 0, conv.weight.data_ptr(), wt.data_ptr(), 0.0, self.s)
             L.vc_conv3x3_tap_fwd(B, H, H, C, O, pad, x.data_ptr(), ldx, wt.data_ptr(), conv.bias.data_ptr(),
                                  y.data_ptr(), O, scr, self.SCRATCH, self.s)
         elif _IMPLICIT_CONV:
@@ -287,15 +307,14 @@ class _Program:
 
         def bwd():
             dy = self.grad_of(y)
-            if _TAP_CONV:
-                dwt = self.new(O * K)
-                L.vc_conv3x3_tap_wgrad(B, H, H, C, O, pad, x.data_ptr(), ldx, dy.data_ptr(), O, dwt.data_ptr(), scr,
-                                       self.SCRATCH, self.s)
-                L.vc_conv3x3_pack(O, C, 2, dwt.data_ptr(), self.pgrad(conv.weight), 0.0, self.s)
+            if _TAP_CONV:   # the weight gradient stored in the torch layout by the wgrad launch itself
+                L.vc_conv3x3_tap_wgrad_oihw(B, H, H, C, O, pad, x.data_ptr(), ldx, dy.data_ptr(), O,
+                                            self.pgrad(conv.weight), scr, self.SCRATCH, self.s)
                 L.vc_colsum(M, O, dy.data_ptr(), O, self.pgrad(conv.bias), 0.0, scr, self.SCRATCH, self.s)
-                if id(x) not in self.no_grad_ids:
-                    L.vc_conv3x3_tap_dgrad(B, H, H, C, O, pad, dy.data_ptr(), O, wt.data_ptr(), 1.0,
-                                           self.grad_of(x).data_ptr(), ldx, scr, self.SCRATCH, self.s)
+                if id(x) not in self.no_grad_ids:   # every row's C columns written (ldx padding never read)
+                    gx, beta = self.acc(x)
+                    L.vc_conv3x3_tap_dgrad(B, H, H, C, O, pad, dy.data_ptr(), O, wt.data_ptr(), beta, gx.data_ptr(),
+                                           ldx, scr, self.SCRATCH, self.s)
                 return
             if _IMPLICIT_CONV:
                 L.vc_conv3x3_wgrad(B, H, H, C, O, pad, x.data_ptr(), ldx, None, None, None, None, dy.data_ptr(), O,
@@ -329,9 +348,10 @@ class _Program:
                              self.SCRATCH, self.s)
 
         def bwd():
+            gy, beta = self.acc(y)
             self.L.vc_bn_bwd(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
                              z.data_ptr() if relu else None, C, mean.data_ptr(), invstd.data_ptr(),
-                             bn.weight.data_ptr(), self.grad_of(y).data_ptr(), C, 1.0, self.pgrad(bn.weight),
+                             bn.weight.data_ptr(), gy.data_ptr(), C, beta, self.pgrad(bn.weight),
                              self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.s)
 
         self.record(bwd, y, z)
@@ -357,8 +377,8 @@ class _Program:
 
         def bwd():
             d = self.grad_of(out)
-            self.add_into(self.grad_of(b), d, M, O)
-            self.add_into(self.grad_of(a), d, M, O)
+            self.acc_into(b, d, M, O)
+            self.acc_into(a, d, M, O)
 
         self.record(bwd, a, b, out)
         if not pool:
@@ -371,10 +391,13 @@ class _Program:
         self.L.vc_maxpool2_fwd(self.B, H, H, C, x.data_ptr(), C, y.data_ptr(), arg.data_ptr(), self.s)
 
         def bwd():
-            tmp = self.new(x.numel())
+            gx, beta = self.acc(x)
+            # the pool backward writes every input element: straight into x's gradient on its first write
+            tmp = gx if beta == 0.0 else self.new(x.numel())
             self.L.vc_maxpool2_bwd(self.B, H, H, C, self.grad_of(y).data_ptr(), arg.data_ptr(), tmp.data_ptr(), C,
                                    self.s)
-            self.add_into(self.grad_of(x), tmp, self.B * H * H, C)
+            if beta != 0.0:
+                self.add_into(gx, tmp, self.B * H * H, C)
 
         self.record(bwd, x, y, arg)
         return y
@@ -385,11 +408,15 @@ class _Program:
 
         def bwd():
             dptr, ld = dout_of()
-            tmp = self.new(M * C)
-            self.L.vc_mul2_2d(M, C, dptr, ld, b.data_ptr(), C, tmp.data_ptr(), C, self.s)
-            self.add_into(self.grad_of(a), tmp, M, C)
-            self.L.vc_mul2_2d(M, C, dptr, ld, a.data_ptr(), C, tmp.data_ptr(), C, self.s)
-            self.add_into(self.grad_of(b), tmp, M, C)
+            tmp = None
+            for t, other in ((a, b), (b, a)):   # dt (+)= dout * other; first write straight into dt
+                g, beta = self.acc(t)
+                if beta == 0.0:
+                    self.L.vc_mul2_2d(M, C, dptr, ld, other.data_ptr(), C, g.data_ptr(), C, self.s)
+                else:
+                    tmp = tmp if tmp is not None else self.new(M * C)
+                    self.L.vc_mul2_2d(M, C, dptr, ld, other.data_ptr(), C, tmp.data_ptr(), C, self.s)
+                    self.add_into(g, tmp, M, C)
 
         self.record(bwd, a, b)
 
@@ -406,8 +433,30 @@ class _Program:
         x, _ = self.unit(x, 256, H, 256, mod.conv2)
         return x
 
+    def pack_all(self):
+        """every 3x3 conv's tap-major weights in one arena, packed by one launch (vc_conv3x3_pack_many)"""
+        self.wts = {}
+        if not _TAP_CONV:
+            return
+        convs = [c for c in self.m.modules() if isinstance(c, nn.Conv2d) and tuple(c.kernel_size) == (3, 3)]
+        sizes = [c.out_channels * 9 * ((c.in_channels + 3) // 4 * 4) for c in convs]
+        arena = self.new(sum(sizes))
+        self.keep[id(arena)] = arena
+        n = len(convs)
+        shapes = (ctypes.c_int * (2 * n))(*[v for c in convs for v in (c.out_channels, c.in_channels)])
+        src = (ctypes.c_void_p * n)(*[c.weight.data_ptr() for c in convs])
+        dst = (ctypes.c_void_p * n)()
+        off = 0
+        for i, (c, k) in enumerate(zip(convs, sizes)):
+            self.wts[id(c)] = arena[off:off + k]
+            dst[i] = arena.data_ptr() + F32 * off
+            off += k
+        self.L.vc_conv3x3_pack_many(n, ctypes.addressof(shapes), ctypes.addressof(src), ctypes.addressof(dst),
+                                    self.s)
+
     def run(self):
         m, L, B, P = self.m, self.L, self.B, self.P
+        self.pack_all()
         c1, c2 = m.c1, m.c2
         x1, x2 = self.nhwc(self.x1), self.nhwc(self.x2)
         HW = P * P
@@ -474,8 +523,8 @@ class _Program:
         conv6 = m.cm.conv6
         self.gemm(1, 0, m.ncls, C, Mo, dlogits.data_ptr(), m.ncls, x.data_ptr(), C, 0.0, self.pgrad(conv6.weight), C,
                   bias_grad=self.pgrad(conv6.bias))
-        self.gemm(0, 0, Mo, C, m.ncls, dlogits.data_ptr(), m.ncls, conv6.weight.data_ptr(), C, 1.0,
-                  self.grad_of(x).data_ptr(), C)
+        gx, beta = self.acc(x)
+        self.gemm(0, 0, Mo, C, m.ncls, dlogits.data_ptr(), m.ncls, conv6.weight.data_ptr(), C, beta, gx.data_ptr(), C)
         for fn in reversed(self.tape):
             fn()
         self.tape, self.g, self.keep = [], {}, {}

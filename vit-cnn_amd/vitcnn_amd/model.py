@@ -82,11 +82,11 @@ _TRACER = None   # launch-structure recorder of tools/critical_path.py (None in 
 _GROUP = True        # grouped launches of independent fp32 GEMMs
 # bf16 mode diagnostics (tools/bf16_sites.py): GEMM issue indices kept in fp32, and a log of call sites
 _BF16_EXACT: set = set()
-# bf16 mode: bf16 operands only for products with K >= this that are not weight gradients (the im2col'ed
-# 3x3 convs, K = 9 Cin): the short-K products are launch-latency-bound, where bf16 saves nothing and costs
-# the grouped launch (bf16 GEMMs launch alone), and the long-K weight gradients run slower on the bf16
-# kernel than on the fp32 split-K one; 0 = every GEMM bf16 (round 2's mode)
-_BF16_MIN_K = 1024
+# bf16 mode: bf16 operands for products with K >= this that are not weight gradients; 0 = every GEMM
+# bf16 (the reference's autocast mode).  Round 4: with bf16 MFMAs in the pipelined kernel (grouped like the
+# fp32 problems) every GEMM in bf16 is the fastest: 1.67-1.69 vs 1.78 ms/step with 1024 (round 3's value,
+# the im2col'ed 3x3 convs only) on one box, fp32 1.805 (profiles/r04_ab_bf16_min_k.log)
+_BF16_MIN_K = 0
 _GEMM_SITES = None
 _LANE_MAP = []       # logical lane -> stream index (empty: lane i on stream i)
 # the channel-feature backward chain's lane: 1 = after the local-conv chain on lane 1 (default); 3 = on
