@@ -277,7 +277,8 @@ def dominant_kernel_roofline(model, batch, reps):
 
 def gemm_roofline(model, batch, reps):
     """The largest GEMM of the step (hsi1.local_feature im2col'ed 3x3 conv, M = B*49, N = 256,
-    K = 9*144) timed the same way; MFMA-bound (fp32 peak).  Reported beside the dominant kernel."""
+    K = 9*144; the automatic choice, round 4: the LDS-DMA pipelined kernel) timed the same way;
+    MFMA-bound (fp32 peak).  Reported beside the dominant kernel."""
     from vitcnn_amd._lib import lib
     from vitcnn_amd.model import _Program
     dev = model.flat_params.device
@@ -296,7 +297,8 @@ def gemm_roofline(model, batch, reps):
     t = time_kernel(fn, reps, stream)
     flops = 2.0 * M * N * K
     achieved = flops / t / 1e12
-    return {"kernel": "gemm_f32_mfma<false,true> (hsi1.local_feature conv3x3, M=%d N=%d K=%d)" % (M, N, K),
+    return {"kernel": "gp::gemm_pipe<64,64> fp32, LDS-DMA pipelined (hsi1.local_feature conv3x3, M=%d N=%d K=%d)"
+            % (M, N, K),
             "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "avg_launch_us": round(t * 1e6, 2),
             "flop_per_launch": flops}
@@ -683,7 +685,8 @@ def time_steps(step, dev, steps, world, warm_s=WARM_S):
 
 def bf16_gemm_roofline(model, batch, reps):
     """The largest contraction of the step in bf16-operand mode (hsi1.local_feature 3x3 conv, M = B*49,
-    N = 256, K = 1296 on v_mfma_f32_16x16x32_bf16, fp32 accumulation) against the dense bf16 peak."""
+    N = 256, K = 1296: the pipelined kernel's v_mfma_f32_16x16x32_bf16 over fp32 LDS stages, fp32
+    accumulation) against the dense bf16 peak."""
     from vitcnn_amd._lib import lib
     from vitcnn_amd.model import _Program
     dev = model.flat_params.device
@@ -702,7 +705,8 @@ def bf16_gemm_roofline(model, batch, reps):
     t = time_kernel(fn, reps, stream)
     flops = 2.0 * M * N * K
     achieved = flops / t / 1e12
-    return {"kernel": "gemm_mfma<bf16> (hsi1.local_feature conv3x3, M=%d N=%d K=%d)" % (M, N, K),
+    return {"kernel": "gp::gemm_pipe<64,64> bf16 MFMA over fp32 stages (hsi1.local_feature conv3x3, M=%d N=%d K=%d)"
+            % (M, N, K),
             "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_BF16_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_MFMA_TFLOPS, 5), "avg_launch_us": round(t * 1e6, 2),
             "flop_per_launch": flops}

@@ -19,6 +19,10 @@ constexpr int NB = 8;       // rows (or partials) per lane whose loads a BatchNo
 #define VC_BN_RL 16
 #endif
 constexpr int BN_RL = VC_BN_RL, BN_T = 64 * BN_RL;
+// the one-launch (group barrier) kernels: 256-thread blocks, so a grid's blocks are co-resident (a
+// 1024-thread block holds a whole CU's wave slots at their register count: a 256-block barrier grid could
+// never finish beside other work); they compute the same 16 partial lanes (4 per thread), bit-identically
+constexpr int BNF_T = 256;
 
 __global__ __launch_bounds__(256) void ln_fwd(int R, int C, const float* __restrict__ x, long ldx,
                                               const float* __restrict__ w, const float* __restrict__ b, float eps,
@@ -180,35 +184,44 @@ __device__ __forceinline__ void bn_dx_store(float* p, float beta_dx, float v) {
 // BN_RL partial lanes): on return (after a barrier) tot[0][cl] / tot[1][cl] hold channel cx*64+cl's two sums,
 // visible to every thread of the block.  Every consumer (the separate final kernels and the fused
 // apply kernels) sums in this one order, so their results agree bit for bit.
+template <int T = BN_T>
 __device__ __forceinline__ void bn_part_sums(int P, int C, const double* __restrict__ part, int cx,
                                              double (*tot)[64]) {
+  // T threads = T / 64 real lanes, each computing BN_RL / (T / 64) of the BN_RL partial lanes in turn (the
+  // same per-lane sums and combine order at any block size: bit-identical results)
+  constexpr int RT = T / 64, VPT = BN_RL / RT;
+  static_assert(RT * VPT == BN_RL, "block size");
   __shared__ double shr[2][BN_RL][64];
-  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int cl = threadIdx.x & 63, pt = threadIdx.x >> 6;
   const int c = cx * 64 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-    // NB partials per lane loaded before they are summed (one round of dependent loads per batch of
-    // NB instead of one per 4); the sums keep the partial order
-    for (int p0 = pl; p0 < P; p0 += BN_RL * NB) {
-      double a[NB], bq[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int p = p0 + BN_RL * i;
-        a[i] = p < P ? part[(long)p * 2 * C + c] : 0.0;
-        bq[i] = p < P ? part[(long)p * 2 * C + C + c] : 0.0;
-      }
+  for (int j = 0; j < VPT; ++j) {
+    const int pl = pt + RT * j;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C) {
+      // NB partials per lane loaded before they are summed (one round of dependent loads per batch of
+      // NB instead of one per 4); the sums keep the partial order
+      for (int p0 = pl; p0 < P; p0 += BN_RL * NB) {
+        double a[NB], bq[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
-        if (p0 + BN_RL * i < P) {
-          s1 += a[i];
-          s2 += bq[i];
+        for (int i = 0; i < NB; ++i) {
+          const int p = p0 + BN_RL * i;
+          a[i] = p < P ? part[(long)p * 2 * C + c] : 0.0;
+          bq[i] = p < P ? part[(long)p * 2 * C + C + c] : 0.0;
         }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          if (p0 + BN_RL * i < P) {
+            s1 += a[i];
+            s2 += bq[i];
+          }
+      }
     }
+    shr[0][pl][cl] = s1;
+    shr[1][pl][cl] = s2;
   }
-  shr[0][pl][cl] = s1;
-  shr[1][pl][cl] = s2;
   __syncthreads();
-  if (pl == 0) {
+  if (pt == 0) {
     double t1 = shr[0][0][cl], t2 = shr[1][0][cl];
 #pragma unroll
     for (int l = 1; l < BN_RL; ++l) {
@@ -257,19 +270,20 @@ __device__ __forceinline__ void bn_stats_reduce(int P, int C, long M, const floa
 }
 
 // y = relu?((x - mean) * invstd * w + b) over rows [r0, r1) of channel c (row lane rl)
+template <int NL = BN_RL>   // row lanes of the block (rl in [0, NL))
 __device__ __forceinline__ void bn_apply_rows(const float* __restrict__ x, long ldx, float mf, float isf, float wc,
                                               float bc, int relu, float* __restrict__ y, long ldy, long r0, long r1,
                                               int c, int rl) {
-  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
+  for (long rb = r0 + rl; rb < r1; rb += NL * NB) {   // NB rows' loads in flight
     float xv[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) xv[i] = rb + BN_RL * i < r1 ? x[(rb + BN_RL * i) * ldx + c] : 0.f;
+    for (int i = 0; i < NB; ++i) xv[i] = rb + NL * i < r1 ? x[(rb + NL * i) * ldx + c] : 0.f;
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      if (rb + BN_RL * i < r1) {
+      if (rb + NL * i < r1) {
         float v = bn_fwd_elem(xv[i], mf, isf, wc, bc);
         if (relu) v = fmaxf(v, 0.f);
-        y[(rb + BN_RL * i) * ldy + c] = v;
+        y[(rb + NL * i) * ldy + c] = v;
       }
   }
 }
@@ -297,33 +311,39 @@ __global__ __launch_bounds__(BN_T) void bn_apply_stats(int M, int C, const float
 
 // partial block (channel group blockIdx.x, rows [blockIdx.y * rows_per, ...)) of the statistics:
 // part[blockIdx.y][0 / 1][c] = its shifted sums
+template <int T = BN_T>
 __device__ __forceinline__ void bn_stats_partial(int M, int C, const float* __restrict__ x, long ldx, int rows_per,
                                                  double* __restrict__ part) {
+  constexpr int RT = T / 64, VPT = BN_RL / RT;   // virtual row lanes per thread (see bn_part_sums)
   __shared__ double sh[2][BN_RL][64];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int cl = threadIdx.x & 63, rt = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per;
   const long r1 = min((long)M, r0 + rows_per);
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-    const double k = x[c];
-    for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight, summed in row order
-      float v[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i) v[i] = rb + BN_RL * i < r1 ? x[(rb + BN_RL * i) * ldx + c] : 0.f;
+  for (int j = 0; j < VPT; ++j) {
+    const int rl = rt + RT * j;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C) {
+      const double k = x[c];
+      for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight, summed in row order
+        float v[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
-        if (rb + BN_RL * i < r1) {
-          const double d = (double)v[i] - k;
-          s1 += d;
-          s2 = fma(d, d, s2);
-        }
+        for (int i = 0; i < NB; ++i) v[i] = rb + BN_RL * i < r1 ? x[(rb + BN_RL * i) * ldx + c] : 0.f;
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          if (rb + BN_RL * i < r1) {
+            const double d = (double)v[i] - k;
+            s1 += d;
+            s2 = fma(d, d, s2);
+          }
+      }
     }
+    sh[0][rl][cl] = s1;
+    sh[1][rl][cl] = s2;
   }
-  sh[0][rl][cl] = s1;
-  sh[1][rl][cl] = s2;
   __syncthreads();
-  if (rl == 0 && c < C) {
+  if (rt == 0 && c < C) {
     double* p = part + (long)blockIdx.y * 2 * C + c;
     double t1 = sh[0][0][cl], t2 = sh[1][0][cl];
 #pragma unroll
@@ -351,7 +371,7 @@ __global__ __launch_bounds__(BN_T) void bn_stats_sums(int M, int C, const float*
 // channel group meet at a group barrier (cnt[2 * blockIdx.x], zeroed, left zero), then each reduces the
 // group's partials (bn_part_sums: the same order as bn_stats_final / bn_apply_stats) and applies the
 // normalisation to its own rows (re-read from L2).  Bit-identical to bn_stats_sums + bn_apply_stats.
-__global__ __launch_bounds__(BN_T) void bn_forward_fused(int M, int C, const float* __restrict__ x, long ldx,
+__global__ __launch_bounds__(BNF_T) void bn_forward_fused(int M, int C, const float* __restrict__ x, long ldx,
                                                         int rows_per, double* __restrict__ part,
                                                         unsigned int* __restrict__ cnt, float eps, float momentum,
                                                         float* __restrict__ save_mean, float* __restrict__ save_invstd,
@@ -359,10 +379,10 @@ __global__ __launch_bounds__(BN_T) void bn_forward_fused(int M, int C, const flo
                                                         const float* __restrict__ w, const float* __restrict__ b,
                                                         int relu, float* __restrict__ y, long ldy) {
   __shared__ double tot[2][64];
-  bn_stats_partial(M, C, x, ldx, rows_per, part);
+  bn_stats_partial<BNF_T>(M, C, x, ldx, rows_per, part);
   unsigned int* gc = cnt + 2 * blockIdx.x;
   block_group_sync(gc, gridDim.y);
-  bn_part_sums(gridDim.y, C, part, blockIdx.x, tot);
+  bn_part_sums<BNF_T>(gridDim.y, C, part, blockIdx.x, tot);
   block_group_leave(gc, gc + 1, gridDim.y);
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -371,7 +391,7 @@ __global__ __launch_bounds__(BN_T) void bn_forward_fused(int M, int C, const flo
   bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
                      run_var, blockIdx.y == 0 && rl == 0);
   const long r0 = (long)blockIdx.y * rows_per;
-  bn_apply_rows(x, ldx, mf, isf, w[c], b[c], relu, y, ldy, r0, min((long)M, r0 + rows_per), c, rl);
+  bn_apply_rows<BNF_T / 64>(x, ldx, mf, isf, w[c], b[c], relu, y, ldy, r0, min((long)M, r0 + rows_per), c, rl);
 }
 
 __global__ __launch_bounds__(BN_T) void bn_stats_final(int P, int C, long M, const float* __restrict__ x,
@@ -421,43 +441,49 @@ __device__ __forceinline__ void bn_bwd_reduce(int P, int C, const double* __rest
 }
 
 // partial block of the backward sums: part[blockIdx.y][0 / 1][c] = sum dyv, sum dyv * xhat over its rows
+template <int T = BN_T>
 __device__ __forceinline__ void bn_bwd_partial(int M, int C, const float* __restrict__ dy, long lddy,
                                                const float* __restrict__ x, long ldx,
                                                const float* __restrict__ relu_out, long ldo,
                                                const float* __restrict__ mean, const float* __restrict__ invstd,
                                                int rows_per, double* __restrict__ part) {
+  constexpr int RT = T / 64, VPT = BN_RL / RT;   // virtual row lanes per thread (see bn_part_sums)
   __shared__ double sh[2][BN_RL][64];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int cl = threadIdx.x & 63, rt = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per;
   const long r1 = min((long)M, r0 + rows_per);
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C) {
-    const float mu = mean[c], is = invstd[c];
-    for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight, summed in row order
-      float dv[NB], xv[NB], ov[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const long r = rb + BN_RL * i;
-        const bool ok = r < r1;
-        dv[i] = ok ? dy[r * lddy + c] : 0.f;
-        xv[i] = ok ? x[r * ldx + c] : 0.f;
-        ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
-      }
+  for (int j = 0; j < VPT; ++j) {
+    const int rl = rt + RT * j;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C) {
+      const float mu = mean[c], is = invstd[c];
+      for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight, summed in row order
+        float dv[NB], xv[NB], ov[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
-        if (rb + BN_RL * i < r1) {
-          float d = dv[i];
-          if (relu_out && !(ov[i] > 0.f)) d = 0.f;
-          s1 += d;
-          s2 += (double)d * ((xv[i] - mu) * is);
+        for (int i = 0; i < NB; ++i) {
+          const long r = rb + BN_RL * i;
+          const bool ok = r < r1;
+          dv[i] = ok ? dy[r * lddy + c] : 0.f;
+          xv[i] = ok ? x[r * ldx + c] : 0.f;
+          ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
         }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          if (rb + BN_RL * i < r1) {
+            float d = dv[i];
+            if (relu_out && !(ov[i] > 0.f)) d = 0.f;
+            s1 += d;
+            s2 += (double)d * ((xv[i] - mu) * is);
+          }
+      }
     }
+    sh[0][rl][cl] = s1;
+    sh[1][rl][cl] = s2;
   }
-  sh[0][rl][cl] = s1;
-  sh[1][rl][cl] = s2;
   __syncthreads();
-  if (rl == 0 && c < C) {
+  if (rt == 0 && c < C) {
     double* p = part + (long)blockIdx.y * 2 * C + c;
     double t1 = sh[0][0][cl], t2 = sh[1][0][cl];
 #pragma unroll
@@ -489,17 +515,18 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_final(int P, int C, const double*
 }
 
 // dx rows [r0, r1) of channel c (row lane rl) from the channel's sums s1, s2 (train) -- or w*invstd*dyv (eval)
+template <int NL = BN_RL>   // row lanes of the block (rl in [0, NL))
 __device__ __forceinline__ void bn_bwd_apply_rows(int train, int M, const float* __restrict__ dy, long lddy,
                                                   const float* __restrict__ x, long ldx,
                                                   const float* __restrict__ relu_out, long ldo, float mu, float is,
                                                   float wc, double s1, double s2, float* __restrict__ dx, long lddx,
                                                   float beta_dx, long r0, long r1, int c, int rl) {
   const float invM = 1.f / (float)M;
-  for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight
+  for (long rb = r0 + rl; rb < r1; rb += NL * NB) {   // NB rows' loads in flight
     float dv[NB], xv[NB], ov[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const long r = rb + BN_RL * i;
+      const long r = rb + NL * i;
       const bool ok = r < r1;
       dv[i] = ok ? dy[r * lddy + c] : 0.f;
       xv[i] = ok && train ? x[r * ldx + c] : 0.f;
@@ -507,13 +534,13 @@ __device__ __forceinline__ void bn_bwd_apply_rows(int train, int M, const float*
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      if (rb + BN_RL * i < r1) {
+      if (rb + NL * i < r1) {
         float d = dv[i];
         if (relu_out && !(ov[i] > 0.f)) d = 0.f;
         float v;
         if (train) v = bn_bwd_elem(d, xv[i], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
         else v = (wc * is) * d;
-        bn_dx_store(dx + (rb + BN_RL * i) * lddx + c, beta_dx, v);
+        bn_dx_store(dx + (rb + NL * i) * lddx + c, beta_dx, v);
       }
   }
 }
@@ -550,7 +577,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_sums(int train, int M, int 
 // channel group's barrier (cnt[2 * blockIdx.x], zeroed, left zero), reduce the partials in
 // bn_part_sums' order and write dx for their own rows (re-read from L2).  Bit-identical to
 // bn_bwd_sums + bn_bwd_apply_sums.
-__global__ __launch_bounds__(BN_T) void bn_bwd_fused(int M, int C, const float* __restrict__ dy, long lddy,
+__global__ __launch_bounds__(BNF_T) void bn_bwd_fused(int M, int C, const float* __restrict__ dy, long lddy,
                                                     const float* __restrict__ x, long ldx,
                                                     const float* __restrict__ relu_out, long ldo,
                                                     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -559,10 +586,10 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_fused(int M, int C, const float* 
                                                     float* __restrict__ dx, long lddx, float beta_dx,
                                                     float* __restrict__ dw, float* __restrict__ db, float beta_w) {
   __shared__ double tot[2][64];
-  bn_bwd_partial(M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, rows_per, part);
+  bn_bwd_partial<BNF_T>(M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, rows_per, part);
   unsigned int* gc = cnt + 2 * blockIdx.x;
   block_group_sync(gc, gridDim.y);
-  bn_part_sums(gridDim.y, C, part, blockIdx.x, tot);
+  bn_part_sums<BNF_T>(gridDim.y, C, part, blockIdx.x, tot);
   block_group_leave(gc, gc + 1, gridDim.y);
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -573,7 +600,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_fused(int M, int C, const float* 
     if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
   }
   const long r0 = (long)blockIdx.y * rows_per;
-  bn_bwd_apply_rows(1, M, dy, lddy, x, ldx, relu_out, ldo, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
+  bn_bwd_apply_rows<BNF_T / 64>(1, M, dy, lddy, x, ldx, relu_out, ldo, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
                     min((long)M, r0 + rows_per), c, rl);
 }
 
@@ -606,10 +633,15 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
 constexpr int BN_APPLY_ROWS = 64;   // rows per block of the fused (partials-reducing) apply kernels
 
 // the single-launch (group barrier) kernels: two zeroed counters per 64-channel group, and a grid small
-// enough that all its blocks are resident together (256 CUs x >= 4 blocks of BN_T threads)
+// enough that its blocks are resident together even beside a second barrier grid (256 CUs x 4 blocks of
+// BNF_T threads at ~33 KB of LDS: up to 1024 resident; tools/residency_lab.hip, profiles/r04_residency_lab*.log).
+// Measured slower than the two launches, so off in the product (knob VITCNN_BN_FUSED=1, probe library):
+// ViT-CNN step 1.815-1.825 -> 1.946-1.950 ms, FusAtNet 19.5 -> 20.7 ms (profiles/r04_ab_bn_fused.log) --
+// the barrier (one agent-scope release + acquire per block, i.e. an L2 writeback and invalidate, and 64
+// arrivals polled on one counter) costs ~10-20 us per launch, more than the launch and the re-read it saves.
 static bool bn_fused_fits(int C, int P, const unsigned int* counters, int n_counters) {
   const long groups = vc_cdiv(C, 64);
-  return counters && n_counters >= 2 * groups && groups * P <= 1024 && vc_knob("VITCNN_BN_FUSED", 0);
+  return counters && n_counters >= 2 * groups && groups * P <= 512 && vc_knob("VITCNN_BN_FUSED", 0);
 }
 
 int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
@@ -925,7 +957,7 @@ VC_EXPORT int vc_bn_forward_ex(int train, long M, int C, const float* x, long ld
   const int P = vc_cdiv(M, rows_per);
   VC_REQUIRE((long)P * C * 2 <= ws_doubles && P <= 65535);
   if (bn_fused_fits(C, P, counters, n_counters)) {   // one launch: group barrier
-    hipLaunchKernelGGL(bn_forward_fused, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, ldx, rows_per,
+    hipLaunchKernelGGL(bn_forward_fused, dim3(vc_cdiv(C, 64), P), dim3(BNF_T), 0, stream, (int)M, C, x, ldx, rows_per,
                        wsd, counters, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy);
     VC_CHECK_LAUNCH();
     return VC_OK;
@@ -968,7 +1000,7 @@ VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy,
   VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_doubles && P <= 65535);
   double* sums = wsd + (long)P * C * 2;
   if (train && dx && bn_fused_fits(C, P, counters, n_counters)) {   // one launch: group barrier
-    hipLaunchKernelGGL(bn_bwd_fused, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
+    hipLaunchKernelGGL(bn_bwd_fused, dim3(vc_cdiv(C, 64), P), dim3(BNF_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
                        relu_out, ldo, mean, invstd, w, rows_per, wsd, counters, dx, lddx, beta_dx, dw, db, beta_w);
     VC_CHECK_LAUNCH();
     return VC_OK;

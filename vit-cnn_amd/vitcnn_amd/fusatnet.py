@@ -341,18 +341,20 @@ class _Program:
         if self.train:
             bn.num_batches_tracked.add_(1)
         z = self.new(*y.shape) if self.grad else y
-        self.L.vc_bn_forward(1 if self.train else 0, M, C, y.data_ptr(), C, bn.eps,
-                             bn.momentum if bn.momentum is not None else BN_MOMENTUM, mean.data_ptr(),
-                             invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
-                             bn.weight.data_ptr(), bn.bias.data_ptr(), relu, z.data_ptr(), C, self.scr.data_ptr(),
-                             self.SCRATCH, self.s)
+        # train: one launch where the grid allows (group barrier over the stream's zeroed counters)
+        self.L.vc_bn_forward_ex(1 if self.train else 0, M, C, y.data_ptr(), C, bn.eps,
+                                bn.momentum if bn.momentum is not None else BN_MOMENTUM, mean.data_ptr(),
+                                invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                                bn.weight.data_ptr(), bn.bias.data_ptr(), relu, z.data_ptr(), C, self.scr.data_ptr(),
+                                self.SCRATCH, self.cnt, N_COUNTERS, self.s)
 
         def bwd():
             gy, beta = self.acc(y)
-            self.L.vc_bn_bwd(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
-                             z.data_ptr() if relu else None, C, mean.data_ptr(), invstd.data_ptr(),
-                             bn.weight.data_ptr(), gy.data_ptr(), C, beta, self.pgrad(bn.weight),
-                             self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.s)
+            self.L.vc_bn_bwd_ex(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
+                                z.data_ptr() if relu else None, C, mean.data_ptr(), invstd.data_ptr(),
+                                bn.weight.data_ptr(), gy.data_ptr(), C, beta, self.pgrad(bn.weight),
+                                self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.cnt, N_COUNTERS,
+                                self.s)
 
         self.record(bwd, y, z)
         return z
