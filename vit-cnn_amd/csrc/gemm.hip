@@ -1331,11 +1331,10 @@ static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws, bo
   PipePlan p;
   p.bm = 64;
   p.bn = 64;
-  p.ns = 2;
-  if (!bf) {   // bf16 operands: the 64 x 64, 2-stage kernel only
+  p.ns = vc_knob("VITCNN_PIPE_NS", 2) == 4 ? 4 : 2;   // ring depth (knob: probe library)
+  if (!bf) {   // bf16 operands: 64 x 64 tiles only
     if (g_tune.bm) p.bm = g_tune.bm;
     if (g_tune.bn) p.bn = g_tune.bn;
-    p.ns = vc_knob("VITCNN_PIPE_NS", 2) == 4 ? 4 : 2;   // ring depth (knob: probe library)
   }
   p.tn = vc_cdiv(Ne, p.bn);
   p.tm = vc_cdiv(M, p.bm);
@@ -1393,15 +1392,21 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
     else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_);   \
     else VC_GP(64, 64, 2, 2, NS_);                                  \
   } while (0)
-#define VC_GPB(TA_, TB_) \
-  hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, TA_, TB_, 2, true>), grid, dim3(256), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
+#define VC_GPB(TA_, TB_, NS_) \
+  hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, TA_, TB_, NS_, true>), grid, dim3(256), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
+#define VC_GPB_T(NS_)                              \
+  do {                                             \
+    if (transA && transB) VC_GPB(true, true, NS_); \
+    else if (transA) VC_GPB(true, false, NS_);     \
+    else if (transB) VC_GPB(false, true, NS_);     \
+    else VC_GPB(false, false, NS_);                \
+  } while (0)
   if (bf) {
-    if (transA && transB) VC_GPB(true, true);
-    else if (transA) VC_GPB(true, false);
-    else if (transB) VC_GPB(false, true);
-    else VC_GPB(false, false);
+    if (p.ns == 4) VC_GPB_T(4);
+    else VC_GPB_T(2);
   } else if (p.ns == 4) VC_GP_T(4);
   else VC_GP_T(2);
+#undef VC_GPB_T
 #undef VC_GPB
 #undef VC_GP_T
 #undef VC_GP
