@@ -1,5 +1,5 @@
 """GPU tool: one vc_gemm_ex shape, repeated, for kernel-level profiling (rocprofv3 --pmc / --stats).
-usage: python tools/gemm_one.py TA TB M N K [flags] [reps] [bias_grad]
+usage: [VITCNN_TUNE=bm,bn,nsplit] python tools/gemm_one.py TA TB M N K [flags] [reps] [bias_grad]
 Prints the average time per call (HIP events) and TFLOP/s."""
 import os
 import sys
@@ -30,6 +30,12 @@ def main():
     args = (ta, tb, M, N, K, 1.0, A.data_ptr(), M if ta else K, 0, B.data_ptr(), K if tb else N, 0, 0.0,
             C.data_ptr(), N, 0, 1, None, None, 0, 0, flags, bg.data_ptr() if bgrad else None, ws.data_ptr(),
             ws.numel(), cnt.data_ptr(), cnt.numel(), st)
+    tune = os.environ.get("VITCNN_TUNE")   # "bm,bn,nsplit": forced tile / split (probe library)
+    if tune:
+        from vitcnn_amd._lib import probe_lib
+        L = probe_lib()
+        bm, bn, ns = (int(v) for v in tune.split(","))
+        L.vc_gemm_tune(bm, bn, ns, 0, -1)
     for _ in range(5):
         L.vc_gemm_ex(*args)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

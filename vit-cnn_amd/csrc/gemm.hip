@@ -1332,10 +1332,9 @@ static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws, bo
   p.bm = 64;
   p.bn = 64;
   p.ns = vc_knob("VITCNN_PIPE_NS", 2) == 4 ? 4 : 2;   // ring depth (knob: probe library)
-  if (!bf) {   // bf16 operands: 64 x 64 tiles only
-    if (g_tune.bm) p.bm = g_tune.bm;
-    if (g_tune.bn) p.bn = g_tune.bn;
-  }
+  if (g_tune.bm) p.bm = g_tune.bm;
+  if (g_tune.bn) p.bn = g_tune.bn;
+  if (bf && p.bm == 128 && p.bn == 128) p.bn = 64;   // (no 128 x 128 build)
   p.tn = vc_cdiv(Ne, p.bn);
   p.tm = vc_cdiv(M, p.bm);
   const long tiles = (long)p.tn * p.tm;
@@ -1392,21 +1391,23 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
     else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_);   \
     else VC_GP(64, 64, 2, 2, NS_);                                  \
   } while (0)
-#define VC_GPB(TA_, TB_, NS_) \
-  hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, TA_, TB_, NS_, true>), grid, dim3(256), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
-#define VC_GPB_T(NS_)                              \
-  do {                                             \
-    if (transA && transB) VC_GPB(true, true, NS_); \
-    else if (transA) VC_GPB(true, false, NS_);     \
-    else if (transB) VC_GPB(false, true, NS_);     \
-    else VC_GPB(false, false, NS_);                \
+#define VC_GPB(BM_, BN_, WM_, WN_, TA_, TB_, NS_) \
+  hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, TA_, TB_, NS_, true>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
+#define VC_GPB_L(BM_, BN_, WM_, WN_, NS_)                          \
+  do {                                                             \
+    if (transA && transB) VC_GPB(BM_, BN_, WM_, WN_, true, true, NS_); \
+    else if (transA) VC_GPB(BM_, BN_, WM_, WN_, true, false, NS_);     \
+    else if (transB) VC_GPB(BM_, BN_, WM_, WN_, false, true, NS_);     \
+    else VC_GPB(BM_, BN_, WM_, WN_, false, false, NS_);                \
   } while (0)
-  if (bf) {
-    if (p.ns == 4) VC_GPB_T(4);
-    else VC_GPB_T(2);
+  if (bf) {   // tiles other than 64 x 64 / 2 stages: measurement knobs (probe library)
+    if (p.bm == 128 && p.bn == 64) VC_GPB_L(128, 64, 4, 2, 2);
+    else if (p.bm == 64 && p.bn == 128) VC_GPB_L(64, 128, 2, 4, 2);
+    else if (p.ns == 4) VC_GPB_L(64, 64, 2, 2, 4);
+    else VC_GPB_L(64, 64, 2, 2, 2);
   } else if (p.ns == 4) VC_GP_T(4);
   else VC_GP_T(2);
-#undef VC_GPB_T
+#undef VC_GPB_L
 #undef VC_GPB
 #undef VC_GP_T
 #undef VC_GP
