@@ -34,6 +34,7 @@ _FLAG = lambda v: v not in ("0", "", "false", "False")  # noqa: E731
 SWITCHES = {
     "VITCNN_IMPLICIT_CONV": ("model", "_IMPLICIT_CONV", _FLAG),
     "VITCNN_DEFER_WGRAD": ("model", "_DEFER_WGRAD", _FLAG),
+    "VITCNN_DEFER_WGRAD1": ("model", "_DEFER_WGRAD1", _FLAG),
     "VITCNN_SCAN_FUSED": ("model", "_SCAN_FUSED", _FLAG),
     "VITCNN_ROW_CHAIN": ("model", "_ROW_CHAIN", _FLAG),
     "VITCNN_GLF_FUSED": ("model", "_GLF_FUSED", _FLAG),

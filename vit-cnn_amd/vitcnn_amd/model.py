@@ -40,6 +40,7 @@ BN_MOM = 0.1
 NDIR = 10
 N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
 WGRAD_LANE = 2             # backward: lane 0's deferred weight gradients (lane 2 is idle after the forward)
+WGRAD1_LANE = 3            # backward: lane 1's deferred weight gradients (lane 3: after the fusion1 / LiDAR chain)
 # Program switches.  Module constants -- the product reads no environment: each selects between two
 # forms the tests hold to the same parity (or bit-identity), and the measurement tools set them from
 # VITCNN_<NAME> variables through tools/knobs.py (tools/ab_env.sh A/B runs).  The defaults are the
@@ -54,6 +55,11 @@ _IMPLICIT_CONV = False
 # (one fork each); forking each one separately measured slower (2.39 -> 2.63 ms: every cross-lane
 # graph edge costs more than one GEMM's overlap gains); False: every weight gradient in place
 _DEFER_WGRAD = True
+# lane 1's weight gradients (GLfusion, local conv, channel feature) queued and issued on WGRAD1_LANE at the end
+# of the block's lane-1 chain, so lane 1 -- the critical path since round 3 -- runs the data gradients only.
+# Measured slower: 1.80-1.81 -> 1.99-2.02 ms (profiles/r04_ab_defer_wgrad1.log): the block's grouped weight
+# gradients then run beside lane 0's scan backward and stretch it more than lane 1 gains
+_DEFER_WGRAD1 = False
 SIDE_SCRATCH = 1 << 23     # floats of scratch per side stream
 PARAM_ALIGN = 4            # floats: flat-buffer alignment (16 B) of every parameter of >= ALIGN_MIN elements
 ALIGN_MIN = 64
@@ -534,6 +540,8 @@ class _Program:
         self.lanes_on = _LANES
         self.wgrad_tail = None
         self.pending_wgrads = []
+        self.wgrad_tail1 = None
+        self.pending_wgrads1 = []
         self._grouping = None      # the open GEMM group's state (host address) while gemm_group() collects
         self._group_lane = 0
         _, self.P, self.BUF, self.I64 = model._ptrs()
@@ -965,13 +973,13 @@ class _Program:
                 self.mm_nn(M, K, N, dY, lddy, self.P[wname], K, dX, K, beta=beta_dx, relu_mask=relu_mask)
 
     def _deferring(self, defer):
-        return defer and _DEFER_WGRAD and self.lanes_on and self.cur == 0
+        return defer and _DEFER_WGRAD and self.lanes_on and (self.cur == 0 or (self.cur == 1 and _DEFER_WGRAD1))
 
     def defer_wgrad(self, defer, M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=0):
         """C[M,N] = A^T B (a weight gradient, mm_tn), now or -- defer on lane 0 with lanes on -- at the next
         flush_wgrads()"""
         if self._deferring(defer):
-            self.pending_wgrads.append(
+            (self.pending_wgrads if self.cur == 0 else self.pending_wgrads1).append(
                 lambda: self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad))
         else:
             self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad)
@@ -990,9 +998,22 @@ class _Program:
             self.wgrad_tail = self.mark()
         self.pending_wgrads = []
 
+    def flush_wgrads1(self):
+        """lane 1's queued weight gradients (the GLfusion / local / channel chains' 1x1 and 3x3 convs) on
+        WGRAD1_LANE, forked from lane 1 at the end of its block chain: lane 1 keeps only the data gradients"""
+        if not self.pending_wgrads1:
+            return
+        e = self.mark()
+        with self.lane(WGRAD1_LANE, e):
+            with self.gemm_group():
+                for fn in self.pending_wgrads1:
+                    fn()
+            self.wgrad_tail1 = self.mark()
+        self.pending_wgrads1 = []
+
     def wgrad_events(self):
-        """the weight-gradient lane's latest event, as a list (empty if nothing was deferred)"""
-        return [self.wgrad_tail] if self.wgrad_tail is not None else []
+        """the weight-gradient lanes' latest events, as a list (empty if nothing was deferred)"""
+        return [e for e in (self.wgrad_tail, self.wgrad_tail1) if e is not None]
 
     def conv1x1_bn_relu_bwd(self, seq, X, M, Cin, Cout, dOut, dX, beta_dx, defer=False):
         ws = self.ws
@@ -1012,7 +1033,7 @@ class _Program:
     def _tap_dgrad(self, blk):
         return _TAP_DGRAD and self.ws_grad and not self.implicit_conv and blk.cin % 4 == 0
 
-    def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx, tap=False, masked=False):
+    def conv_bn_relu3_bwd(self, pfx, X, H, Cin, Cout, dOut, dX, beta_dx, tap=False, masked=False, defer=False):
         """tap: the data gradient by vc_conv3x3_tap_dgrad over the tap-major weight block() packed;
         masked: dOut has been through the ReLU backward already (its producer's GEMM epilogue)"""
         B, ws = self.B, self.ws
@@ -1042,7 +1063,7 @@ class _Program:
             col = ws.f(pfx + ".col", B * S * 9 * Cin)
             dcol = ws.f(pfx + ".dcol", B * S * 9 * Cin)
             self.linear_bwd(pfx + ".conv.weight", pfx + ".conv.bias", dpre, B * S, Cout, 9 * Cin, col, 9 * Cin, dcol,
-                            0.0)
+                            0.0, defer=defer)
             self.L.vc_col2im3x3(B, H, H, Cin, dcol, dxbn, self.s)
         self.bn_bwd(pfx + ".bn", pfx + ".bn", dxbn, Cin, X, Cin, 0, B * H * H, Cin, dX, Cin, beta_dx)
 
@@ -1092,7 +1113,8 @@ class _Program:
         with self.lane(1, e0):
             # GLfusionBlock FusionLayer + non-local branch (lane 1) -> dFc, dFl
             CAT1, dCAT1 = f(pfx + ".CAT1", M * 2 * Cout), f(pfx + ".dCAT1", M * 2 * Cout)
-            self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout, dFM, dCAT1, 0.0)
+            self.conv1x1_bn_relu_bwd(pfx + ".FusionLayer.FusionLayer", CAT1, M, 2 * Cout, Cout, dFM, dCAT1, 0.0,
+                                     defer=True)
             dFc, dFl = f(pfx + ".dFc", M * Cout), f(pfx + ".dFl", M * Cout)
             if _GLF_FUSED:
                 self.L.vc_add2_2d_dup(M, Cout, dCAT1, 2 * Cout, dCAT1 + F32 * Cout, 2 * Cout, dFc, Cout, dFl, Cout,
@@ -1104,7 +1126,7 @@ class _Program:
             WP, dWP = f(pfx + ".WP", M * Cout), f(pfx + ".dWP", M * Cout)
             self.bn_bwd(nl + ".W.1", pfx + ".W1", dCAT1, 2 * Cout, WP, Cout, 0, M, Cout, dWP, Cout, 0.0)
             O, dO = f(pfx + ".O", M * Ci), f(pfx + ".dO", M * Ci)
-            self.linear_bwd(nl + ".W.0.weight", nl + ".W.0.bias", dWP, M, Cout, Ci, O, Ci, dO, 0.0)
+            self.linear_bwd(nl + ".W.0.weight", nl + ".W.0.bias", dWP, M, Cout, Ci, O, Ci, dO, 0.0, defer=True)
             TH, PP, ATT = f(pfx + ".TH", M * Ci), f(pfx + ".PP", B * Pk * 2 * Ci), f(pfx + ".ATT", M * Pk)
             dTH, dPP = f(pfx + ".dTH", M * Ci), f(pfx + ".dPP", B * Pk * 2 * Ci)
             dPG = f(pfx + ".dPG", M * 2 * Ci)
@@ -1116,15 +1138,16 @@ class _Program:
                 self.L.vc_maxpool2_bwd(B, Hs, Hs, 2 * Ci, dPP, PA, dPG, 2 * Ci, self.s)
             # phi | g (stacked, one weight + one data gradient) and theta: one grouped launch
             with self.gemm_group():
-                self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, 2 * Ci, Cout, Fc, Cout, dFc, 1.0)
+                self.linear_bwd(nl + ".phi.0.weight", nl + ".phi.0.bias", dPG, M, 2 * Ci, Cout, Fc, Cout, dFc, 1.0,
+                                defer=True)
                 # dFl's last contribution; its epilogue applies the local conv's ReLU backward (mask Fl)
                 self.linear_bwd(nl + ".theta.weight", nl + ".theta.bias", dTH, M, Ci, Cout, Fl, Cout, dFl, 1.0,
-                                relu_mask=Fl)
+                                relu_mask=Fl, defer=True)
             side = self.lanes_on and _CH_LANE != 1
             e_pg = self.mark() if side else None
             # local feature: BN -> conv3x3 -> ReLU backward (first accumulation into dX)
             self.conv_bn_relu3_bwd(pfx + ".local_feature", X, H, Cin, Cout, dFl, dX or 0, 1.0, tap=self._tap_dgrad(blk),
-                                   masked=True)
+                                   masked=True, defer=True)
             e_loc = self.mark() if side else None
         # channel feature: ln4 -> TokenLearner -> conv1x1, after the local chain on lane 1 (or, measurement
         # switch _CH_LANE, on a lane of its own beside it: see _CH_ORDERED)
@@ -1137,11 +1160,12 @@ class _Program:
                 self.wait(e_loc)   # the dX accumulations in program order: local, then channel
             with self.gemm_group():
                 self.linear_bwd(pfx + ".channel_feature.weight", pfx + ".channel_feature.bias", dCF, rows, Cout,
-                                Cin, X, Cin, 0, 0.0)
+                                Cin, X, Cin, 0, 0.0, defer=True)
                 if dX:
                     self.mm_nn(rows, Cin, Cout, dCF, Cout, self.P[pfx + ".channel_feature.weight"], Cin, dX, Cin,
                                beta=1.0)
             e_ch = (self.mark(), e_loc) if side else (self.mark(),)
+            self.flush_wgrads1()   # lane 1's weight gradients, beside lane 0's chain
         # global feature: ln3 -> TokenLearner -> change_dim
         Zg, dZg = f(pfx + ".global_feature.Z", M * Cout), f(pfx + ".dZg", M * Cout)
         self.ln_bwd(pfx + ".ln3", pfx + ".Fg", dFg, Zg, M, Cout, dZg, 0.0, defer=True)
@@ -1328,7 +1352,7 @@ class _Program:
                            dF2, self.G["classifier.weight"], self.G["classifier.bias"], self.s)
         dH1, dH2 = ws.f("dH1", B * S1 * C1o), ws.f("dH2", B * S2 * C2o)
         dL1, dL2 = ws.f("dL1", B * S1 * 16), ws.f("dL2", B * S2 * 32)
-        self.wgrad_tail = None
+        self.wgrad_tail = self.wgrad_tail1 = None
         self.fusion_bwd("fusion2", self.H2, C2o, self.L2, 32, B * S2, 128, dF2, dH2, 0.0, dL2, 0.0, defer=True)
         e_f2 = self.mark()
         with self.lane(3, e_f2):  # fusion1 + LiDAR branch on lane 3
