@@ -1633,7 +1633,10 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
     if (group) {
       const int Ne = N + (bias_grad ? 1 : 0);
       const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr, bf);
-      if (p.bm == 64 && p.bn == 64 && p.ns == 2) {   // the grouped kernel's configuration
+      // a problem whose own grid fills the chip launches alone (knob GEMM_GROUP_MAXB: the largest grid
+      // that joins a group; probe library)
+      const long own = (long)p.tn * p.tm * p.nsplit;
+      if (p.bm == 64 && p.bn == 64 && p.ns == 2 && own <= vc_knob("VITCNN_GEMM_GROUP_MAXB", 1L << 30)) {
         const long need = p.nsplit > 1 ? ((long)p.nsplit * M * Ne + 63) / 64 * 64 : 0;
         GroupState& st = *group;
         if (st.np == GROUP_MAX || st.ws_used + need > ws_floats) {
