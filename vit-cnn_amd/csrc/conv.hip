@@ -86,12 +86,15 @@ __global__ void col2im3x3(int total, FastDiv fC, FastDiv fW, FastDiv fH, const f
 // [S][9*CC] (S = OH*OW) go through LDS, where the stride-9 channel reads are bank-conflict free (9 odd).
 // Same arithmetic and summation order as the per-thread kernels (bit-identical).
 constexpr int C2I_T = 512, C2I_W = C2I_T / 64, C2I_CC = 32, C2I_JK = (9 * C2I_CC + 63) / 64;
+// LDS pitch of a staged pixel: 33 floats, so a wave's col-row reads (channel j / 9, tap j % 9: taps 32
+// floats apart at pitch 32, i.e. 2 banks for 9 taps) spread over the banks
+constexpr int C2I_CP = C2I_CC + 1;
 
 __global__ __launch_bounds__(C2I_T) void im2col3x3_lds(int nchunk, int H, int W, int C,
                                                       const float* __restrict__ x, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd, const float* __restrict__ w,
                                                       const float* __restrict__ b, float* __restrict__ col) {
-  extern __shared__ float img[];   // [H*W][C2I_CC]
+  extern __shared__ float img[];   // [H*W][C2I_CP]
   const int bb = blockIdx.x / nchunk, c0 = (blockIdx.x - bb * nchunk) * C2I_CC, nc = min(C2I_CC, C - c0);
   const int OW = W - 2, S = (H - 2) * OW, HW = H * W;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(C2I_T) void im2col3x3_lds(int nchunk, int H, int W,
 #pragma unroll
       for (int k = 0; k < NBP; ++k) {
         const int p = p0 + k * PP;
-        if (p < HW) img[p * C2I_CC + c] = v[k] * sc + sh;
+        if (p < HW) img[p * C2I_CP + c] = v[k] * sc + sh;
       }
     }
   }
@@ -126,11 +129,11 @@ __global__ __launch_bounds__(C2I_T) void im2col3x3_lds(int nchunk, int H, int W,
 #pragma unroll
   for (int k = 0; k < C2I_JK; ++k) {
     const int j = lane + 64 * k, c = j / 9, t = j - 9 * c, kh = t / 3, kw = t - 3 * kh;
-    off[k] = j < seg ? (kh * W + kw) * C2I_CC + c : -1;
+    off[k] = j < seg ? (kh * W + kw) * C2I_CP + c : -1;
   }
   float* cb = col + (long)bb * S * 9 * C + 9 * c0;
   for (int m = wave; m < S; m += C2I_W) {
-    const int oh = m / OW, ow = m - oh * OW, base = (oh * W + ow) * C2I_CC;
+    const int oh = m / OW, ow = m - oh * OW, base = (oh * W + ow) * C2I_CP;
     float* row = cb + (long)m * 9 * C;
 #pragma unroll
     for (int k = 0; k < C2I_JK; ++k)
@@ -262,7 +265,7 @@ VC_API int vc_im2col3x3(int B, int H, int W, int C, const float* x, const float*
   if (const int cc = c2i_chunk(H, W, C)) {
     const int nchunk = vc_cdiv(C, cc);
     VC_REQUIRE_I32((long)B * nchunk);
-    hipLaunchKernelGGL(im2col3x3_lds, dim3(B * nchunk), dim3(C2I_T), sizeof(float) * H * W * cc, stream, nchunk, H, W,
+    hipLaunchKernelGGL(im2col3x3_lds, dim3(B * nchunk), dim3(C2I_T), sizeof(float) * H * W * (cc + 1), stream, nchunk, H, W,
                        C, x, bn_mean, bn_invstd, bn_w, bn_b, col);
     VC_CHECK_LAUNCH();
     return VC_OK;

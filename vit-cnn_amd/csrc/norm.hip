@@ -704,6 +704,7 @@ __global__ __launch_bounds__(BN_T) void glf_combine_stats(int M, int C, const fl
 // invstd are bit-identical to vc_bn_stats'), the sample-0 blocks write save_* and the running stats,
 // and the chunk is staged BN-applied in LDS and written as col rows.
 constexpr int IBS_CC = 32, IBS_T = 64 * BN_RL / 2, IBS_W = IBS_T / 64, IBS_JK = (9 * IBS_CC + 63) / 64;
+constexpr int IBS_CP = IBS_CC + 1;   // LDS pitch of a staged pixel (conv.hip C2I_CP: bank spread of the tap reads)
 static_assert(IBS_T == IBS_CC * BN_RL, "one thread per (channel, partial lane)");
 
 __global__ __launch_bounds__(IBS_T) void im2col3x3_bnstats(int nchunk, int H, int W, int C, long M, int P,
@@ -713,7 +714,7 @@ __global__ __launch_bounds__(IBS_T) void im2col3x3_bnstats(int nchunk, int H, in
                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
                                                           const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ b, float* __restrict__ col) {
-  extern __shared__ float img[];   // [H*W][IBS_CC]
+  extern __shared__ float img[];   // [H*W][IBS_CP]
   __shared__ double shr[2][BN_RL][IBS_CC];
   __shared__ float scs[IBS_CC], shs[IBS_CC];
   const int bb = blockIdx.x / nchunk, c0 = (blockIdx.x - bb * nchunk) * IBS_CC, nc = min(IBS_CC, C - c0);
@@ -773,7 +774,7 @@ __global__ __launch_bounds__(IBS_T) void im2col3x3_bnstats(int nchunk, int H, in
 #pragma unroll
       for (int k = 0; k < NBP; ++k) {
         const int p = p0 + k * PP;
-        if (p < HW) img[p * IBS_CC + c] = v[k] * sc + sh;
+        if (p < HW) img[p * IBS_CP + c] = v[k] * sc + sh;
       }
     }
   }
@@ -783,11 +784,11 @@ __global__ __launch_bounds__(IBS_T) void im2col3x3_bnstats(int nchunk, int H, in
 #pragma unroll
   for (int k = 0; k < IBS_JK; ++k) {
     const int j = lane + 64 * k, cc = j / 9, t = j - 9 * cc, kh = t / 3, kw = t - 3 * kh;
-    off[k] = j < seg ? (kh * W + kw) * IBS_CC + cc : -1;
+    off[k] = j < seg ? (kh * W + kw) * IBS_CP + cc : -1;
   }
   float* cb = col + (long)bb * S * 9 * C + 9 * c0;
   for (int m = wave; m < S; m += IBS_W) {
-    const int oh = m / OW, ow = m - oh * OW, base = (oh * W + ow) * IBS_CC;
+    const int oh = m / OW, ow = m - oh * OW, base = (oh * W + ow) * IBS_CP;
     float* row = cb + (long)m * 9 * C;
 #pragma unroll
     for (int k = 0; k < IBS_JK; ++k)
@@ -1069,7 +1070,7 @@ VC_EXPORT int vc_bn_im2col3x3(int B, int H, int W, int C, const float* x, float 
   VC_CHECK_LAUNCH();
   const int nchunk = vc_cdiv(C, IBS_CC);
   VC_REQUIRE_I32((long)B * nchunk);
-  hipLaunchKernelGGL(im2col3x3_bnstats, dim3(B * nchunk), dim3(IBS_T), sizeof(float) * H * W * IBS_CC, stream, nchunk,
+  hipLaunchKernelGGL(im2col3x3_bnstats, dim3(B * nchunk), dim3(IBS_T), sizeof(float) * H * W * IBS_CP, stream, nchunk,
                      H, W, C, M, P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, x, bn_w, bn_b, col);
   VC_CHECK_LAUNCH();
   return VC_OK;
