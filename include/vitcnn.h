@@ -210,9 +210,11 @@ VC_API int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, cons
                                 const float* wt, float beta, float* dx, long lddx, float* ws, long ws_floats,
                                 hipStream_t stream);
 /* wgrad written straight into the torch layout dw [O][C][3][3] (overwritten): vc_conv3x3_tap_wgrad +
- * vc_conv3x3_pack mode 2 with beta 0 in one call, bit-identical (the same sums, stored transposed). */
+ * vc_conv3x3_pack mode 2 with beta 0 in one call, bit-identical (the same sums, stored transposed); db
+ * (nullable, overwritten) also receives the bias gradient sum over output pixels of dy (the blocks of the
+ * first output tile column sum their staged dy tiles: no separate column-sum launches). */
 VC_API int vc_conv3x3_tap_wgrad_oihw(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
-                                     const float* dy, long lddy, float* dw, float* ws, long ws_floats,
+                                     const float* dy, long lddy, float* dw, float* db, float* ws, long ws_floats,
                                      hipStream_t stream);
 /* train-mode BatchNorm(x) (statistics as vc_bn_stats_ex: save_* and running stats written) followed by
  * vc_im2col3x3 of the normalised x, the statistics' final reduction done inside the im2col launch

@@ -107,10 +107,19 @@ def test_conv_tap_fwd_wgrad_dgrad(B, H, C, O, pad, ldx, ws_log2):
     assert torch.isnan(dx[:, C:]).all()          # the row padding is never written
     # the weight gradient stored straight into the torch layout: bit-identical to wgrad + pack mode 2
     dw2 = torch.full((O, C, 3, 3), 7.0, device=DEV)
-    L.vc_conv3x3_tap_wgrad_oihw(B, H, H, C, O, pad, xd.data_ptr(), ldx, dyd.data_ptr(), O, dw2.data_ptr(), wsp,
-                                wsn, s)
+    L.vc_conv3x3_tap_wgrad_oihw(B, H, H, C, O, pad, xd.data_ptr(), ldx, dyd.data_ptr(), O, dw2.data_ptr(), None,
+                                wsp, wsn, s)
     torch.cuda.synchronize()
     assert torch.equal(dw2, dw)
+    # ... and with the fused bias gradient: the weight gradient unchanged, db = column sums of dy
+    dw3 = torch.full((O, C, 3, 3), 7.0, device=DEV)
+    db = torch.full((O,), 9.0, device=DEV)
+    L.vc_conv3x3_tap_wgrad_oihw(B, H, H, C, O, pad, xd.data_ptr(), ldx, dyd.data_ptr(), O, dw3.data_ptr(),
+                                db.data_ptr(), wsp, wsn, s)
+    torch.cuda.synchronize()
+    assert torch.equal(dw3, dw)
+    db_ref = dy64.sum(dim=(0, 2, 3))
+    assert _rel(db, db_ref) < 2e-6 * (B * OH * OH) ** 0.5, _rel(db, db_ref)
 
 
 @pytest.mark.gpu

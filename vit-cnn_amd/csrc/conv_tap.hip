@@ -54,6 +54,8 @@ struct TapArgs {
   float beta;                    // dgrad: dx = beta dx + ...
   float* part;                   // split-K slabs [nsplit][M][N]
   int oihw;                      // wgrad: out is the torch layout [O][C][3][3] (else dWt [O][9C])
+  float* dbias;                  // wgrad (nullable): the bias gradient sum_p dy[p][o], from the n-tile-0
+                                 // blocks' staged dy tiles (split: column 9C of the slabs, a.N = 9C + 1)
   int vx, vdy, vw;               // float4 loads allowed (16-B aligned base, ld % 4 == 0)
   FastDiv fOW, fOHW, fW, fHW;
 };
@@ -193,6 +195,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     }
   };
 
+  // wgrad bias gradient: the blocks of n-tile 0 also sum their staged dy^T tile over k (thread: output
+  // row tid & 127, k half tid >> 7; fixed order: k within the half, k-tiles in order, then the halves)
+  const bool do_b = MODE == WGRAD && a.dbias && blockIdx.x == 0;
+  float bacc = 0.f;
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -207,6 +213,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
       store();
       __syncthreads();
       if (kt + 1 < kt1) load(kt + 1);
+      if (do_b) {
+        const int mm = tid & 127, hh = tid >> 7;
+#pragma unroll
+        for (int k = 0; k < TK / 2; ++k) bacc += As[(hh * (TK / 2) + k) * PA + mm];
+      }
 #pragma unroll
       for (int ks = 0; ks < TK / 2; ++ks) {
         const int k = 2 * ks + h;
@@ -225,6 +236,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 
   // C/D of 32x32: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   const bool split = gridDim.z > 1;
+  if (do_b) {   // (block-uniform) the two k halves combined through the idle B image
+    const int mm = tid & 127, hh = tid >> 7;
+    if (hh == 1) Bs[mm] = bacc;
+    __syncthreads();
+    const int row = m0 + mm;
+    if (hh == 0 && row < a.M) {
+      const float v = bacc + Bs[mm];
+      if (split) a.part[((long)blockIdx.z * a.M + row) * a.N + 9 * a.C] = v;
+      else a.dbias[row] = v;
+    }
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -261,16 +283,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     }
 }
 
-// split-K combine in fixed slice order, then the mode's epilogue
+// one combined element: the mode's epilogue
 template <int MODE>
-__global__ __launch_bounds__(256) void conv_tap_reduce(TapArgs a, int nsplit) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long)a.M * a.N) return;
+__device__ __forceinline__ void tap_reduce_store(const TapArgs& a, long e, float s) {
   const int row = (int)(e / a.N), col = (int)(e - (long)row * a.N);
-  const long slab = (long)a.M * a.N;
-  float s = 0.f;
-#pragma unroll 8
-  for (int z = 0; z < nsplit; ++z) s += a.part[z * slab + e];   // 8 slab loads in flight, summed in z order
+  if (MODE == WGRAD && col == 9 * a.C) {   // the bias-gradient column (a.N = 9C + 1)
+    a.dbias[row] = s;
+    return;
+  }
   if (MODE == WGRAD && a.oihw) {   // torch layout [O][C][3][3]: col = tap * C + c
     const int tap = col / a.C, c = col - tap * a.C;
     a.out[((long)row * a.C + c) * 9 + tap] = s;
@@ -280,6 +300,37 @@ __global__ __launch_bounds__(256) void conv_tap_reduce(TapArgs a, int nsplit) {
   if (MODE == FWD) *o = s + (a.bias ? a.bias[col] : 0.f);
   else if (MODE == DGRAD) *o = (a.beta != 0.f ? a.beta * *o : 0.f) + s;
   else *o = s;
+}
+
+// split-K combine in fixed slice order, then the mode's epilogue.  vec: a thread sums 4 consecutive
+// elements of the flattened [M][N] slabs as float4s (slab size and workspace 16-B aligned), else one
+template <int MODE>
+__global__ __launch_bounds__(256) void conv_tap_reduce(TapArgs a, int nsplit, int vec) {
+  const long slab = (long)a.M * a.N;
+  if (vec) {
+    const long e0 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (e0 >= slab) return;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+    for (int z = 0; z < nsplit; ++z) {   // 8 slab loads in flight, each element summed in z order
+      const float4 v = *reinterpret_cast<const float4*>(a.part + z * slab + e0);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (e0 + i < slab) tap_reduce_store<MODE>(a, e0 + i, sv[i]);
+    return;
+  }
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= slab) return;
+  float s = 0.f;
+#pragma unroll 8
+  for (int z = 0; z < nsplit; ++z) s += a.part[z * slab + e];   // 8 slab loads in flight, summed in z order
+  tap_reduce_store<MODE>(a, e, s);
 }
 
 // weight layouts: w [O][C][9] (torch) -> Wt [O][9][Cw] (mode 0; Cw = C rounded up to 4, zero padding, so
@@ -318,6 +369,8 @@ struct PackMany {
   float* dst[PACK_MAX];
 };
 
+// thread -> (o, c): its 9 taps are 36 contiguous source bytes (a wave reads one contiguous run) and 9
+// stores at consecutive c (each a contiguous wave run)
 __global__ __launch_bounds__(256) void conv_pack_many(PackMany P) {
   const int b = blockIdx.x;
   int i = 0;
@@ -325,11 +378,15 @@ __global__ __launch_bounds__(256) void conv_pack_many(PackMany P) {
     if (b >= P.start[k]) i = k;
   const int O = P.O[i], C = P.C[i], Cw = (C + 3) & ~3;
   const long e = (long)(b - P.start[i]) * 256 + threadIdx.x;
-  if (e >= (long)O * 9 * Cw) return;
-  const int c = (int)(e % Cw);
-  const long ot = e / Cw;
-  const int tap = (int)(ot % 9), o = (int)(ot / 9);
-  P.dst[i][e] = c < C ? P.src[i][((long)o * C + c) * 9 + tap] : 0.f;
+  if (e >= (long)O * Cw) return;
+  const int c = (int)(e % Cw), o = (int)(e / Cw);
+  float v[9];
+  const float* s = P.src[i] + ((long)o * C + c) * 9;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) v[t] = c < C ? s[t] : 0.f;
+  float* d = P.dst[i] + (long)o * 9 * Cw + c;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) d[(long)t * Cw] = v[t];
 }
 
 bool vec_ok(const float* p, long ld) { return p && ((uintptr_t)p % 16 == 0) && (ld % 4 == 0); }
@@ -353,7 +410,9 @@ int launch_tap(TapArgs& a, int grid_n, int grid_m, float* ws, long ws_floats, hi
   VC_CHECK_LAUNCH();
   if (nsplit > 1) {
     const long n = (long)a.M * a.N;
-    hipLaunchKernelGGL(conv_tap_reduce<MODE>, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, a, nsplit);
+    const int vec = (n % 4 == 0) && ((uintptr_t)ws % 16 == 0);
+    hipLaunchKernelGGL(conv_tap_reduce<MODE>, dim3(vc_cdiv(vec ? n / 4 : n, 256)), dim3(256), 0, stream, a, nsplit,
+                       vec);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;
@@ -396,7 +455,7 @@ VC_EXPORT int vc_conv3x3_pack_many(int n, const int* shapes, const float* const*
       P.src[k] = src[i0 + k];
       P.dst[k] = dst[i0 + k];
       P.start[k] = (int)total;
-      total += vc_cdiv((long)O * 9 * ((C + 3) & ~3), 256);
+      total += vc_cdiv((long)O * ((C + 3) & ~3), 256);
       VC_REQUIRE(total < (1L << 31));
     }
     P.start[P.n] = (int)total;
@@ -423,7 +482,7 @@ VC_EXPORT int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, con
 }
 
 static int tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx, const float* dy, long lddy,
-                     float* dwt, int oihw, float* ws, long ws_floats, hipStream_t stream) {
+                     float* dwt, int oihw, float* db, float* ws, long ws_floats, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H >= 3 - 2 * pad && W >= 3 - 2 * pad && C > 0 && O > 0 && (pad == 0 || pad == 1));
   VC_REQUIRE(x && dy && dwt && ldx >= C && lddy >= O);
   TapArgs a = geo(B, H, W, C, O, pad);
@@ -436,6 +495,8 @@ static int tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x,
   a.nk = vc_cdiv(a.P, TK);
   a.x = x; a.ldx = ldx; a.dy = dy; a.lddy = lddy; a.out = dwt; a.ldo = 9L * C;
   a.oihw = oihw;
+  a.dbias = db;
+  if (db) a.N = 9 * C + 1;   // the split slabs' bias column
   a.vx = vec_ok(x, ldx); a.vdy = vec_ok(dy, lddy);
   return launch_tap<WGRAD>(a, 9 * a.tpt, vc_cdiv(O, TM), ws, ws_floats, stream);
 }
@@ -443,13 +504,13 @@ static int tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x,
 VC_EXPORT int vc_conv3x3_tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
                                    const float* dy, long lddy, float* dwt, float* ws, long ws_floats,
                                    hipStream_t stream) {
-  return tap_wgrad(B, H, W, C, O, pad, x, ldx, dy, lddy, dwt, 0, ws, ws_floats, stream);
+  return tap_wgrad(B, H, W, C, O, pad, x, ldx, dy, lddy, dwt, 0, nullptr, ws, ws_floats, stream);
 }
 
 VC_EXPORT int vc_conv3x3_tap_wgrad_oihw(int B, int H, int W, int C, int O, int pad, const float* x, long ldx,
-                                        const float* dy, long lddy, float* dw, float* ws, long ws_floats,
+                                        const float* dy, long lddy, float* dw, float* db, float* ws, long ws_floats,
                                         hipStream_t stream) {
-  return tap_wgrad(B, H, W, C, O, pad, x, ldx, dy, lddy, dw, 1, ws, ws_floats, stream);
+  return tap_wgrad(B, H, W, C, O, pad, x, ldx, dy, lddy, dw, 1, db, ws, ws_floats, stream);
 }
 
 VC_EXPORT int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, const float* dy, long lddy,

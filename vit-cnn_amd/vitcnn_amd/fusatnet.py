@@ -307,10 +307,9 @@ class _Program:
 
         def bwd():
             dy = self.grad_of(y)
-            if _TAP_CONV:   # the weight gradient stored in the torch layout by the wgrad launch itself
+            if _TAP_CONV:   # weight gradient in the torch layout and the bias gradient, by the wgrad launch
                 L.vc_conv3x3_tap_wgrad_oihw(B, H, H, C, O, pad, x.data_ptr(), ldx, dy.data_ptr(), O,
-                                            self.pgrad(conv.weight), scr, self.SCRATCH, self.s)
-                L.vc_colsum(M, O, dy.data_ptr(), O, self.pgrad(conv.bias), 0.0, scr, self.SCRATCH, self.s)
+                                            self.pgrad(conv.weight), self.pgrad(conv.bias), scr, self.SCRATCH, self.s)
                 if id(x) not in self.no_grad_ids:   # every row's C columns written (ldx padding never read)
                     gx, beta = self.acc(x)
                     L.vc_conv3x3_tap_dgrad(B, H, H, C, O, pad, dy.data_ptr(), O, wt.data_ptr(), beta, gx.data_ptr(),
@@ -339,7 +338,7 @@ class _Program:
     def bn_relu(self, y, M, C, bn, relu=1):
         mean, invstd = self.new(C), self.new(C)
         if self.train:
-            bn.num_batches_tracked.add_(1)
+            self.nbt.append(bn.num_batches_tracked)   # incremented together at the end of run()
         z = self.new(*y.shape) if self.grad else y
         # train: one launch where the grid allows (group barrier over the stream's zeroed counters)
         self.L.vc_bn_forward_ex(1 if self.train else 0, M, C, y.data_ptr(), C, bn.eps,
@@ -457,6 +456,13 @@ class _Program:
                                     self.s)
 
     def run(self):
+        self.nbt = []
+        out = self._run()
+        if self.nbt:   # every executed BatchNorm's num_batches_tracked += 1: one multi-tensor launch
+            torch._foreach_add_(self.nbt, 1)
+        return out
+
+    def _run(self):
         m, L, B, P = self.m, self.L, self.B, self.P
         self.pack_all()
         c1, c2 = m.c1, m.c2
