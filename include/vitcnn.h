@@ -158,6 +158,13 @@ VC_API int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy, co
                         const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
                         float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w,
                         float* ws, long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream);
+/* vc_bn_bwd_ex through the ReLU that follows the BatchNorm, its decisions recomputed from x, the saved
+ * statistics and the affine (w, b) with the forward's own arithmetic instead of read from the forward's
+ * output: bit-identical to vc_bn_bwd_ex with relu_out = that output, one [M, C] read less per pass. */
+VC_API int vc_bn_bwd_relu_ex(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
+                             const float* mean, const float* invstd, const float* w, const float* b, float* dx,
+                             long lddx, float beta_dx, float* dw, float* db, float beta_w, float* ws, long ws_floats,
+                             unsigned int* counters, int n_counters, hipStream_t stream);
 
 /* ---------------------------------------------------------------- layout / spatial
  * NCHW input patches (the reference's batch layout, datasets.py:571-572) -> channels-last. */

@@ -695,3 +695,37 @@ def test_bn_one_launch_barrier_is_bit_identical(L, probe, ws, M, C, relu, monkey
     for o in outs[1:]:
         for a_, b_ in zip(outs[0], o):
             assert torch.equal(a_, b_)
+
+
+@pytest.mark.parametrize("train", [1, 0])
+@pytest.mark.parametrize("M,C", [(3136, 256), (5184, 144), (37, 200), (7744, 64)])
+def test_bn_bwd_relu_affine_is_bit_identical(L, ws, train, M, C):
+    """vc_bn_bwd_relu_ex (the ReLU decisions recomputed from x and the affine) == vc_bn_bwd_ex with
+    relu_out = the forward's output, bit for bit: dx, dw, db (with and without counters)"""
+    x = (rnd(M, C, seed=91, scale=2.0) + 0.3).to(DEV)
+    w, b = (rnd(C, seed=92) + 0.5).to(DEV), rnd(C, seed=93).to(DEV)
+    dy = rnd(M, C, seed=94).to(DEV)
+    rm, rv = (rnd(C, seed=95) * 0.1).to(DEV), (rnd(C, seed=96).abs() + 0.5).to(DEV)
+    mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    z = torch.empty(M, C, device=DEV)
+    L.vc_bn_forward(train, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(w), P(b), 1, P(z), C, P(ws),
+                    ws.numel(), S())
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    outs = []
+    for affine in (False, True):
+        for c_ in (None, cnt):
+            dx = torch.full((M, C), 0.25, device=DEV)
+            dw, db = torch.full((C,), 2.0, device=DEV), torch.full((C,), 3.0, device=DEV)
+            cp, cn = (P(c_), c_.numel()) if c_ is not None else (None, 0)
+            if affine:
+                L.vc_bn_bwd_relu_ex(train, M, C, P(dy), C, P(x), C, P(mean), P(inv), P(w), P(b), P(dx), C, 1.0, P(dw),
+                                    P(db), 0.5, P(ws), ws.numel(), cp, cn, S())
+            else:
+                L.vc_bn_bwd_ex(train, M, C, P(dy), C, P(x), C, P(z), C, P(mean), P(inv), P(w), P(dx), C, 1.0, P(dw),
+                               P(db), 0.5, P(ws), ws.numel(), cp, cn, S())
+            torch.cuda.synchronize()
+            outs.append([t.cpu() for t in (dx, dw, db)])
+    assert (z > 0).any() and (z == 0).any()
+    for o in outs[1:]:
+        for a_, b_ in zip(outs[0], o):
+            assert torch.equal(a_, b_)

@@ -18,7 +18,8 @@ PROBE_PATH = os.path.join(_REPO, "vit-cnn_amd", "vitcnn_amd", "libvitcnn_probe.s
 PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITCNN_BN_PCAP", "VITCNN_BN_IM2COL",
                "VITCNN_BN_GLF", "VITCNN_SCAN_RBS", "VITCNN_SCAN_SELECT_RS", "VITCNN_SCAN_TAIL",
                "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE",
-               "VITCNN_PIPE_NS", "VITCNN_BN_FUSED", "VITCNN_GEMM_GROUP_MAXB")
+               "VITCNN_PIPE_NS", "VITCNN_BN_FUSED", "VITCNN_GEMM_GROUP_MAXB",
+               "VITCNN_TAP_TARGET")
 
 
 def use_probe():
@@ -45,6 +46,7 @@ SWITCHES = {
     "VITCNN_BF16_MIN_K": ("model", "_BF16_MIN_K", int),
     "VITCNN_LANE_MAP": ("model", "_LANE_MAP", lambda v: [int(x) for x in v.split(",") if x]),
     "VITCNN_BN_TICKETS": ("model", "_BN_TICKETS", _FLAG),
+    "VITCNN_BN_RELU_AFFINE": ("model", "_BN_RELU_AFFINE", _FLAG),
     "VITCNN_CH_LANE": ("model", "_CH_LANE", int),
     "VITCNN_CH_ORDERED": ("model", "_CH_ORDERED", _FLAG),
     "VITCNN_FUSAT_IM2COL": ("fusatnet", "_TAP_CONV", lambda v: not _FLAG(v)),

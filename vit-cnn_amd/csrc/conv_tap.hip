@@ -398,8 +398,9 @@ int launch_tap(TapArgs& a, int grid_n, int grid_m, float* ws, long ws_floats, hi
   const long tiles = (long)grid_n * grid_m;
   int nsplit = 1;
   if (vc_knob("VITCNN_TAP_NOSPLIT", 0)) ws = nullptr;
-  if (ws && tiles < 768 && a.nk >= 8) {
-    nsplit = (int)std::max<long>(1, std::min<long>(768 / tiles, a.nk / 4));
+  const long target = vc_knob("VITCNN_TAP_TARGET", 768);   // blocks the split aims at (knob: probe library)
+  if (ws && tiles < target && a.nk >= 8) {
+    nsplit = (int)std::max<long>(1, std::min<long>(target / tiles, a.nk / 4));
     while (nsplit > 1 && (long)nsplit * a.M * a.N > ws_floats) --nsplit;
   }
   a.kper = vc_cdiv(a.nk, nsplit);

@@ -180,6 +180,16 @@ __device__ __forceinline__ void bn_dx_store(float* p, float beta_dx, float v) {
   *p = beta_dx != 0.f ? fmaf(beta_dx, *p, v) : v;
 }
 
+// The ReLU after a BatchNorm, for its backward: the decisions read from the forward's output (out, ld),
+// or recomputed from x and the affine (w, b) with bn_fwd_elem -- the forward's own arithmetic on the same
+// saved statistics, so the same decisions without reading the output; neither: no ReLU
+struct ReluSrc {
+  const float* out;
+  long ld;
+  const float* w;
+  const float* b;
+};
+
 // The fixed-order reduction of the [P][2][C] fp64 partials of channel group cx (block = 64 channels x
 // BN_RL partial lanes): on return (after a barrier) tot[0][cl] / tot[1][cl] hold channel cx*64+cl's two sums,
 // visible to every thread of the block.  Every consumer (the separate final kernels and the fused
@@ -443,8 +453,7 @@ __device__ __forceinline__ void bn_bwd_reduce(int P, int C, const double* __rest
 // partial block of the backward sums: part[blockIdx.y][0 / 1][c] = sum dyv, sum dyv * xhat over its rows
 template <int T = BN_T>
 __device__ __forceinline__ void bn_bwd_partial(int M, int C, const float* __restrict__ dy, long lddy,
-                                               const float* __restrict__ x, long ldx,
-                                               const float* __restrict__ relu_out, long ldo,
+                                               const float* __restrict__ x, long ldx, ReluSrc rs,
                                                const float* __restrict__ mean, const float* __restrict__ invstd,
                                                int rows_per, double* __restrict__ part) {
   constexpr int RT = T / 64, VPT = BN_RL / RT;   // virtual row lanes per thread (see bn_part_sums)
@@ -459,6 +468,7 @@ __device__ __forceinline__ void bn_bwd_partial(int M, int C, const float* __rest
     double s1 = 0.0, s2 = 0.0;
     if (c < C) {
       const float mu = mean[c], is = invstd[c];
+      const float rw = rs.b ? rs.w[c] : 0.f, rbc = rs.b ? rs.b[c] : 0.f;
       for (long rb = r0 + rl; rb < r1; rb += BN_RL * NB) {   // NB rows' loads in flight, summed in row order
         float dv[NB], xv[NB], ov[NB];
 #pragma unroll
@@ -467,13 +477,14 @@ __device__ __forceinline__ void bn_bwd_partial(int M, int C, const float* __rest
           const bool ok = r < r1;
           dv[i] = ok ? dy[r * lddy + c] : 0.f;
           xv[i] = ok ? x[r * ldx + c] : 0.f;
-          ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
+          ov[i] = ok && rs.out ? rs.out[r * rs.ld + c] : 1.f;
         }
 #pragma unroll
         for (int i = 0; i < NB; ++i)
           if (rb + BN_RL * i < r1) {
             float d = dv[i];
-            if (relu_out && !(ov[i] > 0.f)) d = 0.f;
+            if (rs.out && !(ov[i] > 0.f)) d = 0.f;
+            if (rs.b && !(bn_fwd_elem(xv[i], mu, is, rw, rbc) > 0.f)) d = 0.f;
             s1 += d;
             s2 += (double)d * ((xv[i] - mu) * is);
           }
@@ -497,13 +508,12 @@ __device__ __forceinline__ void bn_bwd_partial(int M, int C, const float* __rest
 }
 
 __global__ __launch_bounds__(BN_T) void bn_bwd_sums(int M, int C, const float* __restrict__ dy, long lddy,
-                                                   const float* __restrict__ x, long ldx,
-                                                   const float* __restrict__ relu_out, long ldo,
+                                                   const float* __restrict__ x, long ldx, ReluSrc rs,
                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
                                                    int rows_per, double* __restrict__ part,
                                                    unsigned int* __restrict__ cnt, double* __restrict__ sums,
                                                    float* __restrict__ dw, float* __restrict__ db, float beta_w) {
-  bn_bwd_partial(M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, rows_per, part);
+  bn_bwd_partial(M, C, dy, lddy, x, ldx, rs, mean, invstd, rows_per, part);
   if (!cnt || !block_last_arriver(cnt + blockIdx.x, gridDim.y)) return;
   bn_bwd_reduce(gridDim.y, C, part, blockIdx.x, sums, dw, db, beta_w);
 }
@@ -517,11 +527,12 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_final(int P, int C, const double*
 // dx rows [r0, r1) of channel c (row lane rl) from the channel's sums s1, s2 (train) -- or w*invstd*dyv (eval)
 template <int NL = BN_RL>   // row lanes of the block (rl in [0, NL))
 __device__ __forceinline__ void bn_bwd_apply_rows(int train, int M, const float* __restrict__ dy, long lddy,
-                                                  const float* __restrict__ x, long ldx,
-                                                  const float* __restrict__ relu_out, long ldo, float mu, float is,
+                                                  const float* __restrict__ x, long ldx, ReluSrc rs, float mu, float is,
                                                   float wc, double s1, double s2, float* __restrict__ dx, long lddx,
                                                   float beta_dx, long r0, long r1, int c, int rl) {
   const float invM = 1.f / (float)M;
+  const float rw = rs.b ? rs.w[c] : 0.f, rbc = rs.b ? rs.b[c] : 0.f;
+  const bool need_x = train || rs.b;
   for (long rb = r0 + rl; rb < r1; rb += NL * NB) {   // NB rows' loads in flight
     float dv[NB], xv[NB], ov[NB];
 #pragma unroll
@@ -529,14 +540,15 @@ __device__ __forceinline__ void bn_bwd_apply_rows(int train, int M, const float*
       const long r = rb + NL * i;
       const bool ok = r < r1;
       dv[i] = ok ? dy[r * lddy + c] : 0.f;
-      xv[i] = ok && train ? x[r * ldx + c] : 0.f;
-      ov[i] = ok && relu_out ? relu_out[r * ldo + c] : 1.f;
+      xv[i] = ok && need_x ? x[r * ldx + c] : 0.f;
+      ov[i] = ok && rs.out ? rs.out[r * rs.ld + c] : 1.f;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
       if (rb + NL * i < r1) {
         float d = dv[i];
-        if (relu_out && !(ov[i] > 0.f)) d = 0.f;
+        if (rs.out && !(ov[i] > 0.f)) d = 0.f;
+        if (rs.b && !(bn_fwd_elem(xv[i], mu, is, rw, rbc) > 0.f)) d = 0.f;
         float v;
         if (train) v = bn_bwd_elem(d, xv[i], mu, is, wc, (float)s1 * invM, (float)s2 * invM);
         else v = (wc * is) * d;
@@ -550,8 +562,7 @@ __device__ __forceinline__ void bn_bwd_apply_rows(int train, int M, const float*
 // all write dx = beta_dx*dx + w*invstd*(dyv - s1/M - xhat*s2/M) (train) or w*invstd*dyv (eval) for
 // their rows -- the same arithmetic as bn_bwd_final + bn_bwd_apply.
 __global__ __launch_bounds__(BN_T) void bn_bwd_apply_sums(int train, int M, int C, const float* __restrict__ dy,
-                                                         long lddy, const float* __restrict__ x, long ldx,
-                                                         const float* __restrict__ relu_out, long ldo,
+                                                         long lddy, const float* __restrict__ x, long ldx, ReluSrc rs,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ invstd,
                                                          const float* __restrict__ w, int P,
@@ -569,7 +580,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_sums(int train, int M, int 
     if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
   }
   const long r0 = (long)blockIdx.y * rows_per_block;
-  bn_bwd_apply_rows(train, M, dy, lddy, x, ldx, relu_out, ldo, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
+  bn_bwd_apply_rows(train, M, dy, lddy, x, ldx, rs, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
                     min((long)M, r0 + rows_per_block), c, rl);
 }
 
@@ -578,15 +589,14 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_sums(int train, int M, int 
 // bn_part_sums' order and write dx for their own rows (re-read from L2).  Bit-identical to
 // bn_bwd_sums + bn_bwd_apply_sums.
 __global__ __launch_bounds__(BNF_T) void bn_bwd_fused(int M, int C, const float* __restrict__ dy, long lddy,
-                                                    const float* __restrict__ x, long ldx,
-                                                    const float* __restrict__ relu_out, long ldo,
+                                                    const float* __restrict__ x, long ldx, ReluSrc rs,
                                                     const float* __restrict__ mean, const float* __restrict__ invstd,
                                                     const float* __restrict__ w, int rows_per,
                                                     double* __restrict__ part, unsigned int* __restrict__ cnt,
                                                     float* __restrict__ dx, long lddx, float beta_dx,
                                                     float* __restrict__ dw, float* __restrict__ db, float beta_w) {
   __shared__ double tot[2][64];
-  bn_bwd_partial<BNF_T>(M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, rows_per, part);
+  bn_bwd_partial<BNF_T>(M, C, dy, lddy, x, ldx, rs, mean, invstd, rows_per, part);
   unsigned int* gc = cnt + 2 * blockIdx.x;
   block_group_sync(gc, gridDim.y);
   bn_part_sums<BNF_T>(gridDim.y, C, part, blockIdx.x, tot);
@@ -600,13 +610,13 @@ __global__ __launch_bounds__(BNF_T) void bn_bwd_fused(int M, int C, const float*
     if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
   }
   const long r0 = (long)blockIdx.y * rows_per;
-  bn_bwd_apply_rows<BNF_T / 64>(1, M, dy, lddy, x, ldx, relu_out, ldo, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
+  bn_bwd_apply_rows<BNF_T / 64>(1, M, dy, lddy, x, ldx, rs, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
                     min((long)M, r0 + rows_per), c, rl);
 }
 
 // train: dx = w*invstd*(dyv - s1/M - xhat*s2/M);  eval (sums == null): dx = w*invstd*dyv
 __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, long lddy, const float* __restrict__ x,
-                             long ldx, const float* __restrict__ relu_out, long ldo, const float* __restrict__ mean,
+                             long ldx, ReluSrc rs, const float* __restrict__ mean,
                              const float* __restrict__ invstd, const float* __restrict__ w,
                              const double* __restrict__ sums, float* __restrict__ dx, long lddx, float beta_dx) {
   const int C = fC.div;
@@ -615,8 +625,9 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
   int c;
   const long r = fdivmod(idx, fC, c);
   float d = dy[r * lddy + c];
-  if (relu_out && !(relu_out[r * ldo + c] > 0.f)) d = 0.f;
   const float is = invstd[c];
+  if (rs.out && !(rs.out[r * rs.ld + c] > 0.f)) d = 0.f;
+  if (rs.b && !(bn_fwd_elem(x[r * ldx + c], mean[c], is, rs.w[c], rs.b[c]) > 0.f)) d = 0.f;
   float v;
   if (sums) {
     const float invM = 1.f / (float)M;
@@ -988,10 +999,10 @@ VC_EXPORT int vc_bn_apply(long M, int C, const float* x, long ldx, const float* 
 // BN backward (optionally through a following ReLU whose output is relu_out).
 // dx = beta_dx*dx + ...;  dw/db = beta_w*dw/db + ... (either may be null).  counters (optional):
 // >= ceil(C/64) zeroed arrival counters (left zero): the sums are reduced inside the partial launch.
-VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
-                           const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
-                           float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w, float* ws,
-                           long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream) {
+static int bn_bwd_impl(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx, ReluSrc rs,
+                       const float* mean, const float* invstd, const float* w, float* dx, long lddx, float beta_dx,
+                       float* dw, float* db, float beta_w, float* ws, long ws_floats, unsigned int* counters,
+                       int n_counters, hipStream_t stream) {
   VC_REQUIRE(C > 0 && M > 0 && M < (1L << 31) && ((uintptr_t)ws & 7) == 0);
   // per-row-block partial sums [P][2][C] and the final [2][C] sums are fp64
   double* wsd = reinterpret_cast<double*>(ws);
@@ -1002,7 +1013,7 @@ VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy,
   double* sums = wsd + (long)P * C * 2;
   if (train && dx && bn_fused_fits(C, P, counters, n_counters)) {   // one launch: group barrier
     hipLaunchKernelGGL(bn_bwd_fused, dim3(vc_cdiv(C, 64), P), dim3(BNF_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
-                       relu_out, ldo, mean, invstd, w, rows_per, wsd, counters, dx, lddx, beta_dx, dw, db, beta_w);
+                       rs, mean, invstd, w, rows_per, wsd, counters, dx, lddx, beta_dx, dw, db, beta_w);
     VC_CHECK_LAUNCH();
     return VC_OK;
   }
@@ -1010,12 +1021,12 @@ VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy,
   // reduces the partials itself
   unsigned int* cnt = (!(train && dx) && counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;
   hipLaunchKernelGGL(bn_bwd_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
-                     relu_out, ldo, mean, invstd, rows_per, wsd, cnt, sums, dw, db, beta_w);
+                     rs, mean, invstd, rows_per, wsd, cnt, sums, dw, db, beta_w);
   VC_CHECK_LAUNCH();
   if (!cnt && dx) {   // the channel-tiled apply reduces the partials itself: one launch fewer
     const int rpb = BN_APPLY_ROWS;
     hipLaunchKernelGGL(bn_bwd_apply_sums, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, train,
-                       (int)M, C, dy, lddy, x, ldx, relu_out, ldo, mean, invstd, w, P, wsd, dx, lddx, beta_dx, dw,
+                       (int)M, C, dy, lddy, x, ldx, rs, mean, invstd, w, P, wsd, dx, lddx, beta_dx, dw,
                        db, beta_w, rpb);
     VC_CHECK_LAUNCH();
     return VC_OK;
@@ -1027,11 +1038,30 @@ VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy,
   if (dx) {
     VC_REQUIRE_I32(M * C);
     hipLaunchKernelGGL(bn_bwd_apply, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)M, make_fastdiv(C), dy,
-                       lddy, x, ldx, relu_out, ldo, mean, invstd, w, train ? sums : (const double*)nullptr, dx, lddx,
+                       lddy, x, ldx, rs, mean, invstd, w, train ? sums : (const double*)nullptr, dx, lddx,
                        beta_dx);
     VC_CHECK_LAUNCH();
   }
   return VC_OK;
+}
+
+VC_EXPORT int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
+                           const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
+                           float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w, float* ws,
+                           long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream) {
+  return bn_bwd_impl(train, M, C, dy, lddy, x, ldx, ReluSrc{relu_out, ldo, nullptr, nullptr}, mean, invstd, w, dx, lddx,
+                     beta_dx, dw, db, beta_w, ws, ws_floats, counters, n_counters, stream);
+}
+
+// BN backward through the ReLU that follows it, the ReLU's decisions recomputed from x, the saved statistics
+// and the affine (w, b) -- bit-identical to vc_bn_bwd_ex with relu_out = the forward's output, one read less
+VC_EXPORT int vc_bn_bwd_relu_ex(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,
+                                const float* mean, const float* invstd, const float* w, const float* b, float* dx,
+                                long lddx, float beta_dx, float* dw, float* db, float beta_w, float* ws, long ws_floats,
+                                unsigned int* counters, int n_counters, hipStream_t stream) {
+  VC_REQUIRE(w && b);
+  return bn_bwd_impl(train, M, C, dy, lddy, x, ldx, ReluSrc{nullptr, 0, w, b}, mean, invstd, w, dx, lddx, beta_dx,
+                     dw, db, beta_w, ws, ws_floats, counters, n_counters, stream);
 }
 
 VC_EXPORT int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, const float* x, long ldx,

@@ -349,8 +349,15 @@ class _Program:
 
         def bwd():
             gy, beta = self.acc(y)
+            if relu:   # the ReLU decisions recomputed from y and the affine: z is not read again
+                self.L.vc_bn_bwd_relu_ex(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
+                                         mean.data_ptr(), invstd.data_ptr(), bn.weight.data_ptr(),
+                                         bn.bias.data_ptr(), gy.data_ptr(), C, beta, self.pgrad(bn.weight),
+                                         self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.cnt,
+                                         N_COUNTERS, self.s)
+                return
             self.L.vc_bn_bwd_ex(1 if self.train else 0, M, C, self.grad_of(z).data_ptr(), C, y.data_ptr(), C,
-                                z.data_ptr() if relu else None, C, mean.data_ptr(), invstd.data_ptr(),
+                                None, C, mean.data_ptr(), invstd.data_ptr(),
                                 bn.weight.data_ptr(), gy.data_ptr(), C, beta, self.pgrad(bn.weight),
                                 self.pgrad(bn.bias), 0.0, self.scr.data_ptr(), self.SCRATCH, self.cnt, N_COUNTERS,
                                 self.s)

@@ -102,6 +102,7 @@ _LANE_MAP = []       # logical lane -> stream index (empty: lane i on stream i)
 # the two read-modify-write GEMM epilogues race, and the result depends on the schedule)
 _CH_LANE = 1
 _CH_ORDERED = True
+_BN_RELU_AFFINE = True   # BN + ReLU backward: the ReLU decisions recomputed from the BN input and affine
 _BN_TICKETS = False  # BN reductions without dx in the last-arriving block: measured ~1% slower (every arrival is an
 #                     agent-scope release = L2 writeback); with dx the counters select the one-launch kernels
 
@@ -929,6 +930,13 @@ class _Program:
     # ---------------------------------------------------------------- backward
     def bn_bwd(self, pfx, tag, dY, lddy, X, ldx, relu_out, M, C, dX, lddx, beta_dx):
         ws = self.ws
+        if relu_out and _BN_RELU_AFFINE:
+            # the ReLU decisions recomputed from X and the affine (vc_bn_bwd_relu_ex: same bits, one read less)
+            self.L.vc_bn_bwd_relu_ex(self.train, M, C, dY, lddy, X, ldx, ws.f(tag + ".bm", C), ws.f(tag + ".bi", C),
+                                     self.P[pfx + ".weight"], self.P[pfx + ".bias"], dX or None, lddx, beta_dx,
+                                     self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n,
+                                     self._cnt[self.cur] if (dX or _BN_TICKETS) else None, N_COUNTERS, self.s)
+            return
         self.L.vc_bn_bwd_ex(self.train, M, C, dY, lddy, X, ldx, relu_out or None, C, ws.f(tag + ".bm", C),
                             ws.f(tag + ".bi", C), self.P[pfx + ".weight"], dX or None, lddx, beta_dx,
                             self.G[pfx + ".weight"], self.G[pfx + ".bias"], 0.0, self.scr_p, self.scr_n,
