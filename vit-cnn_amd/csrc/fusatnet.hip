@@ -38,6 +38,18 @@ __global__ void mul2_2d(int total, FastDiv fC, const float* __restrict__ a, long
   out[m * ldo + c] = a[m * lda + c] * b[m * ldb + c];
 }
 
+// the same with 4 consecutive channels per thread (C, the leading dimensions and the bases 16-B aligned)
+__global__ void mul2_2d_v4(int total4, FastDiv fC4, const float* __restrict__ a, long lda, const float* __restrict__ b,
+                           long ldb, float* __restrict__ out, long ldo) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total4) return;
+  int c4;
+  const long m = fdivmod(idx, fC4, c4);
+  const float4 x = *reinterpret_cast<const float4*>(a + m * lda + 4 * c4);
+  const float4 y = *reinterpret_cast<const float4*>(b + m * ldb + 4 * c4);
+  *reinterpret_cast<float4*>(out + m * ldo + 4 * c4) = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
+}
+
 // out[b, hw, c] = mean_{p < HWp} pooled[b, p, c] * F[b, hw, c]   (AdaptiveAvgPool2d(1) then broadcast product)
 __global__ void pool_scale(int total, FastDiv fC, FastDiv fHW, int HWp, const float* __restrict__ pooled,
                            const float* __restrict__ F, long ldf, float* __restrict__ out, long ldo) {
@@ -80,23 +92,53 @@ __global__ void col2im3x3_pad(int total, FastDiv fC, FastDiv fW, FastDiv fH, int
 }
 
 // backward of pool_scale: one thread per (b, c): s = mean_p pooled; dF (+)= s * dout; dpooled = sum_hw dout*F / HWp
-__global__ void pool_scale_bwd(int B, int HW, int HWp, int C, const float* __restrict__ pooled,
-                               const float* __restrict__ F, long ldf, const float* __restrict__ dout, long lddo,
-                               float* __restrict__ dF, long lddf, float* __restrict__ dpooled) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * C) return;
-  const int b = idx / C, c = idx % C;
-  float s = 0.f;
-  for (int p = 0; p < HWp; ++p) s += pooled[((long)b * HWp + p) * C + c];
-  s /= (float)HWp;
+// block = (64 channels, sample b) x PS_RL row lanes over the HW pixels (8 pixels' loads in flight per lane);
+// the lanes' ds partials summed in lane order through LDS (fixed order)
+constexpr int PS_RL = 8;
+__global__ __launch_bounds__(64 * PS_RL) void pool_scale_bwd(int B, int HW, int HWp, int C,
+                                                            const float* __restrict__ pooled,
+                                                            const float* __restrict__ F, long ldf,
+                                                            const float* __restrict__ dout, long lddo,
+                                                            float* __restrict__ dF, long lddf,
+                                                            float* __restrict__ dpooled) {
+  __shared__ float sh[PS_RL][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
   float ds = 0.f;
-  for (int hw = 0; hw < HW; ++hw) {
-    const long m = (long)b * HW + hw;
-    const float g = dout[m * lddo + c];
-    ds += g * F[m * ldf + c];
-    dF[m * lddf + c] += s * g;
+  if (c < C) {
+    float s = 0.f;
+    for (int p = 0; p < HWp; ++p) s += pooled[((long)b * HWp + p) * C + c];
+    s /= (float)HWp;
+    constexpr int NBH = 8;
+    for (int h0 = rl; h0 < HW; h0 += PS_RL * NBH) {
+      float g[NBH], f[NBH], d[NBH];
+#pragma unroll
+      for (int i = 0; i < NBH; ++i) {
+        const int hw = h0 + PS_RL * i;
+        const long m = (long)b * HW + (hw < HW ? hw : 0);
+        const bool ok = hw < HW;
+        g[i] = ok ? dout[m * lddo + c] : 0.f;
+        f[i] = ok ? F[m * ldf + c] : 0.f;
+        d[i] = ok ? dF[m * lddf + c] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < NBH; ++i) {
+        const int hw = h0 + PS_RL * i;
+        if (hw < HW) {
+          ds += g[i] * f[i];
+          dF[((long)b * HW + hw) * lddf + c] = d[i] + s * g[i];
+        }
+      }
+    }
   }
-  for (int p = 0; p < HWp; ++p) dpooled[((long)b * HWp + p) * C + c] = ds / (float)HWp;
+  sh[rl][cl] = ds;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float t = sh[0][cl];
+#pragma unroll
+    for (int l = 1; l < PS_RL; ++l) t += sh[l][cl];
+    for (int p = 0; p < HWp; ++p) dpooled[((long)b * HWp + p) * C + c] = t / (float)HWp;
+  }
 }
 
 }  // namespace
@@ -115,7 +157,8 @@ VC_API int vc_col2im3x3_pad(int B, int H, int W, int C, int pad, const float* dc
 VC_API int vc_pool_scale_bwd(int B, int HW, int HWp, int C, const float* pooled, const float* F, long ldf,
                              const float* dout, long lddo, float* dF, long lddf, float* dpooled, hipStream_t stream) {
   VC_REQUIRE(B > 0 && HW > 0 && HWp > 0 && C > 0);
-  hipLaunchKernelGGL(pool_scale_bwd, dim3(vc_cdiv((long)B * C, 256)), dim3(256), 0, stream, B, HW, HWp, C, pooled, F,
+  VC_REQUIRE(B < 65536);
+  hipLaunchKernelGGL(pool_scale_bwd, dim3(vc_cdiv(C, 64), B), dim3(64 * PS_RL), 0, stream, B, HW, HWp, C, pooled, F,
                      ldf, dout, lddo, dF, lddf, dpooled);
   VC_CHECK_LAUNCH();
   return VC_OK;
@@ -139,8 +182,14 @@ VC_API int vc_mul2_2d(long M, int C, const float* a, long lda, const float* b, l
   VC_REQUIRE(M >= 0 && C > 0);
   if (M == 0) return VC_OK;
   VC_REQUIRE_I32(M * C);
-  hipLaunchKernelGGL(mul2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C), a, lda,
-                     b, ldb, out, ldo);
+  const bool v4 = C % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)a % 16) == 0 &&
+                  ((uintptr_t)b % 16) == 0 && ((uintptr_t)out % 16) == 0;
+  if (v4)
+    hipLaunchKernelGGL(mul2_2d_v4, dim3(vc_cdiv(M * C / 4, 256)), dim3(256), 0, stream, (int)(M * C / 4),
+                       make_fastdiv(C / 4), a, lda, b, ldb, out, ldo);
+  else
+    hipLaunchKernelGGL(mul2_2d, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, (int)(M * C), make_fastdiv(C), a,
+                       lda, b, ldb, out, ldo);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
