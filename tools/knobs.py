@@ -19,7 +19,8 @@ PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITC
                "VITCNN_BN_GLF", "VITCNN_SCAN_RBS", "VITCNN_SCAN_SELECT_RS", "VITCNN_SCAN_TAIL",
                "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE",
                "VITCNN_PIPE_NS", "VITCNN_BN_FUSED", "VITCNN_GEMM_GROUP_MAXB",
-               "VITCNN_TAP_TARGET")
+               "VITCNN_TAP_TARGET", "VITCNN_TAP_PIPE", "VITCNN_CONV_PIPE_TILES_F", "VITCNN_CONV_PIPE_TILES_W",
+               "VITCNN_CONV_PIPE_TILES_D")
 
 
 def use_probe():

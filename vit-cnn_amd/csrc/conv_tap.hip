@@ -25,6 +25,7 @@
 // im2col GEMM the 128 x 128 tile halves the operand bytes per flop (the long-K convs were
 // operand-bandwidth-bound at ~50 TF/s).
 #include "common.h"
+#include "mfma_tiles.h"
 
 #include <algorithm>
 
@@ -39,6 +40,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 enum { FWD = 0, WGRAD = 1, DGRAD = 2 };
 
 struct TapArgs {
+  int nb;                  // batch
   int H, W, C, O, pad, OH, OW;
   int Cw;                  // Wt row pitch per tap: C rounded up to 4 (zero padding)
   int M, N;                // GEMM output extents (N: total output columns; wgrad 9C)
@@ -389,6 +391,167 @@ __global__ __launch_bounds__(256) void conv_pack_many(PackMany P) {
   for (int t = 0; t < 9; ++t) d[(long)t * Cw] = v[t];
 }
 
+// ---- conv_pipe: the same three implicit GEMMs on the LDS-DMA pipeline of the GEMM kernels (gemm.hip
+// gp::gemm_pipe, mfma_tiles.h): 64 x 64 output tiles on 4 waves, a 2-stage ring of 32-wide k-tiles filled
+// by buffer_load ... lds (one 16-B chunk per lane, no register staging, no LDS transposes), counted vmcnt
+// waits, one barrier per k-tile, v_mfma_f32_16x16x4_f32.  The gathers become per-lane DMA offsets: a
+// K-contiguous image row is one gathered input / output-gradient row (FWD / DGRAD A) or a weight row (FWD B);
+// a row-contiguous image k-row is one dy row (WGRAD A), one gathered input row (WGRAD B) or a weight row
+// (DGRAD B).  Rows outside the (padded) image, channels past C / O and pixels past the slice get an offset
+// past the buffer's end: the DMA writes zeros.  Needs C, O, ldx, lddy multiples of 4 and 16-B aligned bases
+// (otherwise conv_tap above).  On FusAtNet-sized products the pipelined GEMM runs at 100-110 TF/s against
+// conv_tap's 77-91 (tools/gemm_one.py, round 4).
+constexpr int CP_B = 64;   // output tile (both sides)
+
+template <int MODE>
+__global__ __launch_bounds__(256) void conv_pipe(TapArgs a, int tn, int nsplit, unsigned total) {
+  constexpr int BM = CP_B, BN = CP_B, WN = 2, NW = 4, NS = 2;
+  constexpr int WTM = BM / 2, WTN = BN / 2, MT = WTM / 16, NT = WTN / 16;
+  constexpr int SA_B = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int LOADS = (BM / 8 + BN / 8) / NW;
+  constexpr bool TA = MODE == WGRAD;   // A image [k][m] (row-contiguous) for the weight gradient
+  constexpr bool TB = MODE != FWD;     // B image [k][n] for the data and weight gradients
+  typedef g2::Stage<false, TA, BM, false> SA;
+  typedef g2::Stage<false, TB, BN, false> SB;
+  __shared__ __attribute__((aligned(1024))) char smem[gp::ring_bytes<BM, BN, NS>()];
+  __shared__ float bsh[4][64];
+  int zs, xn, ym, zb;
+  const int tm = (a.M + BM - 1) / BM;
+  gp::tile_coords(gp::xcd_linear(blockIdx.x, total), nsplit, tn, tm, 1, zs, xn, ym, zb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = ym * BM;
+  const int ntap = MODE == WGRAD ? xn / a.tpt : 0;
+  const int n0 = MODE == WGRAD ? (xn - ntap * a.tpt) * BN : xn * BN;
+  const int kt0 = zs * a.kper, kt1 = min(a.nk, kt0 + a.kper);
+  const unsigned OOB = gp::OOB;
+  const long in_rows = (long)a.nb * a.H * a.W, out_rows = (long)a.nb * a.OH * a.OW;
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), (short)0,
+                                                    a.x ? (int)(in_rows * a.ldx * 4) : 0, 0x00020000);
+  const auto rdy = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dy), (short)0,
+                                                     a.dy ? (int)(out_rows * a.lddy * 4) : 0, 0x00020000);
+  const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.w), (short)0,
+                                                    a.w ? (int)((long)a.O * 9 * a.Cw * 4) : 0, 0x00020000);
+  // K-contiguous fills (FWD A / B, DGRAD A): this lane's two image rows, decomposed once
+  int kb_[2], ki_[2], kj_[2];
+  bool kok_[2];
+  if constexpr (MODE != WGRAD) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int rloc = 8 * (wave + NW * q) + (lane >> 3);
+      const int m = m0 + rloc;
+      kok_[q] = m < a.M;
+      if (MODE == FWD) split_out(a, kok_[q] ? m : 0, kb_[q], ki_[q], kj_[q]);
+      else split_in(a, kok_[q] ? m : 0, kb_[q], ki_[q], kj_[q]);
+    }
+  }
+  auto issue = [&](int t) {
+    char* st = smem + (t % NS) * STAGE;
+    const int kt = kt0 + t;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = wave + NW * q;   // wave-instruction: 1 KB of each image
+      // K-contiguous chunk coordinates
+      const int rloc = 8 * i + (lane >> 3), kk = 4 * ((lane & 7) ^ ((rloc >> 1) & 7));
+      // row-contiguous chunk coordinates (4 k-rows x 16 chunks per instruction)
+      const int kr = 4 * i + (lane >> 4), sq = lane & 15;
+      const int col = (((sq >> 2) ^ ((kr >> 2) & 1)) << 4) + ((sq & 3) << 2);
+      unsigned va, vb;
+      if constexpr (MODE == FWD) {
+        const int tap = kt / a.tpt, c = (kt - tap * a.tpt) * 32 + kk;
+        const int row = in_row(a, kb_[q], ki_[q], kj_[q], tap);
+        va = (kok_[q] && row >= 0 && c < a.C) ? (unsigned)(((long)row * a.ldx + c) * 4) : OOB;
+        const int o = n0 + rloc;
+        vb = (o < a.O && c < a.Cw) ? (unsigned)(((long)o * 9 * a.Cw + (long)tap * a.Cw + c) * 4) : OOB;
+      } else if constexpr (MODE == DGRAD) {
+        const int tap = kt / a.tpt, o0 = (kt - tap * a.tpt) * 32;
+        const int row = out_row(a, kb_[q], ki_[q], kj_[q], tap), o = o0 + kk;
+        va = (kok_[q] && row >= 0 && o < a.O) ? (unsigned)(((long)row * a.lddy + o) * 4) : OOB;
+        const int ob = o0 + kr, c = n0 + col;
+        vb = (ob < a.O && c < a.Cw) ? (unsigned)(((long)ob * 9 * a.Cw + (long)tap * a.Cw + c) * 4) : OOB;
+      } else {
+        const int p = kt * 32 + kr, o = m0 + col, c = n0 + col;
+        va = (p < a.P && o < a.O) ? (unsigned)(((long)p * a.lddy + o) * 4) : OOB;
+        int row = -1;
+        if (p < a.P) {
+          int b, y, x;
+          split_out(a, p, b, y, x);
+          row = in_row(a, b, y, x, ntap);
+        }
+        vb = (row >= 0 && c < a.C) ? (unsigned)(((long)row * a.ldx + c) * 4) : OOB;
+      }
+      if constexpr (MODE == WGRAD) gp::dma16(rdy, st + i * 1024, va);
+      else if constexpr (MODE == FWD) gp::dma16(rx, st + i * 1024, va);
+      else gp::dma16(rdy, st + i * 1024, va);
+      if constexpr (MODE == FWD) gp::dma16(rw, st + SA_B + i * 1024, vb);
+      else if constexpr (MODE == DGRAD) gp::dma16(rw, st + SA_B + i * 1024, vb);
+      else gp::dma16(rx, st + SA_B + i * 1024, vb);
+    }
+  };
+  f32x4 acc[1][MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[0][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // weight gradient's bias column: the n-tile-0 blocks sum their staged dy tile (A, [k][m]) over k --
+  // thread (m = tid & 63, k quarter tid >> 6), k-tiles in order, the quarters in order at the end
+  const bool do_b = MODE == WGRAD && a.dbias && xn == 0;
+  float bacc = 0.f;
+  const int nk = kt1 > kt0 ? kt1 - kt0 : 0;
+  if (nk > 0) issue(0);
+  for (int t = 0; t < nk; ++t) {
+    gp::vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the slot refilled below
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 1 < nk) issue(t + 1);
+    const char* cur = smem + (t % NS) * STAGE;
+    if (do_b) {
+      const int mm = tid & 63, kq = tid >> 6;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bacc += *reinterpret_cast<const float*>(cur + SA::rc_off(8 * kq + k, mm));
+    }
+    g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
+  }
+  (void)LOADS;
+  const bool split = nsplit > 1;
+  if (do_b) {
+    const int mm = tid & 63, kq = tid >> 6;
+    bsh[kq][mm] = bacc;
+    __syncthreads();
+    const int row = m0 + mm;
+    if (kq == 0 && row < a.M) {
+      const float v = ((bsh[0][mm] + bsh[1][mm]) + bsh[2][mm]) + bsh[3][mm];
+      if (split) a.part[((long)zs * a.M + row) * a.N + 9 * a.C] = v;
+      else a.dbias[row] = v;
+    }
+  }
+  // C/D map of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + r;
+        const int nl = n0 + wn * WTN + ni * 16 + (lane & 15);
+        const int nmax = MODE == FWD ? a.O : a.C;
+        if (m >= a.M || nl >= nmax) continue;
+        const float v = acc[0][mi][ni][r];
+        const int col = MODE == WGRAD ? ntap * a.C + nl : nl;
+        if (split) {
+          a.part[((long)zs * a.M + m) * a.N + col] = v;
+        } else if (MODE == WGRAD && a.oihw) {
+          a.out[((long)m * a.C + nl) * 9 + ntap] = v;
+        } else {
+          float* o = a.out + (long)m * a.ldo + col;
+          if (MODE == FWD) *o = v + (a.bias ? a.bias[col] : 0.f);
+          else if (MODE == DGRAD) *o = (a.beta != 0.f ? a.beta * *o : 0.f) + v;
+          else *o = v;
+        }
+      }
+}
+
 bool vec_ok(const float* p, long ld) { return p && ((uintptr_t)p % 16 == 0) && (ld % 4 == 0); }
 
 template <int MODE>
@@ -419,14 +582,54 @@ int launch_tap(TapArgs& a, int grid_n, int grid_m, float* ws, long ws_floats, hi
   return VC_OK;
 }
 
+// the pipelined kernel's launch: split K (slices of >= 4 k-tiles, towards ~512 blocks) only for grids
+// of < 128 tiles -- the plan of gemm.hip's plan_pipe; the same split-K combine as conv_tap
+template <int MODE>
+int launch_conv_pipe(TapArgs& a, int grid_n, float* ws, long ws_floats, hipStream_t stream) {
+  const int tm = vc_cdiv(a.M, CP_B);
+  const long tiles = (long)grid_n * tm;
+  int nsplit = 1;
+  // grids smaller than this split K (knobs; per direction)
+  static const char* const knob[3] = {"VITCNN_CONV_PIPE_TILES_F", "VITCNN_CONV_PIPE_TILES_W", "VITCNN_CONV_PIPE_TILES_D"};
+  const long below = vc_knob(knob[MODE], 1024);
+  if (ws && tiles < below)
+    nsplit = (int)std::max<long>(1, std::min<long>(std::min<long>((4 * below + tiles - 1) / tiles, a.nk / 4), 64));
+  while (nsplit > 1 && (long)nsplit * a.M * a.N > ws_floats) --nsplit;
+  a.kper = vc_cdiv(a.nk, nsplit);
+  nsplit = vc_cdiv(a.nk, a.kper);
+  a.part = nsplit > 1 ? ws : nullptr;
+  const long total = tiles * nsplit;
+  VC_REQUIRE(total < (1L << 31));
+  hipLaunchKernelGGL(conv_pipe<MODE>, dim3((unsigned)total), dim3(256), 0, stream, a, grid_n, nsplit, (unsigned)total);
+  VC_CHECK_LAUNCH();
+  if (nsplit > 1) {
+    const long n = (long)a.M * a.N;
+    const int vec = (n % 4 == 0) && ((uintptr_t)ws % 16 == 0);
+    hipLaunchKernelGGL(conv_tap_reduce<MODE>, dim3(vc_cdiv(vec ? n / 4 : n, 256)), dim3(256), 0, stream, a, nsplit,
+                       vec);
+    VC_CHECK_LAUNCH();
+  }
+  return VC_OK;
+}
+
+// can the pipelined kernel take this conv: whole 16-B chunks everywhere (C, O and the leading dimensions
+// multiples of 4, 16-B aligned bases) and operands under 2 GB (32-bit buffer offsets); knob TAP_PIPE=0 keeps
+// conv_tap (probe library)
+bool conv_pipe_ok(int mode, const TapArgs& a, const void* p0, long ld0, const void* p1, long ld1) {
+  const long in_b = (long)a.nb * a.H * a.W * 4, out_b = (long)a.nb * a.OH * a.OW * 4;
+  return (vc_knob("VITCNN_TAP_PIPE", 1 << WGRAD) >> mode & 1) && a.C % 4 == 0 && a.O % 4 == 0 && ld0 % 4 == 0 && ld1 % 4 == 0 &&
+         ((uintptr_t)p0 % 16) == 0 && ((uintptr_t)p1 % 16) == 0 && in_b * std::max(ld0, ld1) < (1L << 31) &&
+         out_b * std::max(ld0, ld1) < (1L << 31) && (long)a.O * 9 * a.Cw * 4 < (1L << 31);
+}
+
 TapArgs geo(int B, int H, int W, int C, int O, int pad) {
   TapArgs a{};
+  a.nb = B;
   a.H = H; a.W = W; a.C = C; a.O = O; a.pad = pad;
   a.Cw = (C + 3) & ~3;
   a.OH = H + 2 * pad - 2; a.OW = W + 2 * pad - 2;
   a.fOW = make_fastdiv(a.OW); a.fOHW = make_fastdiv(a.OH * a.OW);
   a.fW = make_fastdiv(W); a.fHW = make_fastdiv(H * W);
-  (void)B;
   return a;
 }
 
@@ -479,6 +682,7 @@ VC_EXPORT int vc_conv3x3_tap_fwd(int B, int H, int W, int C, int O, int pad, con
   a.nk = 9 * a.tpt;
   a.x = x; a.ldx = ldx; a.w = wt; a.bias = bias; a.out = y; a.ldo = ldy;
   a.vx = vec_ok(x, ldx); a.vw = vec_ok(wt, a.Cw);
+  if (conv_pipe_ok(FWD, a, x, ldx, wt, 4)) return launch_conv_pipe<FWD>(a, vc_cdiv(O, CP_B), ws, ws_floats, stream);
   return launch_tap<FWD>(a, vc_cdiv(O, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
 }
 
@@ -499,6 +703,10 @@ static int tap_wgrad(int B, int H, int W, int C, int O, int pad, const float* x,
   a.dbias = db;
   if (db) a.N = 9 * C + 1;   // the split slabs' bias column
   a.vx = vec_ok(x, ldx); a.vdy = vec_ok(dy, lddy);
+  if (conv_pipe_ok(WGRAD, a, x, ldx, dy, lddy)) {
+    a.tpt = vc_cdiv(C, CP_B);   // n-tiles per tap
+    return launch_conv_pipe<WGRAD>(a, 9 * a.tpt, ws, ws_floats, stream);
+  }
   return launch_tap<WGRAD>(a, 9 * a.tpt, vc_cdiv(O, TM), ws, ws_floats, stream);
 }
 
@@ -528,5 +736,6 @@ VC_EXPORT int vc_conv3x3_tap_dgrad(int B, int H, int W, int C, int O, int pad, c
   a.nk = 9 * a.tpt;
   a.dy = dy; a.lddy = lddy; a.w = wt; a.out = dx; a.ldo = lddx; a.beta = beta;
   a.vdy = vec_ok(dy, lddy); a.vw = vec_ok(wt, a.Cw);
+  if (conv_pipe_ok(DGRAD, a, dy, lddy, wt, 4)) return launch_conv_pipe<DGRAD>(a, vc_cdiv(C, CP_B), ws, ws_floats, stream);
   return launch_tap<DGRAD>(a, vc_cdiv(C, TN), vc_cdiv(a.M, TM), ws, ws_floats, stream);
 }
