@@ -15,7 +15,7 @@ for _p in (_REPO, os.path.join(_REPO, "vit-cnn_amd")):
         sys.path.insert(0, _p)
 PROBE_PATH = os.path.join(_REPO, "vit-cnn_amd", "vitcnn_amd", "libvitcnn_probe.so")
 # the C ABI's kernel knobs (read by libvitcnn_probe.so only, common.h vc_knob)
-PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITCNN_BN_PCAP", "VITCNN_BN_IM2COL",
+PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITCNN_BN_PCAP", "VITCNN_BN_APPLY_ROWS", "VITCNN_BN_IM2COL",
                "VITCNN_BN_GLF", "VITCNN_SCAN_RBS", "VITCNN_SCAN_SELECT_RS", "VITCNN_SCAN_TAIL",
                "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE",
                "VITCNN_PIPE_NS", "VITCNN_BN_FUSED", "VITCNN_GEMM_GROUP_MAXB",

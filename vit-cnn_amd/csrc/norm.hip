@@ -642,6 +642,7 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
 // rows per partial block: at most 64 partials per 64-channel group (the fixed-order reduction reads
 // P/4 of them per thread), at least 32 rows each, fewer partials if the fp64 workspace is short
 constexpr int BN_APPLY_ROWS = 64;   // rows per block of the fused (partials-reducing) apply kernels
+int bn_apply_rows() { return (int)std::max(16L, vc_knob("VITCNN_BN_APPLY_ROWS", BN_APPLY_ROWS)); }   // knob: probe
 
 // the single-launch (group barrier) kernels: two zeroed counters per 64-channel group, and a grid small
 // enough that its blocks are resident together even beside a second barrier grid (256 CUs x 4 blocks of
@@ -977,7 +978,7 @@ VC_EXPORT int vc_bn_forward_ex(int train, long M, int C, const float* x, long ld
   hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
                      (unsigned int*)nullptr, eps, momentum, save_mean, save_invstd, run_mean, run_var);
   VC_CHECK_LAUNCH();
-  const int rpb = BN_APPLY_ROWS;
+  const int rpb = bn_apply_rows();
   hipLaunchKernelGGL(bn_apply_stats, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, (int)M, C, x, ldx,
                      P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy, rpb);
   VC_CHECK_LAUNCH();
@@ -1024,7 +1025,7 @@ static int bn_bwd_impl(int train, long M, int C, const float* dy, long lddy, con
                      rs, mean, invstd, rows_per, wsd, cnt, sums, dw, db, beta_w);
   VC_CHECK_LAUNCH();
   if (!cnt && dx) {   // the channel-tiled apply reduces the partials itself: one launch fewer
-    const int rpb = BN_APPLY_ROWS;
+    const int rpb = bn_apply_rows();
     hipLaunchKernelGGL(bn_bwd_apply_sums, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, train,
                        (int)M, C, dy, lddy, x, ldx, rs, mean, invstd, w, P, wsd, dx, lddx, beta_dx, dw,
                        db, beta_w, rpb);
