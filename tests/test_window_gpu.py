@@ -124,25 +124,60 @@ def test_test_whole_image_matches_reference_loop():
 
 
 def test_train_and_val_over_device_batches(tmp_path, monkeypatch):
-    """One epoch of model_utils.train over PatchBatcher batches (flip augmentation on), then val."""
+    """model_utils.train over PatchBatcher batches (flip augmentation on) on a learnable synthetic scene
+    (4 classes in spatial blocks, class-dependent spectra + noise; label 0 ignored): the optimizer moves
+    the parameters, the training loss falls, val() equals an independent count over the same batches,
+    and the trained model separates the classes well above chance (0.25)."""
     _need_gpu()
     from vitcnn_amd import model_utils as mu
     from vitcnn_amd.window import PatchBatcher
     monkeypatch.chdir(tmp_path)
     rng = np.random.default_rng(1)
     W, H = 40, 36
-    img1 = rng.random((W, H, 144), dtype=np.float32)
-    img2 = rng.random((W, H, 1), dtype=np.float32)
-    gt = rng.integers(0, 16, size=(W, H))
-    model, opt, crit, hp = mu.get_model("Multimodality_Mamba", n_classes=16, n_bands=(144, 1), ignored_labels=[0],
+    gt = np.zeros((W, H), dtype=np.int64)
+    gt[:20, :18], gt[20:, :18], gt[:20, 18:], gt[20:, 18:] = 1, 2, 3, 4
+    gt[::7, ::5] = 0                                               # scattered ignored pixels
+    mean1 = rng.random((5, 144), dtype=np.float32)
+    img1 = (mean1[gt] + 0.3 * rng.standard_normal((W, H, 144))).astype(np.float32)
+    img2 = (gt[..., None] / 4.0 + 0.3 * rng.standard_normal((W, H, 1))).astype(np.float32)
+    model, opt, crit, hp = mu.get_model("Multimodality_Mamba", n_classes=5, n_bands=(144, 1), ignored_labels=[0],
                                         dataset="synthetic", device=torch.device(DEV))
+    p0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
     loader = PatchBatcher(img1, img2, gt, 9, ignored_labels=[0], batch_size=64, flip_augmentation=True, device=DEV)
-    best = mu.train("t", 0, None, model, opt, crit, loader, 1, scheduler=hp["scheduler"], display_iter=0,
+    val_loader = PatchBatcher(img1, img2, gt, 9, ignored_labels=[0], batch_size=64, device=DEV)
+
+    def mean_loss():
+        tot, n = 0.0, 0
+        with torch.no_grad():
+            for d1, d2, t in val_loader:
+                tot += float(crit(model(d1, d2), t)) * t.numel()
+                n += t.numel()
+        return tot / n
+
+    loss0 = mean_loss()
+    best = mu.train("t", 0, None, model, opt, crit, loader, 3, scheduler=hp["scheduler"], display_iter=0,
                     device=torch.device(DEV))
     assert best is not None and set(best.keys()) == set(model.state_dict().keys())
-    acc = mu.val(model, loader, device=DEV)
-    assert 0.0 <= acc <= 1.0
-    assert all(np.isfinite(v.float().cpu().numpy()).all() for v in model.state_dict().values())
+    sd = model.state_dict()
+    assert all(torch.isfinite(v.float()).all() for v in sd.values())
+    moved = [k for k, v in sd.items() if v.is_floating_point() and not torch.equal(v, p0[k])]
+    # ~1020 trained tensors; the rest of the 1470 floating-point entries belong to modules of the reference's
+    # parameter tree that its forward never calls (kept for the state_dict) or are unused running stats
+    assert len(moved) >= 1000, len(moved)
+    assert any(k.startswith("hsi1.global_view.layers.0.") for k in moved)
+    loss1 = mean_loss()
+    assert loss1 < 0.7 * loss0, (loss0, loss1)
+    acc = mu.val(model, val_loader, device=DEV)
+    correct = counted = 0
+    with torch.no_grad():
+        for d1, d2, t in val_loader:
+            pred = model(d1, d2).argmax(dim=1).cpu().numpy()
+            t = t.cpu().numpy()
+            keep = pred != 0
+            correct += int(((pred == t) & keep).sum())
+            counted += int(keep.sum())
+    assert acc == correct / counted
+    assert acc > 0.6, acc
 
 
 def test_test_whole_image_production_batch_matches_reference_loop():

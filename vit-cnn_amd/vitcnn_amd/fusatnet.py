@@ -6,16 +6,20 @@ Forward (train-mode BatchNorm with running-stat updates, or eval-mode) is a prog
 over channels-last [B, H, W, C] rows: every 3x3 conv is the tap-major implicit GEMM
 `vc_conv3x3_tap_fwd` (conv_tap.hip: operand rows gathered from the channels-last map as float4 runs,
 k = tap * C + c, weights repacked tap-major once per step by `vc_conv3x3_pack`, bias fused; no im2col
-matrix), BatchNorm `vc_bn_stats` + `vc_bn_apply` (ReLU fused), residual adds `vc_add2_2d`, pools
+matrix; all tap-major packs in one `vc_conv3x3_pack_many` launch per step), train-mode BatchNorm + ReLU
+`vc_bn_forward_ex` (partial statistics + a fused final/apply launch), residual adds `vc_add2_2d`, pools
 `vc_maxpool2_fwd` / `vc_pool_scale`, products `vc_mul2_2d`, the concatenation is written in place.
 (The module constant `_TAP_CONV = False` restores the rounds 1-2 formulation, `vc_im2col3x3_pad` +
 `vc_gemm`, for measurements.)
 
 Backward: the reference's own autograd raises (the in-place `x += identity` on a saved ReLU output,
 :44, :61).  This path defines the out-of-place semantics (`b = relu(bn2(conv2(a)))
-+ a`) and runs a hand-written backward over a tape of the forward's ops (conv: `vc_conv3x3_tap_wgrad`
-with the bias gradient, `vc_conv3x3_tap_dgrad` over the tap-major weights; `vc_bn_bwd` with the ReLU
-mask; maxpool, pooled-scale and product backwards); the parameter gradients land in one flat gradient
++ a`) and runs a hand-written backward over a tape of the forward's ops (conv: `vc_conv3x3_tap_wgrad_oihw`,
+the weight gradient stored in the torch layout with the bias gradient fused, through the LDS-DMA
+pipelined `conv_pipe` where C and O are multiples of 4; `vc_conv3x3_tap_dgrad` over the tap-major
+weights; `vc_bn_bwd_relu_ex`, the ReLU decisions recomputed from the BN input and affine; maxpool,
+pooled-scale and product backwards; every gradient buffer written by its first writer with beta 0 instead
+of zero-filled); the parameter gradients land in one flat gradient
 (`flat_params.grad`) for the fused Adam (vitcnn_amd.optim.AdamW, weight_decay 0).
 """
 from __future__ import annotations
