@@ -199,12 +199,12 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
                                                 const float* __restrict__ out, const float* __restrict__ dout,
                                                 const float* __restrict__ lse, float scale,
                                                 float* __restrict__ dqkv) {
-  extern __shared__ f32x4 lds4[];  // 4 * T * 64 B + 2 * T * 4 B (37.9 KB at T = 146)
-  f32x4* Qs = lds4;
-  f32x4* Ks = lds4 + T * 4;
-  f32x4* Vs = lds4 + 2 * T * 4;
-  f32x4* dOs = lds4 + 3 * T * 4;
-  float* Ls = (float*)(lds4 + 4 * T * 4);
+  extern __shared__ f32x4 lds4[];  // 2 * T * 64 B + 2 * T * 4 B (19.8 KB at T = 146)
+  f32x4* Ks = lds4;                // pass 1
+  f32x4* Vs = lds4 + T * 4;
+  f32x4* Qs = lds4;                // pass 2 (the same bytes)
+  f32x4* dOs = lds4 + T * 4;
+  float* Ls = (float*)(lds4 + 2 * T * 4);
   float* Ds = Ls + T;
   const float* Qf = (const float*)Qs;
   const float* Kf = (const float*)Ks;
@@ -212,23 +212,36 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int ld = 3 * H * 16, ldo = H * 16;
   const float* base = qkv + (long)b * T * ld;
-  for (int i = threadIdx.x; i < T * 4; i += blockDim.x) {
-    const int t = i >> 2, q4 = i & 3;
-    Qs[i] = *(const f32x4*)(base + (long)t * ld + h * 16 + q4 * 4);
-    Ks[i] = *(const f32x4*)(base + (long)t * ld + H * 16 + h * 16 + q4 * 4);
-    Vs[i] = *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4);
-    dOs[i] = *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4);
-  }
-  // rowsum(dO * O): 16 lanes per row, coalesced
-  for (int i0 = 0; i0 < T * 16; i0 += blockDim.x) {
-    const int idx = i0 + threadIdx.x;
-    const int r = idx >> 4, d = idx & 15;
-    float v = 0.f;
-    if (idx < T * 16) v = out[((long)b * T + r) * ldo + h * 16 + d] * dout[((long)b * T + r) * ldo + h * 16 + d];
-    v = group16_sum(v);
-    if (d == 0 && idx < T * 16) {
-      Ds[r] = v;
-      Ls[r] = lse[((long)b * H + h) * T + r] * ATT_LOG2E;   // base-2 lse
+  // the operands the pass walks staged (pass 1: K, V; pass 2: Q, dO; each pass reads its own 16 rows of
+  // the other two straight from global memory) with rowsum(dO * O) in the same loop: 4 lanes per row (one
+  // float4 of each array), every load of a lane issued before its first use; the row's four dot products
+  // summed across the lanes (xor 1, xor 2)
+  const bool p1 = blockIdx.y == 0;
+  for (int i0 = 0; i0 < T * 4; i0 += blockDim.x) {   // uniform trip count: the shuffles see whole rows
+    const int i = i0 + threadIdx.x;
+    const bool ok = i < T * 4;
+    const int t = ok ? i >> 2 : 0, q4 = i & 3;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 av = ok ? *(const f32x4*)(base + (long)t * ld + (p1 ? H * 16 : 0) + h * 16 + q4 * 4) : z;
+    const f32x4 vv = (ok && p1) ? *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4) : z;
+    const f32x4 gv = ok ? *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4) : z;
+    const f32x4 ov = ok ? *(const f32x4*)(out + ((long)b * T + t) * ldo + h * 16 + q4 * 4) : z;
+    const float lt = (ok && q4 == 0) ? lse[((long)b * H + h) * T + t] : 0.f;
+    if (ok) {
+      if (p1) {
+        Ks[i] = av;
+        Vs[i] = vv;
+      } else {
+        Qs[i] = av;
+        dOs[i] = gv;
+      }
+    }
+    float v = ((ov.x * gv.x + ov.y * gv.y) + ov.z * gv.z) + ov.w * gv.w;
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if (ok && q4 == 0) {
+      Ds[t] = v;
+      Ls[t] = lt * ATT_LOG2E;   // base-2 lse
     }
   }
   __syncthreads();
@@ -238,7 +251,8 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   const int c = lane & 15, g = lane >> 4;
   const int ri = min(r0 + c, T - 1);
   if (blockIdx.y == 0) {  // pass 1: dq of queries r0 .. r0 + 15 (query c of this lane)
-    const f32x4 qv = Qs[ri * 4 + g], gv = dOs[ri * 4 + g];
+    const f32x4 qv = *(const f32x4*)(base + (long)ri * ld + h * 16 + g * 4);
+    const f32x4 gv = *(const f32x4*)(dout + ((long)b * T + ri) * ldo + h * 16 + g * 4);
     const float scale2 = scale * ATT_LOG2E;
     const float lq = Ls[ri], dq_ = Ds[ri];
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;  // dQ^T[d = 4g + r][q = c], even / odd tiles
@@ -268,7 +282,8 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
     if (k0 < T) tile(k0, acc0);
     if (r0 + c < T) *(f32x4*)(dqkv + ((long)b * T + r0 + c) * ld + h * 16 + g * 4) = (acc0 + acc1) * scale;
   } else {  // pass 2: dk, dv of keys r0 .. r0 + 15 (key c of this lane)
-    const f32x4 kv = Ks[ri * 4 + g], vv = Vs[ri * 4 + g];
+    const f32x4 kv = *(const f32x4*)(base + (long)ri * ld + H * 16 + h * 16 + g * 4);
+    const f32x4 vv = *(const f32x4*)(base + (long)ri * ld + 2 * H * 16 + h * 16 + g * 4);
     const float scale2 = scale * ATT_LOG2E;
     // dK^T / dV^T [d = 4g + r][key = c], even / odd query tiles
     f32x4 adk0 = {0.f, 0.f, 0.f, 0.f}, adk1 = adk0, adv0 = adk0, adv1 = adk0;
@@ -451,7 +466,7 @@ VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale,
 VC_API int vc_s2eft_attn_bwd(int B, int T, int H, const float* qkv, const float* out, const float* dout,
                              const float* lse, float scale, float* dqkv, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_bwd, dim3(B * H, 2), dim3(64 * ((T + 15) / 16)), 4 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
+  hipLaunchKernelGGL(attn_bwd, dim3(B * H, 2), dim3(64 * ((T + 15) / 16)), 2 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
                      dout, lse, scale, dqkv);
   VC_CHECK_LAUNCH();
   return VC_OK;
