@@ -75,9 +75,10 @@ VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
  * gradients, parallel branches).  `group` is caller-owned host memory of VC_GEMM_GROUP_BYTES bytes
  * (8-byte aligned) holding the group's state -- the library keeps none, so distinct groups (one per
  * stream / thread) are independent and every entry point stays reentrant.  vc_gemm_group_begin
- * opens it for `stream`; vc_gemm_group_add takes vc_gemm_ex's arguments (minus the stream): the fp32
- * problems of the k-major and of the pipelined kernel are recorded, anything else (bf16 operands,
- * long K) launches at once on the group's stream; vc_gemm_group_end launches the recorded problems as
+ * opens it for `stream`; vc_gemm_group_add takes vc_gemm_ex's arguments (minus the stream): fp32
+ * problems of the k-major kernel and fp32 / bf16 problems of the pipelined 64x64 kernel are recorded;
+ * anything else (bf16 problems on the legacy tiles, long K) launches at once on the group's stream;
+ * vc_gemm_group_end launches the recorded problems as
  * one grid per kernel (up to 8 problems each) plus one grouped split-K reduce.  A problem's plan
  * depends on its shape and the workspace / counters passed to it only, so its result is bit-identical
  * grouped or alone.  The problems must not depend on each other; each takes its own
@@ -141,12 +142,11 @@ VC_API int vc_bn_bwd(int train, long M, int C, const float* dy, long lddy, const
                      const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
                      float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w,
                      float* ws, long ws_floats, hipStream_t stream);
-/* The same with zeroed arrival counters (left zero; per stream, as vc_gemm_ex's).  With >= 2*ceil(C/64)
- * of them vc_bn_forward_ex (train) and vc_bn_bwd_ex (train, dx given) run as ONE launch: the partial
- * blocks of each 64-channel group meet at a group barrier, reduce the partials and apply in place
- * (grids up to 1024 blocks; larger ones take the two-launch path) -- bit-identical to the two-launch
- * kernels.  Otherwise vc_bn_stats_ex and vc_bn_bwd_ex without dx (>= ceil(C/64) counters) reduce per
- * channel in the last-arriving partial block, one launch fewer than without counters. */
+/* The same with zeroed arrival counters (left zero; per stream, as vc_gemm_ex's).  vc_bn_stats_ex and
+ * vc_bn_bwd_ex without dx (>= ceil(C/64) counters) reduce per channel in the last-arriving partial block,
+ * one launch fewer than without counters; vc_bn_forward_ex and vc_bn_bwd_ex with dx ignore them (the
+ * channel-tiled apply reduces the partials itself: two launches).  Results are bit-identical with and
+ * without counters. */
 VC_API int vc_bn_forward_ex(int train, long M, int C, const float* x, long ldx, float eps, float momentum,
                             float* save_mean, float* save_invstd, float* run_mean, float* run_var, const float* w,
                             const float* b, int relu, float* y, long ldy, float* ws, long ws_floats,

@@ -35,6 +35,21 @@ def test_c_abi_library_exports_every_declared_symbol():
     assert set(_lib.parse_header().keys()) == declared
 
 
+def test_product_loader_ignores_the_environment():
+    """no environment variable can point the product path at another build (the probe
+    library's VITCNN_* knobs change results); only a tool's explicit use_library_for_tools call can."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from vitcnn_amd import _lib; "
+            "L = _lib.lib(); print(L.path)") % os.path.join(REPO, "vit-cnn_amd")
+    probe = os.path.join(REPO, "vit-cnn_amd", "vitcnn_amd", "libvitcnn_probe.so")
+    env = dict(os.environ, VITCNN_LIB=probe, VITCNN_BN_FUSED="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert os.path.basename(out.strip()) == "libvitcnn_hip.so"
+    from vitcnn_amd import _lib
+    assert "os.environ" not in open(_lib.__file__).read()
+
+
 def test_c_abi_rejects_bad_shapes_without_a_gpu():
     from vitcnn_amd._lib import lib
     L = lib()

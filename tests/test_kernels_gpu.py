@@ -667,31 +667,30 @@ def test_bn_glf_combine_matches_stats_then_combine(L, M, C):
         assert torch.equal(a_, b_)
 
 
-@pytest.mark.parametrize("M,C,relu", [(3136, 256, 1), (3136, 512, 1), (5184, 144, 0), (37, 200, 1), (7744, 64, 1)])
-def test_bn_one_launch_barrier_is_bit_identical(L, probe, ws, M, C, relu, monkeypatch):
-    """The one-launch BatchNorm forward / backward (probe library, VITCNN_BN_FUSED=1: partial blocks meet at
-    a per-channel-group barrier; off in the product, measured slower) == the product's two launches, bit for
-    bit, twice in a row with the counters left zero"""
-    monkeypatch.setenv("VITCNN_BN_FUSED", "1")
+@pytest.mark.parametrize("M,C,relu", [(3136, 256, 1), (5184, 144, 0), (37, 200, 1)])
+def test_bn_ex_counters_do_not_change_results(L, ws, M, C, relu):
+    """vc_bn_forward_ex / vc_bn_bwd_ex with arrival counters == without, bit for bit, and the counters are
+    left zero (round 5: the one-launch spin-barrier forms are gone; the counters select
+    only the backward-without-dx last-arriver reduction)"""
     x = (rnd(M, C, seed=81, scale=2.0) + 3.0).to(DEV)
     w, b = (rnd(C, seed=82) + 1.0).to(DEV), rnd(C, seed=83).to(DEV)
     dy = rnd(M, C, seed=84).to(DEV)
     cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
     outs = []
-    for lib_, reps in ((L, 1), (probe, 2)):
-        for _ in range(reps):
-            rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
-            mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
-            y = torch.full((M, C), float("nan"), device=DEV)
-            dx = torch.full((M, C), 0.5, device=DEV)
-            dw, db = torch.full((C,), 2.0, device=DEV), torch.full((C,), 3.0, device=DEV)
-            lib_.vc_bn_forward_ex(1, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(w), P(b), relu, P(y), C,
-                                  P(ws), ws.numel(), P(cnt), cnt.numel(), S())
-            lib_.vc_bn_bwd_ex(1, M, C, P(dy), C, P(x), C, P(y) if relu else None, C, P(mean), P(inv), P(w), P(dx), C,
-                              1.0, P(dw), P(db), 0.5, P(ws), ws.numel(), P(cnt), cnt.numel(), S())
-            torch.cuda.synchronize()
-            outs.append([t.cpu() for t in (y, mean, inv, rm, rv, dx, dw, db)])
-            assert int(cnt.abs().sum()) == 0
+    for c_ in (None, cnt, cnt):
+        cp, cn = (P(c_), c_.numel()) if c_ is not None else (None, 0)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        y = torch.full((M, C), float("nan"), device=DEV)
+        dx = torch.full((M, C), 0.5, device=DEV)
+        dw, db = torch.full((C,), 2.0, device=DEV), torch.full((C,), 3.0, device=DEV)
+        L.vc_bn_forward_ex(1, M, C, P(x), C, 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(w), P(b), relu, P(y), C,
+                           P(ws), ws.numel(), cp, cn, S())
+        L.vc_bn_bwd_ex(1, M, C, P(dy), C, P(x), C, P(y) if relu else None, C, P(mean), P(inv), P(w), P(dx), C,
+                       1.0, P(dw), P(db), 0.5, P(ws), ws.numel(), cp, cn, S())
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (y, mean, inv, rm, rv, dx, dw, db)])
+        assert int(cnt.abs().sum()) == 0
     for o in outs[1:]:
         for a_, b_ in zip(outs[0], o):
             assert torch.equal(a_, b_)

@@ -237,6 +237,12 @@ def _sampler_worker(rank, world, port, out):
         got = [b[0][:, 0, 0, 0].long().tolist() for b in sh]
         epochs.append((got, sorted(ds.seen), len(sh)))
     out[rank] = epochs
+    # the ranks' global torch RNG stays in step through a sharded pass (only rank 0 draws the order,
+    # from a dedicated generator; every rank consumes the same one draw for its seed)
+    torch.manual_seed(5)
+    for _ in sh:
+        pass
+    out[100 + rank] = float(torch.rand(1))
     dist.destroy_process_group()
 
 
@@ -260,6 +266,68 @@ def test_sharded_loader_samples_at_the_sampler():
             assert out[r][e][1] == mine, r                       # nothing else was assembled on this rank
     # a new permutation each pass (the loader's RandomSampler on rank 0)
     assert [out[0][0][0]] != [out[0][1][0]]
+    assert len({out[100 + r] for r in range(world)}) == 1
+
+
+def test_sharded_loader_sampler_mode_needs_a_group():
+    """without a process group each 'rank' would draw its own permutation -- refused"""
+    from vitcnn_amd import parallel
+    loader = torch.utils.data.DataLoader(_CountingDS(10), batch_size=4, shuffle=True)
+    with pytest.raises(RuntimeError, match="process group"):
+        list(parallel.ShardedLoader(loader, 0, 2))
+    got = [b[0][:, 0, 0, 0].long().tolist() for b in parallel.ShardedLoader(loader, 0, 1)]
+    assert sorted(i for b in got for i in b) == list(range(10))
+
+
+def test_sharded_loader_streams_plain_iterables():
+    """ADVICE r4: an iterable without len-indexing is streamed -- each owned batch is yielded as it arrives;
+    only the wrap-around padding batches (the first `world` of the pass) are buffered"""
+    from vitcnn_amd import parallel
+
+    class _Stream:
+        def __init__(self, n):
+            self.n, self.log = n, []
+
+        def __len__(self):
+            return self.n
+
+        def __iter__(self):
+            for b in range(self.n):
+                self.log.append(("make", b))
+                yield b
+
+    for n, world in ((7, 3), (6, 3), (1, 2), (5, 2)):
+        for r in range(world):
+            st = _Stream(n)
+            sh = parallel.ShardedLoader(st, r, world)
+            assert sh.mode == "iterate"
+            out = []
+            for b in sh:
+                st.log.append(("use", b))
+                out.append(b)
+            assert out == parallel.rank_batches(n, r, world)
+            # owned batches are used right after they are made (streamed), not after the whole pass
+            for b in range(r, n, world):
+                i = st.log.index(("make", b))
+                assert st.log[i + 1] == ("use", b)
+
+
+def test_check_loader_shard_lets_world1_loaders_through(monkeypatch):
+    """a world-1 PatchBatcher under a process group is not a self-sharding loader; train() wraps it"""
+    from vitcnn_amd import parallel
+    monkeypatch.setattr(parallel, "is_distributed", lambda: True)
+    monkeypatch.setattr(parallel, "world", lambda: 2)
+    monkeypatch.setattr(parallel, "rank", lambda: 1)
+
+    class _PB1:
+        rank, world, seed = 0, 1, 3
+    parallel.check_loader_shard(_PB1())
+    assert not parallel.is_sharded(_PB1())
+
+    class _PBbad:
+        rank, world, seed = 0, 2, 3
+    with pytest.raises(RuntimeError, match="does not match"):
+        parallel.check_loader_shard(_PBbad())
 
 
 def test_patch_batcher_shards_are_equal_and_disjoint():

@@ -18,17 +18,19 @@ PROBE_PATH = os.path.join(_REPO, "vit-cnn_amd", "vitcnn_amd", "libvitcnn_probe.s
 PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITCNN_BN_PCAP", "VITCNN_BN_APPLY_ROWS", "VITCNN_BN_IM2COL",
                "VITCNN_BN_GLF", "VITCNN_SCAN_RBS", "VITCNN_SCAN_SELECT_RS", "VITCNN_SCAN_TAIL",
                "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE",
-               "VITCNN_PIPE_NS", "VITCNN_BN_FUSED", "VITCNN_GEMM_GROUP_MAXB",
+               "VITCNN_PIPE_NS", "VITCNN_GEMM_GROUP_MAXB",
                "VITCNN_TAP_TARGET", "VITCNN_TAP_PIPE", "VITCNN_CONV_PIPE_TILES_F", "VITCNN_CONV_PIPE_TILES_W",
                "VITCNN_CONV_PIPE_TILES_D")
 
 
 def use_probe():
-    """load libvitcnn_probe.so instead of the product library (call before the library is first used)"""
-    os.environ.setdefault("VITCNN_LIB", PROBE_PATH)
+    """bind lib() to libvitcnn_probe.so (call before the library is first used).  The product loader reads
+    no environment; this tool-side switch honours VITCNN_LIB (an A/B build, tools/ab_steps.sh) or the probe."""
+    from vitcnn_amd import _lib
+    _lib.use_library_for_tools(os.environ.get("VITCNN_LIB", PROBE_PATH))
 
 
-if any(k in os.environ for k in PROBE_KNOBS):
+if "VITCNN_LIB" in os.environ or any(k in os.environ for k in PROBE_KNOBS):
     use_probe()
 
 # env name -> (module, attribute, parser)

@@ -200,46 +200,6 @@ __device__ __forceinline__ bool block_last_arriver(unsigned int* cnt, unsigned n
   return last != 0;
 }
 
-// Barrier of the n blocks of one group of a launch (their arrival counter `arrive`, zero on entry):
-// every block publishes its stores (agent-scope release), arrives, and waits until all n have arrived
-// (acquire).  Only for grids whose blocks can all be resident at once (the host checks the grid size):
-// a waiting block holds its slot while the group's remaining blocks are placed as other work retires.
-// The wait is bounded (~1 s) so a broken launch ends instead of hanging the device.
-__device__ __forceinline__ void block_group_sync(unsigned int* arrive, unsigned n) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // polled with an atomic read-modify-write (+0, the zero opaque to the compiler, which would turn a
-    // literal +0 into a load): a load may be served by this XCD's L2, which other XCDs' arrivals do
-    // not update
-    unsigned zero;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-    for (int it = 0; it < (1 << 22); ++it) {
-      if (__hip_atomic_fetch_add(arrive, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) break;
-      __builtin_amdgcn_s_sleep(4);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-
-// After block_group_sync, once the block no longer needs the group's published data: the last of the
-// n blocks to leave (counter `depart`, zero on entry) re-zeroes both counters for the next launch --
-// every block has passed the wait by then.
-__device__ __forceinline__ void block_group_leave(unsigned int* arrive, unsigned int* depart, unsigned n) {
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(depart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == n - 1) {
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(depart, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
 

@@ -19,10 +19,6 @@ constexpr int NB = 8;       // rows (or partials) per lane whose loads a BatchNo
 #define VC_BN_RL 16
 #endif
 constexpr int BN_RL = VC_BN_RL, BN_T = 64 * BN_RL;
-// the one-launch (group barrier) kernels: 256-thread blocks, so a grid's blocks are co-resident (a
-// 1024-thread block holds a whole CU's wave slots at their register count: a 256-block barrier grid could
-// never finish beside other work); they compute the same 16 partial lanes (4 per thread), bit-identically
-constexpr int BNF_T = 256;
 
 __global__ __launch_bounds__(256) void ln_fwd(int R, int C, const float* __restrict__ x, long ldx,
                                               const float* __restrict__ w, const float* __restrict__ b, float eps,
@@ -377,33 +373,6 @@ __global__ __launch_bounds__(BN_T) void bn_stats_sums(int M, int C, const float*
   bn_stats_reduce(gridDim.y, C, M, x, part, blockIdx.x, eps, momentum, save_mean, save_invstd, run_mean, run_var);
 }
 
-// The whole train-mode forward in one launch: grid (ceil(C/64), P) partial blocks; the P blocks of a
-// channel group meet at a group barrier (cnt[2 * blockIdx.x], zeroed, left zero), then each reduces the
-// group's partials (bn_part_sums: the same order as bn_stats_final / bn_apply_stats) and applies the
-// normalisation to its own rows (re-read from L2).  Bit-identical to bn_stats_sums + bn_apply_stats.
-__global__ __launch_bounds__(BNF_T) void bn_forward_fused(int M, int C, const float* __restrict__ x, long ldx,
-                                                        int rows_per, double* __restrict__ part,
-                                                        unsigned int* __restrict__ cnt, float eps, float momentum,
-                                                        float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                                        float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                        const float* __restrict__ w, const float* __restrict__ b,
-                                                        int relu, float* __restrict__ y, long ldy) {
-  __shared__ double tot[2][64];
-  bn_stats_partial<BNF_T>(M, C, x, ldx, rows_per, part);
-  unsigned int* gc = cnt + 2 * blockIdx.x;
-  block_group_sync(gc, gridDim.y);
-  bn_part_sums<BNF_T>(gridDim.y, C, part, blockIdx.x, tot);
-  block_group_leave(gc, gc + 1, gridDim.y);
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  if (c >= C) return;
-  float mf, isf;
-  bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
-                     run_var, blockIdx.y == 0 && rl == 0);
-  const long r0 = (long)blockIdx.y * rows_per;
-  bn_apply_rows<BNF_T / 64>(x, ldx, mf, isf, w[c], b[c], relu, y, ldy, r0, min((long)M, r0 + rows_per), c, rl);
-}
-
 __global__ __launch_bounds__(BN_T) void bn_stats_final(int P, int C, long M, const float* __restrict__ x,
                                                       const double* __restrict__ part, float eps, float momentum,
                                                       float* __restrict__ save_mean, float* __restrict__ save_invstd,
@@ -584,36 +553,6 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_sums(int train, int M, int 
                     min((long)M, r0 + rows_per_block), c, rl);
 }
 
-// The whole train-mode backward in one launch: grid (ceil(C/64), P) partial blocks meet at their
-// channel group's barrier (cnt[2 * blockIdx.x], zeroed, left zero), reduce the partials in
-// bn_part_sums' order and write dx for their own rows (re-read from L2).  Bit-identical to
-// bn_bwd_sums + bn_bwd_apply_sums.
-__global__ __launch_bounds__(BNF_T) void bn_bwd_fused(int M, int C, const float* __restrict__ dy, long lddy,
-                                                    const float* __restrict__ x, long ldx, ReluSrc rs,
-                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                    const float* __restrict__ w, int rows_per,
-                                                    double* __restrict__ part, unsigned int* __restrict__ cnt,
-                                                    float* __restrict__ dx, long lddx, float beta_dx,
-                                                    float* __restrict__ dw, float* __restrict__ db, float beta_w) {
-  __shared__ double tot[2][64];
-  bn_bwd_partial<BNF_T>(M, C, dy, lddy, x, ldx, rs, mean, invstd, rows_per, part);
-  unsigned int* gc = cnt + 2 * blockIdx.x;
-  block_group_sync(gc, gridDim.y);
-  bn_part_sums<BNF_T>(gridDim.y, C, part, blockIdx.x, tot);
-  block_group_leave(gc, gc + 1, gridDim.y);
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  if (c >= C) return;
-  const double s1 = tot[0][cl], s2 = tot[1][cl];
-  if (blockIdx.y == 0 && rl == 0) {
-    if (dw) dw[c] = (beta_w != 0.f ? beta_w * dw[c] : 0.f) + (float)s2;
-    if (db) db[c] = (beta_w != 0.f ? beta_w * db[c] : 0.f) + (float)s1;
-  }
-  const long r0 = (long)blockIdx.y * rows_per;
-  bn_bwd_apply_rows<BNF_T / 64>(1, M, dy, lddy, x, ldx, rs, mean[c], invstd[c], w[c], s1, s2, dx, lddx, beta_dx, r0,
-                    min((long)M, r0 + rows_per), c, rl);
-}
-
 // train: dx = w*invstd*(dyv - s1/M - xhat*s2/M);  eval (sums == null): dx = w*invstd*dyv
 __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, long lddy, const float* __restrict__ x,
                              long ldx, ReluSrc rs, const float* __restrict__ mean,
@@ -644,18 +583,11 @@ __global__ void bn_bwd_apply(int M, FastDiv fC, const float* __restrict__ dy, lo
 constexpr int BN_APPLY_ROWS = 64;   // rows per block of the fused (partials-reducing) apply kernels
 int bn_apply_rows() { return (int)std::max(16L, vc_knob("VITCNN_BN_APPLY_ROWS", BN_APPLY_ROWS)); }   // knob: probe
 
-// the single-launch (group barrier) kernels: two zeroed counters per 64-channel group, and a grid small
-// enough that its blocks are resident together even beside a second barrier grid (256 CUs x 4 blocks of
-// BNF_T threads at ~33 KB of LDS: up to 1024 resident; tools/residency_lab.hip, profiles/r04_residency_lab*.log).
-// Measured slower than the two launches, so off in the product (knob VITCNN_BN_FUSED=1, probe library):
-// ViT-CNN step 1.815-1.825 -> 1.946-1.950 ms, FusAtNet 19.5 -> 20.7 ms (profiles/r04_ab_bn_fused.log) --
-// the barrier (one agent-scope release + acquire per block, i.e. an L2 writeback and invalidate, and 64
-// arrivals polled on one counter) costs ~10-20 us per launch, more than the launch and the re-read it saves.
-static bool bn_fused_fits(int C, int P, const unsigned int* counters, int n_counters) {
-  const long groups = vc_cdiv(C, 64);
-  return counters && n_counters >= 2 * groups && groups * P <= 512 && vc_knob("VITCNN_BN_FUSED", 0);
-}
-
+// The one-launch forms of round 4 (partial blocks meeting at a per-channel-group spin barrier) were
+// measured slower than the two launches (ViT-CNN 1.82 -> 1.95 ms, FusAtNet 19.5 -> 20.7 ms,
+// profiles/r04_ab_bn_fused.log) and a spin barrier without a co-residency guarantee can deadlock beside
+// other streams' work, so they were removed; counters now only select the
+// last-arriving-block reduction of a backward without dx.
 int bn_rows_per(long M, int C, long ws_doubles, long reserve_doubles) {
   // most partials per channel (knob BN_PCAP, probe library)
   const int pcap = (int)std::max(16L, std::min(1024L, vc_knob("VITCNN_BN_PCAP", 64)));
@@ -969,12 +901,8 @@ VC_EXPORT int vc_bn_forward_ex(int train, long M, int C, const float* x, long ld
   const int rows_per = bn_rows_per(M, C, ws_doubles, 0);
   const int P = vc_cdiv(M, rows_per);
   VC_REQUIRE((long)P * C * 2 <= ws_doubles && P <= 65535);
-  if (bn_fused_fits(C, P, counters, n_counters)) {   // one launch: group barrier
-    hipLaunchKernelGGL(bn_forward_fused, dim3(vc_cdiv(C, 64), P), dim3(BNF_T), 0, stream, (int)M, C, x, ldx, rows_per,
-                       wsd, counters, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy);
-    VC_CHECK_LAUNCH();
-    return VC_OK;
-  }
+  (void)counters;
+  (void)n_counters;
   hipLaunchKernelGGL(bn_stats_sums, dim3(vc_cdiv(C, 64), P), dim3(BN_T), 0, stream, (int)M, C, x, ldx, rows_per, wsd,
                      (unsigned int*)nullptr, eps, momentum, save_mean, save_invstd, run_mean, run_var);
   VC_CHECK_LAUNCH();
@@ -1012,12 +940,6 @@ static int bn_bwd_impl(int train, long M, int C, const float* dy, long lddy, con
   const int P = vc_cdiv(M, rows_per);
   VC_REQUIRE((long)P * C * 2 + 2L * C <= ws_doubles && P <= 65535);
   double* sums = wsd + (long)P * C * 2;
-  if (train && dx && bn_fused_fits(C, P, counters, n_counters)) {   // one launch: group barrier
-    hipLaunchKernelGGL(bn_bwd_fused, dim3(vc_cdiv(C, 64), P), dim3(BNF_T), 0, stream, (int)M, C, dy, lddy, x, ldx,
-                       rs, mean, invstd, w, rows_per, wsd, counters, dx, lddx, beta_dx, dw, db, beta_w);
-    VC_CHECK_LAUNCH();
-    return VC_OK;
-  }
   // tickets (the last-arriving partial block reduces) only without dx: with dx the channel-tiled apply
   // reduces the partials itself
   unsigned int* cnt = (!(train && dx) && counters && n_counters >= vc_cdiv(C, 64)) ? counters : nullptr;

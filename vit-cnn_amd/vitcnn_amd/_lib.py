@@ -11,7 +11,7 @@ import os
 import re
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libvitcnn_hip.so")   # the product library (VITCNN_LIB: a tool's override)
+LIB_PATH = os.path.join(_PKG, "libvitcnn_hip.so")   # the product library: the only one lib() ever loads
 _HEADER_CANDIDATES = [
     os.path.join(_PKG, "..", "..", "include", "vitcnn.h"),
     os.path.join(_PKG, "vitcnn.h"),
@@ -63,7 +63,7 @@ PROBE_PATH = os.path.join(_PKG, "libvitcnn_probe.so")
 
 class _Lib:
     def __init__(self, path=None):
-        path = path or os.environ.get("VITCNN_LIB", LIB_PATH)
+        path = path or LIB_PATH
         if not os.path.exists(path):
             raise RuntimeError(
                 f"HIP extension not built: {path} is missing (run `make -C vit-cnn_amd/csrc` "
@@ -108,9 +108,23 @@ _LIB = None
 
 
 def lib() -> _Lib:
+    """the product library, libvitcnn_hip.so next to this file.  No environment variable can point it
+    elsewhere: a tool that A/Bs another build calls `use_library_for_tools` first."""
     global _LIB
     if _LIB is None:
         _LIB = _Lib()
+    return _LIB
+
+
+def use_library_for_tools(path: str) -> _Lib:
+    """Measurement tools only (tools/knobs.py): bind `lib()` to another build of the same header -- the
+    probe library or an A/B build -- before the product path first loads.  Raises if the product library
+    is already bound, so a process never mixes two builds."""
+    global _LIB
+    if _LIB is not None and os.path.abspath(_LIB.path) != os.path.abspath(path):
+        raise RuntimeError(f"lib() already bound to {_LIB.path}; cannot switch to {path}")
+    if _LIB is None:
+        _LIB = _Lib(path)
     return _LIB
 
 
@@ -119,7 +133,7 @@ _PROBE = None
 
 def probe_lib() -> _Lib:
     """libvitcnn_probe.so (`make -C vit-cnn_amd/csrc probe`): the same sources built with -DVC_PROBE, whose
-    measurement knobs read VITCNN_* environment variables per call (tools/, and tests comparing two
+    measurement knobs read VITCNN_* variables per call (tools/, and tests comparing two
     bit-identical kernel forms in one process).  The product path never loads it."""
     global _PROBE
     if _PROBE is None:

@@ -344,7 +344,7 @@ class _Program:
         if self.train:
             self.nbt.append(bn.num_batches_tracked)   # incremented together at the end of run()
         z = self.new(*y.shape) if self.grad else y
-        # train: one launch where the grid allows (group barrier over the stream's zeroed counters)
+        # train: statistics partials + the channel-tiled apply that reduces them (two launches)
         self.L.vc_bn_forward_ex(1 if self.train else 0, M, C, y.data_ptr(), C, bn.eps,
                                 bn.momentum if bn.momentum is not None else BN_MOMENTUM, mean.data_ptr(),
                                 invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),

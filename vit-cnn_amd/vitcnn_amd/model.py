@@ -727,7 +727,7 @@ class _Program:
         tag, ws = seq + ".1", self.ws
         mean, inv = ws.f(tag + ".bm", Cout), ws.f(tag + ".bi", Cout)
         out = ws.f(seq + ".out", M * Cout)
-        # one launch (group barrier over the lane's zeroed counters), include/vitcnn.h vc_bn_forward_ex
+        # statistics partials + the channel-tiled apply that reduces them (two launches), include/vitcnn.h
         self.L.vc_bn_forward_ex(self.train, M, Cout, pre, Cout, BN_EPS, BN_MOM, mean, inv,
                                 self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"],
                                 self.P[tag + ".weight"], self.P[tag + ".bias"], 1, out, Cout, self.scr_p, self.scr_n,

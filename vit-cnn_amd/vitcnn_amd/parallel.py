@@ -349,28 +349,57 @@ class ShardedLoader:
 
     def _iter_sampler(self):
         ld = self.loader
+        if self.world > 1 and not is_distributed():
+            raise RuntimeError("ShardedLoader(mode='sampler') with world > 1 needs a process group: each rank would "
+                               "draw its own sample order and the shards would overlap")
+        # the order is drawn by rank 0's sampler from a dedicated generator (seeded from rank 0's torch RNG, the
+        # draw a single-process epoch makes), so the ranks' global RNG states stay in step: every rank consumes
+        # one draw for the seed, only rank 0 uses it
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())
         if is_distributed():
-            order = _broadcast_order(list(iter(ld.sampler)) if rank() == 0 else [], self.group)
+            order = _broadcast_order(self._draw_order(seed) if rank() == 0 else [], self.group)
         else:
-            order = list(iter(ld.sampler))
+            order = self._draw_order(seed)
         bs = ld.batch_size
         batches = [order[i:i + bs] for i in range(0, len(order), bs)]
         if ld.drop_last and batches and len(batches[-1]) < bs:
             batches.pop()
         mine = [batches[b] for b in rank_batches(len(batches), self.rank, self.world)]
-        sub = torch.utils.data.DataLoader(ld.dataset, batch_sampler=mine, num_workers=ld.num_workers,
-                                          collate_fn=ld.collate_fn, pin_memory=ld.pin_memory,
-                                          worker_init_fn=ld.worker_init_fn)
+        kw = dict(num_workers=ld.num_workers, collate_fn=ld.collate_fn, pin_memory=ld.pin_memory,
+                  worker_init_fn=ld.worker_init_fn, timeout=ld.timeout, generator=ld.generator,
+                  multiprocessing_context=ld.multiprocessing_context)
+        if ld.num_workers > 0:
+            kw.update(persistent_workers=ld.persistent_workers, prefetch_factor=ld.prefetch_factor)
+        sub = torch.utils.data.DataLoader(ld.dataset, batch_sampler=mine, **kw)
         yield from sub
 
+    def _draw_order(self, seed):
+        """the loader's sampler order; a RandomSampler without its own generator draws from a dedicated one"""
+        smp = self.loader.sampler
+        if isinstance(smp, torch.utils.data.RandomSampler) and smp.generator is None:
+            g = torch.Generator()
+            g.manual_seed(seed)
+            smp.generator = g
+            try:
+                return list(iter(smp))
+            finally:
+                smp.generator = None
+        return list(iter(smp))
+
     def _iter_discard(self):
-        want = rank_batches(len(self.loader), self.rank, self.world)
-        need = set(want)
+        """stream the pass: a batch this rank owns at its first position (b % world == rank, b < n) is yielded
+        as it arrives; only the wrap-around padding batches (positions j >= n repeat batch j % n, all among the
+        pass's first `world` batches) are kept until the pass ends"""
+        n = len(self.loader)
+        pad = [j % n for j in range(n, -(-n // self.world) * self.world) if j % self.world == self.rank] if n else []
+        need_pad = set(pad)
         kept = {}
         for b, item in enumerate(self.loader):
-            if b in need:
+            if b in need_pad:
                 kept[b] = item
-        for b in want:
+            if b % self.world == self.rank:
+                yield item
+        for b in pad:
             yield kept[b]
 
 
@@ -389,8 +418,8 @@ def check_loader_shard(loader, group=None):
     group: its rank and world are this process's, and every rank built it from the same seed (the
     shuffled order the shards are cut from is then the same permutation on every rank).  Raises
     RuntimeError otherwise -- nothing else would notice overlapping or missing shards."""
-    if not is_distributed() or getattr(loader, "world", None) is None:
-        return
+    if not is_distributed() or getattr(loader, "world", None) is None or int(loader.world) <= 1:
+        return   # a world-1 loader does not shard itself: train() wraps it in a ShardedLoader
     if int(loader.world) != world() or int(loader.rank) != rank():
         raise RuntimeError(f"loader shard (rank {loader.rank} of {loader.world}) does not match the process group "
                            f"(rank {rank()} of {world()})")
