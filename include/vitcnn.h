@@ -71,6 +71,16 @@ VC_API int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha, 
  * library keeps none and accepts only the automatic configuration (0, 0, 0, 0, -1). */
 VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
 
+/* Deferred split-K reduction: flags&128 (F_DEFER) -- the product's split-K slabs go to the caller's `ws` (a
+ * buffer of its own, from its start, left intact) and are NOT reduced; a later call with the same arguments
+ * and flags&256 (F_REDUCE_ONLY) launches only that reduction (inside a group: it joins the group's one
+ * grouped reduce).  Lets a chain keep a weight gradient's reduce off its critical stream.  A product that
+ * does not split, or whose kernel has no deferred form, ignores both bits (F_REDUCE_ONLY is then a no-op).
+ * vc_gemm_defer_floats: the slab floats an F_DEFER call of the product needs, given the capacity ws_floats
+ * it is planned with (0: nothing deferred). */
+VC_API int vc_gemm_defer_floats(int transA, int transB, int M, int N, int K, const float* A, long lda,
+                                const float* B, long ldb, int batch, int bias_grad, int flags, long ws_floats);
+
 /* Grouped launches: a horizontal fusion of independent products (a layer's weight and data
  * gradients, parallel branches).  `group` is caller-owned host memory of VC_GEMM_GROUP_BYTES bytes
  * (8-byte aligned) holding the group's state -- the library keeps none, so distinct groups (one per
@@ -359,24 +369,33 @@ VC_API int vc_rowchain_ln_params(int rows, int E, const float* ln_part, float* d
 VC_API int vc_rowchain_ln_part_floats(int rows, int E);
 
 /* ---------------------------------------------------------------- TokenLearner
- * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64).  params: S x 5 floats
- * [conv.0.weight(2), conv.0.bias, conv.1.weight, conv.1.bias]; bn_buffers: S x 2
- * [running_mean, running_var]; stats: S x 2 fp64 [mean, invstd] saved for the backward (the
- * per-token statistics and gradient sums accumulate in fp64, as torch's CPU BatchNorm does);
- * a: [B, S, HW] spatial weights.  The pooled tokens Z = a x / HW are a vc_gemm. */
-VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg,
+ * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64) over x [B*HW, C] channels-last
+ * (C % 4 == 0, ldx % 4 == 0, x / dZ 16-B aligned, S <= 128).  params: S x 5 floats [conv.0.weight(2),
+ * conv.0.bias, conv.1.weight, conv.1.bias]; bn_buffers: S x 2 [running_mean, running_var]; stats: 2 S + 8
+ * fp64 -- per token [mean, invstd] of its BN(1) input, then the shared moments of the pooled (max, mean)
+ * pair [n, mbar, vbar, Cmm, Cmv, Cvv, Km, Kv] -- kept for the backward (statistics and gradient sums in
+ * fp64, as torch's CPU BatchNorm accumulates); ws: vc_tl_ws_floats(B, HW, S) floats of per-call-site
+ * scratch (8-B aligned).  vc_tl_pixel_stats leaves the moment partials in ws for vc_tl_fwd. */
+VC_API int vc_tl_ws_floats(int B, int HW, int S);
+/* per pixel row of x [M, C] (C <= 512): channel max, its first argmax, channel mean; + moment partials */
+VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg, double* ws,
                              hipStream_t stream);
-VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          float* bn_buffers, float eps, float momentum, double* stats, float* a, hipStream_t stream);
-VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          const double* stats, const float* da, float* df, float* dparams, hipStream_t stream);
-/* mask [B, S, HW] uint8 = the ReLU decisions (BN(1) output > 0) attn_fwd / attn_bwd take, from the
+/* stats (train: batch statistics from the moments, running statistics updated; eval: the running ones),
+ * the attention maps a [B, S, HW] (optional, may be null) and the pooled tokens Z [B, S, C] =
+ * (1/HW) a x, in one launch */
+VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
+                     const float* avg, const float* params, float* bn_buffers, float eps, float momentum,
+                     const double* ws, double* stats, float* a, float* Z, hipStream_t stream);
+/* backward from dZ [B, S, C]: dx [B*HW, C] (ld lddx, overwritten) = (1/HW) a^T dZ + the pooled-path gradient
+ * (argmax channel and mean), dparams (S x 5, overwritten); da [B, S, HW] floats of scratch (the attention
+ * maps' gradient).  Two launches. */
+VC_API int vc_tl_bwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
+                     const float* avg, const int* amx, const float* params, const double* stats, const float* dZ,
+                     float* da, double* ws, float* dx, long lddx, float* dparams, hipStream_t stream);
+/* mask [B, S, HW] uint8 = the ReLU decisions (BN(1) output > 0) vc_tl_fwd / vc_tl_bwd take, from the
  * same stats (test instrumentation: the float64 parity yardstick follows the HIP path's fp32 ties) */
 VC_API int vc_tl_relu_mask(int B, int HW, int S, const float* mx, const float* avg, const float* params,
                            const double* stats, unsigned char* mask, hipStream_t stream);
-/* dx[i,:] += d(avg)/C, dx[i, argmax] += d(max), summed over the S tokens (accumulates) */
-VC_API int vc_tl_pixel_bwd(long M, int C, int S, const float* df, const float* params, const int* amx, float* dx,
-                           long lddx, hipStream_t stream);
 
 /* ---------------------------------------------------------------- non-local cross attention
  * NONLocalBlock2D core (Mutimodality_Mamba7.py:143-152): softmax(theta phi^T) g, no scaling.

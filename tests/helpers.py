@@ -82,6 +82,13 @@ def relu_masks_from_workspace(model, B):
     grab("lidar2", P - 4, 32)
     grab("fusion1.FusionLayer", P - 2, 128)
     grab("fusion2.FusionLayer", P - 4, 128)
+    # NonLocal 2x2 max-pool decisions of the phi | g maps (the winning tap of each window, [B, Pk, 2 Ci]):
+    # windows whose values tie to within fp32 rounding are decisions, like the ReLU ties above (DESIGN.md s. 6)
+    for blk, H, cout in (("hsi1", P, model.hsi1.cout), ("hsi2", P - 2, model.hsi2.cout)):
+        Hs, Ci = H - 2, cout // 2
+        Pk = (Hs // 2) ** 2
+        pa = ws.tensor(blk + ".PA")[: B * Pk * 2 * Ci].view(B, Pk, 2 * Ci).cpu().long()
+        masks[blk + ".FusionLayer.cross_attention.pool"] = pa
     return masks
 
 
@@ -105,7 +112,7 @@ def tl_pooled_from_workspace(model, B):
 
 def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None):
     """oracle train step in which the conv/fusion ReLUs use the given masks (pre * mask) instead of
-    their own sign test.  A pre-activation within rounding distance of zero is an fp32 tie that the
+    their own sign test, and the NonLocal 2x2 max pools the given winning taps (`<prefix>.pool` entries).  A pre-activation within rounding distance of zero is an fp32 tie that the
     HIP path and the CPU reference may resolve differently; evaluating the float64 yardstick with the
     HIP path's decisions keeps such a tie from being scored as a gradient error.
 
@@ -114,8 +121,31 @@ def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None)
     mean, so the fp32 rounding of the pooled values is amplified by 1/std.  The yardstick then takes
     the HIP path's pooled VALUES (gradients still flow to the argmax channel and to every channel
     through the mean, exactly as in the reference)."""
-    orig = (O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner)
+    orig = (O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner, O.non_local)
     F = torch.nn.functional
+
+    def pool_taps(pre, taps):
+        """2x2 / stride-2 max pool of pre [B, C, H, W] with the given winning taps [B, Pk, C] (t = 2 dh + dw)"""
+        b, c, h, w = pre.shape
+        ph, pw = h // 2, w // 2
+        win = pre[:, :, :2 * ph, :2 * pw].reshape(b, c, ph, 2, pw, 2).permute(0, 1, 2, 4, 3, 5).reshape(b, c, ph, pw, 4)
+        idx = taps.transpose(1, 2).reshape(b, c, ph, pw, 1)
+        return torch.gather(win, 4, idx)[..., 0]
+
+    def non_local(P, pfx, x, y, z):   # oracle non_local (:140-159) with the HIP path's max-pool decisions
+        key = pfx + ".pool"
+        if key not in masks:
+            return orig[3](P, pfx, x, y, z)
+        b = x.shape[0]
+        taps = masks[key]
+        ci = taps.shape[2] // 2
+        theta = O.conv2d(P, pfx + ".theta", x).flatten(2).transpose(1, 2)
+        phi = pool_taps(O.conv2d(P, pfx + ".phi.0", y), taps[:, :, :ci]).flatten(2)
+        att = torch.softmax(theta @ phi, dim=-1)
+        g = pool_taps(O.conv2d(P, pfx + ".g.0", z), taps[:, :, ci:]).flatten(2).transpose(1, 2)
+        o = (att @ g).transpose(1, 2).reshape(b, -1, *x.shape[2:])
+        wy = O.batchnorm(P, pfx + ".W.1", O.conv2d(P, pfx + ".W.0", o))
+        return wy + z
 
     def bn_conv3(P, pfx, x):
         pre = O.conv2d(P, pfx + ".conv", O.batchnorm(P, pfx + ".bn", x))
@@ -145,8 +175,8 @@ def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None)
             toks.append((x * a).mean(dim=(-2, -1)))
         return torch.stack(toks, dim=1)
 
-    O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner = bn_conv3, conv1x1, token_learner
+    O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner, O.non_local = bn_conv3, conv1x1, token_learner, non_local
     try:
         return O.train_step(state, hsi, lidar, target, weight)
     finally:
-        O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner = orig
+        O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner, O.non_local = orig

@@ -148,15 +148,10 @@ def test_train_world2_hip_ranks(tmp_path):
                 if g is None:
                     continue
                 dst[k] = dst.get(k, 0) + g.double() / WORLD
-    # Every tensor element-wise (test_gradients_b4's criterion), except the TokenLearner BN(1) tokenizers:
-    # BN(1) normalises a 2->1 conv of the channel max / mean whose spread over a B=4 batch can be a tiny
-    # fraction of its mean, so the backward multiplies the fp32 rounding of the upstream gradient by
-    # 1/std; on this scene a few tokenizers' tiny gradients land outside the
-    # element-wise bound while the CPU reference (whose BN backward accumulates in double) does not.
-    # Those are held to test_b64_against_reference_golden's per-tensor norm criterion instead.
+    # Every tensor element-wise (test_gradients_b4's criterion), the TokenLearner tokenizers included (VERDICT r4
+    # item 1: round 4 held them to a norm only; the cause of their divergence is in DESIGN.md section 6)
     gmax = max(float(g.abs().max()) for g in ref64.values())
     floor = 1e-5 * gmax
-    nmax = max(float(g.norm()) for g in ref32.values())
     bad = []
     for n, off in r0["poff"].items():
         shape = r0["shapes"][n]
@@ -164,11 +159,6 @@ def test_train_world2_hip_ranks(tmp_path):
         got = got_mean[off:off + numel].view(shape)
         if n not in ref64:
             assert float(got.abs().max()) == 0.0, n
-            continue
-        if ".tokenizers." in n:
-            gn, rn = float(got.norm()), float(ref32[n].norm())
-            if not abs(gn - rn) <= 2e-3 * rn + 5e-5 * nmax:
-                bad.append((n, "norm", gn, rn))
             continue
         err = float((got - ref64[n]).abs().max())
         err32 = float((ref32[n] - ref64_own[n]).abs().max())

@@ -37,13 +37,45 @@ def scene():
 def oracle_run(sd, hsi, lidar, target, masks, pooled, dtype):
     """oracle step with TokenLearner intermediates retained; masks/pooled None = the oracle's own."""
     cap = {}
-    orig = (O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner)
+    orig = (O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner, O.layernorm, O.non_local)
+    orig_ln = O.layernorm
+
+    def non_local(P, pfx, x, y, z):   # NonLocal intermediates kept (NCHW / [B, HW, Ci] as the oracle has them)
+        b = x.shape[0]
+        theta = O.conv2d(P, pfx + ".theta", x)
+        theta.retain_grad()
+        th = theta.flatten(2).transpose(1, 2)
+        phi_pre = O.conv2d(P, pfx + ".phi.0", y)
+        phi_pre.retain_grad()
+        phi = F.max_pool2d(phi_pre, 2).flatten(2)
+        s_ = th @ phi
+        s_.retain_grad()
+        att = torch.softmax(s_, dim=-1)
+        g_pre = O.conv2d(P, pfx + ".g.0", z)
+        g_pre.retain_grad()
+        g = F.max_pool2d(g_pre, 2).flatten(2).transpose(1, 2)
+        o = (att @ g).transpose(1, 2).reshape(b, -1, *x.shape[2:])
+        o.retain_grad()
+        wy = O.batchnorm(P, pfx + ".W.1", O.conv2d(P, pfx + ".W.0", o))
+        cap[pfx] = dict(theta=theta, phi_pre=phi_pre, g_pre=g_pre, o=o, s=s_, att=att, sv=s_, gpv=g_pre, ppv=phi_pre)
+        return wy + z
+
+    def layernorm(P, pfx, x):   # ln3 / ln4: keep the LayerNorm's input and output gradients
+        y = orig_ln(P, pfx, x)
+        if pfx.endswith(".ln3") or pfx.endswith(".ln4"):
+            x.retain_grad()
+            y.retain_grad()
+            cap[pfx] = dict(x=x, y=y)
+        return y
 
     def bn_conv3(P, pfx, x):
         pre = O.conv2d(P, pfx + ".conv", O.batchnorm(P, pfx + ".bn", x))
         return pre * masks[pfx].to(pre.dtype) if masks and pfx in masks else torch.relu(pre)
 
     def conv1x1(P, pfx, x):
+        if pfx.endswith("FusionLayer.FusionLayer"):
+            x.retain_grad()
+            cap[pfx] = dict(cat=x)
         pre = O.batchnorm(P, pfx + ".1", O.conv2d(P, pfx + ".0", x))
         return pre * masks[pfx].to(pre.dtype) if masks and pfx in masks else torch.relu(pre)
 
@@ -71,16 +103,24 @@ def oracle_run(sd, hsi, lidar, target, masks, pooled, dtype):
         cap[pfx] = dict(Z=Z, f=fs, a=As, x=x)
         return Z
 
-    O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner = bn_conv3, conv1x1, token_learner
+    O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner, O.layernorm, O.non_local = (bn_conv3, conv1x1, token_learner,
+                                                                                      layernorm, non_local)
     try:
         sdd = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in sd.items()}
         st = O.make_state(sdd)
         w = O.ce_class_weights(16).to(dtype)
         O.train_step(st, hsi.to(dtype), lidar.to(dtype), target, w)
     finally:
-        O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner = orig
+        O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner, O.layernorm, O.non_local = orig
     out = {}
     for pfx, c in cap.items():
+        if "theta" in c or "cat" in c:
+            out[pfx] = {k: (v.grad.detach().double() if k not in ("att", "sv", "gpv", "ppv") else v.detach().double()) for k, v in c.items()}
+            continue
+        if "f" not in c:
+            out[pfx] = dict(lnx=c["x"].detach().double(), dlnx=c["x"].grad.detach().double(),
+                            dlny=c["y"].grad.detach().double())
+            continue
         S = len(c["f"])
         out[pfx] = dict(dZ=c["Z"].grad.detach().double(),                                  # [B,S,C]
                         da=torch.cat([a.grad for a in c["a"]], 1).detach().double(),       # [B,S,H,W]
@@ -141,6 +181,47 @@ def main():
         y32, g32 = oracle_run(sd, hsi, lidar, tt, None, None, torch.float32)
         o64, go64 = oracle_run(sd, hsi, lidar, tt, None, None, torch.float64)
         print(f"=== rank {rank} batch targets {tt.tolist()}")
+        for blk, H in (("hsi1", 9), ("hsi2", 7)):
+            Hs = H - 2
+            S = Hs * Hs
+            C = model.hsi1.cout if blk == "hsi1" else model.hsi2.cout
+            Ci = C // 2
+            M = B * S
+            nl = y64[blk + ".FusionLayer.cross_attention"]
+            cat = y64[blk + ".FusionLayer.FusionLayer"]["cat"]
+            cl = lambda t: t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])   # noqa: E731  NCHW -> rows x C
+            def rep(name, hip, ref):
+                e = (hip - ref).abs().max(1).values
+                w = int(torch.argmax(e))
+                print(f"   {blk} {name}: err {float(e.max()):.3e} (|ref| {float(ref.abs().max()):.3e}) worst row {w} "
+                      f"(b {w // S}, s {w % S})")
+            rep("dCAT1 local half", ws.tensor(blk + ".dCAT1")[:M * 2 * C].view(M, 2 * C)[:, :C].double().cpu(), cl(cat)[:, :C])
+            rep("dCAT1 global half", ws.tensor(blk + ".dCAT1")[:M * 2 * C].view(M, 2 * C)[:, C:].double().cpu(), cl(cat)[:, C:])
+            dpg = ws.tensor(blk + ".dPG")[:M * 2 * Ci].view(M, 2 * Ci).double().cpu()
+            rep("dphi (pre-pool)", dpg[:, :Ci], cl(nl["phi_pre"]))
+            rep("dg (pre-pool)", dpg[:, Ci:], cl(nl["g_pre"]))
+            rep("dtheta", ws.tensor(blk + ".dTH")[:M * Ci].view(M, Ci).double().cpu(), cl(nl["theta"]))
+            rep("dO", ws.tensor(blk + ".dO")[:M * Ci].view(M, Ci).double().cpu(), cl(nl["o"]))
+            Pk = (Hs // 2) ** 2
+            att_h = ws.tensor(blk + ".ATT")[:M * Pk].view(M, Pk).double().cpu()
+            rep("att (fwd)", att_h, nl["att"].reshape(M, Pk))
+            print(f"   {blk} scores: max |s| {float(nl['sv'].abs().max()):.3e}; att max {float(nl['att'].max()):.4f}")
+            # max-pool decisions: HIP taps vs the float64 argmax, and how close the two candidates are
+            pa = ws.tensor(blk + ".PA")[:B * Pk * 2 * Ci].view(B, Pk, 2 * Ci).cpu().long()
+            pgh = ws.tensor(blk + ".PG")[:M * 2 * Ci].view(B, Hs, Hs, 2 * Ci).double().cpu()
+            for name, pre, off in (("phi", nl["ppv"], 0), ("g", nl["gpv"], Ci)):
+                ph = Hs // 2
+                win = pre[:, :, :2 * ph, :2 * ph].reshape(B, Ci, ph, 2, ph, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, Ci, ph, ph, 4)
+                t64 = win.argmax(-1)                                   # first max, like the kernels
+                th = pa[:, :, off:off + Ci].transpose(1, 2).reshape(B, Ci, ph, ph)
+                diff = (t64 != th).nonzero()
+                print(f"   {blk} pool {name}: {len(diff)} of {th.numel()} windows choose a different tap than float64")
+                for d in diff[:4].tolist():
+                    bb, cc, i, j = d
+                    w64 = win[bb, cc, i, j]
+                    hw = pgh[bb, 2 * i:2 * i + 2, 2 * j:2 * j + 2, off + cc].reshape(4)
+                    print(f"      b {bb} ch {cc} win ({i},{j}): f64 {w64.tolist()} -> tap {int(t64[bb, cc, i, j])}; "
+                          f"HIP {hw.tolist()} -> tap {int(th[bb, cc, i, j])}")
         for pfx in TLS:
             blk = pfx.split(".")[0]
             H = 9 if blk == "hsi1" else 7
@@ -149,7 +230,7 @@ def main():
             dzname = blk + (".dZc" if "channel" in pfx else ".dZg")
             dZh = ws.tensor(dzname)[:B * S * C].view(B, S, C).double().cpu()
             dah = ws.tensor(pfx + ".da")[:B * S * HW].view(B, S, HW).double().cpu()
-            dfh = ws.tensor(pfx + ".df")[:S * B * HW].view(S, B * HW).double().cpu()
+            dfh = ws.tensor(pfx + ".df")[:S * B * HW].view(S, B * HW).double().cpu() if pfx + ".df" in ws.t else None
             mx = ws.tensor(pfx + ".mx")[:B * HW].double().cpu()
             avg = ws.tensor(pfx + ".avg")[:B * HW].double().cpu()
             stats = ws.tensor(pfx + ".st")[:2 * S].double().cpu()
@@ -175,10 +256,32 @@ def main():
             worst = torch.argsort(err_tok, descending=True)[:args.top]
             print(f"-- {pfx}: S={S} gmax={gmax:.3e}; dZ err {float((dZh - Y['dZ']).abs().max()):.3e} "
                   f"(ref32 {float((Y32['dZ'].double() - Yo['dZ']).abs().max()):.3e}, |dZ| {float(Y['dZ'].abs().max()):.3e})")
+            lnp = blk + (".ln4" if "channel" in pfx else ".ln3")
+            lnY = y64[lnp]
+            dyname = blk + (".dFc" if "channel" in pfx else ".dFg")
+            dFh = ws.tensor(dyname)[:B * S * C].view(B * S, C).double().cpu()
+            Zh = ws.tensor(pfx + ".Z")[:B * S * C].view(B * S, C).double().cpu()
+            dFr = lnY["dlny"].reshape(B * S, C)
+            Zr = lnY["lnx"].reshape(B * S, C)
+            # LayerNorm backward in float64 from the HIP path's own dy and x
+            w_ln = model.flat_params.detach()[model._poff[lnp + ".weight"]:model._poff[lnp + ".weight"] + C].double().cpu()
+            mu = Zh.mean(1, keepdim=True)
+            var = Zh.var(1, unbiased=False, keepdim=True)
+            rs = 1.0 / torch.sqrt(var + 1e-6)
+            xh = (Zh - mu) * rs
+            gg = dFh * w_ln
+            dZre = rs * (gg - gg.mean(1, keepdim=True) - xh * (gg * xh).mean(1, keepdim=True))
+            rowerr = (dZh.reshape(B * S, C) - Y["dZ"].reshape(B * S, C)).abs().max(1).values
+            wr = int(torch.argmax(rowerr))
+            print(f"   LN {lnp}: dy err {float((dFh - dFr).abs().max()):.3e} (|dy| {float(dFr.abs().max()):.3e}); "
+                  f"x err {float((Zh - Zr).abs().max()):.3e} (|x| {float(Zr.abs().max()):.3e}); "
+                  f"dx(HIP) vs f64-LN-bwd(HIP dy, x) {float((dZh.reshape(B * S, C) - dZre).abs().max()):.3e}; "
+                  f"worst dZ row {wr} (b {wr // S}, s {wr % S}) err {float(rowerr[wr]):.3e}, row std/|mean| "
+                  f"{float(Zh[wr].std() / Zh[wr].mean().abs()):.3e}, rstd {float(rs[wr]):.3e}")
             for s in worst.tolist():
                 ea = float((dah[:, s] - da64[:, s]).abs().max())
                 ea32 = float((Y32["da"].view(B, S, HW)[:, s].double() - Yo["da"].view(B, S, HW)[:, s]).abs().max())
-                ef = float((dfh[s] - df64[s]).abs().max())
+                ef = float((dfh[s] - df64[s]).abs().max()) if dfh is not None else float("nan")
                 ef_re = float((d_re[s] - df64[s]).abs().max())
                 sd_std = float(1.0 / stats[2 * s + 1])
                 print(f"   tok {s:2d}: param err {float(err_tok[s]):.3e} (ref32 {float((g32t[s].double() - go64t[s]).abs().max()):.3e}) "

@@ -1,283 +1,573 @@
-// TokenLearner(S) = S independent SpatialAttention modules (Mutimodality_Mamba7.py:26-64),
-// fused: the channel max / mean of the input are shared by all S tokens, so they are computed
-// once per pixel; each token then only needs a 2->1 1x1 conv, a BatchNorm2d(1) over the whole
-// batch (train: batch stats + running update), ReLU and sigmoid to produce its spatial weight
-// map a[b, s, :] (one workgroup per token, two-pass block reductions).  The weighted spatial
-// mean Z[b, s, :] = mean_p a[b, s, p] x[b, p, :] is a batched GEMM (vc_gemm).
+// TokenLearner(S) = S independent SpatialAttention modules (Mutimodality_Mamba7.py:26-64), fused:
+//   pooled[p] = (max_c x[p, c], mean_c x[p, c])                       shared by all S tokens
+//   f_s[p]    = w0_s max + w1_s mean + b_s                             2->1 1x1 conv (:37)
+//   a[b,s,p]  = sigmoid(ReLU(BN_s(f_s)[p]))                            BatchNorm2d(1) over B*HW (:38-48)
+//   Z[b,s,:]  = mean_p a[b,s,p] x[b,p,:]                               (:61-63; a vc_gemm)
 //
-// Parameter layout: the S SpatialAttention modules' parameters are contiguous in the flat
-// parameter buffer in state_dict order, 5 floats per token
-//   [conv.0.weight (2), conv.0.bias, conv.1.weight (gamma), conv.1.bias (beta)],
-// and their BN buffers 2 floats per token [running_mean, running_var].
+// Round 5 layout (the round-4 kernels ran one 1024-thread block per token, 25 / 49
+// blocks walking all B*HW elements serially, 4 x 35 + 4 x 16 us per step).  f_s is LINEAR in the pooled
+// pair, so every token's batch statistics follow from the moments of (max, mean) over the batch, which
+// all tokens share:
+//   mean_f = w0 mbar + w1 vbar + b,   n var_f = w0^2 Cmm + 2 w0 w1 Cmv + w1^2 Cvv
+// with Cxy the centred second moments, accumulated in fp64 against a shift K = the pooled values of row 0
+// (d = m - K is exact in fp64; |mbar - K| is within the data's range, so Cmm = sum d^2 - (sum d)^2 / n
+// keeps ~15 digits -- these BN(1) inputs have a spread ~1e-3 of their mean).  The forward is then:
+//   pixel_stats  (one wave per pixel row; 64 rows per block) + the block's shifted moment partials
+//   attn_fwd     grid (sample chunks x token groups): every block combines the partials (fixed order),
+//                derives its tokens' statistics, and writes a for its samples
+// and the backward, with g1 = da sigmoid'(bn) [bn > 0], s1 = sum g1, s2 = sum g1 xh:
+//   attn_bwd     grid (tokens x element chunks): per-token fp64 partials of s1, s2 and of the centred
+//                sums sum g1 (m - mbar), sum g1 (v - vbar)
+//   pixel_bwd    one wave per pixel row, a lane per token: df = gamma invstd (g1 - s1/n - xh s2/n)
+//                recomputed in fp64, dmax / dmean summed over the tokens, the input gradient row updated;
+//                block 0 also finishes the 5 parameter gradients per token from the partials:
+//                  dw0 = gamma invstd (sum g1 (m - mbar) - s2/n invstd (w0 Cmm + w1 Cmv))   (and dw1 alike)
+//                  db  = 0 in train mode (sum xh = 0), dgamma = s2, dbeta = s1
+// Every sum is in a fixed order (no atomics): the results are run-to-run identical.
+//
+// Parameter layout: the S SpatialAttention modules' parameters are contiguous in the flat parameter
+// buffer in state_dict order, 5 floats per token [conv.0.weight (2), conv.0.bias, conv.1.weight (gamma),
+// conv.1.bias (beta)], their BN buffers 2 floats per token [running_mean, running_var].
+// stats (fp64, [2 S + 8]): per token (mean_f, invstd), then the shared moments
+//   [n, mbar, vbar, Cmm, Cmv, Cvv, Km, Kv].
 #include "common.h"
 
 namespace {
 
 constexpr int TPAR = 5, TBUF = 2;
+constexpr int PS_RW = 16;            // pixel rows per wave in pixel_stats
+constexpr int PS_ROWS = 4 * PS_RW;   // rows per 256-thread block = one moment partial
+constexpr int NMOM = 5;              // partial: sum dm, sum dv, sum dm^2, sum dm dv, sum dv^2
+constexpr int NBS = 4;               // backward partial: s1, s2, sum g1 (m - mbar), sum g1 (v - vbar)
 
-// per pixel (row of C channels): max (+ first argmax) and mean; one wave per row
-__global__ __launch_bounds__(256) void pixel_stats(long M, int C, const float* __restrict__ x, long ldx,
-                                                   float* __restrict__ mx, int* __restrict__ amx,
-                                                   float* __restrict__ avg) {
-  const int lane = threadIdx.x & 63;
-  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= M) return;
-  const float* xr = x + r * ldx;
-  float best = -INFINITY, s = 0.f;
-  int bi = 0x7fffffff;
-  for (int c0 = lane; c0 < C; c0 += 64 * 8) {   // 8 of the lane's channels loaded, then scanned in order
-    float xv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xv[j] = c0 + 64 * j < C ? xr[c0 + 64 * j] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + 64 * j;
-      if (c < C) {
-        const float v = xv[j];
-        s += v;
-        if (v > best) {
-          best = v;
-          bi = c;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ob = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (ob > best || (ob == best && oi < bi)) {
-      best = ob;
-      bi = oi;
-    }
-  }
-  s = wave_sum(s);
-  if (lane == 0) {
-    mx[r] = best;
-    amx[r] = bi;
-    avg[r] = s / C;
-  }
-}
-
-constexpr int TLT = 1024;  // threads per token block (16 waves): the token's B*HW elements are the long axis
-
-// Reductions over a token's B*HW elements accumulate in fp64, like torch's CPU BatchNorm
-// (acc_type<float> = double): these BN(1) inputs have a tiny spread around a large mean, so
-// fp32 sums lose ~3 digits in the statistics and in the backward's dgamma / dbeta / dx terms.
-__device__ __forceinline__ double block_sum(double v, double* red) {
+__device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  double r = 0.0;
-#pragma unroll
-  for (int i = 0; i < TLT / 64; ++i) r += red[i];
-  __syncthreads();
-  return r;
+  return v;
 }
 
-// K independent block sums in one pass (one pair of barriers instead of K); each value is summed in
-// block_sum's order, so the results are bit-identical to K block_sum calls
+// K independent fp64 sums over a 256-thread block (4 waves), fixed order; every thread gets the totals
 template <int K>
-__device__ __forceinline__ void block_sums(double (&v)[K], double* red) {
+__device__ __forceinline__ void block256_sums_d(double (&v)[K], double* red) {
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  for (int k = 0; k < K; ++k) v[k] = wave_sum_d(v[k]);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
-    for (int k = 0; k < K; ++k) red[k * (TLT / 64) + w] = v[k];
+    for (int k = 0; k < K; ++k) red[k * 4 + w] = v[k];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    double r = 0.0;
-#pragma unroll
-    for (int i = 0; i < TLT / 64; ++i) r += red[k * (TLT / 64) + i];
-    v[k] = r;
-  }
+  for (int k = 0; k < K; ++k) v[k] = ((red[k * 4] + red[k * 4 + 1]) + red[k * 4 + 2]) + red[k * 4 + 3];
   __syncthreads();
 }
 
-// the token's 2->1 conv output for pixel i, in fp64: BN(1) normalises values with a tiny spread
-// around a large mean, so the fp32 rounding of the conv would be amplified by 1/std
+// max (+ first argmax) and mean of RB pixel rows, wave-wide (every lane gets the results): the rows' loads
+// are issued together (one latency per RB rows), then each row is scanned in channel order -- per row the
+// same arithmetic as a one-row pass, so the results do not depend on RB.  C <= 512 (host check).
+template <int RB>
+__device__ __forceinline__ void rows_stats(const float* __restrict__ x, long ldx, int r0, int nr, int C, int lane,
+                                           float (&best)[RB], int (&bi)[RB], float (&mean)[RB]) {
+  float xv[RB][8];
+#pragma unroll
+  for (int k = 0; k < RB; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = lane + 64 * j;
+      xv[k][j] = (k < nr && c < C) ? x[(long)(r0 + k) * ldx + c] : 0.f;
+    }
+#pragma unroll
+  for (int k = 0; k < RB; ++k) {
+    float bk = -INFINITY, s = 0.f;
+    int ik = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = lane + 64 * j;
+      if (c < C) {
+        const float v = xv[k][j];
+        s += v;
+        if (v > bk) {
+          bk = v;
+          ik = c;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(bk, o, 64);
+      const int oi = __shfl_xor(ik, o, 64);
+      if (ob > bk || (ob == bk && oi < ik)) {
+        bk = ob;
+        ik = oi;
+      }
+    }
+    best[k] = bk;
+    bi[k] = ik;
+    mean[k] = wave_sum(s) / C;
+  }
+}
+
+constexpr int PS_RB = 4;   // rows per batch of loads
+
+// Block = PS_ROWS pixel rows (4 waves x PS_RW rows): mx / amx / avg per row, and the block's moment
+// partial of (max, mean) shifted by row 0's values -> part[blockIdx.x * NMOM + j] (part may be null)
+__global__ __launch_bounds__(256) void pixel_stats(int M, int C, const float* __restrict__ x, long ldx,
+                                                   float* __restrict__ mx, int* __restrict__ amx,
+                                                   float* __restrict__ avg, double* __restrict__ part) {
+  __shared__ float sm[PS_ROWS], sv[PS_ROWS];
+  __shared__ double red[NMOM * 4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * PS_ROWS;
+  float km, kv;   // the shift: row 0's pooled values (the same code, so the same values as mx[0], avg[0])
+  if (part) {
+    float b1[1], m1[1];
+    int i1[1];
+    rows_stats<1>(x, ldx, 0, 1, C, lane, b1, i1, m1);
+    km = b1[0];
+    kv = m1[0];
+  }
+#pragma unroll
+  for (int j0 = 0; j0 < PS_RW; j0 += PS_RB) {
+    const int rl = w * PS_RW + j0, r = r0 + rl;
+    const int nr = min(PS_RB, M - r);
+    if (nr <= 0) break;
+    float best[PS_RB], mean[PS_RB];
+    int bi[PS_RB];
+    rows_stats<PS_RB>(x, ldx, r, nr, C, lane, best, bi, mean);
+    if (lane < nr) {   // lane k stores row k
+      float bk = best[0], mk = mean[0];
+      int ik = bi[0];
+#pragma unroll
+      for (int k = 1; k < PS_RB; ++k)
+        if (lane == k) {
+          bk = best[k];
+          mk = mean[k];
+          ik = bi[k];
+        }
+      mx[r + lane] = bk;
+      amx[r + lane] = ik;
+      avg[r + lane] = mk;
+      sm[rl + lane] = bk;
+      sv[rl + lane] = mk;
+    }
+  }
+  if (!part) return;
+  __syncthreads();
+  double v[NMOM] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (threadIdx.x < PS_ROWS && r0 + (int)threadIdx.x < M) {
+    const double dm = (double)sm[threadIdx.x] - (double)km, dv = (double)sv[threadIdx.x] - (double)kv;
+    v[0] = dm;
+    v[1] = dv;
+    v[2] = dm * dm;
+    v[3] = dm * dv;
+    v[4] = dv * dv;
+  }
+  block256_sums_d(v, red);
+  if (threadIdx.x < NMOM) part[(long)blockIdx.x * NMOM + threadIdx.x] = v[threadIdx.x];
+}
+
+// the shared moments from the P pixel_stats partials, fixed order (every block computes them alike):
+// out = [n, mbar, vbar, Cmm, Cmv, Cvv] (fp64)
+__device__ __forceinline__ void combine_moments(int P, long n, const double* __restrict__ part, float km, float kv,
+                                                double* red, double (&out)[6]) {
+  double v[NMOM] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int p = threadIdx.x; p < P; p += 256) {
+    double t[NMOM];
+#pragma unroll
+    for (int j = 0; j < NMOM; ++j) t[j] = part[(long)p * NMOM + j];
+#pragma unroll
+    for (int j = 0; j < NMOM; ++j) v[j] += t[j];
+  }
+  block256_sums_d(v, red);
+  const double nd = (double)n;
+  out[0] = nd;
+  out[1] = (double)km + v[0] / nd;
+  out[2] = (double)kv + v[1] / nd;
+  out[3] = v[2] - v[0] * v[0] / nd;
+  out[4] = v[3] - v[0] * v[1] / nd;
+  out[5] = v[4] - v[1] * v[1] / nd;
+}
+
+// the token's 2->1 conv output for pixel (m, v) in fp64 (exact products of fp32 values), and its BN(1)
+// output: forward, backward and vc_tl_relu_mask share this one expression, so they take identical ReLU
+// decisions
 __device__ __forceinline__ double tl_fv(float m, float v, float w0, float w1, float bc) {
   return (double)w0 * m + (double)w1 * v + (double)bc;
 }
-__device__ __forceinline__ double tl_f(const float* __restrict__ mx, const float* __restrict__ avg, long i, float w0,
-                                       float w1, float bc) {
-  return tl_fv(mx[i], avg[i], w0, w1, bc);
-}
-
-// the token's BN(1) output for pixel i: forward, backward and vc_tl_relu_mask share this one
-// expression, so they take identical ReLU decisions
 __device__ __forceinline__ float tl_bnv(float m, float v, float w0, float w1, float bc, double mean, double invstd,
                                         float gam, float bet, double& xh) {
   xh = (tl_fv(m, v, w0, w1, bc) - mean) * invstd;
   return (float)xh * gam + bet;
 }
-__device__ __forceinline__ float tl_bn(const float* __restrict__ mx, const float* __restrict__ avg, long i, float w0,
-                                       float w1, float bc, double mean, double invstd, float gam, float bet,
-                                       double& xh) {
-  return tl_bnv(mx[i], avg[i], w0, w1, bc, mean, invstd, gam, bet, xh);
+
+// g1 = d(loss)/d(BN output) through sigmoid(ReLU(.)) for one element
+__device__ __forceinline__ double tl_g1(float m, float v, const float* p, double mean, double invstd, float dav,
+                                        double& xh) {
+  const float bn = tl_bnv(m, v, p[0], p[1], p[2], mean, invstd, p[3], p[4], xh);
+  if (!(bn > 0.f)) return 0.0;
+  const float sg = sigmoid_f(bn);
+  return (double)(dav * sg * (1.f - sg));
 }
 
-// A token block's pass over its n elements i = threadIdx.x + TLT * k in increasing k: the (mx, avg)
-// pairs of NBT consecutive k are loaded before any is used (one round of dependent loads per NBT
-// elements instead of one per element), then fn(i, mx[i], avg[i]) runs in the same element order as
-// a plain loop, so every accumulation is bit-identical to it.
-constexpr int NBT = 8;
-template <typename Fn>
-__device__ __forceinline__ void tl_pass(long n, const float* __restrict__ mx, const float* __restrict__ avg, Fn fn) {
-  for (long i0 = threadIdx.x; i0 < n; i0 += (long)TLT * NBT) {
-    float m[NBT], v[NBT];
-#pragma unroll
-    for (int j = 0; j < NBT; ++j) {
-      const long i = i0 + (long)TLT * j;
-      m[j] = i < n ? mx[i] : 0.f;
-      v[j] = i < n ? avg[i] : 0.f;
+// v_mfma_f32_16x16x4_f32 over 16-wide k chunks with the k order permuted alike on both operands: in step j of
+// a chunk, lane group g = lane / 16 supplies k = 16 kc + 4 g + j, so each lane feeds the four steps from ONE
+// float4 of each operand (a[i] = A(row, 16 kc + 4 g + i), b[i] = B(16 kc + 4 g + i, col)).  The result is
+// the chunk's sum over its 16 k in the MFMA's order; acc[r] = C(row 4 g + r, col lane % 16).
+__device__ __forceinline__ void mfma_k16(const f32x4& a, const f32x4& b, f32x4& acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 ld4_lds(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+constexpr int TL_CT = 64;   // output columns (channels) per block of the pooling kernels
+
+// the token statistics of the block into LDS: tok_mean / tok_inv [S] (train: from the shared moments, which
+// every block combines alike; eval: the running statistics); block (0, 0) publishes stats (and the moments)
+// and updates the running statistics
+__device__ __forceinline__ void tl_token_stats(int train, long n, int S, const float* __restrict__ mx,
+                                               const float* __restrict__ avg, const float* __restrict__ par,
+                                               float* __restrict__ buf, float eps, float momentum,
+                                               const double* __restrict__ part, int P, double* __restrict__ stats,
+                                               double* red, double* tok_mean, double* tok_inv) {
+  double mom[6];
+  combine_moments(P, n, part, mx[0], avg[0], red, mom);
+  const bool pub = blockIdx.x == 0 && blockIdx.y == 0;
+  for (int s = threadIdx.x; s < S; s += 256) {
+    const float* p = par + (long)s * TPAR;
+    const double w0 = p[0], w1 = p[1], bc = p[2];
+    double mean, invstd;
+    if (train) {
+      mean = w0 * mom[1] + w1 * mom[2] + bc;
+      const double m2 = fmax(w0 * w0 * mom[3] + 2.0 * w0 * w1 * mom[4] + w1 * w1 * mom[5], 0.0);
+      const double var = m2 / (double)n;
+      invstd = 1.0 / sqrt(var + (double)eps);
+      if (pub && buf) {
+        float* bb = buf + (long)s * TBUF;
+        const double unb = n > 1 ? m2 / (double)(n - 1) : var;
+        bb[0] = (float)((1.0 - momentum) * bb[0] + momentum * mean);
+        bb[1] = (float)((1.0 - momentum) * bb[1] + momentum * unb);
+      }
+    } else {
+      const float* bb = buf + (long)s * TBUF;
+      mean = bb[0];
+      invstd = 1.0 / sqrt((double)bb[1] + (double)eps);
     }
-#pragma unroll
-    for (int j = 0; j < NBT; ++j) {
-      const long i = i0 + (long)TLT * j;
-      if (i < n) fn(i, m[j], v[j]);
+    tok_mean[s] = mean;
+    tok_inv[s] = invstd;
+    if (pub) {
+      stats[2 * s] = mean;
+      stats[2 * s + 1] = invstd;
     }
   }
+  if (pub && threadIdx.x < 8) {
+    double v = (double)avg[0];
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (threadIdx.x == j) v = mom[j];
+    if (threadIdx.x == 6) v = (double)mx[0];
+    stats[2 * S + threadIdx.x] = v;
+  }
+  __syncthreads();
 }
 
-// one block per token s; a[(b*S + s)*HW + p]
-__global__ __launch_bounds__(1024) void attn_fwd(int train, int B, int HW, FastDiv fHW, int S, const float* __restrict__ mx,
-                                                const float* __restrict__ avg, const float* __restrict__ par,
-                                                float* __restrict__ buf, float eps, float momentum,
-                                                double* __restrict__ stats, float* __restrict__ a) {
-  __shared__ double red[TLT / 64];
-  const int s = blockIdx.x;
-  const float* p = par + (long)s * TPAR;
-  const float w0 = p[0], w1 = p[1], bc = p[2], gam = p[3], bet = p[4];
+// Forward: grid (B, ceil(C / 64)); block 256 (4 waves).  The block's sample b: its tokens' statistics, the
+// attention map a[s][q] = sigmoid(ReLU(BN_s(f_s[q]))) of all S tokens in LDS, and the pooled tokens of its 64
+// channels Z[b, s, c] = (1/HW) sum_q a[s][q] x[b, q, c] on MFMA (A = a rows, B = x^T staged in LDS; the pixel
+// axis padded to 16 with zeros).  a is also written to `a_out` (optional, [B, S, HW]) by the y = 0 blocks.
+// LDS: al [Sp][Lp + 4] + xt [64][Lp + 4] floats (Sp = S rounded up to 16, Lp = HW rounded up to 16).
+__global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int C, int S, const float* __restrict__ x,
+                                                   long ldx, const float* __restrict__ mx,
+                                                   const float* __restrict__ avg, const float* __restrict__ par,
+                                                   float* __restrict__ buf, float eps, float momentum,
+                                                   const double* __restrict__ part, int P, double* __restrict__ stats,
+                                                   float* __restrict__ a_out, float* __restrict__ Z) {
+  extern __shared__ __attribute__((aligned(16))) float sm_f[];
+  __shared__ double red[NMOM * 4];
+  __shared__ double tok_mean[128], tok_inv[128];
+  const int b = blockIdx.x, c0 = blockIdx.y * TL_CT;
+  const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15, LS = Lp + 4;
+  float* al = sm_f;              // [Sp][LS]
+  float* xt = sm_f + Sp * LS;    // [64][LS]  x^T of the block's channels
   const long n = (long)B * HW;
-  double mean, invstd;
-  if (train) {
-    double acc = 0.0;
-    tl_pass(n, mx, avg, [&](long, float m, float v) { acc += tl_fv(m, v, w0, w1, bc); });
-    mean = block_sum(acc, red) / (double)n;
-    double q = 0.0;
-    tl_pass(n, mx, avg, [&](long, float m, float v) {
-      const double d = tl_fv(m, v, w0, w1, bc) - mean;
-      q += d * d;
-    });
-    const double m2 = block_sum(q, red);
-    const double var = m2 / (double)n;
-    invstd = 1.0 / sqrt(var + (double)eps);
-    if (threadIdx.x == 0 && buf) {
-      float* bb = buf + (long)s * TBUF;
-      const double unb = n > 1 ? m2 / (double)(n - 1) : var;
-      bb[0] = (float)((1.0 - momentum) * bb[0] + momentum * mean);
-      bb[1] = (float)((1.0 - momentum) * bb[1] + momentum * unb);
+  // the sample's channel tile, transposed into LDS (coalesced rows of 64 channels; zero padding)
+  for (int i = threadIdx.x; i < Lp * TL_CT; i += 256) {
+    const int q = i / TL_CT, cl = i - q * TL_CT;
+    const int c = c0 + cl;
+    xt[cl * LS + q] = (q < HW && c < C) ? x[((long)b * HW + q) * ldx + c] : 0.f;
+  }
+  tl_token_stats(train, n, S, mx, avg, par, buf, eps, momentum, part, P, stats, red, tok_mean, tok_inv);
+  for (int i = threadIdx.x; i < Sp * Lp; i += 256) {
+    const int s = i / Lp, q = i - s * Lp;
+    float av = 0.f;
+    if (s < S && q < HW) {
+      const float* p = par + (long)s * TPAR;
+      double xh;
+      const float bn = tl_bnv(mx[(long)b * HW + q], avg[(long)b * HW + q], p[0], p[1], p[2], tok_mean[s], tok_inv[s],
+                              p[3], p[4], xh);
+      av = sigmoid_f(fmaxf(bn, 0.f));
+      if (a_out && blockIdx.y == 0) a_out[((long)b * S + s) * HW + q] = av;
     }
-  } else {
-    const float* bb = buf + (long)s * TBUF;
-    mean = bb[0];
-    invstd = 1.0 / sqrt((double)bb[1] + (double)eps);
+    al[s * LS + q] = av;
   }
-  if (threadIdx.x == 0) {  // saved as (mean, invstd) in fp64 for the backward
-    stats[2 * s] = mean;
-    stats[2 * s + 1] = invstd;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
+  const int nst = Sp / 16, nct = TL_CT / 16, nkc = Lp / 16;
+  const float inv_l = 1.f / (float)HW;
+  for (int t = w; t < nst * nct; t += 4) {
+    const int st = t / nct, ct = t - st * nct;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nkc; ++kc) {
+      const int k = 16 * kc + 4 * g;
+      mfma_k16(ld4_lds(al + (16 * st + r16) * LS + k), ld4_lds(xt + (16 * ct + r16) * LS + k), acc);
+    }
+    const int c = c0 + 16 * ct + r16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int s = 16 * st + 4 * g + r;
+      if (s < S && c < C) Z[((long)b * S + s) * C + c] = acc[r] * inv_l;
+    }
   }
-  tl_pass(n, mx, avg, [&](long i, float m, float v) {
-    double xh;
-    const float bn = tl_bnv(m, v, w0, w1, bc, mean, invstd, gam, bet, xh);
-    int q;
-    const long b = fdivmod((int)i, fHW, q);   // n = B * HW < 2^31 (launcher): 32-bit magic division
-    a[((long)b * S + s) * HW + q] = sigmoid_f(fmaxf(bn, 0.f));
-  });
 }
 
-// one block per token: da -> df[s][i] (grad of the 2->1 conv output) + the token's 5 param grads
-__global__ __launch_bounds__(1024) void attn_bwd(int train, int B, int HW, FastDiv fHW, int S, const float* __restrict__ mx,
-                                                const float* __restrict__ avg, const float* __restrict__ par,
-                                                const double* __restrict__ stats, const float* __restrict__ da,
-                                                float* __restrict__ df, float* __restrict__ gpar) {
-  __shared__ double red[3 * (TLT / 64)];
-  const int s = blockIdx.x;
-  const float* p = par + (long)s * TPAR;
-  const float w0 = p[0], w1 = p[1], bc = p[2], gam = p[3], bet = p[4];
-  const double mean = stats[2 * s], invstd = stats[2 * s + 1];
-  const long n = (long)B * HW;
-  // da[b, s, q] of element i = b * HW + q, loaded with the element's (mx, avg) (same batching and
-  // element order as tl_pass)
-  auto pass = [&](auto fn) {
-    for (long i0 = threadIdx.x; i0 < n; i0 += (long)TLT * NBT) {
-      float m[NBT], v[NBT], g[NBT];
+// Backward part 1: grid (B, ceil(S / 16)); block 256.  da[b, s, q] = (1/HW) sum_c dZ[b, s, c] x[b, q, c] for
+// the block's 16 tokens (MFMA, both operands as float4 runs of their rows straight from L2), written to `da`;
+// then per token the fp64 sums over this sample's pixels of g1, g1 xh, g1 (m - mbar), g1 (v - vbar) ->
+// part[(b * S + s) * NBS + j] (summed over the pixel tiles in a fixed order).
+__global__ __launch_bounds__(256) void tl_bwd_da(int B, int HW, int C, int S, const float* __restrict__ x, long ldx,
+                                                 const float* __restrict__ mx, const float* __restrict__ avg,
+                                                 const float* __restrict__ par, const double* __restrict__ stats,
+                                                 const float* __restrict__ dZ, float* __restrict__ da,
+                                                 double* __restrict__ part) {
+  __shared__ double tsum[4][16][NBS];   // [wave][token][sum]
+  const int b = blockIdx.x, s0 = blockIdx.y * 16;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
+  const int Lp = (HW + 15) & ~15, nqt = Lp / 16, nkc = (C + 15) / 16;
+  const double mbar = stats[2 * S + 1], vbar = stats[2 * S + 2];
+  const float inv_l = 1.f / (float)HW;
+  // this lane's A row (token s0 + r16) and the tokens of its accumulator rows (s0 + 4 g + r)
+  const int sa = s0 + r16;
+  const float* arow = dZ + ((long)b * S + min(sa, S - 1)) * C;
+  float tp[4][TPAR];
+  double tmean[4], tinv[4];
 #pragma unroll
-      for (int j = 0; j < NBT; ++j) {
-        const long i = i0 + (long)TLT * j;
-        const bool ok = i < n;
-        int q = 0;
-        const long b = ok ? fdivmod((int)i, fHW, q) : 0;
-        m[j] = ok ? mx[i] : 0.f;
-        v[j] = ok ? avg[i] : 0.f;
-        g[j] = ok ? da[((long)b * S + s) * HW + q] : 0.f;
+  for (int r = 0; r < 4; ++r) {
+    const int s = s0 + 4 * g + r;
+    const bool ok = s < S;
+#pragma unroll
+    for (int j = 0; j < TPAR; ++j) tp[r][j] = ok ? par[(long)s * TPAR + j] : 0.f;
+    tmean[r] = ok ? stats[2 * s] : 0.0;
+    tinv[r] = ok ? stats[2 * s + 1] : 0.0;
+  }
+  double v[4][NBS];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NBS; ++j) v[r][j] = 0.0;
+  for (int qt = w; qt < nqt; qt += 4) {
+    const int qb = 16 * qt + r16;   // this lane's B column (pixel)
+    const float* brow = x + ((long)b * HW + min(qb, HW - 1)) * ldx;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    constexpr int KB = 4;   // k chunks whose loads are issued together
+    for (int kc0 = 0; kc0 < nkc; kc0 += KB) {
+      f32x4 av[KB], bv[KB];
+#pragma unroll
+      for (int u = 0; u < KB; ++u) {
+        const int k = 16 * (kc0 + u) + 4 * g;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const bool kok = kc0 + u < nkc && k < C;
+        av[u] = (kok && sa < S) ? *reinterpret_cast<const f32x4*>(arow + k) : z;
+        bv[u] = (kok && qb < HW) ? *reinterpret_cast<const f32x4*>(brow + k) : z;
       }
 #pragma unroll
-      for (int j = 0; j < NBT; ++j) {
-        const long i = i0 + (long)TLT * j;
-        if (i < n) fn(i, m[j], v[j], g[j]);
+      for (int u = 0; u < KB; ++u)
+        if (kc0 + u < nkc) mfma_k16(av[u], bv[u], acc);
+    }
+    // acc[r] = da(token s0 + 4 g + r, pixel qb') with qb' = 16 qt + r16 for the C/D layout: col = lane % 16
+    const int q = 16 * qt + r16;
+    const float m = q < HW ? mx[(long)b * HW + q] : 0.f, vq = q < HW ? avg[(long)b * HW + q] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int s = s0 + 4 * g + r;
+      const float dav = acc[r] * inv_l;
+      if (s < S && q < HW) {
+        da[((long)b * S + s) * HW + q] = dav;
+        double xh;
+        const double g1 = tl_g1(m, vq, tp[r], tmean[r], tinv[r], dav, xh);
+        v[r][0] += g1;
+        v[r][1] += g1 * xh;
+        v[r][2] += g1 * ((double)m - mbar);
+        v[r][3] += g1 * ((double)vq - vbar);
       }
     }
-  };
-  double s1 = 0.0, s2 = 0.0;
-  pass([&](long, float m, float v, float dav) {
-    double xh;
-    const float bn = tl_bnv(m, v, w0, w1, bc, mean, invstd, gam, bet, xh);
-    float g1 = 0.f;
-    if (bn > 0.f) {
-      const float sg = sigmoid_f(bn);
-      g1 = dav * sg * (1.f - sg);
-    }
-    s1 += g1;
-    s2 += g1 * xh;
-  });
-  {
-    double v2[2] = {s1, s2};
-    block_sums(v2, red);
-    s1 = v2[0];
-    s2 = v2[1];
   }
-  double gw0 = 0.0, gw1 = 0.0, gb = 0.0;
-  pass([&](long i, float m, float v, float dav) {
-    double xh;
-    const float bn = tl_bnv(m, v, w0, w1, bc, mean, invstd, gam, bet, xh);
-    float g1 = 0.f;
-    if (bn > 0.f) {
-      const float sg = sigmoid_f(bn);
-      g1 = dav * sg * (1.f - sg);
+  // per token: the 16 pixel lanes of the row group, then the waves in order
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NBS; ++j) {
+      double t = v[r][j];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+      v[r][j] = t;
     }
-    const double d = train ? gam * invstd * (g1 - s1 / (double)n - xh * s2 / (double)n) : gam * invstd * g1;
-    df[(long)s * n + i] = (float)d;
-    gw0 += d * m;
-    gw1 += d * v;
-    gb += d;
-  });
-  {
-    double v3[3] = {gw0, gw1, gb};
-    block_sums(v3, red);
-    gw0 = v3[0];
-    gw1 = v3[1];
-    gb = v3[2];
-  }
-  if (threadIdx.x == 0) {
-    float* g = gpar + (long)s * TPAR;
-    g[0] = (float)gw0;
-    g[1] = (float)gw1;
-    g[2] = (float)gb;
-    g[3] = (float)s2;
-    g[4] = (float)s1;
+  if (r16 == 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < NBS; ++j) tsum[w][4 * g + r][j] = v[r][j];
+  __syncthreads();
+  if (threadIdx.x < 16 * NBS) {
+    const int tl = threadIdx.x / NBS, j = threadIdx.x - tl * NBS, s = s0 + tl;
+    if (s < S) part[((long)b * S + s) * NBS + j] = ((tsum[0][tl][j] + tsum[1][tl][j]) + tsum[2][tl][j]) + tsum[3][tl][j];
   }
 }
 
-// mask[(b*S + s)*HW + q] = (BN(1) output > 0): the ReLU decisions attn_fwd / attn_bwd took
-__global__ __launch_bounds__(256) void attn_mask(int B, int HW, FastDiv fHW, int S, const float* __restrict__ mx,
+// Backward part 2: grid (B, ceil(C / 64)); block 256.  The tokens' s1 / s2 over the batch (the per-sample
+// partials summed in sample order), then for the block's sample and 64 channels
+//   dx[b, q, c] = (1/HW) sum_s a[s][q] dZ[b, s, c]                      (MFMA; a recomputed)
+//               + (sum_s w1_s df_s[q]) / C + [c == argmax_q] sum_s w0_s df_s[q]
+// with df_s[q] = gamma_s invstd_s (g1 - s1/n - xh s2/n) (train; eval gamma invstd g1) in fp64 (dx overwritten).
+// Block (0, 0) also writes the tokens' 5 parameter gradients (dparams).
+// LDS: at [Lp][Sp + 4] (a^T) + dzt [64][Sp + 4] (dZ^T of the block's channels) floats.
+__global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C, int S, const float* __restrict__ mx,
+                                                 const float* __restrict__ avg, const int* __restrict__ amx,
+                                                 const float* __restrict__ par, const double* __restrict__ stats,
+                                                 const float* __restrict__ dZ, const float* __restrict__ da,
+                                                 const double* __restrict__ part, float* __restrict__ dx, long lddx,
+                                                 float* __restrict__ gpar) {
+  extern __shared__ __attribute__((aligned(16))) float sm_f[];
+  __shared__ double q4[4][128][2];     // per token, 4 sample-quarter sums of s1, s2
+  __shared__ double tsum[2][128];      // s1, s2
+  __shared__ double pq[2][2][128];     // per pixel, two token-half sums of (gm, ga)
+  const int b = blockIdx.x, c0 = blockIdx.y * TL_CT;
+  const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15, SS = Sp + 4;
+  float* at = sm_f;                 // [Lp][SS]
+  float* dzt = sm_f + Lp * SS;      // [64][SS]
+  const long n = (long)B * HW;
+  const double nd = (double)n;
+  // dZ^T of the block's channels (rows of dZ are 64-channel runs: coalesced)
+  for (int i = threadIdx.x; i < Sp * TL_CT; i += 256) {
+    const int s = i / TL_CT, cl = i - s * TL_CT;
+    const int c = c0 + cl;
+    dzt[cl * SS + s] = (s < S && c < C) ? dZ[((long)b * S + s) * C + c] : 0.f;
+  }
+  // s1 / s2 per token: the samples in 4 interleaved quarters, then the quarters in order
+  for (int i = threadIdx.x; i < 4 * S; i += 256) {
+    const int s = i >> 2, u = i & 3;
+    double t1 = 0.0, t2 = 0.0;
+    for (int bb0 = u; bb0 < B; bb0 += 16) {
+      double p1[4], p2[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int bb = bb0 + 4 * k;
+        p1[k] = bb < B ? part[((long)bb * S + s) * NBS] : 0.0;
+        p2[k] = bb < B ? part[((long)bb * S + s) * NBS + 1] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        t1 += p1[k];
+        t2 += p2[k];
+      }
+    }
+    q4[u][s][0] = t1;
+    q4[u][s][1] = t2;
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < S; s += 256) {
+    tsum[0][s] = ((q4[0][s][0] + q4[1][s][0]) + q4[2][s][0]) + q4[3][s][0];
+    tsum[1][s] = ((q4[0][s][1] + q4[1][s][1]) + q4[2][s][1]) + q4[3][s][1];
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0) {   // parameter gradients: all four sums over the batch, sample order
+    for (int s = threadIdx.x; s < S; s += 256) {
+      double t[NBS] = {0.0, 0.0, 0.0, 0.0};
+      for (int bb = 0; bb < B; ++bb)
+#pragma unroll
+        for (int j = 0; j < NBS; ++j) t[j] += part[((long)bb * S + s) * NBS + j];
+      const float* p = par + (long)s * TPAR;
+      const double w0 = p[0], w1 = p[1], gam = p[3];
+      const double invstd = stats[2 * s + 1];
+      const double* mom = stats + 2 * S;   // n, mbar, vbar, Cmm, Cmv, Cvv
+      double gw0, gw1, gb;
+      if (train) {
+        const double k = t[1] / nd * invstd;
+        gw0 = gam * invstd * (t[2] - k * (w0 * mom[3] + w1 * mom[4]));
+        gw1 = gam * invstd * (t[3] - k * (w0 * mom[4] + w1 * mom[5]));
+        gb = 0.0;   // sum_i df_i = gamma invstd (s1 - s1 - s2/n sum_i xh_i) and sum_i xh_i = 0
+      } else {
+        gw0 = gam * invstd * (t[2] + mom[1] * t[0]);
+        gw1 = gam * invstd * (t[3] + mom[2] * t[0]);
+        gb = gam * invstd * t[0];
+      }
+      float* gp = gpar + (long)s * TPAR;
+      gp[0] = (float)gw0;
+      gp[1] = (float)gw1;
+      gp[2] = (float)gb;
+      gp[3] = (float)t[1];
+      gp[4] = (float)t[0];
+    }
+  }
+  __syncthreads();
+  // a^T recomputed, and the pixel gradients gm / ga over two token halves (fixed order)
+  const int half = (S + 1) / 2;
+  for (int i = threadIdx.x; i < 2 * Lp; i += 256) {
+    const int q = i >> 1, h = i & 1;
+    const bool qok = q < HW;
+    const float m = qok ? mx[(long)b * HW + q] : 0.f, v = qok ? avg[(long)b * HW + q] : 0.f;
+    double gm = 0.0, ga = 0.0;
+    const int sb = h * half, se = h ? S : half;
+    for (int s = sb; s < se; ++s) {
+      const float* p = par + (long)s * TPAR;
+      const double mean = stats[2 * s], invstd = stats[2 * s + 1];
+      double xh;
+      const float bn = tl_bnv(m, v, p[0], p[1], p[2], mean, invstd, p[3], p[4], xh);
+      at[q * SS + s] = qok ? sigmoid_f(fmaxf(bn, 0.f)) : 0.f;
+      if (qok) {
+        const float dav = da[((long)b * S + s) * HW + q];
+        double g1 = 0.0;
+        if (bn > 0.f) {
+          const float sg = sigmoid_f(bn);
+          g1 = (double)(dav * sg * (1.f - sg));
+        }
+        const double gi = (double)p[3] * invstd;
+        const double d = train ? gi * (g1 - tsum[0][s] / nd - xh * tsum[1][s] / nd) : gi * g1;
+        gm += d * (double)p[0];
+        ga += d * (double)p[1];
+      }
+    }
+    if (h == 1)
+      for (int s = S; s < Sp; ++s) at[q * SS + s] = 0.f;
+    pq[h][0][q] = gm;
+    pq[h][1][q] = ga;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
+  const int nqt = Lp / 16, nct = TL_CT / 16, nkc = Sp / 16;
+  const float inv_l = 1.f / (float)HW;
+  for (int t = w; t < nqt * nct; t += 4) {
+    const int qt = t / nct, ct = t - qt * nct;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nkc; ++kc) {
+      const int k = 16 * kc + 4 * g;
+      mfma_k16(ld4_lds(at + (16 * qt + r16) * SS + k), ld4_lds(dzt + (16 * ct + r16) * SS + k), acc);
+    }
+    const int c = c0 + 16 * ct + r16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = 16 * qt + 4 * g + r;
+      if (q < HW && c < C) {
+        const float gmf = (float)(pq[0][0][q] + pq[1][0][q]);
+        const float gaf = (float)((pq[0][1][q] + pq[1][1][q]) / (double)C);
+        const int am = amx[(long)b * HW + q];
+        dx[((long)b * HW + q) * lddx + c] = acc[r] * inv_l + (gaf + (c == am ? gmf : 0.f));
+      }
+    }
+  }
+}
+
+// mask[(b*S + s)*HW + q] = (BN(1) output > 0): the ReLU decisions attn_fwd / attn_bwd / pixel_bwd take
+__global__ __launch_bounds__(256) void attn_mask(int B, int HW, int S, const float* __restrict__ mx,
                                                  const float* __restrict__ avg, const float* __restrict__ par,
                                                  const double* __restrict__ stats, unsigned char* __restrict__ mask) {
   const int s = blockIdx.y;
@@ -285,59 +575,68 @@ __global__ __launch_bounds__(256) void attn_mask(int B, int HW, FastDiv fHW, int
   if (i >= n) return;
   const float* p = par + (long)s * TPAR;
   double xh;
-  const float bn = tl_bn(mx, avg, i, p[0], p[1], p[2], stats[2 * s], stats[2 * s + 1], p[3], p[4], xh);
-  int q;
-  const long bq = fdivmod((int)i, fHW, q);
-  mask[(bq * S + s) * HW + q] = bn > 0.f ? 1 : 0;
-}
-
-// dx[i, c] += davg/C + (c == argmax ? dmx : 0),  dmx / davg summed over the S tokens
-__global__ __launch_bounds__(256) void pixel_bwd(long M, int C, int S, const float* __restrict__ df,
-                                                 const float* __restrict__ par, const int* __restrict__ amx,
-                                                 float* __restrict__ dx, long lddx) {
-  const int lane = threadIdx.x & 63;
-  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= M) return;
-  float gm = 0.f, ga = 0.f;
-  for (int s = lane; s < S; s += 64) {
-    const float d = df[(long)s * M + r];
-    gm += d * par[(long)s * TPAR];
-    ga += d * par[(long)s * TPAR + 1];
-  }
-  gm = wave_sum(gm);
-  ga = wave_sum(ga) / (float)C;
-  const int am = amx[r];
-  float* dr = dx + r * lddx;
-  for (int c = lane; c < C; c += 64) dr[c] += ga + (c == am ? gm : 0.f);
+  const float bn = tl_bnv(mx[i], avg[i], p[0], p[1], p[2], stats[2 * s], stats[2 * s + 1], p[3], p[4], xh);
+  const long b = i / HW, q = i - b * HW;
+  mask[(b * S + s) * HW + q] = bn > 0.f ? 1 : 0;
 }
 
 }  // namespace
 
-VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg,
+static long tl_pix_partials(long M) { return (long)vc_cdiv(M, PS_ROWS) * NMOM; }
+
+VC_API int vc_tl_ws_floats(int B, int HW, int S) {
+  if (B <= 0 || HW <= 0 || S <= 0) return -1;
+  const long dbl = tl_pix_partials((long)B * HW) + (long)B * S * NBS;
+  return (int)(2 * dbl + 2);
+}
+
+VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg, double* ws,
                              hipStream_t stream) {
-  VC_REQUIRE(M >= 0 && C > 0);
+  VC_REQUIRE(M >= 0 && C > 0 && C <= 512);
+  VC_REQUIRE_I32(M);
   if (M == 0) return VC_OK;
-  hipLaunchKernelGGL(pixel_stats, dim3(vc_cdiv(M, 4)), dim3(256), 0, stream, M, C, x, ldx, mx, amx, avg);
+  hipLaunchKernelGGL(pixel_stats, dim3(vc_cdiv(M, PS_ROWS)), dim3(256), 0, stream, (int)M, C, x, ldx, mx, amx, avg,
+                     ws);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
 
-VC_API int vc_tl_attn_fwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          float* bn_buffers, float eps, float momentum, double* stats, float* a, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && HW > 0 && S > 0);
-  VC_REQUIRE_I32((long)B * HW);
-  hipLaunchKernelGGL(attn_fwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, make_fastdiv(HW), S, mx, avg, params, bn_buffers, eps,
-                     momentum, stats, a);
+static size_t tl_fwd_lds(int HW, int S) {
+  const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15;
+  return (size_t)(Sp + TL_CT) * (Lp + 4) * sizeof(float);
+}
+static size_t tl_bwd_lds(int HW, int S) {
+  const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15;
+  return (size_t)(Lp + TL_CT) * (Sp + 4) * sizeof(float);
+}
+
+VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
+                     const float* avg, const float* params, float* bn_buffers, float eps, float momentum,
+                     const double* ws, double* stats, float* a, float* Z, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && HW > 0 && C > 0 && S > 0 && S <= 128 && ws && stats && Z);
+  VC_REQUIRE(tl_fwd_lds(HW, S) <= 160 * 1024);
+  VC_REQUIRE_I32((long)B * HW * (S > C ? S : C));
+  const int P = vc_cdiv((long)B * HW, PS_ROWS);
+  hipLaunchKernelGGL(tl_fwd_pool, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_fwd_lds(HW, S), stream, train, B, HW, C,
+                     S, x, ldx, mx, avg, params, bn_buffers, eps, momentum, ws, P, stats, a, Z);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
 
-VC_API int vc_tl_attn_bwd(int train, int B, int HW, int S, const float* mx, const float* avg, const float* params,
-                          const double* stats, const float* da, float* df, float* dparams, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && HW > 0 && S > 0);
-  VC_REQUIRE_I32((long)B * HW);
-  hipLaunchKernelGGL(attn_bwd, dim3(S), dim3(TLT), 0, stream, train, B, HW, make_fastdiv(HW), S, mx, avg, params, stats, da, df,
-                     dparams);
+VC_API int vc_tl_bwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
+                     const float* avg, const int* amx, const float* params, const double* stats, const float* dZ,
+                     float* da, double* ws, float* dx, long lddx, float* dparams, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && HW > 0 && HW <= 128 && C > 0 && C % 4 == 0 && ldx % 4 == 0 && S > 0 && S <= 128 && ws && da &&
+             dx);
+  VC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)dZ & 15) == 0);
+  VC_REQUIRE(tl_bwd_lds(HW, S) <= 160 * 1024);
+  VC_REQUIRE_I32((long)B * HW * (S > C ? S : C));
+  double* part = ws + tl_pix_partials((long)B * HW);
+  hipLaunchKernelGGL(tl_bwd_da, dim3(B, vc_cdiv(S, 16)), dim3(256), 0, stream, B, HW, C, S, x, ldx, mx, avg, params,
+                     stats, dZ, da, part);
+  VC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(tl_bwd_dx, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_bwd_lds(HW, S), stream, train, B, HW, C, S,
+                     mx, avg, amx, params, stats, dZ, da, part, dx, lddx, dparams);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -346,17 +645,8 @@ VC_API int vc_tl_relu_mask(int B, int HW, int S, const float* mx, const float* a
                            const double* stats, unsigned char* mask, hipStream_t stream) {
   VC_REQUIRE(B > 0 && HW > 0 && S > 0);
   VC_REQUIRE_I32((long)B * HW);
-  hipLaunchKernelGGL(attn_mask, dim3(vc_cdiv((long)B * HW, 256), S), dim3(256), 0, stream, B, HW, make_fastdiv(HW), S, mx, avg, params,
+  hipLaunchKernelGGL(attn_mask, dim3(vc_cdiv((long)B * HW, 256), S), dim3(256), 0, stream, B, HW, S, mx, avg, params,
                      stats, mask);
-  VC_CHECK_LAUNCH();
-  return VC_OK;
-}
-
-VC_API int vc_tl_pixel_bwd(long M, int C, int S, const float* df, const float* params, const int* amx, float* dx,
-                           long lddx, hipStream_t stream) {
-  VC_REQUIRE(M >= 0 && C > 0 && S > 0);
-  if (M == 0) return VC_OK;
-  hipLaunchKernelGGL(pixel_bwd, dim3(vc_cdiv(M, 4)), dim3(256), 0, stream, M, C, S, df, params, amx, dx, lddx);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

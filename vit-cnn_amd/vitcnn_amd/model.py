@@ -65,6 +65,11 @@ PARAM_ALIGN = 4            # floats: flat-buffer alignment (16 B) of every param
 ALIGN_MIN = 64
 GEMM_GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES (include/vitcnn.h)
 GEMM_MASK = 64             # vc_gemm flags: the addend is a ReLU mask (include/vitcnn.h)
+GEMM_DEFER = 128           # vc_gemm flags: split-K slabs left unreduced in the caller's buffer
+GEMM_REDUCE_ONLY = 256     # vc_gemm flags: only the reduction of an earlier GEMM_DEFER product
+# lane 1's weight-gradient split-K reductions queued for the weight-gradient lane (the products stay in the
+# chain's grouped launches): every grouped launch of the lane-1 backward chain loses its reduce launch
+_DEFER_REDUCE = True
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 # the Mamba direction conv + x_proj folded into the scan launch and the dt_proj / x_proj data gradients +
@@ -574,9 +579,10 @@ class _Program:
         self._ev_i += 1
         return e
 
-    def gemm(self, *args, exact=False):
+    def gemm(self, *args, exact=False, ws=None):
         """vc_gemm_ex on the current lane with its scratch and split-K tile counters; args are
-        vc_gemm's up to bias_grad (flags at index 21 get the model's precision bit unless `exact`)"""
+        vc_gemm's up to bias_grad (flags at index 21 get the model's precision bit unless `exact`);
+        ws = (pointer, floats): a caller-owned slab buffer instead of the lane's scratch (GEMM_DEFER)"""
         i = self._gemm_i
         self._gemm_i += 1
         if _GEMM_SITES is not None:
@@ -586,10 +592,11 @@ class _Program:
         if self.gemm_flags and not exact and i not in _BF16_EXACT and args[4] >= _BF16_MIN_K and not (
                 _BF16_MIN_K and args[0]):
             args = args[:21] + (args[21] | self.gemm_flags,) + args[22:]
+        wp, wn = ws if ws is not None else (self.scr_p, self.scr_n)
         if self._grouping is not None and self._group_lane == self.cur:
-            self.L.vc_gemm_group_add(self._grouping, *args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS)
+            self.L.vc_gemm_group_add(self._grouping, *args, wp, wn, self._cnt[self.cur], N_COUNTERS)
         else:
-            self.L.vc_gemm_ex(*args, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
+            self.L.vc_gemm_ex(*args, wp, wn, self._cnt[self.cur], N_COUNTERS, self.s)
 
     @contextlib.contextmanager
     def gemm_group(self):
@@ -665,11 +672,11 @@ class _Program:
         self.gemm(0, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, relu_mask or None,
                   N if relu_mask else 0, 0, GEMM_MASK if relu_mask else 0, None)
 
-    def mm_tn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0, bias_grad=0):
+    def mm_tn(self, M, N, K, A, lda, Bm, ldb, C, ldc, alpha=1.0, beta=0.0, bias_grad=0, flags=0, ws=None):
         """C[M,N] = alpha * A^T B, A stored [K, M] (weight gradients: M,N small, K = rows);
         bias_grad[M] (optional) = alpha * column sums of A, fused into the same GEMM"""
-        self.gemm(1, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, 0,
-                       bias_grad or None)
+        self.gemm(1, 0, M, N, K, alpha, A, lda, 0, Bm, ldb, 0, beta, C, ldc, 0, 1, None, None, 0, 0, flags,
+                  bias_grad or None, ws=ws)
 
     def colsum(self, R, C, X, ldx, out, beta=0.0):
         self.L.vc_colsum_ex(R, C, X, ldx, out, beta, self.scr_p, self.scr_n, self._cnt[self.cur], N_COUNTERS, self.s)
@@ -739,19 +746,23 @@ class _Program:
         self.L.vc_cat2_fwd(M, C1, C2, X1, C1, X2, C2, 1 if C1 == C2 else 0, cat, self.s)
         return self.conv1x1_bn_relu(pfx + ".FusionLayer", cat, M, C1 + C2, Cout)
 
+    def tl_ws(self, pfx, L_, S):
+        """the TokenLearner call site's fp64 scratch (moment / gradient partials, include/vitcnn.h)"""
+        return self.ws.get(pfx + ".tlw", (self.L.vc_tl_ws_floats(self.B, L_, S) + 1) // 2, torch.float64).data_ptr()
+
     def token_learner(self, pfx, X, L_, C, S):
+        """TokenLearner(S) forward (Mutimodality_Mamba7.py:51-64): the pooled channel max / mean per pixel, then
+        the tokens' BN(1) statistics, attention maps and pooled tokens Z [B, S, C] in one launch"""
         B, ws = self.B, self.ws
         rows = B * L_
         mx, amx, avg = ws.f(pfx + ".mx", rows), ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), ws.f(pfx + ".avg",
                                                                                                            rows)
-        self.L.vc_tl_pixel_stats(rows, C, X, C, mx, amx, avg, self.s)
-        st = ws.get(pfx + ".st", 2 * S, torch.float64).data_ptr()
-        a = ws.f(pfx + ".a", B * S * L_)
-        self.L.vc_tl_attn_fwd(self.train, B, L_, S, mx, avg, self.P[pfx + ".tokenizers.0.conv.0.weight"],
-                              self.BUF[pfx + ".tokenizers.0.conv.1.running_mean"], BN_EPS, BN_MOM, st, a, self.s)
+        tlw = self.tl_ws(pfx, L_, S)
+        self.L.vc_tl_pixel_stats(rows, C, X, C, mx, amx, avg, tlw, self.s)
+        st = ws.get(pfx + ".st", 2 * S + 8, torch.float64).data_ptr()
         Z = ws.f(pfx + ".Z", B * S * C)
-        self.gemm(0, 0, S, C, L_, 1.0 / L_, a, L_, S * L_, X, C, L_ * C, 0.0, Z, C, S * C, B, None, None, 0, 0, 0,
-                       None)
+        self.L.vc_tl_fwd(self.train, B, L_, C, S, X, C, mx, avg, self.P[pfx + ".tokenizers.0.conv.0.weight"],
+                         self.BUF[pfx + ".tokenizers.0.conv.1.running_mean"], BN_EPS, BN_MOM, tlw, st, None, Z, self.s)
         return Z
 
     def block(self, blk, pfx, X, H):
@@ -985,12 +996,24 @@ class _Program:
 
     def defer_wgrad(self, defer, M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=0):
         """C[M,N] = A^T B (a weight gradient, mm_tn), now or -- defer on lane 0 with lanes on -- at the next
-        flush_wgrads()"""
+        flush_wgrads().  On lane 1 (_DEFER_REDUCE) the product runs now, in the chain's grouped launch, but its
+        split-K reduction is queued for the weight-gradient lane (GEMM_DEFER: the slabs wait in a buffer of
+        the product's own), so the chain's next kernel does not wait for it."""
         if self._deferring(defer):
             (self.pending_wgrads if self.cur == 0 else self.pending_wgrads1).append(
                 lambda: self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad))
-        else:
-            self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad)
+            return
+        if defer and _DEFER_REDUCE and self.lanes_on and self.cur == 1:
+            fl = self.gemm_flags if K >= _BF16_MIN_K else 0
+            need = self.L.vc_gemm_defer_floats(1, 0, M, N, K, A, lda, Bm, ldb, 1, 1 if bias_grad else 0, fl,
+                                               self.scr_n)
+            if need > 0:
+                buf = (self.ws.f("defer.%x" % C, need), need)
+                self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad, flags=GEMM_DEFER, ws=buf)
+                self.pending_wgrads1.append(lambda: self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad,
+                                                               flags=GEMM_REDUCE_ONLY, ws=buf))
+                return
+        self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad)
 
     def flush_wgrads(self):
         """issue the queued parameter-gradient work (weight-gradient GEMMs, grouped; LayerNorm and scan
@@ -1076,21 +1099,14 @@ class _Program:
         self.bn_bwd(pfx + ".bn", pfx + ".bn", dxbn, Cin, X, Cin, 0, B * H * H, Cin, dX, Cin, beta_dx)
 
     def token_learner_bwd(self, pfx, X, L_, C, S, dZ, dX):
-        """dX (overwritten) = gradient of the TokenLearner input."""
+        """dX (overwritten) = gradient of the TokenLearner input; the tokenizers' parameter gradients"""
         B, ws = self.B, self.ws
         rows = B * L_
-        a, st = ws.f(pfx + ".a", B * S * L_), ws.get(pfx + ".st", 2 * S, torch.float64).data_ptr()
+        st = ws.get(pfx + ".st", 2 * S + 8, torch.float64).data_ptr()
         da = ws.f(pfx + ".da", B * S * L_)
-        with self.gemm_group():
-            self.gemm(0, 1, S, L_, C, 1.0 / L_, dZ, C, S * C, X, C, L_ * C, 0.0, da, L_, S * L_, B, None, None, 0, 0,
-                      0, None)
-            self.gemm(1, 0, L_, C, S, 1.0 / L_, a, L_, S * L_, dZ, C, S * C, 0.0, dX, C, L_ * C, B, None, None, 0, 0,
-                      0, None)
-        df = ws.f(pfx + ".df", S * rows)
-        par = self.P[pfx + ".tokenizers.0.conv.0.weight"]
-        self.L.vc_tl_attn_bwd(self.train, B, L_, S, ws.f(pfx + ".mx", rows), ws.f(pfx + ".avg", rows), par, st, da, df,
-                              self.G[pfx + ".tokenizers.0.conv.0.weight"], self.s)
-        self.L.vc_tl_pixel_bwd(rows, C, S, df, par, ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), dX, C, self.s)
+        self.L.vc_tl_bwd(self.train, B, L_, C, S, X, C, ws.f(pfx + ".mx", rows), ws.f(pfx + ".avg", rows),
+                         ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), self.P[pfx + ".tokenizers.0.conv.0.weight"],
+                         st, dZ, da, self.tl_ws(pfx, L_, S), dX, C, self.G[pfx + ".tokenizers.0.conv.0.weight"], self.s)
 
     def block_bwd(self, blk, pfx, X, H, dOut, dX, dx_ready):
         """dX (accumulated, beta=1) = gradient w.r.t. the block input, or None to skip input grads;
