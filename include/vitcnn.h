@@ -71,6 +71,12 @@ VC_API int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha, 
  * library keeps none and accepts only the automatic configuration (0, 0, 0, 0, -1). */
 VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
 
+/* C [M, N] = A [M, K] W [N, K]^T + bias on the pipelined kernel (no split-K; flags & 2: bf16 operands) with the
+ * BatchNorm statistics partials of C computed in the epilogue: colstats [ceil(M/64)][2][N] fp64 sums of (C - bias)
+ * and (C - bias)^2 per 64-row tile -- the conv1x1 + BN forward's statistics pass folded into its GEMM
+ * (vc_bn_apply_partials finishes the BatchNorm).  A, W 16-B aligned, K, lda, ldw multiples of 4. */
+VC_API int vc_gemm_colstats(int M, int N, int K, const float* A, long lda, const float* W, long ldw, const float* bias,
+                            float* C, long ldc, int flags, double* colstats, hipStream_t stream);
 /* Deferred split-K reduction: flags&128 (F_DEFER) -- the product's split-K slabs go to the caller's `ws` (a
  * buffer of its own, from its start, left intact) and are NOT reduced; a later call with the same arguments
  * and flags&256 (F_REDUCE_ONLY) launches only that reduction (inside a group: it joins the group's one
@@ -168,6 +174,13 @@ VC_API int vc_bn_bwd_ex(int train, long M, int C, const float* dy, long lddy, co
                         const float* relu_out, long ldo, const float* mean, const float* invstd, const float* w,
                         float* dx, long lddx, float beta_dx, float* dw, float* db, float beta_w,
                         float* ws, long ws_floats, unsigned int* counters, int n_counters, hipStream_t stream);
+/* train-mode BatchNorm forward from fp64 partials another kernel produced ([P][2][C]: per partial p, sum (x - shift[c])
+ * and sum (x - shift[c])^2 over its rows; vc_gemm_colstats writes them with P = ceil(M / 64), shift = its bias):
+ * save_* and the running statistics as vc_bn_forward, y = relu?(BN(x)); one launch */
+VC_API int vc_bn_apply_partials(long M, int C, const float* x, long ldx, int P, const double* part, const float* shift,
+                                float eps, float momentum, float* save_mean, float* save_invstd, float* run_mean,
+                                float* run_var, const float* w, const float* b, int relu, float* y, long ldy,
+                                hipStream_t stream);
 /* vc_bn_bwd_ex through the ReLU that follows the BatchNorm, its decisions recomputed from x, the saved
  * statistics and the affine (w, b) with the forward's own arithmetic instead of read from the forward's
  * output: bit-identical to vc_bn_bwd_ex with relu_out = that output, one [M, C] read less per pass. */

@@ -667,6 +667,40 @@ def test_bn_glf_combine_matches_stats_then_combine(L, M, C):
         assert torch.equal(a_, b_)
 
 
+@pytest.mark.parametrize("M,N,K,bf", [(3136, 256, 512, 0), (1600, 144, 288, 0), (3136, 128, 272, 0),
+                                     (1600, 128, 176, 0), (130, 72, 40, 0), (3136, 256, 512, 1)])
+def test_gemm_colstats_and_bn_apply_partials(L, M, N, K, bf):
+    """vc_gemm_colstats (conv1x1 with the BatchNorm statistics partials in the GEMM epilogue) + vc_bn_apply_partials
+    == the GEMM, then train-mode BatchNorm2d + ReLU, in float64 (running statistics included)"""
+    A = (rnd(M, K, seed=71) + 0.3).to(DEV)
+    W = (rnd(N, K, seed=72) * 0.2).to(DEV)
+    bias = (rnd(N, seed=73) + 2.0).to(DEV)
+    g, bb = (rnd(N, seed=74) + 1.0).to(DEV), rnd(N, seed=75).to(DEV)
+    P_ = -(-M // 64)
+    pre = torch.full((M, N), float("nan"), device=DEV)
+    cs = torch.full((2 * P_ * N,), float("nan"), dtype=torch.float64, device=DEV)
+    assert L.vc_gemm_colstats(M, N, K, P(A), K, P(W), K, P(bias), P(pre), N, 2 if bf else 0, P(cs), S()) == 0
+    rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+    mean, inv = torch.empty(N, device=DEV), torch.empty(N, device=DEV)
+    y = torch.full((M, N), float("nan"), device=DEV)
+    assert L.vc_bn_apply_partials(M, N, P(pre), N, P_, P(cs), P(bias), 1e-5, 0.1, P(mean), P(inv), P(rm), P(rv), P(g),
+                                  P(bb), 1, P(y), N, S()) == 0
+    torch.cuda.synchronize()
+    A64, W64 = A.cpu().double(), W.cpu().double()
+    if bf:   # the bf16 operands the MFMAs see
+        A64, W64 = A.cpu().bfloat16().double(), W.cpu().bfloat16().double()
+    ref_pre = A64 @ W64.t() + bias.cpu().double()
+    assert rel_err(pre.cpu(), ref_pre) < 1e-5
+    # the BatchNorm of the GEMM's own (fp32) output, float64
+    x = pre.cpu().double()
+    rm64, rv64 = torch.zeros(N, dtype=torch.float64), torch.ones(N, dtype=torch.float64)
+    ref_y = torch.relu(torch.nn.functional.batch_norm(x, rm64, rv64, g.cpu().double(), bb.cpu().double(), True, 0.1,
+                                                      1e-5))
+    assert rel_err(y.cpu(), ref_y) < 1e-5
+    assert rel_err(mean.cpu(), x.mean(0)) < 1e-6
+    assert rel_err(rm.cpu(), rm64) < 1e-6 and rel_err(rv.cpu(), rv64) < 1e-6
+
+
 @pytest.mark.parametrize("M,C,relu", [(3136, 256, 1), (5184, 144, 0), (37, 200, 1)])
 def test_bn_ex_counters_do_not_change_results(L, ws, M, C, relu):
     """vc_bn_forward_ex / vc_bn_bwd_ex with arrival counters == without, bit for bit, and the counters are

@@ -55,6 +55,10 @@ struct GemmArgs {
   float* part;                        // split-K partial slabs [batch*nsplit][M][Ne]
   unsigned int* cnt;                  // per-tile arrival counters (zero on entry, left zero) or null
   Epi epi;
+  // BatchNorm statistics of the output (gemm_pipe, nsplit == 1 only; vc_gemm_colstats): per 64-row tile ym and
+  // column n, fp64 sum (y - shift[n]) -> colstats[ym * 2 N + n] and sum (y - shift[n])^2 -> [... + N + n]
+  double* colstats = nullptr;
+  const float* shift = nullptr;
 };
 
 __device__ __forceinline__ void store_out(const GemmArgs& g, int zb, int m, int n, float acc) {
@@ -765,6 +769,54 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
   }
 
   // C/D map of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
+  if (g.colstats) {   // the output's BatchNorm statistics partials (single slice: the values are final)
+    double cs[NT][2];
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni) {
+      const int n = n0 + wn * WTN + ni * 16 + (lane & 15);
+      const double k = n < g.N ? (double)g.shift[n] : 0.0;
+      double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + r;
+          if (m < g.M && n < g.N) {
+            float* cp = g.C + (long)m * g.ldc + n;
+            const float v = epilogue(g.epi, acc[0][mi][ni][r], cp, m, n);
+            *cp = v;
+            const double d = (double)v - k;
+            s1 += d;
+            s2 += d * d;
+          }
+        }
+      // the 4 row groups of the wave (lanes c, c + 16, c + 32, c + 48), pairwise in a fixed order
+      s1 += __shfl_xor(s1, 16, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      cs[ni][0] = s1;
+      cs[ni][1] = s2;
+    }
+    // the WM row waves of the tile: through the idle LDS ring (all waves are past their last k-tile reads)
+    double* red = reinterpret_cast<double*>(smem);   // [2][WM][BN]
+    __syncthreads();
+    if (lane < 16)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) red[(j * WM + wm) * BN + wn * WTN + ni * 16 + lane] = cs[ni][j];
+    __syncthreads();
+    for (int t = tid; t < 2 * BN; t += NTH) {
+      const int j = t / BN, cl = t - j * BN, n = n0 + cl;
+      if (n >= g.N) continue;
+      double v = red[(j * WM) * BN + cl];
+#pragma unroll
+      for (int w2 = 1; w2 < WM; ++w2) v += red[(j * WM + w2) * BN + cl];
+      g.colstats[(long)ym * 2 * g.N + (long)j * g.N + n] = v;
+    }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
@@ -1363,6 +1415,32 @@ VC_EXPORT int vc_gemm_group_add(void* group, int transA, int transB, int M, int 
                            n_counters, st->stream, st);
   if (rc && !st->err) st->err = rc;
   return rc;
+}
+
+// C[M, N] = A[M, K] W[N, K]^T + bias (fp32 or, flags & 2, bf16 operands) on the pipelined kernel without split-K,
+// with the BatchNorm statistics partials of C written by the epilogue (shift = bias): colstats [ceil(M/64)][2][N]
+// fp64, the layout vc_bn_apply_partials reduces.  Needs the pipelined kernel's operand alignment (else 1).
+VC_EXPORT int vc_gemm_colstats(int M, int N, int K, const float* A, long lda, const float* W, long ldw,
+                               const float* bias, float* C, long ldc, int flags, double* colstats, hipStream_t stream) {
+  VC_REQUIRE(M > 0 && N > 0 && K > 0 && bias && colstats);
+  VC_REQUIRE(pipe_fits(0, 1, M, N, K, A, lda, W, ldw, 1, nullptr));
+  const bool bf = (flags & F_BF16) != 0;
+  PipePlan p = plan_pipe(M, N, K, 0, false, bf);   // no workspace: no split
+  VC_REQUIRE(p.nsplit == 1 && p.bm == 64 && p.bn == 64 && p.ns == 2);
+  Epi epi{1.f, 0.f, bias, nullptr, 0, M, 0};
+  GemmArgs g{M, N, K, N, p.k_chunk, 1, A, lda, 0, W, ldw, 0, C, ldc, 0, nullptr, nullptr, nullptr, epi};
+  g.colstats = colstats;
+  g.shift = bias;
+  const long total = (long)p.tn * p.tm;
+  dim3 grid((unsigned)total);
+  if (bf)
+    hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2, true>), grid, dim3(256), 0, stream, g, p.tn, p.tm,
+                       (unsigned)total, 1, 1);
+  else
+    hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2>), grid, dim3(256), 0, stream, g, p.tn, p.tm,
+                       (unsigned)total, 1, 1);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
 }
 
 // floats of the caller-owned slab buffer an F_DEFER call of this problem writes (0: no split, nothing deferred),

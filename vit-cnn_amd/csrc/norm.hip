@@ -297,19 +297,22 @@ __device__ __forceinline__ void bn_apply_rows(const float* __restrict__ x, long 
 // Fused final + apply (train mode): grid (ceil(C/64), ceil(M/rows_per_block)); every block reduces
 // the channel group's partials itself (bn_part_sums), the blocks of row 0 write save_* and the running
 // statistics, and all apply y = relu?((x - mean) * invstd * w + b) to their rows.
+// shift: the per-channel shift of the partial sums (x itself, i.e. row 0, for bn_stats_sums' partials; the GEMM's
+// bias for vc_gemm_colstats' epilogue partials)
 __global__ __launch_bounds__(BN_T) void bn_apply_stats(int M, int C, const float* __restrict__ x, long ldx, int P,
                                                       const double* __restrict__ part, float eps, float momentum,
                                                       float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                                       float* __restrict__ run_mean, float* __restrict__ run_var,
                                                       const float* __restrict__ w, const float* __restrict__ b,
-                                                      int relu, float* __restrict__ y, long ldy, int rows_per_block) {
+                                                      int relu, float* __restrict__ y, long ldy, int rows_per_block,
+                                                      const float* __restrict__ shift) {
   __shared__ double tot[2][64];
   bn_part_sums(P, C, part, blockIdx.x, tot);
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   if (c >= C) return;
   float mf, isf;
-  bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, x, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
+  bn_stats_from_sums(tot[0][cl], tot[1][cl], c, M, shift, eps, momentum, mf, isf, save_mean, save_invstd, run_mean,
                      run_var, blockIdx.y == 0 && rl == 0);
   const long r0 = (long)blockIdx.y * rows_per_block;
   bn_apply_rows(x, ldx, mf, isf, w[c], b[c], relu, y, ldy, r0, min((long)M, r0 + rows_per_block), c, rl);
@@ -908,7 +911,21 @@ VC_EXPORT int vc_bn_forward_ex(int train, long M, int C, const float* x, long ld
   VC_CHECK_LAUNCH();
   const int rpb = bn_apply_rows();
   hipLaunchKernelGGL(bn_apply_stats, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, (int)M, C, x, ldx,
-                     P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy, rpb);
+                     P, wsd, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy, rpb, x);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+// train-mode BatchNorm forward from fp64 partials another kernel left (vc_gemm_colstats: P = ceil(M / 64) row tiles,
+// [P][2][C] sums of (x - shift[c]) and (x - shift[c])^2): one launch, statistics + running stats + apply (+ ReLU)
+VC_EXPORT int vc_bn_apply_partials(long M, int C, const float* x, long ldx, int P, const double* part,
+                                   const float* shift, float eps, float momentum, float* save_mean, float* save_invstd,
+                                   float* run_mean, float* run_var, const float* w, const float* b, int relu, float* y,
+                                   long ldy, hipStream_t stream) {
+  VC_REQUIRE(C > 0 && M > 0 && M < (1L << 31) && P > 0 && P <= 65535 && part && shift);
+  const int rpb = bn_apply_rows();
+  hipLaunchKernelGGL(bn_apply_stats, dim3(vc_cdiv(C, 64), vc_cdiv(M, rpb)), dim3(BN_T), 0, stream, (int)M, C, x, ldx,
+                     P, part, eps, momentum, save_mean, save_invstd, run_mean, run_var, w, b, relu, y, ldy, rpb, shift);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

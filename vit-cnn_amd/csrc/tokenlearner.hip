@@ -35,7 +35,7 @@
 namespace {
 
 constexpr int TPAR = 5, TBUF = 2;
-constexpr int PS_RW = 16;            // pixel rows per wave in pixel_stats
+constexpr int PS_RW = 4;             // pixel rows per wave in pixel_stats (one batch of loads)
 constexpr int PS_ROWS = 4 * PS_RW;   // rows per 256-thread block = one moment partial
 constexpr int NMOM = 5;              // partial: sum dm, sum dv, sum dm^2, sum dm dv, sum dv^2
 constexpr int NBS = 4;               // backward partial: s1, s2, sum g1 (m - mbar), sum g1 (v - vbar)
@@ -61,19 +61,19 @@ __device__ __forceinline__ void block256_sums_d(double (&v)[K], double* red) {
   __syncthreads();
 }
 
-// max (+ first argmax) and mean of RB pixel rows, wave-wide (every lane gets the results): the rows' loads
-// are issued together (one latency per RB rows), then each row is scanned in channel order -- per row the
-// same arithmetic as a one-row pass, so the results do not depend on RB.  C <= 512 (host check).
+// max (+ first argmax) and mean of RB pixel rows (row indices rows[k], valid when rows[k] >= 0), wave-wide (every
+// lane gets the results): the rows' loads are issued together (one latency for RB rows), then each row is scanned
+// in channel order -- per row the same arithmetic as a one-row pass, whatever RB.  C <= 512 (host check).
 template <int RB>
-__device__ __forceinline__ void rows_stats(const float* __restrict__ x, long ldx, int r0, int nr, int C, int lane,
-                                           float (&best)[RB], int (&bi)[RB], float (&mean)[RB]) {
+__device__ __forceinline__ void rows_stats(const float* __restrict__ x, long ldx, const int (&rows)[RB], int C,
+                                           int lane, float (&best)[RB], int (&bi)[RB], float (&mean)[RB]) {
   float xv[RB][8];
 #pragma unroll
   for (int k = 0; k < RB; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = lane + 64 * j;
-      xv[k][j] = (k < nr && c < C) ? x[(long)(r0 + k) * ldx + c] : 0.f;
+      xv[k][j] = (rows[k] >= 0 && c < C) ? x[(long)rows[k] * ldx + c] : 0.f;
     }
 #pragma unroll
   for (int k = 0; k < RB; ++k) {
@@ -106,54 +106,45 @@ __device__ __forceinline__ void rows_stats(const float* __restrict__ x, long ldx
   }
 }
 
-constexpr int PS_RB = 4;   // rows per batch of loads
-
-// Block = PS_ROWS pixel rows (4 waves x PS_RW rows): mx / amx / avg per row, and the block's moment
-// partial of (max, mean) shifted by row 0's values -> part[blockIdx.x * NMOM + j] (part may be null)
+// Block = PS_ROWS pixel rows, PS_RW per wave, loaded in one batch together with row 0 (the moments' shift K:
+// the same code, so the same values as mx[0], avg[0]): mx / amx / avg per row, and the block's moment partial
+// of (max, mean) -> part[blockIdx.x * NMOM + j] (part may be null)
 __global__ __launch_bounds__(256) void pixel_stats(int M, int C, const float* __restrict__ x, long ldx,
                                                    float* __restrict__ mx, int* __restrict__ amx,
                                                    float* __restrict__ avg, double* __restrict__ part) {
   __shared__ float sm[PS_ROWS], sv[PS_ROWS];
   __shared__ double red[NMOM * 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r0 = blockIdx.x * PS_ROWS;
-  float km, kv;   // the shift: row 0's pooled values (the same code, so the same values as mx[0], avg[0])
-  if (part) {
-    float b1[1], m1[1];
-    int i1[1];
-    rows_stats<1>(x, ldx, 0, 1, C, lane, b1, i1, m1);
-    km = b1[0];
-    kv = m1[0];
-  }
+  const int r0 = blockIdx.x * PS_ROWS + w * PS_RW;
+  int rows[PS_RW + 1];
+  rows[0] = part ? 0 : -1;
 #pragma unroll
-  for (int j0 = 0; j0 < PS_RW; j0 += PS_RB) {
-    const int rl = w * PS_RW + j0, r = r0 + rl;
-    const int nr = min(PS_RB, M - r);
-    if (nr <= 0) break;
-    float best[PS_RB], mean[PS_RB];
-    int bi[PS_RB];
-    rows_stats<PS_RB>(x, ldx, r, nr, C, lane, best, bi, mean);
-    if (lane < nr) {   // lane k stores row k
-      float bk = best[0], mk = mean[0];
-      int ik = bi[0];
+  for (int k = 0; k < PS_RW; ++k) rows[k + 1] = r0 + k < M ? r0 + k : -1;
+  float best[PS_RW + 1], mean[PS_RW + 1];
+  int bi[PS_RW + 1];
+  rows_stats<PS_RW + 1>(x, ldx, rows, C, lane, best, bi, mean);
+  if (lane < PS_RW && r0 + lane < M) {   // lane k stores row k
+    float bk = best[1], mk = mean[1];
+    int ik = bi[1];
 #pragma unroll
-      for (int k = 1; k < PS_RB; ++k)
-        if (lane == k) {
-          bk = best[k];
-          mk = mean[k];
-          ik = bi[k];
-        }
-      mx[r + lane] = bk;
-      amx[r + lane] = ik;
-      avg[r + lane] = mk;
-      sm[rl + lane] = bk;
-      sv[rl + lane] = mk;
-    }
+    for (int k = 1; k < PS_RW; ++k)
+      if (lane == k) {
+        bk = best[k + 1];
+        mk = mean[k + 1];
+        ik = bi[k + 1];
+      }
+    mx[r0 + lane] = bk;
+    amx[r0 + lane] = ik;
+    avg[r0 + lane] = mk;
+    sm[w * PS_RW + lane] = bk;
+    sv[w * PS_RW + lane] = mk;
   }
   if (!part) return;
+  const float km = best[0], kv = mean[0];
   __syncthreads();
   double v[NMOM] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (threadIdx.x < PS_ROWS && r0 + (int)threadIdx.x < M) {
+  const int rb = blockIdx.x * PS_ROWS;
+  if (threadIdx.x < PS_ROWS && rb + (int)threadIdx.x < M) {
     const double dm = (double)sm[threadIdx.x] - (double)km, dv = (double)sv[threadIdx.x] - (double)kv;
     v[0] = dm;
     v[1] = dv;
@@ -425,12 +416,15 @@ __global__ __launch_bounds__(256) void tl_bwd_da(int B, int HW, int C, int S, co
 }
 
 // Backward part 2: grid (B, ceil(C / 64)); block 256.  The tokens' s1 / s2 over the batch (the per-sample
-// partials summed in sample order), then for the block's sample and 64 channels
-//   dx[b, q, c] = (1/HW) sum_s a[s][q] dZ[b, s, c]                      (MFMA; a recomputed)
+// partials summed in 4 interleaved sample quarters, then the quarters in order), then for the block's sample
+// and 64 channels
+//   dx[b, q, c] = (1/HW) sum_s a[s][q] dZ[b, s, c]                      (MFMA; a recomputed into LDS)
 //               + (sum_s w1_s df_s[q]) / C + [c == argmax_q] sum_s w0_s df_s[q]
-// with df_s[q] = gamma_s invstd_s (g1 - s1/n - xh s2/n) (train; eval gamma invstd g1) in fp64 (dx overwritten).
-// Block (0, 0) also writes the tokens' 5 parameter gradients (dparams).
-// LDS: at [Lp][Sp + 4] (a^T) + dzt [64][Sp + 4] (dZ^T of the block's channels) floats.
+// with df_s[q] = gamma_s invstd_s (g1 - s1/n - xh s2/n) (train; eval gamma invstd g1) in fp64 (dx overwritten):
+// the sums over the tokens in 8 chunks (8 adjacent lanes per pixel), then the chunks pairwise in a fixed order.
+// Block (0, 0) also writes the tokens' 5 parameter gradients (dparams).  The product runs as dx^T [c][q]: the
+// A operand (dZ rows, 16 channels x 4 tokens per MFMA) straight from L2, the B operand (a [s][q]) from LDS --
+// a small LDS footprint, so these blocks leave room for the selective-scan blocks running beside them.
 __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C, int S, const float* __restrict__ mx,
                                                  const float* __restrict__ avg, const int* __restrict__ amx,
                                                  const float* __restrict__ par, const double* __restrict__ stats,
@@ -438,129 +432,162 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
                                                  const double* __restrict__ part, float* __restrict__ dx, long lddx,
                                                  float* __restrict__ gpar) {
   extern __shared__ __attribute__((aligned(16))) float sm_f[];
-  __shared__ double q4[4][128][2];     // per token, 4 sample-quarter sums of s1, s2
-  __shared__ double tsum[2][128];      // s1, s2
-  __shared__ double pq[2][2][128];     // per pixel, two token-half sums of (gm, ga)
+  __shared__ double q4[4][128][2];     // per token, 4 sample-quarter sums of two of the partial columns
+  __shared__ double tsum[2][128];      // s1 / n, s2 / n
+  __shared__ double tst[2][128];       // mean, invstd
+  __shared__ float tpar[128][TPAR];
+  __shared__ float gq[2][128];         // per pixel: sum_s w0 df, (sum_s w1 df) / C
   const int b = blockIdx.x, c0 = blockIdx.y * TL_CT;
-  const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15, SS = Sp + 4;
-  float* at = sm_f;                 // [Lp][SS]
-  float* dzt = sm_f + Lp * SS;      // [64][SS]
+  const bool b00 = blockIdx.x == 0 && blockIdx.y == 0;
+  const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15, LS = Lp + 4;
+  float* al = sm_f;                 // [S4][LS]  a[s][q] (zero padded)
   const long n = (long)B * HW;
   const double nd = (double)n;
-  // dZ^T of the block's channels (rows of dZ are 64-channel runs: coalesced)
-  for (int i = threadIdx.x; i < Sp * TL_CT; i += 256) {
-    const int s = i / TL_CT, cl = i - s * TL_CT;
-    const int c = c0 + cl;
-    dzt[cl * SS + s] = (s < S && c < C) ? dZ[((long)b * S + s) * C + c] : 0.f;
+  for (int i = threadIdx.x; i < S * TPAR; i += 256) tpar[i / TPAR][i % TPAR] = par[i];
+  for (int s = threadIdx.x; s < S; s += 256) {
+    tst[0][s] = stats[2 * s];
+    tst[1][s] = stats[2 * s + 1];
   }
-  // s1 / s2 per token: the samples in 4 interleaved quarters, then the quarters in order
-  for (int i = threadIdx.x; i < 4 * S; i += 256) {
-    const int s = i >> 2, u = i & 3;
-    double t1 = 0.0, t2 = 0.0;
-    for (int bb0 = u; bb0 < B; bb0 += 16) {
-      double p1[4], p2[4];
+  // the batch sums of partial columns j0, j0 + 1: 4 interleaved sample quarters, then the quarters in order
+  auto batch_sums = [&](int j0) {
+    for (int i = threadIdx.x; i < 4 * S; i += 256) {
+      const int s = i >> 2, u = i & 3;
+      double t0 = 0.0, t1 = 0.0;
+      for (int bb0 = u; bb0 < B; bb0 += 16) {
+        double p0[4], p1[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int bb = bb0 + 4 * k;
-        p1[k] = bb < B ? part[((long)bb * S + s) * NBS] : 0.0;
-        p2[k] = bb < B ? part[((long)bb * S + s) * NBS + 1] : 0.0;
-      }
+        for (int k = 0; k < 4; ++k) {
+          const int bb = bb0 + 4 * k;
+          p0[k] = bb < B ? part[((long)bb * S + s) * NBS + j0] : 0.0;
+          p1[k] = bb < B ? part[((long)bb * S + s) * NBS + j0 + 1] : 0.0;
+        }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        t1 += p1[k];
-        t2 += p2[k];
+        for (int k = 0; k < 4; ++k) {
+          t0 += p0[k];
+          t1 += p1[k];
+        }
       }
+      q4[u][s][0] = t0;
+      q4[u][s][1] = t1;
     }
-    q4[u][s][0] = t1;
-    q4[u][s][1] = t2;
+    __syncthreads();
+  };
+  batch_sums(0);
+  for (int s = threadIdx.x; s < S; s += 256) {
+    tsum[0][s] = (((q4[0][s][0] + q4[1][s][0]) + q4[2][s][0]) + q4[3][s][0]) / nd;
+    tsum[1][s] = (((q4[0][s][1] + q4[1][s][1]) + q4[2][s][1]) + q4[3][s][1]) / nd;
   }
   __syncthreads();
-  for (int s = threadIdx.x; s < S; s += 256) {
-    tsum[0][s] = ((q4[0][s][0] + q4[1][s][0]) + q4[2][s][0]) + q4[3][s][0];
-    tsum[1][s] = ((q4[0][s][1] + q4[1][s][1]) + q4[2][s][1]) + q4[3][s][1];
-  }
-  if (blockIdx.x == 0 && blockIdx.y == 0) {   // parameter gradients: all four sums over the batch, sample order
+  if (b00) {   // parameter gradients: the other two partial columns too
+    batch_sums(2);
     for (int s = threadIdx.x; s < S; s += 256) {
-      double t[NBS] = {0.0, 0.0, 0.0, 0.0};
-      for (int bb = 0; bb < B; ++bb)
-#pragma unroll
-        for (int j = 0; j < NBS; ++j) t[j] += part[((long)bb * S + s) * NBS + j];
-      const float* p = par + (long)s * TPAR;
-      const double w0 = p[0], w1 = p[1], gam = p[3];
-      const double invstd = stats[2 * s + 1];
+      const double t0 = tsum[0][s] * nd, t1 = tsum[1][s] * nd;
+      const double t2 = ((q4[0][s][0] + q4[1][s][0]) + q4[2][s][0]) + q4[3][s][0];
+      const double t3 = ((q4[0][s][1] + q4[1][s][1]) + q4[2][s][1]) + q4[3][s][1];
+      const double w0 = tpar[s][0], w1 = tpar[s][1], gam = tpar[s][3];
+      const double invstd = tst[1][s];
       const double* mom = stats + 2 * S;   // n, mbar, vbar, Cmm, Cmv, Cvv
       double gw0, gw1, gb;
       if (train) {
-        const double k = t[1] / nd * invstd;
-        gw0 = gam * invstd * (t[2] - k * (w0 * mom[3] + w1 * mom[4]));
-        gw1 = gam * invstd * (t[3] - k * (w0 * mom[4] + w1 * mom[5]));
+        const double k = t1 / nd * invstd;
+        gw0 = gam * invstd * (t2 - k * (w0 * mom[3] + w1 * mom[4]));
+        gw1 = gam * invstd * (t3 - k * (w0 * mom[4] + w1 * mom[5]));
         gb = 0.0;   // sum_i df_i = gamma invstd (s1 - s1 - s2/n sum_i xh_i) and sum_i xh_i = 0
       } else {
-        gw0 = gam * invstd * (t[2] + mom[1] * t[0]);
-        gw1 = gam * invstd * (t[3] + mom[2] * t[0]);
-        gb = gam * invstd * t[0];
+        gw0 = gam * invstd * (t2 + mom[1] * t0);
+        gw1 = gam * invstd * (t3 + mom[2] * t0);
+        gb = gam * invstd * t0;
       }
       float* gp = gpar + (long)s * TPAR;
       gp[0] = (float)gw0;
       gp[1] = (float)gw1;
       gp[2] = (float)gb;
-      gp[3] = (float)t[1];
-      gp[4] = (float)t[0];
+      gp[3] = (float)t1;
+      gp[4] = (float)t0;
     }
   }
-  __syncthreads();
-  // a^T recomputed, and the pixel gradients gm / ga over two token halves (fixed order)
-  const int half = (S + 1) / 2;
-  for (int i = threadIdx.x; i < 2 * Lp; i += 256) {
-    const int q = i >> 1, h = i & 1;
+  // a recomputed into LDS, and the pixel gradients: lane group of 8 per pixel, lane k of it sums the tokens
+  // k, k + 8, ... (fixed order), then the 8 lanes pairwise
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < 8 * Lp; i += 256) {
+    const int q = i >> 3, k = i & 7;
     const bool qok = q < HW;
     const float m = qok ? mx[(long)b * HW + q] : 0.f, v = qok ? avg[(long)b * HW + q] : 0.f;
     double gm = 0.0, ga = 0.0;
-    const int sb = h * half, se = h ? S : half;
-    for (int s = sb; s < se; ++s) {
-      const float* p = par + (long)s * TPAR;
-      const double mean = stats[2 * s], invstd = stats[2 * s + 1];
-      double xh;
-      const float bn = tl_bnv(m, v, p[0], p[1], p[2], mean, invstd, p[3], p[4], xh);
-      at[q * SS + s] = qok ? sigmoid_f(fmaxf(bn, 0.f)) : 0.f;
-      if (qok) {
-        const float dav = da[((long)b * S + s) * HW + q];
+    for (int s0 = k; s0 < S4; s0 += 32) {
+      float dav[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int s = s0 + 8 * u;
+        dav[u] = (qok && s < S) ? da[((long)b * S + s) * HW + q] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int s = s0 + 8 * u;
+        if (s >= S4) continue;
+        if (s >= S || !qok) {
+          if (s < S4) al[s * LS + q] = 0.f;
+          continue;
+        }
+        const float* p = tpar[s];
+        double xh;
+        const float bn = tl_bnv(m, v, p[0], p[1], p[2], tst[0][s], tst[1][s], p[3], p[4], xh);
+        al[s * LS + q] = sigmoid_f(fmaxf(bn, 0.f));
         double g1 = 0.0;
         if (bn > 0.f) {
           const float sg = sigmoid_f(bn);
-          g1 = (double)(dav * sg * (1.f - sg));
+          g1 = (double)(dav[u] * sg * (1.f - sg));
         }
-        const double gi = (double)p[3] * invstd;
-        const double d = train ? gi * (g1 - tsum[0][s] / nd - xh * tsum[1][s] / nd) : gi * g1;
+        const double gi = (double)p[3] * tst[1][s];
+        const double d = train ? gi * (g1 - tsum[0][s] - xh * tsum[1][s]) : gi * g1;
         gm += d * (double)p[0];
         ga += d * (double)p[1];
       }
     }
-    if (h == 1)
-      for (int s = S; s < Sp; ++s) at[q * SS + s] = 0.f;
-    pq[h][0][q] = gm;
-    pq[h][1][q] = ga;
+    // 8 lanes (k = 0..7) of pixel q: ((k0 + k1) + (k2 + k3)) + ((k4 + k5) + (k6 + k7))
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      gm += __shfl_xor(gm, o, 64);
+      ga += __shfl_xor(ga, o, 64);
+    }
+    if ((lane & 7) == 0 && q < 128) {
+      gq[0][q] = (float)gm;
+      gq[1][q] = (float)(ga / (double)C);
+    }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
-  const int nqt = Lp / 16, nct = TL_CT / 16, nkc = Sp / 16;
+  // dx^T tiles: rows = channels (16 per tile), cols = pixels (16 per tile), k = tokens (4 per MFMA)
+  const int w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
+  const int nqt = Lp / 16, nct = TL_CT / 16, nk = S4 / 4;
   const float inv_l = 1.f / (float)HW;
   for (int t = w; t < nqt * nct; t += 4) {
-    const int qt = t / nct, ct = t - qt * nct;
+    const int ct = t / nqt, qt = t - ct * nqt;
+    const int ca = c0 + 16 * ct + r16;   // this lane's A row (channel)
+    const bool cok = ca < C;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nkc; ++kc) {
-      const int k = 16 * kc + 4 * g;
-      mfma_k16(ld4_lds(at + (16 * qt + r16) * SS + k), ld4_lds(dzt + (16 * ct + r16) * SS + k), acc);
-    }
-    const int c = c0 + 16 * ct + r16;
+    constexpr int KB = 8;
+    for (int k0 = 0; k0 < nk; k0 += KB) {
+      float av[KB], bv[KB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = 16 * qt + 4 * g + r;
-      if (q < HW && c < C) {
-        const float gmf = (float)(pq[0][0][q] + pq[1][0][q]);
-        const float gaf = (float)((pq[0][1][q] + pq[1][1][q]) / (double)C);
-        const int am = amx[(long)b * HW + q];
-        dx[((long)b * HW + q) * lddx + c] = acc[r] * inv_l + (gaf + (c == am ? gmf : 0.f));
+      for (int u = 0; u < KB; ++u) {
+        const int s = 4 * (k0 + u) + g;
+        av[u] = (k0 + u < nk && s < S && cok) ? dZ[((long)b * S + s) * C + ca] : 0.f;
+        bv[u] = k0 + u < nk ? al[s * LS + 16 * qt + r16] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < KB; ++u)
+        if (k0 + u < nk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+    // acc[r] = dx^T (channel c0 + 16 ct + 4 g + r, pixel 16 qt + r16): 4 adjacent channels of one pixel row
+    const int q = 16 * qt + r16, cb = c0 + 16 * ct + 4 * g;
+    if (q < HW) {
+      const float gmf = gq[0][q], gaf = gq[1][q];
+      const int am = amx[(long)b * HW + q];
+      float* dr = dx + ((long)b * HW + q) * lddx;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = cb + r;
+        if (c < C) dr[c] = acc[r] * inv_l + (gaf + (c == am ? gmf : 0.f));
       }
     }
   }
@@ -606,8 +633,8 @@ static size_t tl_fwd_lds(int HW, int S) {
   return (size_t)(Sp + TL_CT) * (Lp + 4) * sizeof(float);
 }
 static size_t tl_bwd_lds(int HW, int S) {
-  const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15;
-  return (size_t)(Lp + TL_CT) * (Sp + 4) * sizeof(float);
+  const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15;
+  return (size_t)S4 * (Lp + 4) * sizeof(float);
 }
 
 VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,

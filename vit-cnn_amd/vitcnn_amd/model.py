@@ -69,7 +69,9 @@ GEMM_DEFER = 128           # vc_gemm flags: split-K slabs left unreduced in the 
 GEMM_REDUCE_ONLY = 256     # vc_gemm flags: only the reduction of an earlier GEMM_DEFER product
 # lane 1's weight-gradient split-K reductions queued for the weight-gradient lane (the products stay in the
 # chain's grouped launches): every grouped launch of the lane-1 backward chain loses its reduce launch
-_DEFER_REDUCE = True
+_DEFER_REDUCE = False   # measured slower: 1.74-1.79 -> 2.00-2.09 ms (profiles/r05_ab_defer_reduce.log)
+# conv1x1 + BatchNorm (+ ReLU) forward: the statistics partials computed in the GEMM epilogue (vc_gemm_colstats)
+_GEMM_BNSTATS = True
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 # the Mamba direction conv + x_proj folded into the scan launch and the dt_proj / x_proj data gradients +
@@ -730,10 +732,21 @@ class _Program:
     def conv1x1_bn_relu(self, seq, X, M, Cin, Cout):
         """Sequential(Conv2d 1x1, BatchNorm2d, ReLU) (FusionLayer of GLfusionBlock / fusionBlock)."""
         pre = self.ws.f(seq + ".pre", M * Cout)
-        self.mm_nt(M, Cout, Cin, X, Cin, self.P[seq + ".0.weight"], Cin, pre, Cout, bias=self.P[seq + ".0.bias"])
         tag, ws = seq + ".1", self.ws
         mean, inv = ws.f(tag + ".bm", Cout), ws.f(tag + ".bi", Cout)
         out = ws.f(seq + ".out", M * Cout)
+        W, bias = self.P[seq + ".0.weight"], self.P[seq + ".0.bias"]
+        if self.train and _GEMM_BNSTATS and Cin % 4 == 0 and X % 16 == 0 and W % 16 == 0:
+            # the BatchNorm statistics pass folded into the GEMM's epilogue (partials per 64-row tile, shift = the
+            # conv bias), then one statistics + apply + ReLU launch: 2 launches instead of 3
+            P_ = -(-M // 64)
+            cs = ws.get(seq + ".cs", 2 * P_ * Cout, torch.float64).data_ptr()
+            self.L.vc_gemm_colstats(M, Cout, Cin, X, Cin, W, Cin, bias, pre, Cout, self.gemm_flags, cs, self.s)
+            self.L.vc_bn_apply_partials(M, Cout, pre, Cout, P_, cs, bias, BN_EPS, BN_MOM, mean, inv,
+                                        self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"],
+                                        self.P[tag + ".weight"], self.P[tag + ".bias"], 1, out, Cout, self.s)
+            return out
+        self.mm_nt(M, Cout, Cin, X, Cin, W, Cin, pre, Cout, bias=bias)
         # statistics partials + the channel-tiled apply that reduces them (two launches), include/vitcnn.h
         self.L.vc_bn_forward_ex(self.train, M, Cout, pre, Cout, BN_EPS, BN_MOM, mean, inv,
                                 self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"],
