@@ -17,7 +17,7 @@ PROBE_PATH = os.path.join(_REPO, "vit-cnn_amd", "vitcnn_amd", "libvitcnn_probe.s
 # the C ABI's kernel knobs (read by libvitcnn_probe.so only, common.h vc_knob)
 PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITCNN_BN_PCAP", "VITCNN_BN_APPLY_ROWS", "VITCNN_BN_IM2COL",
                "VITCNN_BN_GLF", "VITCNN_SCAN_RBS", "VITCNN_SCAN_SELECT_RS", "VITCNN_SCAN_TAIL",
-               "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE",
+               "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE", "VITCNN_GEMM_PIPE_SMALL",
                "VITCNN_PIPE_NS", "VITCNN_GEMM_GROUP_MAXB",
                "VITCNN_TAP_TARGET", "VITCNN_TAP_PIPE", "VITCNN_CONV_PIPE_TILES_F", "VITCNN_CONV_PIPE_TILES_W",
                "VITCNN_CONV_PIPE_TILES_D")
@@ -55,6 +55,7 @@ SWITCHES = {
     "VITCNN_FUSAT_IM2COL": ("fusatnet", "_TAP_CONV", lambda v: not _FLAG(v)),
     "VITCNN_DEFER_REDUCE": ("model", "_DEFER_REDUCE", _FLAG),
     "VITCNN_GEMM_BNSTATS": ("model", "_GEMM_BNSTATS", _FLAG),
+    "VITCNN_PG_LANE2": ("model", "_PG_LANE2", _FLAG),
 }
 
 

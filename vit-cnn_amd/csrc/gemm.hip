@@ -1090,9 +1090,14 @@ static bool pipe_fits(int transA, int transB, int M, int N, int K, const float* 
   return ab < (1L << 31) && bb < (1L << 31);
 }
 
-// the shapes it pays on (tools/gemm_census.py): enough work per launch that the pipeline fills
+// the shapes it pays on (tools/gemm_census.py, profiles/r04_gemm_census.log): enough work per launch that the
+// pipeline fills, and (round 5) the small ones of the step with K <= 4096 and an output of >= 2048 elements --
+// the NonLocal / hsi2 products of 1600 rows, 2-3 us faster each than on the k-major kernel; the long-K skinny
+// weight gradients (K = 10 B L rows, M or N < 64) stay on the k-major kernel, which was faster there
 static bool pipe_wanted(int M, int N, int K) {
-  return vc_knob("VITCNN_GEMM_PIPE", 1) && (long)M * N * K >= (1L << 24) && K >= 128 && M >= 128 && N >= 64;
+  if (!vc_knob("VITCNN_GEMM_PIPE", 1)) return false;
+  if ((long)M * N * K >= (1L << 24) && K >= 128 && M >= 128 && N >= 64) return true;
+  return vc_knob("VITCNN_GEMM_PIPE_SMALL", 1) && K <= 4096 && M >= 16 && N >= 16 && (long)M * N >= 2048;
 }
 
 struct PipePlan {

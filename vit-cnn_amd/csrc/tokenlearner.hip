@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void tl_bwd_da(int B, int HW, int C, int S, co
     const int qb = 16 * qt + r16;   // this lane's B column (pixel)
     const float* brow = x + ((long)b * HW + min(qb, HW - 1)) * ldx;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    constexpr int KB = 4;   // k chunks whose loads are issued together
+    constexpr int KB = 4;   // k chunks whose loads are issued together (8: 182 VGPRs, slower)
     for (int kc0 = 0; kc0 < nkc; kc0 += KB) {
       f32x4 av[KB], bv[KB];
 #pragma unroll
@@ -441,8 +441,22 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
   const bool b00 = blockIdx.x == 0 && blockIdx.y == 0;
   const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15, LS = Lp + 4;
   float* al = sm_f;                 // [S4][LS]  a[s][q] (zero padded)
+  float* dzl = sm_f + S4 * LS;      // [S4][64 + 4]  dZ[b, s, c0 + cl] (zero padded)
+  constexpr int DZS = TL_CT + 4;
   const long n = (long)B * HW;
   const double nd = (double)n;
+  for (int i = threadIdx.x; i < S4 * (TL_CT / 4); i += 256) {   // float4 runs of the block's 64 channels
+    const int s = i / (TL_CT / 4), c4 = 4 * (i - s * (TL_CT / 4)), c = c0 + c4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (s < S) {
+      const float* src = dZ + ((long)b * S + s) * C + c;
+      if (c + 3 < C) v = *reinterpret_cast<const f32x4*>(src);
+      else
+        for (int j = 0; j < 4; ++j)
+          if (c + j < C) v[j] = src[j];
+    }
+    *reinterpret_cast<f32x4*>(dzl + s * DZS + c4) = v;
+  }
   for (int i = threadIdx.x; i < S * TPAR; i += 256) tpar[i / TPAR][i % TPAR] = par[i];
   for (int s = threadIdx.x; s < S; s += 256) {
     tst[0][s] = stats[2 * s];
@@ -562,21 +576,11 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
   const float inv_l = 1.f / (float)HW;
   for (int t = w; t < nqt * nct; t += 4) {
     const int ct = t / nqt, qt = t - ct * nqt;
-    const int ca = c0 + 16 * ct + r16;   // this lane's A row (channel)
-    const bool cok = ca < C;
+    const int cl = 16 * ct + r16;   // this lane's A row (channel, block-local)
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    constexpr int KB = 8;
-    for (int k0 = 0; k0 < nk; k0 += KB) {
-      float av[KB], bv[KB];
-#pragma unroll
-      for (int u = 0; u < KB; ++u) {
-        const int s = 4 * (k0 + u) + g;
-        av[u] = (k0 + u < nk && s < S && cok) ? dZ[((long)b * S + s) * C + ca] : 0.f;
-        bv[u] = k0 + u < nk ? al[s * LS + 16 * qt + r16] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < KB; ++u)
-        if (k0 + u < nk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    for (int k = 0; k < nk; ++k) {
+      const int s = 4 * k + g;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dzl[s * DZS + cl], al[s * LS + 16 * qt + r16], acc, 0, 0, 0);
     }
     // acc[r] = dx^T (channel c0 + 16 ct + 4 g + r, pixel 16 qt + r16): 4 adjacent channels of one pixel row
     const int q = 16 * qt + r16, cb = c0 + 16 * ct + 4 * g;
@@ -634,7 +638,7 @@ static size_t tl_fwd_lds(int HW, int S) {
 }
 static size_t tl_bwd_lds(int HW, int S) {
   const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15;
-  return (size_t)S4 * (Lp + 4) * sizeof(float);
+  return (size_t)S4 * (Lp + 4 + TL_CT + 4) * sizeof(float);
 }
 
 VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,

@@ -72,6 +72,8 @@ GEMM_REDUCE_ONLY = 256     # vc_gemm flags: only the reduction of an earlier GEM
 _DEFER_REDUCE = False   # measured slower: 1.74-1.79 -> 2.00-2.09 ms (profiles/r05_ab_defer_reduce.log)
 # conv1x1 + BatchNorm (+ ReLU) forward: the statistics partials computed in the GEMM epilogue (vc_gemm_colstats)
 _GEMM_BNSTATS = True
+# GLfusion forward: the NonLocal phi | g projection on the channel lane (2) right after ln4, theta alone on lane 1
+_PG_LANE2 = True
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 # the Mamba direction conv + x_proj folded into the scan launch and the dt_proj / x_proj data gradients +
@@ -869,6 +871,11 @@ class _Program:
                        bias=P[pfx + ".channel_feature.bias"])
             Zc = self.token_learner(pfx + ".channel_token", CF, L_, Cout, S)
             Fc = self.layernorm(pfx + ".ln4", Zc, B * S, Cout, pfx + ".Fc")
+            if _PG_LANE2 and self.lanes_on:
+                # the NonLocal phi | g projection of Fc on this lane, beside lane 1's local conv (_PG_LANE2)
+                nl = pfx + ".FusionLayer.cross_attention"
+                self.mm_nt(B * S, 2 * Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, ws.f(pfx + ".PG", B * S * 2 * Ci),
+                           2 * Ci, bias=P[nl + ".phi.0.bias"])
             e_fc = self.mark()
         with self.lane(1, e_fc):
             FM = self.glfusion(pfx, Fl, Fc, Cout, S, Ci, Pk, Hs)
@@ -883,9 +890,10 @@ class _Program:
         PG = ws.f(pfx + ".PG", M * 2 * Ci)
         with self.gemm_group():
             self.mm_nt(M, Ci, Cout, Fl, Cout, P[nl + ".theta.weight"], Cout, TH, Ci, bias=P[nl + ".theta.bias"])
-            # phi | g as one product over their stacked weights / biases (_build_flat keeps them adjacent)
-            self.mm_nt(M, 2 * Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, PG, 2 * Ci,
-                       bias=P[nl + ".phi.0.bias"])
+            if not (_PG_LANE2 and self.lanes_on):
+                # phi | g as one product over their stacked weights / biases (_build_flat keeps them adjacent)
+                self.mm_nt(M, 2 * Ci, Cout, Fc, Cout, P[nl + ".phi.0.weight"], Cout, PG, 2 * Ci,
+                           bias=P[nl + ".phi.0.bias"])
         PP = ws.f(pfx + ".PP", B * Pk * 2 * Ci)
         PA = ws.get(pfx + ".PA", B * Pk * 2 * Ci, torch.uint8).data_ptr()
         ATT, O = ws.f(pfx + ".ATT", M * Pk), ws.f(pfx + ".O", M * Ci)
