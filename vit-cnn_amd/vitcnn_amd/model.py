@@ -73,7 +73,7 @@ _DEFER_REDUCE = False   # measured slower: 1.74-1.79 -> 2.00-2.09 ms (profiles/r
 # conv1x1 + BatchNorm (+ ReLU) forward: the statistics partials computed in the GEMM epilogue (vc_gemm_colstats)
 _GEMM_BNSTATS = True
 # GLfusion forward: the NonLocal phi | g projection on the channel lane (2) right after ln4, theta alone on lane 1
-_PG_LANE2 = True
+_PG_LANE2 = False   # measured slower: 1.745 -> 1.758-1.762 ms (profiles/r05_ab_pg_lane2.log)
 N_COUNTERS = 1 << 16       # split-K tile counters per stream
 
 # the Mamba direction conv + x_proj folded into the scan launch and the dt_proj / x_proj data gradients +
