@@ -446,6 +446,9 @@ __device__ __forceinline__ float reduce_scatter8_row(const float (&v)[8]) {
 // written by exactly one of them.  Same partners and operand order as reduce_scatter8_row, so the
 // result is bit-identical.  s_nop 1: the DPP operands may have been written by the two preceding VALU
 // instructions.
+#ifndef VC_DPP_PAIRWISE
+#define VC_DPP_PAIRWISE 0   // 1: the per-pair blocks below (one s_nop each) instead of dpp_stage12
+#endif
 template <int CTRL_ASM>
 __device__ __forceinline__ float dpp_pair_add(float a, float b);
 template <>
@@ -468,14 +471,41 @@ __device__ __forceinline__ float dpp_pair_add<1>(float a, float b) {   // row_ha
       : "=&v"(r) : "v"(a), "v"(b));
   return r;
 }
+// Both bank-masked stages in one block: 12 DPP adds behind ONE s_nop.  Every stage-2 operand was
+// written at least two instructions earlier (y0 at 1, y2 at 5 -> read at 9; y1 at 3, y3 at 7 -> read
+// at 11), so only the block's entry needs the wait states; the per-pair form paid 6 s_nop per token.
+__device__ __forceinline__ void dpp_stage12(const float (&v)[8], float& z0, float& z1) {
+  float y0, y1, y2, y3;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %2, %6, %6 row_mirror row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %10, %10 row_mirror row_mask:0xf bank_mask:0xc bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %7, %7 row_mirror row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %11, %11 row_mirror row_mask:0xf bank_mask:0xc bound_ctrl:1\n\t"
+      "v_add_f32_dpp %4, %8, %8 row_mirror row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %4, %12, %12 row_mirror row_mask:0xf bank_mask:0xc bound_ctrl:1\n\t"
+      "v_add_f32_dpp %5, %9, %9 row_mirror row_mask:0xf bank_mask:0x3 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %5, %13, %13 row_mirror row_mask:0xf bank_mask:0xc bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %2, %2 row_half_mirror row_mask:0xf bank_mask:0x5 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %4, %4 row_half_mirror row_mask:0xf bank_mask:0xa bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %3, %3 row_half_mirror row_mask:0xf bank_mask:0x5 bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %5, %5 row_half_mirror row_mask:0xf bank_mask:0xa bound_ctrl:1"
+      : "=&v"(z0), "=&v"(z1), "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+}
 __device__ __forceinline__ float reduce_scatter8_row_bm(const float (&v)[8]) {
   const int l = threadIdx.x & 15;
   const bool b1 = l & 2;
-  float y4[4], z[2];
+  float z[2];
+#if VC_DPP_PAIRWISE
+  float y4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) y4[j] = dpp_pair_add<0>(v[j], v[j + 4]);
 #pragma unroll
   for (int j = 0; j < 2; ++j) z[j] = dpp_pair_add<1>(y4[j], y4[j + 2]);
+#else
+  dpp_stage12(v, z[0], z[1]);
+#endif
   const float keep = b1 ? z[1] : z[0], send = b1 ? z[0] : z[1];
   const float w = keep + dpp_mov<0x4E>(send);
   return w + dpp_mov<0xB1>(w);
