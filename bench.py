@@ -82,13 +82,13 @@ def time_kernel(fn, reps, stream):
     return s.elapsed_time(e) / reps * 1e-3
 
 
-PMC_PROFILES = ("r03_pmc.json", "r02_pmc_s4.json", "r02_pmc.json", "r01_pmc.json")   # newest first
+PMC_PROFILES = ("r05_pmc.json", "r03_pmc.json", "r02_pmc_s4.json", "r02_pmc.json", "r01_pmc.json")   # newest first
 
 
 def _pmc_from_profile(kernel_key):
     """Per-launch PMC record of `kernel_key` from the newest committed profile that has it
     (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ passes, separate runs: tools/pmc_step.sh ->
-    tools/pmc_summary_json.py -> profiles/r02_pmc_s4.json; tools/pmc_to_json.py before it), or None."""
+    tools/pmc_summary_json.py -> profiles/r05_pmc.json; tools/pmc_to_json.py before it), or None."""
     for name in PMC_PROFILES:
         path = os.path.join(REPO, "profiles", name)
         if not os.path.exists(path):

@@ -701,17 +701,28 @@ __device__ __forceinline__ void mma_ktile_bf(const char* As, const char* Bs, int
 // The block's output tile: (xn, ym) of K slice zs / batch zb, tn x tm tiles per slice (the arrival
 // counter's index of the in-launch combine, g.cnt; null = slabs for a separate reduce).  `smem` is the
 // block's LDS ring (ring_bytes), shared by the single-problem and the grouped kernel.
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false>
+//
+// KS = 2 (fp32): twice the waves, the k-split pair of each wave tile sharing the ring -- wave half kh runs
+// sub-step kh of every k-tile (g2::mma_substep), so each SIMD holds two waves whose LDS waits and DMA
+// issue overlap the other's MFMAs (one wave per SIMD left the 16x16x4 issue idle ~half the time on a
+// one-block-per-CU grid); the halves' accumulators are g2's NC = 2 partials, summed acc0 + acc1 through
+// the idle ring before the epilogue, which the kh = 0 waves run.
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false, int KS = 1>
 __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int xn, int ym, int tn, int tm, int G,
                                           char* smem) {
-  constexpr int NW = WM * WN, NTH = 64 * NW;
+  constexpr int NWT = WM * WN;                  // waves per k-split half
+  constexpr int NW = NWT * KS, NTH = 64 * NW;   // all waves (they share the DMA of a stage)
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int SA_B = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int LOADS = (BM / 8 + BN / 8) / NW;   // DMA wave-instructions per wave and stage
   static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static_assert(KS == 1 || (KS == 2 && !BF), "k-split waves: fp32 only");
+  static_assert(KS == 1 || NWT * MT * NT * 4 * 64 * 4 <= ring_bytes<BM, BN, NS>(), "partials fit the ring");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
+  const int kh = wave / NWT, wt = wave % NWT;
+  const int wm = wt / WN, wn = wt % WN;
+  const bool out_wave = kh == 0;
   const int z = zb * g.nsplit + zs;
   const int m0 = ym * BM, n0 = xn * BN;
   const int kbeg = zs * g.k_chunk;
@@ -765,7 +776,28 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
       asm volatile("" ::: "memory");
     }
     if constexpr (BF) mma_ktile_bf<MT, NT, SA, SB>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc[0]);
+    else if constexpr (KS == 2) g2::mma_substep<MT, NT, SA, SB>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, kh, acc[0]);
     else g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
+  }
+  if constexpr (KS == 2) {   // acc = sub-step-0 partial + sub-step-1 partial (g2's NC = 2 order)
+    float* xch = reinterpret_cast<float*>(smem);   // [NWT][MT][NT][4][64]
+    __syncthreads();                               // every wave past its last ring read
+    if (kh == 1)
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xch[(((wt * MT + mi) * NT + ni) * 4 + r) * 64 + lane] = acc[0][mi][ni][r];
+    __syncthreads();
+    if (kh == 0)
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc[0][mi][ni][r] = acc[0][mi][ni][r] + xch[(((wt * MT + mi) * NT + ni) * 4 + r) * 64 + lane];
   }
 
   // C/D map of the 16x16 MFMAs: col = lane & 15, row = (lane >> 4) * 4 + r
@@ -781,7 +813,7 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + r;
-          if (m < g.M && n < g.N) {
+          if (out_wave && m < g.M && n < g.N) {
             float* cp = g.C + (long)m * g.ldc + n;
             const float v = epilogue(g.epi, acc[0][mi][ni][r], cp, m, n);
             *cp = v;
@@ -801,7 +833,7 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
     // the WM row waves of the tile: through the idle LDS ring (all waves are past their last k-tile reads)
     double* red = reinterpret_cast<double*>(smem);   // [2][WM][BN]
     __syncthreads();
-    if (lane < 16)
+    if (out_wave && lane < 16)
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni)
 #pragma unroll
@@ -825,7 +857,7 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + r;
         const int n = n0 + wn * WTN + ni * 16 + (lane & 15);
-        if (m < g.M && n < g.Ne) {
+        if (out_wave && m < g.M && n < g.Ne) {
           if (g.nsplit > 1) g.part[((long)z * g.M + m) * g.Ne + n] = acc[0][mi][ni][r];
           else store_out(g, zb, m, n, acc[0][mi][ni][r]);
         }
@@ -859,12 +891,13 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
   if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G, int zfast) {
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false, int KS = 1>
+__global__ __launch_bounds__(64 * WM * WN * KS) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G,
+                                                                int zfast) {
   __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS>()];
   int zs, xn, ym, zb;
   tile_coords(xcd_linear(blockIdx.x, total), g.nsplit, tn, tm, zfast, zs, xn, ym, zb);
-  pipe_tile<BM, BN, WM, WN, TA, TB, NS, BF>(g, zb, zs, xn, ym, tn, tm, G, smem);
+  pipe_tile<BM, BN, WM, WN, TA, TB, NS, BF, KS>(g, zb, zs, xn, ym, tn, tm, G, smem);
 }
 
 // Grouped launch: up to GROUP_MAX independent problems (any of the four layouts, a runtime switch) in one
@@ -877,8 +910,9 @@ struct PipeGroup {
   GemmArgs g[GROUP_MAX];
 };
 
-template <int BM, int BN, int WM, int WN, int NS>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_group(PipeGroup P, unsigned total) {
+// KS = 2: fp32 problems only (the host launches a group holding a bf16 problem with KS = 1).
+template <int BM, int BN, int WM, int WN, int NS, int KS = 1>
+__global__ __launch_bounds__(64 * WM * WN * KS) void gemm_pipe_group(PipeGroup P, unsigned total) {
   __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS>()];
   const unsigned lin = xcd_linear(blockIdx.x, total);
   int p = 0;
@@ -900,14 +934,20 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_group(PipeGroup P, uns
   int zs, xn, ym, zb;
   tile_coords(lin - (unsigned)start, g.nsplit, tn, tm, 1, zs, xn, ym, zb);
   switch (variant) {   // 4 BF + 2 TA + TB
-    case 0: pipe_tile<BM, BN, WM, WN, false, false, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 1: pipe_tile<BM, BN, WM, WN, false, true, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 2: pipe_tile<BM, BN, WM, WN, true, false, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 3: pipe_tile<BM, BN, WM, WN, true, true, NS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 4: pipe_tile<BM, BN, WM, WN, false, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 5: pipe_tile<BM, BN, WM, WN, false, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 6: pipe_tile<BM, BN, WM, WN, true, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    default: pipe_tile<BM, BN, WM, WN, true, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 0: pipe_tile<BM, BN, WM, WN, false, false, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 1: pipe_tile<BM, BN, WM, WN, false, true, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 2: pipe_tile<BM, BN, WM, WN, true, false, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 3: pipe_tile<BM, BN, WM, WN, true, true, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    default:
+      if constexpr (KS == 1) {
+        switch (variant) {
+          case 4: pipe_tile<BM, BN, WM, WN, false, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+          case 5: pipe_tile<BM, BN, WM, WN, false, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+          case 6: pipe_tile<BM, BN, WM, WN, true, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+          default: pipe_tile<BM, BN, WM, WN, true, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+        }
+      }
+      break;
   }
 }
 
@@ -1104,6 +1144,16 @@ struct PipePlan {
   int bm, bn, ns, nsplit, k_chunk, tn, tm;
 };
 
+// k-split waves (gp::pipe_tile KS = 2) for fp32 64 x 64 tiles: only where the grid is at most one block
+// per CU and K is long (the local 3x3 convs, M = B 49, K = 9 C: 34.1 -> 31.8 us); elsewhere measured
+// equal or slower (tools/gemm_one.py, profiles/r05_gemm_ks.log; on every pipelined GEMM of the step
+// 1.744 -> 1.757 ms).  Knob (probe library): 0 = this rule, 1 = never, 2 = always.
+static int pipe_ks(long tiles = 0, int nsplit = 1, int K = 0) {
+  const int k = vc_knob("VITCNN_PIPE_KS", 0);
+  if (k) return k == 2 ? 2 : 1;
+  return (nsplit == 1 && tiles > 0 && tiles <= 256 && K >= 1024) ? 2 : 1;
+}
+
 // Launch plan (tools/gemm_lab.hip sweep over the step's 21 critical-path shapes, profiles/r04_gemm_lab.log):
 // 64 x 64 tiles on 4 waves with a 2-stage ring (32 KB: up to 5 blocks per CU) won or tied on nearly every
 // shape; a grid of >= 128 tiles runs unsplit (the split-K slab reduce costs more than the extra blocks
@@ -1156,22 +1206,24 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
   // faster for every split shape of the step, tools/gemm_lab.hip; the in-launch combine reads its slabs there)
   const int zfast = 1;
   dim3 grid((unsigned)total);
-#define VC_GP(BM_, BN_, WM_, WN_, NS_)                                                                          \
+#define VC_GP(BM_, BN_, WM_, WN_, NS_, KS_)                                                                     \
   do {                                                                                                           \
+    const dim3 blk(64 * WM_ * WN_ * KS_);                                                                        \
     if (transA && transB)                                                                                        \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, true, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);   \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, true, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);   \
     else if (transA)                                                                                             \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, false, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, false, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
     else if (transB)                                                                                             \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, true, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, true, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
     else                                                                                                         \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, false, NS_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast); \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, false, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast); \
   } while (0)
 #define VC_GP_T(NS_)                                                \
   do {                                                              \
-    if (p.bm == 128 && p.bn == 64) VC_GP(128, 64, 4, 2, NS_);        \
-    else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_);   \
-    else VC_GP(64, 64, 2, 2, NS_);                                  \
+    if (p.bm == 128 && p.bn == 64) VC_GP(128, 64, 4, 2, NS_, 1);     \
+    else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_, 1); \
+    else if (pipe_ks(tiles, p.nsplit, K) == 2) VC_GP(64, 64, 2, 2, NS_, 2); \
+    else VC_GP(64, 64, 2, 2, NS_, 1);                               \
   } while (0)
 #define VC_GPB(BM_, BN_, WM_, WN_, TA_, TB_, NS_) \
   hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, TA_, TB_, NS_, true>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
@@ -1304,8 +1356,14 @@ static int group_flush(GroupState& st) {
     }
     P.start[np] = (int)total;
     VC_REQUIRE(total < (1L << 31));
-    hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0, st.stream, P,
-                       (unsigned)total);
+    bool any_bf = false;
+    for (int p = 0; p < np; ++p) any_bf |= st.pipes[p].variant >= 4;
+    if (!any_bf && vc_knob("VITCNN_PIPE_KS", 0) == 2)   // (grouped problems: measured no gain)
+      hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2, 2>), dim3((unsigned)total), dim3(512), 0, st.stream, P,
+                         (unsigned)total);
+    else
+      hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0, st.stream, P,
+                         (unsigned)total);
     VC_CHECK_LAUNCH();
   }
   if (red.R.n) {
@@ -1441,6 +1499,9 @@ VC_EXPORT int vc_gemm_colstats(int M, int N, int K, const float* A, long lda, co
   if (bf)
     hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2, true>), grid, dim3(256), 0, stream, g, p.tn, p.tm,
                        (unsigned)total, 1, 1);
+  else if (pipe_ks(total, 1, K) == 2)
+    hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2, false, 2>), grid, dim3(512), 0, stream, g, p.tn,
+                       p.tm, (unsigned)total, 1, 1);
   else
     hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2>), grid, dim3(256), 0, stream, g, p.tn, p.tm,
                        (unsigned)total, 1, 1);

@@ -200,6 +200,27 @@ __device__ __forceinline__ void mma_ktile(const char* As, const char* Bs, int ar
   }
 }
 
+// One sub-step s (k = 16 s .. 16 s + 15 of the k-tile) of mma_ktile's fp32 path into one accumulator set:
+// the pipelined kernel's k-split waves (gp::pipe_tile, KS = 2) each run one sub-step of every k-tile, so
+// their two accumulators are mma_ktile's NC = 2 partials (k = 16 s + 4 g + j, the same fma chains).
+template <int MT, int NT, class SA, class SB>
+__device__ __forceinline__ void mma_substep(const char* As, const char* Bs, int arow, int brow, int lane, int s,
+                                            f32x4 (&acc)[MT][NT]) {
+  uint4 a[MT], b[NT];
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) a[mi] = SA::frag(As, arow + 16 * mi, s, lane);
+#pragma unroll
+  for (int ni = 0; ni < NT; ++ni) b[ni] = SB::frag(Bs, brow + 16 * ni, s, lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[mi][j]), __uint_as_float(b[ni][j]),
+                                                            acc[mi][ni], 0, 0, 0);
+}
+
 }  // namespace g2
 
 namespace gp {
