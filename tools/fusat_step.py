@@ -8,6 +8,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
+sys.path.insert(0, os.path.join(REPO, "tools"))
+sys.path.insert(0, os.path.join(REPO, "vit-cnn_amd"))
+import knobs  # noqa: F401,E402  (measurement switches: tools/knobs.py)
 import bench  # noqa: E402
 
 
