@@ -1172,8 +1172,9 @@ static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws, bo
   const long tiles = (long)p.tn * p.tm;
   const int kt = vc_cdiv(K, gp::KT);
   int nsplit = 1;
+  const long target = vc_knob("VITCNN_PIPE_SPLIT_BLOCKS", 512);   // blocks a split aims at (knob: probe library)
   if (have_ws && tiles < 128)
-    nsplit = (int)std::max<long>(1, std::min<long>(std::min<long>((512 + tiles - 1) / tiles, kt / 4), 64));
+    nsplit = (int)std::max<long>(1, std::min<long>(std::min<long>((target + tiles - 1) / tiles, kt / 4), 64));
   if (g_tune.nsplit) nsplit = std::min(g_tune.nsplit, std::max(1, kt));
   while (nsplit > 1 && (long)nsplit * M * Ne > ws_floats) --nsplit;
   p.k_chunk = kt * gp::KT;

@@ -114,7 +114,7 @@ constexpr float ATT_LN2 = 0.6931471805599453f;
 // step s of lane group g = l >> 4 pairs key (or head-dim) 4g + s on both operands.  Online softmax
 // (running max / sum per query, rescaling the O^T accumulator) between tiles.
 __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __restrict__ qkv, float scale,
-                                                float* __restrict__ out, float* __restrict__ lse) {
+                                                float* __restrict__ out, float* __restrict__ lse, int wpb) {
   extern __shared__ f32x4 lds4[];  // 2 * T * 64 B
   f32x4* Ks = lds4;
   f32x4* Vs = lds4 + T * 4;
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(1024) void attn_fwd(int T, int H, const float* __re
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q0 = wave * 16;
+  const int q0 = (blockIdx.y * wpb + wave) * 16;   // blockIdx.y: chunk of wpb waves
   if (q0 >= T) return;                     // whole wave idle (no LDS barrier follows)
   const int c = lane & 15, g = lane >> 4;
   const int qi = min(q0 + c, T - 1);
@@ -195,10 +195,11 @@ __device__ __forceinline__ f32x4 mfma4(f32x4 a, f32x4 b, f32x4 c) {
   return c;
 }
 
+// Grid (B*H, 2, chunks): blockIdx.y = pass, blockIdx.z = chunk of wpb waves (rows (z wpb + wave) * 16).
 __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __restrict__ qkv,
                                                 const float* __restrict__ out, const float* __restrict__ dout,
                                                 const float* __restrict__ lse, float scale,
-                                                float* __restrict__ dqkv) {
+                                                float* __restrict__ dqkv, int wpb) {
   extern __shared__ f32x4 lds4[];  // 2 * T * 64 B + 2 * T * 4 B (19.8 KB at T = 146)
   f32x4* Ks = lds4;                // pass 1
   f32x4* Vs = lds4 + T * 4;
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
   const int ld = 3 * H * 16, ldo = H * 16;
   const float* base = qkv + (long)b * T * ld;
   // the operands the pass walks staged (pass 1: K, V; pass 2: Q, dO; each pass reads its own 16 rows of
-  // the other two straight from global memory) with rowsum(dO * O) in the same loop: 4 lanes per row (one
+  // the other two straight from global memory) with (pass 2) rowsum(dO * O) in the same loop: 4 lanes per row (one
   // float4 of each array), every load of a lane issued before its first use; the row's four dot products
   // summed across the lanes (xor 1, xor 2)
   const bool p1 = blockIdx.y == 0;
@@ -224,9 +225,9 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
     const f32x4 av = ok ? *(const f32x4*)(base + (long)t * ld + (p1 ? H * 16 : 0) + h * 16 + q4 * 4) : z;
     const f32x4 vv = (ok && p1) ? *(const f32x4*)(base + (long)t * ld + 2 * H * 16 + h * 16 + q4 * 4) : z;
-    const f32x4 gv = ok ? *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4) : z;
-    const f32x4 ov = ok ? *(const f32x4*)(out + ((long)b * T + t) * ldo + h * 16 + q4 * 4) : z;
-    const float lt = (ok && q4 == 0) ? lse[((long)b * H + h) * T + t] : 0.f;
+    const f32x4 gv = (ok && !p1) ? *(const f32x4*)(dout + ((long)b * T + t) * ldo + h * 16 + q4 * 4) : z;
+    const f32x4 ov = (ok && !p1) ? *(const f32x4*)(out + ((long)b * T + t) * ldo + h * 16 + q4 * 4) : z;
+    const float lt = (ok && !p1 && q4 == 0) ? lse[((long)b * H + h) * T + t] : 0.f;
     if (ok) {
       if (p1) {
         Ks[i] = av;
@@ -236,25 +237,31 @@ __global__ __launch_bounds__(1024) void attn_bwd(int T, int H, const float* __re
         dOs[i] = gv;
       }
     }
-    float v = ((ov.x * gv.x + ov.y * gv.y) + ov.z * gv.z) + ov.w * gv.w;
+    float v = fmaf(ov.w, gv.w, fmaf(ov.z, gv.z, fmaf(ov.y, gv.y, ov.x * gv.x)));   // explicit fmas: pass 1's bits
     v += __shfl_xor(v, 1, 64);
     v += __shfl_xor(v, 2, 64);
-    if (ok && q4 == 0) {
+    if (ok && !p1 && q4 == 0) {
       Ds[t] = v;
       Ls[t] = lt * ATT_LOG2E;   // base-2 lse
     }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r0 = wave * 16;
+  const int r0 = (blockIdx.z * wpb + wave) * 16;
   if (r0 >= T) return;
   const int c = lane & 15, g = lane >> 4;
   const int ri = min(r0 + c, T - 1);
   if (blockIdx.y == 0) {  // pass 1: dq of queries r0 .. r0 + 15 (query c of this lane)
     const f32x4 qv = *(const f32x4*)(base + (long)ri * ld + h * 16 + g * 4);
     const f32x4 gv = *(const f32x4*)(dout + ((long)b * T + ri) * ldo + h * 16 + g * 4);
+    const f32x4 ov = *(const f32x4*)(out + ((long)b * T + ri) * ldo + h * 16 + g * 4);
     const float scale2 = scale * ATT_LOG2E;
-    const float lq = Ls[ri], dq_ = Ds[ri];
+    // this query's lse and rowsum(dO * O): pass 1 stages neither; the staging loop's operations and order
+    // (explicit fmas, lane group g in the role of q4: xor 16, xor 32 for xor 1, xor 2), so the bits are pass 2's
+    const float lq = lse[((long)b * H + h) * T + ri] * ATT_LOG2E;
+    float dq_ = fmaf(ov.w, gv.w, fmaf(ov.z, gv.z, fmaf(ov.y, gv.y, ov.x * gv.x)));
+    dq_ += __shfl_xor(dq_, 16, 64);
+    dq_ += __shfl_xor(dq_, 32, 64);
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;  // dQ^T[d = 4g + r][q = c], even / odd tiles
     auto tile = [&](int k0, f32x4& acc) {
       const int key = min(k0 + c, T - 1);
@@ -457,8 +464,10 @@ VC_API int vc_s2eft_strip_cls(int B, int N, int D, const float* dX, float* dE, h
 VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale, float* out, float* lse,
                              hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_fwd, dim3(B * H), dim3(64 * ((T + 15) / 16)), 2 * T * 64, stream, T, H, qkv, scale, out,
-                     lse);
+  const int waves = (T + 15) / 16;
+  const int wpb = std::max(1, std::min(waves, (int)vc_knob("VITCNN_ATTN_FWD_WPB", waves)));   // knob: probe library
+  hipLaunchKernelGGL(attn_fwd, dim3(B * H, vc_cdiv(waves, wpb)), dim3(64 * wpb), 2 * T * 64, stream, T, H, qkv, scale,
+                     out, lse, wpb);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -466,8 +475,12 @@ VC_API int vc_s2eft_attn_fwd(int B, int T, int H, const float* qkv, float scale,
 VC_API int vc_s2eft_attn_bwd(int B, int T, int H, const float* qkv, const float* out, const float* dout,
                              const float* lse, float scale, float* dqkv, hipStream_t stream) {
   VC_REQUIRE(B > 0 && H > 0 && T > 0 && T <= 256);
-  hipLaunchKernelGGL(attn_bwd, dim3(B * H, 2), dim3(64 * ((T + 15) / 16)), 2 * T * 64 + 2 * T * 4, stream, T, H, qkv, out,
-                     dout, lse, scale, dqkv);
+  // waves per block: ceil(waves / 2) (config 5: 2 blocks of 5 waves per pass and head: 24.0 -> 22.2 us with
+  // pass 1's lighter staging, tools/attn_probe.py, profiles/r05_attn_bwd.log); knob: probe library
+  const int waves = (T + 15) / 16;
+  const int wpb = std::max(1, std::min(waves, (int)vc_knob("VITCNN_ATTN_BWD_WPB", (waves + 1) / 2)));
+  hipLaunchKernelGGL(attn_bwd, dim3(B * H, 2, vc_cdiv(waves, wpb)), dim3(64 * wpb), 2 * T * 64 + 2 * T * 4, stream, T,
+                     H, qkv, out, dout, lse, scale, dqkv, wpb);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
