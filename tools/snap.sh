@@ -6,6 +6,5 @@ set -e
 cd "$(dirname "$0")/.."
 rm -rf ab/run
 mkdir -p ab/run
-tar --exclude=./ab --exclude=./gpurun_out --exclude=./.git --exclude='*.log' --exclude=./vit-cnn_amd/csrc/build \
-    --exclude=./profiles -cf - . | tar -xf - -C ab/run
+tar --exclude=./ab --exclude=./gpurun_out --exclude=./.git --exclude='*.log' --exclude=./vit-cnn_amd/csrc/build -cf - . | tar -xf - -C ab/run
 echo "snapshot ab/run: $(du -sh ab/run | cut -f1)"
