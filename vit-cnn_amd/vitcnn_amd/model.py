@@ -937,6 +937,9 @@ class _Program:
                 self.L.vc_nchw_to_nhwc(B, m.c2, Pp * Pp, lidar.data_ptr(), LX, self.s)
             L1 = self.conv_bn_relu3("lidar1", LX, Pp, m.c2, 16)
             L2 = self.conv_bn_relu3("lidar2", L1, Pp - 2, 16, 32)
+            if self.train:   # every BatchNorm's num_batches_tracked += 1 (off lane 0's chain: nothing reads it)
+                tr = self.tab["tracked"]
+                self.L.vc_index_add_i64(tr.numel(), tr.data_ptr(), self.I64, 1, self.s)
         self.L.vc_nchw_to_nhwc(B, m.c1, Pp * Pp, hsi.data_ptr(), X0, self.s)
         ws.t["hsi_in"] = hsi
         self.X0, self.LX = X0, LX
@@ -953,9 +956,6 @@ class _Program:
         feat = ws.f("feat", B * 128)
         self.L.vc_head_fwd(B, S1, S2, 128, m.ncls, F1, F2, self.P["classifier.weight"], self.P["classifier.bias"],
                            feat, logits.data_ptr(), self.s)
-        if self.train:
-            tr = self.tab["tracked"]
-            self.L.vc_index_add_i64(tr.numel(), tr.data_ptr(), self.I64, 1, self.s)
         self.H1, self.H2, self.L1, self.L2, self.F1, self.F2, self.feat = H1, H2, L1, L2, F1, F2, feat
         return logits
 
