@@ -454,6 +454,10 @@ VC_API int vc_ce_fwd(int B, int ncls, const float* logits, const long long* targ
                      long long ignore_index, float* loss, hipStream_t stream);
 VC_API int vc_ce_bwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
                      long long ignore_index, const float* grad_out, float* dlogits, hipStream_t stream);
+/* vc_ce_fwd then vc_ce_bwd with grad_out = 1 in ONE launch (bit-identical to the two): the training step's
+ * loss and dlogits */
+VC_API int vc_ce_fwd_bwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
+                         long long ignore_index, float* loss, float* dlogits, hipStream_t stream);
 /* torch.optim.AdamW step (model_utils.py:309-310) over a flat buffer; hyper = device
  * [lr, beta1, beta2, eps, weight_decay, grad_scale]; step = device float[3] state: step[0] = t is
  * incremented first, step[1..2] receive the bias corrections (1 - beta1^t, sqrt(1 - beta2^t)) */

@@ -485,6 +485,13 @@ def test_weighted_cross_entropy(L, B, ncls):
     torch.cuda.synchronize()
     assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
     assert rel_err(dl.cpu().numpy(), lr.grad.numpy()) < 1e-5
+    # the training step's one-launch form (d(loss) = 1) == the two launches, bit for bit
+    loss1, dl1 = torch.empty(1, device=DEV), torch.empty(B, ncls, device=DEV)
+    one = torch.ones(1, device=DEV)
+    L.vc_ce_bwd(B, ncls, P(ld), P(td), P(wd), -100, P(one), P(dl), S())
+    L.vc_ce_fwd_bwd(B, ncls, P(ld), P(td), P(wd), -100, P(loss1), P(dl1), S())
+    torch.cuda.synchronize()
+    assert torch.equal(loss1, loss) and torch.equal(dl1, dl)
 
 
 @pytest.mark.parametrize("B,S,Pk,Ci", [(3, 49, 9, 128), (2, 25, 4, 72), (2, 81, 16, 64), (2, 49, 9, 70), (1, 7, 1, 4),

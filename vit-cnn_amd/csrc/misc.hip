@@ -202,10 +202,9 @@ __device__ __forceinline__ float block_sum1024(float v, float* red) {
   return r;
 }
 
-__global__ __launch_bounds__(CET) void ce_fwd(int B, int ncls, const float* __restrict__ logits,
-                                              const long long* __restrict__ target, const float* __restrict__ w,
-                                              long long ignore_index, float* __restrict__ loss) {
-  __shared__ float red[CET / 64];
+__device__ __forceinline__ void ce_fwd_body(int B, int ncls, const float* __restrict__ logits,
+                                            const long long* __restrict__ target, const float* __restrict__ w,
+                                            long long ignore_index, float* __restrict__ loss, float* red) {
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   float num = 0.f, den = 0.f;
   for (int b = g; b < B; b += CET / 16) {
@@ -223,11 +222,17 @@ __global__ __launch_bounds__(CET) void ce_fwd(int B, int ncls, const float* __re
   if (threadIdx.x == 0) loss[0] = num / den;
 }
 
-__global__ __launch_bounds__(CET) void ce_bwd(int B, int ncls, const float* __restrict__ logits,
+__global__ __launch_bounds__(CET) void ce_fwd(int B, int ncls, const float* __restrict__ logits,
                                               const long long* __restrict__ target, const float* __restrict__ w,
-                                              long long ignore_index, const float* __restrict__ gout,
-                                              float* __restrict__ dlogits) {
+                                              long long ignore_index, float* __restrict__ loss) {
   __shared__ float red[CET / 64];
+  ce_fwd_body(B, ncls, logits, target, w, ignore_index, loss, red);
+}
+
+__device__ __forceinline__ void ce_bwd_body(int B, int ncls, const float* __restrict__ logits,
+                                            const long long* __restrict__ target, const float* __restrict__ w,
+                                            long long ignore_index, const float* __restrict__ gout,
+                                            float* __restrict__ dlogits, float* red) {
   float den = 0.f;
   for (int b = threadIdx.x; b < B; b += CET) {
     const long long y = target[b];
@@ -247,6 +252,26 @@ __global__ __launch_bounds__(CET) void ce_bwd(int B, int ncls, const float* __re
       dlogits[(long)b * ncls + k] = gs * wy * (p - (k == y ? 1.f : 0.f));
     }
   }
+}
+
+__global__ __launch_bounds__(CET) void ce_bwd(int B, int ncls, const float* __restrict__ logits,
+                                              const long long* __restrict__ target, const float* __restrict__ w,
+                                              long long ignore_index, const float* __restrict__ gout,
+                                              float* __restrict__ dlogits) {
+  __shared__ float red[CET / 64];
+  ce_bwd_body(B, ncls, logits, target, w, ignore_index, gout, dlogits, red);
+}
+
+// the loss and its gradient for d(loss) = 1 in one block: ce_fwd's then ce_bwd's code (the same bits as the
+// two launches), one dependent launch fewer at the head of the training step's backward
+__global__ __launch_bounds__(CET) void ce_fwd_bwd(int B, int ncls, const float* __restrict__ logits,
+                                                  const long long* __restrict__ target, const float* __restrict__ w,
+                                                  long long ignore_index, float* __restrict__ loss,
+                                                  float* __restrict__ dlogits) {
+  __shared__ float red[CET / 64];
+  ce_fwd_body(B, ncls, logits, target, w, ignore_index, loss, red);
+  __syncthreads();   // red reused
+  ce_bwd_body(B, ncls, logits, target, w, ignore_index, nullptr, dlogits, red);
 }
 
 // step[0] = t (incremented), step[1] = 1 - beta1^t, step[2] = sqrt(1 - beta2^t)
@@ -412,6 +437,15 @@ VC_API int vc_ce_bwd(int B, int ncls, const float* logits, const long long* targ
                      long long ignore_index, const float* grad_out, float* dlogits, hipStream_t stream) {
   VC_REQUIRE(B > 0 && ncls > 0);
   hipLaunchKernelGGL(ce_bwd, dim3(1), dim3(CET), 0, stream, B, ncls, logits, target, weight, ignore_index, grad_out,
+                     dlogits);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_ce_fwd_bwd(int B, int ncls, const float* logits, const long long* target, const float* weight,
+                         long long ignore_index, float* loss, float* dlogits, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && ncls > 0 && loss && dlogits);
+  hipLaunchKernelGGL(ce_fwd_bwd, dim3(1), dim3(CET), 0, stream, B, ncls, logits, target, weight, ignore_index, loss,
                      dlogits);
   VC_CHECK_LAUNCH();
   return VC_OK;
