@@ -127,10 +127,9 @@ __global__ __launch_bounds__(256) void head_fwd(int S1, int S2, int C, int ncls,
   }
 }
 
-__global__ __launch_bounds__(256) void head_bwd_x(int S1, int S2, int C, int ncls, const float* __restrict__ dlog,
-                                                  const float* __restrict__ W, float* __restrict__ df1,
-                                                  float* __restrict__ df2) {
-  const int b = blockIdx.x;
+__device__ __forceinline__ void head_bwd_x(int b, int S1, int S2, int C, int ncls, const float* __restrict__ dlog,
+                                           const float* __restrict__ W, float* __restrict__ df1,
+                                           float* __restrict__ df2) {
   for (int c = threadIdx.x; c < C; c += 256) {
     float g = 0.f;
     for (int k = 0; k < ncls; ++k) g += dlog[(long)b * ncls + k] * W[(long)k * C + c];
@@ -140,14 +139,14 @@ __global__ __launch_bounds__(256) void head_bwd_x(int S1, int S2, int C, int ncl
   }
 }
 
-// grid (ncls, ceil((C+1)/64)): 64 columns x 4 batch groups per block, fixed-order LDS combine;
-// column C is the bias gradient (sum over b of dlogits)
-__global__ __launch_bounds__(256) void head_bwd_w(int B, int C, int ncls, const float* __restrict__ dlog,
-                                                  const float* __restrict__ feat, float* __restrict__ dW,
-                                                  float* __restrict__ db) {
+// block (k, y) of the (ncls, ceil((C+1)/64)) weight-gradient tiles: 64 columns x 4 batch groups, fixed-order LDS
+// combine; column C is the bias gradient (sum over b of dlogits)
+__device__ __forceinline__ void head_bwd_w(int k, int y, int B, int C, int ncls, const float* __restrict__ dlog,
+                                           const float* __restrict__ feat, float* __restrict__ dW,
+                                           float* __restrict__ db) {
   __shared__ float red[4][64];
-  const int k = blockIdx.x, cl = threadIdx.x & 63, bg = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + cl;
+  const int cl = threadIdx.x & 63, bg = threadIdx.x >> 6;
+  const int c = y * 64 + cl;
   float acc = 0.f;
   if (c <= C)
     for (int b = bg; b < B; b += 4) acc += dlog[(long)b * ncls + k] * (c < C ? feat[(long)b * C + c] : 1.f);
@@ -158,6 +157,21 @@ __global__ __launch_bounds__(256) void head_bwd_w(int B, int C, int ncls, const 
     if (c < C) dW[(long)k * C + c] = v;
     else db[k] = v;
   }
+}
+
+// the head backward in one grid: blocks [0, B) the feature gradient of sample b, the rest the classifier's weight
+// and bias gradient tiles (independent halves: one launch instead of two on the step's critical chain)
+__global__ __launch_bounds__(256) void head_bwd(int B, int S1, int S2, int C, int ncls, const float* __restrict__ dlog,
+                                                const float* __restrict__ W, const float* __restrict__ feat,
+                                                float* __restrict__ df1, float* __restrict__ df2,
+                                                float* __restrict__ dW, float* __restrict__ db) {
+  const int bid = blockIdx.x;
+  if (bid < B) {
+    head_bwd_x(bid, S1, S2, C, ncls, dlog, W, df1, df2);
+    return;
+  }
+  const int t = bid - B;
+  head_bwd_w(t % ncls, t / ncls, B, C, ncls, dlog, feat, dW, db);
 }
 
 // Weighted cross entropy, every sample at once: one 1024-thread block, a 16-lane row per sample
@@ -417,10 +431,8 @@ VC_API int vc_head_fwd(int B, int S1, int S2, int C, int ncls, const float* f1, 
 VC_API int vc_head_bwd(int B, int S1, int S2, int C, int ncls, const float* dlogits, const float* W, const float* feat,
                        float* df1, float* df2, float* dW, float* db, hipStream_t stream) {
   VC_REQUIRE(B > 0 && S1 > 0 && S2 > 0 && C > 0 && ncls > 0);
-  hipLaunchKernelGGL(head_bwd_x, dim3(B), dim3(256), 0, stream, S1, S2, C, ncls, dlogits, W, df1, df2);
-  VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(head_bwd_w, dim3(ncls, vc_cdiv(C + 1, 64)), dim3(256), 0, stream, B, C, ncls, dlogits, feat,
-                     dW, db);
+  hipLaunchKernelGGL(head_bwd, dim3(B + ncls * vc_cdiv(C + 1, 64)), dim3(256), 0, stream, B, S1, S2, C, ncls, dlogits,
+                     W, feat, df1, df2, dW, db);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
