@@ -161,12 +161,21 @@ __global__ __launch_bounds__(256) void pixel_stats(int M, int C, const float* __
 __device__ __forceinline__ void combine_moments(int P, long n, const double* __restrict__ part, float km, float kv,
                                                 double* red, double (&out)[6]) {
   double v[NMOM] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int p = threadIdx.x; p < P; p += 256) {
-    double t[NMOM];
+  // two of the thread's partials per round, both loaded before either is added (one latency per two; the
+  // partials still added in p order)
+  for (int p = threadIdx.x; p < P; p += 512) {
+    double t[2][NMOM];
+    const bool two = p + 256 < P;
 #pragma unroll
-    for (int j = 0; j < NMOM; ++j) t[j] = part[(long)p * NMOM + j];
+    for (int j = 0; j < NMOM; ++j) {
+      t[0][j] = part[(long)p * NMOM + j];
+      t[1][j] = two ? part[(long)(p + 256) * NMOM + j] : 0.0;
+    }
 #pragma unroll
-    for (int j = 0; j < NMOM; ++j) v[j] += t[j];
+    for (int j = 0; j < NMOM; ++j) v[j] += t[0][j];
+    if (two)
+#pragma unroll
+      for (int j = 0; j < NMOM; ++j) v[j] += t[1][j];
   }
   block256_sums_d(v, red);
   const double nd = (double)n;
@@ -467,6 +476,23 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
     for (int i = threadIdx.x; i < 4 * S; i += 256) {
       const int s = i >> 2, u = i & 3;
       double t0 = 0.0, t1 = 0.0;
+      if (B <= 64) {   // every load of the quarter issued at once (one latency), summed in the loop's order
+        double p0[16], p1[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int bb = u + 16 * (k >> 2) + 4 * (k & 3);
+          p0[k] = bb < B ? part[((long)bb * S + s) * NBS + j0] : 0.0;
+          p1[k] = bb < B ? part[((long)bb * S + s) * NBS + j0 + 1] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          t0 += p0[k];
+          t1 += p1[k];
+        }
+        q4[u][s][0] = t0;
+        q4[u][s][1] = t1;
+        continue;
+      }
       for (int bb0 = u; bb0 < B; bb0 += 16) {
         double p0[4], p1[4];
 #pragma unroll
