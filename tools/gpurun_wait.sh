@@ -7,7 +7,7 @@ for i in $(seq 1 20); do
   out=$(/usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
   rc=$?
   echo "$out" | tail -25
-  if echo "$out" | grep -q "slot(s) on this pod are busy\|no box\|status=transient"; then
+  if echo "$out" | grep -q "slot(s) on this pod are busy\|no box\|status=transient\|backing off"; then
     sleep 90
     continue
   fi

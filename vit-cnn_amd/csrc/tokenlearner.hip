@@ -290,22 +290,38 @@ __global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int
   const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15, LS = Lp + 4;
   float* al = sm_f;              // [Sp][LS]
   float* xt = sm_f + Sp * LS;    // [64][LS]  x^T of the block's channels
+  float* mxl = xt + TL_CT * LS;  // [Lp] the sample's pooled max / mean, [S][TPAR] the tokens' parameters
+  float* avl = mxl + Lp;
+  float* parl = avl + Lp;
   const long n = (long)B * HW;
-  // the sample's channel tile, transposed into LDS (coalesced rows of 64 channels; zero padding)
-  for (int i = threadIdx.x; i < Lp * TL_CT; i += 256) {
-    const int q = i / TL_CT, cl = i - q * TL_CT;
-    const int c = c0 + cl;
-    xt[cl * LS + q] = (q < HW && c < C) ? x[((long)b * HW + q) * ldx + c] : 0.f;
+  // the sample's channel tile, transposed into LDS (coalesced rows of 64 channels; zero padding), 4 loads of a
+  // thread in flight at a time
+  for (int i0 = threadIdx.x; i0 < Lp * TL_CT; i0 += 4 * 256) {
+    float xv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 256 * u, q = i / TL_CT, c = c0 + (i - q * TL_CT);
+      xv[u] = (i < Lp * TL_CT && q < HW && c < C) ? x[((long)b * HW + q) * ldx + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 256 * u, q = i / TL_CT, cl = i - q * TL_CT;
+      if (i < Lp * TL_CT) xt[cl * LS + q] = xv[u];
+    }
   }
+  for (int i = threadIdx.x; i < Lp; i += 256) {
+    mxl[i] = i < HW ? mx[(long)b * HW + i] : 0.f;
+    avl[i] = i < HW ? avg[(long)b * HW + i] : 0.f;
+  }
+  for (int i = threadIdx.x; i < S * TPAR; i += 256) parl[i] = par[i];
   tl_token_stats(train, n, S, mx, avg, par, buf, eps, momentum, part, P, stats, red, tok_mean, tok_inv);
   for (int i = threadIdx.x; i < Sp * Lp; i += 256) {
     const int s = i / Lp, q = i - s * Lp;
     float av = 0.f;
     if (s < S && q < HW) {
-      const float* p = par + (long)s * TPAR;
+      const float* p = parl + s * TPAR;
       double xh;
-      const float bn = tl_bnv(mx[(long)b * HW + q], avg[(long)b * HW + q], p[0], p[1], p[2], tok_mean[s], tok_inv[s],
-                              p[3], p[4], xh);
+      const float bn = tl_bnv(mxl[q], avl[q], p[0], p[1], p[2], tok_mean[s], tok_inv[s], p[3], p[4], xh);
       av = sigmoid_f(fmaxf(bn, 0.f));
       if (a_out && blockIdx.y == 0) a_out[((long)b * S + s) * HW + q] = av;
     }
@@ -335,12 +351,16 @@ __global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int
 // the block's 16 tokens (MFMA, both operands as float4 runs of their rows straight from L2), written to `da`;
 // then per token the fp64 sums over this sample's pixels of g1, g1 xh, g1 (m - mbar), g1 (v - vbar) ->
 // part[(b * S + s) * NBS + j] (summed over the pixel tiles in a fixed order).
-__global__ __launch_bounds__(256) void tl_bwd_da(int B, int HW, int C, int S, const float* __restrict__ x, long ldx,
-                                                 const float* __restrict__ mx, const float* __restrict__ avg,
-                                                 const float* __restrict__ par, const double* __restrict__ stats,
-                                                 const float* __restrict__ dZ, float* __restrict__ da,
-                                                 double* __restrict__ part) {
-  __shared__ double tsum[4][16][NBS];   // [wave][token][sum]
+// TLDA_W waves per block: one 16-pixel tile per wave up to HW = 16 TLDA_W (a wave with two tiles doubled the
+// block's chain of dependent k-chunk loads)
+constexpr int TLDA_W = 8;
+__global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, int S, const float* __restrict__ x,
+                                                         long ldx, const float* __restrict__ mx,
+                                                         const float* __restrict__ avg, const float* __restrict__ par,
+                                                         const double* __restrict__ stats,
+                                                         const float* __restrict__ dZ, float* __restrict__ da,
+                                                         double* __restrict__ part) {
+  __shared__ double tsum[TLDA_W][16][NBS];   // [wave][token][sum]
   const int b = blockIdx.x, s0 = blockIdx.y * 16;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
   const int Lp = (HW + 15) & ~15, nqt = Lp / 16, nkc = (C + 15) / 16;
@@ -365,7 +385,7 @@ __global__ __launch_bounds__(256) void tl_bwd_da(int B, int HW, int C, int S, co
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int j = 0; j < NBS; ++j) v[r][j] = 0.0;
-  for (int qt = w; qt < nqt; qt += 4) {
+  for (int qt = w; qt < nqt; qt += TLDA_W) {
     const int qb = 16 * qt + r16;   // this lane's B column (pixel)
     const float* brow = x + ((long)b * HW + min(qb, HW - 1)) * ldx;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -420,7 +440,10 @@ __global__ __launch_bounds__(256) void tl_bwd_da(int B, int HW, int C, int S, co
   __syncthreads();
   if (threadIdx.x < 16 * NBS) {
     const int tl = threadIdx.x / NBS, j = threadIdx.x - tl * NBS, s = s0 + tl;
-    if (s < S) part[((long)b * S + s) * NBS + j] = ((tsum[0][tl][j] + tsum[1][tl][j]) + tsum[2][tl][j]) + tsum[3][tl][j];
+    double t = tsum[0][tl][j];
+#pragma unroll
+    for (int ww = 1; ww < TLDA_W; ++ww) t += tsum[ww][tl][j];   // the waves in order
+    if (s < S) part[((long)b * S + s) * NBS + j] = t;
   }
 }
 
@@ -660,7 +683,7 @@ VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx,
 
 static size_t tl_fwd_lds(int HW, int S) {
   const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15;
-  return (size_t)(Sp + TL_CT) * (Lp + 4) * sizeof(float);
+  return (size_t)((Sp + TL_CT) * (Lp + 4) + 2 * Lp + S * TPAR) * sizeof(float);
 }
 static size_t tl_bwd_lds(int HW, int S) {
   const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15;
@@ -689,7 +712,7 @@ VC_API int vc_tl_bwd(int train, int B, int HW, int C, int S, const float* x, lon
   VC_REQUIRE(tl_bwd_lds(HW, S) <= 160 * 1024);
   VC_REQUIRE_I32((long)B * HW * (S > C ? S : C));
   double* part = ws + tl_pix_partials((long)B * HW);
-  hipLaunchKernelGGL(tl_bwd_da, dim3(B, vc_cdiv(S, 16)), dim3(256), 0, stream, B, HW, C, S, x, ldx, mx, avg, params,
+  hipLaunchKernelGGL(tl_bwd_da, dim3(B, vc_cdiv(S, 16)), dim3(64 * TLDA_W), 0, stream, B, HW, C, S, x, ldx, mx, avg, params,
                      stats, dZ, da, part);
   VC_CHECK_LAUNCH();
   hipLaunchKernelGGL(tl_bwd_dx, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_bwd_lds(HW, S), stream, train, B, HW, C, S,
