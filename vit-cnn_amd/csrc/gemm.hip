@@ -1144,6 +1144,10 @@ struct PipePlan {
   int bm, bn, ns, nsplit, k_chunk, tn, tm;
 };
 
+// bf16 64 x 64 tiles on 8 waves (2 x 4 of 32 x 16: two waves per SIMD, half the DMA pieces per wave) instead of 4
+// (knob: probe library)
+static int pipe_bf_w8() { return vc_knob("VITCNN_PIPE_BF_W8", 1) ? 1 : 0; }
+
 // k-split waves (gp::pipe_tile KS = 2) for fp32 64 x 64 tiles: only where the grid is at most one block
 // per CU and K is long (the local 3x3 convs, M = B 49, K = 9 C: 34.1 -> 31.8 us); elsewhere measured
 // equal or slower (tools/gemm_one.py, profiles/r05_gemm_ks.log; on every pipelined GEMM of the step
@@ -1239,6 +1243,7 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
     if (p.bm == 128 && p.bn == 64) VC_GPB_L(128, 64, 4, 2, 2);
     else if (p.bm == 64 && p.bn == 128) VC_GPB_L(64, 128, 2, 4, 2);
     else if (p.ns == 4) VC_GPB_L(64, 64, 2, 2, 4);
+    else if (pipe_bf_w8()) VC_GPB_L(64, 64, 2, 4, 2);
     else VC_GPB_L(64, 64, 2, 2, 2);
   } else if (p.ns == 4) VC_GP_T(4);
   else VC_GP_T(2);
@@ -1361,6 +1366,9 @@ static int group_flush(GroupState& st) {
     for (int p = 0; p < np; ++p) any_bf |= st.pipes[p].variant >= 4;
     if (!any_bf && vc_knob("VITCNN_PIPE_KS", 0) == 2)   // (grouped problems: measured no gain)
       hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2, 2>), dim3((unsigned)total), dim3(512), 0, st.stream, P,
+                         (unsigned)total);
+    else if (any_bf && pipe_bf_w8())   // a bf16 group: 8 waves of 32 x 16 (fp32 members alike)
+      hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 4, 2>), dim3((unsigned)total), dim3(512), 0, st.stream, P,
                          (unsigned)total);
     else
       hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0, st.stream, P,
@@ -1497,10 +1505,14 @@ VC_EXPORT int vc_gemm_colstats(int M, int N, int K, const float* A, long lda, co
   g.shift = bias;
   const long total = (long)p.tn * p.tm;
   dim3 grid((unsigned)total);
-  if (bf)
-    hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2, true>), grid, dim3(256), 0, stream, g, p.tn, p.tm,
-                       (unsigned)total, 1, 1);
-  else if (pipe_ks(total, 1, K) == 2)
+  if (bf) {
+    if (pipe_bf_w8())
+      hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 4, false, true, 2, true>), grid, dim3(512), 0, stream, g, p.tn,
+                         p.tm, (unsigned)total, 1, 1);
+    else
+      hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2, true>), grid, dim3(256), 0, stream, g, p.tn,
+                         p.tm, (unsigned)total, 1, 1);
+  } else if (pipe_ks(total, 1, K) == 2)
     hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2, false, 2>), grid, dim3(512), 0, stream, g, p.tn,
                        p.tm, (unsigned)total, 1, 1);
   else
