@@ -1147,13 +1147,16 @@ struct PipePlan {
 // bf16 64 x 64 tiles on 8 waves (2 x 4 of 32 x 16: two waves per SIMD, half the DMA pieces per wave) instead of 4
 // (knob: probe library)
 static int pipe_bf_w8() { return vc_knob("VITCNN_PIPE_BF_W8", 1) ? 1 : 0; }
+// the same for fp32 tiles: equal or 1-5 % faster on every shape of the step, step 1.714 -> 1.690 ms
+// (profiles/r05_gemm_f32_w8.log; knob: probe library)
+static int pipe_f32_w8() { return vc_knob("VITCNN_PIPE_F32_W8", 1) ? 1 : 0; }
 
-// k-split waves (gp::pipe_tile KS = 2) for fp32 64 x 64 tiles: only where the grid is at most one block
-// per CU and K is long (the local 3x3 convs, M = B 49, K = 9 C: 34.1 -> 31.8 us); elsewhere measured
-// equal or slower (tools/gemm_one.py, profiles/r05_gemm_ks.log; on every pipelined GEMM of the step
-// 1.744 -> 1.757 ms).  Knob (probe library): 0 = this rule, 1 = never, 2 = always.
+// k-split waves (gp::pipe_tile KS = 2) for fp32 64 x 64 tiles.  Rule 0: where the grid is at most one block per CU
+// and K is long (the local 3x3 convs, M = B 49, K = 9 C: 34.1 -> 31.8 us; elsewhere equal or slower,
+// profiles/r05_gemm_ks.log).  Superseded by the 8-wave 2 x 4 layout (pipe_f32_w8: 32.1 us on the local conv and
+// faster elsewhere), so the default is 1 = never.  Knob (probe library): 0 = the rule, 1 = never, 2 = always.
 static int pipe_ks(long tiles = 0, int nsplit = 1, int K = 0) {
-  const int k = vc_knob("VITCNN_PIPE_KS", 0);
+  const int k = vc_knob("VITCNN_PIPE_KS", 1);
   if (k) return k == 2 ? 2 : 1;
   return (nsplit == 1 && tiles > 0 && tiles <= 256 && K >= 1024) ? 2 : 1;
 }
@@ -1228,6 +1231,7 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
     if (p.bm == 128 && p.bn == 64) VC_GP(128, 64, 4, 2, NS_, 1);     \
     else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_, 1); \
     else if (pipe_ks(tiles, p.nsplit, K) == 2) VC_GP(64, 64, 2, 2, NS_, 2); \
+    else if (pipe_f32_w8()) VC_GP(64, 64, 2, 4, NS_, 1);            \
     else VC_GP(64, 64, 2, 2, NS_, 1);                               \
   } while (0)
 #define VC_GPB(BM_, BN_, WM_, WN_, TA_, TB_, NS_) \
@@ -1367,7 +1371,7 @@ static int group_flush(GroupState& st) {
     if (!any_bf && vc_knob("VITCNN_PIPE_KS", 0) == 2)   // (grouped problems: measured no gain)
       hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2, 2>), dim3((unsigned)total), dim3(512), 0, st.stream, P,
                          (unsigned)total);
-    else if (any_bf && pipe_bf_w8())   // a bf16 group: 8 waves of 32 x 16 (fp32 members alike)
+    else if ((any_bf && pipe_bf_w8()) || (!any_bf && pipe_f32_w8()))   // 8 waves of 32 x 16
       hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 4, 2>), dim3((unsigned)total), dim3(512), 0, st.stream, P,
                          (unsigned)total);
     else
@@ -1515,6 +1519,9 @@ VC_EXPORT int vc_gemm_colstats(int M, int N, int K, const float* A, long lda, co
   } else if (pipe_ks(total, 1, K) == 2)
     hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2, false, 2>), grid, dim3(512), 0, stream, g, p.tn,
                        p.tm, (unsigned)total, 1, 1);
+  else if (pipe_f32_w8())
+    hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 4, false, true, 2>), grid, dim3(512), 0, stream, g, p.tn, p.tm,
+                       (unsigned)total, 1, 1);
   else
     hipLaunchKernelGGL((gp::gemm_pipe<64, 64, 2, 2, false, true, 2>), grid, dim3(256), 0, stream, g, p.tn, p.tm,
                        (unsigned)total, 1, 1);
