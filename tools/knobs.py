@@ -20,7 +20,7 @@ PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITC
                "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE", "VITCNN_GEMM_PIPE_SMALL",
                "VITCNN_PIPE_NS", "VITCNN_PIPE_KS", "VITCNN_PIPE_BF_W8", "VITCNN_PIPE_F32_W8", "VITCNN_PIPE_SPLIT_BLOCKS", "VITCNN_GEMM_GROUP_MAXB",
                "VITCNN_TAP_TARGET", "VITCNN_TAP_PIPE", "VITCNN_CONV_PIPE_TILES_F", "VITCNN_CONV_PIPE_TILES_W",
-               "VITCNN_CONV_PIPE_TILES_D", "VITCNN_ATTN_BWD_WPB", "VITCNN_ATTN_FWD_WPB")
+               "VITCNN_CONV_PIPE_TILES_D", "VITCNN_CONV_PIPE_W8", "VITCNN_ATTN_BWD_WPB", "VITCNN_ATTN_FWD_WPB")
 
 
 def use_probe():

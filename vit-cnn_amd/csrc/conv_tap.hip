@@ -403,10 +403,12 @@ __global__ __launch_bounds__(256) void conv_pack_many(PackMany P) {
 // conv_tap's 77-91 (tools/gemm_one.py, round 4).
 constexpr int CP_B = 64;   // output tile (both sides)
 
-template <int MODE>
-__global__ __launch_bounds__(256) void conv_pipe(TapArgs a, int tn, int nsplit, unsigned total) {
-  constexpr int BM = CP_B, BN = CP_B, WN = 2, NW = 4, NS = 2;
-  constexpr int WTM = BM / 2, WTN = BN / 2, MT = WTM / 16, NT = WTN / 16;
+// NW = 8 (round 5): the tile on 2 x 4 waves of 32 x 16 (two waves per SIMD, one DMA piece per operand per wave),
+// as gemm.hip's pipelined kernel
+template <int MODE, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void conv_pipe(TapArgs a, int tn, int nsplit, unsigned total) {
+  constexpr int BM = CP_B, BN = CP_B, WN = NW / 2, NS = 2, QN = 8 / NW;
+  constexpr int WTM = BM / 2, WTN = BN / WN, MT = WTM / 16, NT = WTN / 16;
   constexpr int SA_B = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int LOADS = (BM / 8 + BN / 8) / NW;
   constexpr bool TA = MODE == WGRAD;   // A image [k][m] (row-contiguous) for the weight gradient
@@ -414,7 +416,7 @@ __global__ __launch_bounds__(256) void conv_pipe(TapArgs a, int tn, int nsplit, 
   typedef g2::Stage<false, TA, BM, false> SA;
   typedef g2::Stage<false, TB, BN, false> SB;
   __shared__ __attribute__((aligned(1024))) char smem[gp::ring_bytes<BM, BN, NS>()];
-  __shared__ float bsh[4][64];
+  __shared__ float bsh[NW][64];
   int zs, xn, ym, zb;
   const int tm = (a.M + BM - 1) / BM;
   gp::tile_coords(gp::xcd_linear(blockIdx.x, total), nsplit, tn, tm, 1, zs, xn, ym, zb);
@@ -433,11 +435,11 @@ __global__ __launch_bounds__(256) void conv_pipe(TapArgs a, int tn, int nsplit, 
   const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.w), (short)0,
                                                     a.w ? (int)((long)a.O * 9 * a.Cw * 4) : 0, 0x00020000);
   // K-contiguous fills (FWD A / B, DGRAD A): this lane's two image rows, decomposed once
-  int kb_[2], ki_[2], kj_[2];
-  bool kok_[2];
+  int kb_[QN], ki_[QN], kj_[QN];
+  bool kok_[QN];
   if constexpr (MODE != WGRAD) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < QN; ++q) {
       const int rloc = 8 * (wave + NW * q) + (lane >> 3);
       const int m = m0 + rloc;
       kok_[q] = m < a.M;
@@ -449,7 +451,7 @@ __global__ __launch_bounds__(256) void conv_pipe(TapArgs a, int tn, int nsplit, 
     char* st = smem + (t % NS) * STAGE;
     const int kt = kt0 + t;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < QN; ++q) {
       const int i = wave + NW * q;   // wave-instruction: 1 KB of each image
       // K-contiguous chunk coordinates
       const int rloc = 8 * i + (lane >> 3), kk = 4 * ((lane & 7) ^ ((rloc >> 1) & 7));
@@ -509,7 +511,8 @@ __global__ __launch_bounds__(256) void conv_pipe(TapArgs a, int tn, int nsplit, 
     if (do_b) {
       const int mm = tid & 63, kq = tid >> 6;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) bacc += *reinterpret_cast<const float*>(cur + SA::rc_off(8 * kq + k, mm));
+      for (int k = 0; k < 32 / NW; ++k)
+        bacc += *reinterpret_cast<const float*>(cur + SA::rc_off((32 / NW) * kq + k, mm));
     }
     g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
   }
@@ -521,7 +524,9 @@ __global__ __launch_bounds__(256) void conv_pipe(TapArgs a, int tn, int nsplit, 
     __syncthreads();
     const int row = m0 + mm;
     if (kq == 0 && row < a.M) {
-      const float v = ((bsh[0][mm] + bsh[1][mm]) + bsh[2][mm]) + bsh[3][mm];
+      float v = bsh[0][mm];
+#pragma unroll
+      for (int w2 = 1; w2 < NW; ++w2) v += bsh[w2][mm];   // the k groups in order
       if (split) a.part[((long)zs * a.M + row) * a.N + 9 * a.C] = v;
       else a.dbias[row] = v;
     }
@@ -600,7 +605,12 @@ int launch_conv_pipe(TapArgs& a, int grid_n, float* ws, long ws_floats, hipStrea
   a.part = nsplit > 1 ? ws : nullptr;
   const long total = tiles * nsplit;
   VC_REQUIRE(total < (1L << 31));
-  hipLaunchKernelGGL(conv_pipe<MODE>, dim3((unsigned)total), dim3(256), 0, stream, a, grid_n, nsplit, (unsigned)total);
+  if (vc_knob("VITCNN_CONV_PIPE_W8", 1))   // 8 waves (knob: probe library)
+    hipLaunchKernelGGL((conv_pipe<MODE, 8>), dim3((unsigned)total), dim3(512), 0, stream, a, grid_n, nsplit,
+                       (unsigned)total);
+  else
+    hipLaunchKernelGGL((conv_pipe<MODE, 4>), dim3((unsigned)total), dim3(256), 0, stream, a, grid_n, nsplit,
+                       (unsigned)total);
   VC_CHECK_LAUNCH();
   if (nsplit > 1) {
     const long n = (long)a.M * a.N;
@@ -613,11 +623,12 @@ int launch_conv_pipe(TapArgs& a, int grid_n, float* ws, long ws_floats, hipStrea
 }
 
 // can the pipelined kernel take this conv: whole 16-B chunks everywhere (C, O and the leading dimensions
-// multiples of 4, 16-B aligned bases) and operands under 2 GB (32-bit buffer offsets); knob TAP_PIPE=0 keeps
-// conv_tap (probe library)
+// multiples of 4, 16-B aligned bases) and operands under 2 GB (32-bit buffer offsets).  Round 5, with the 8-wave
+// conv_pipe: every direction (FusAtNet step 18.21 -> 18.04-18.06 ms; wgrad only 18.14,
+// profiles/r05_fusat_conv_pipe_w8.log); knob TAP_PIPE = direction bit mask (probe library)
 bool conv_pipe_ok(int mode, const TapArgs& a, const void* p0, long ld0, const void* p1, long ld1) {
   const long in_b = (long)a.nb * a.H * a.W * 4, out_b = (long)a.nb * a.OH * a.OW * 4;
-  return (vc_knob("VITCNN_TAP_PIPE", 1 << WGRAD) >> mode & 1) && a.C % 4 == 0 && a.O % 4 == 0 && ld0 % 4 == 0 && ld1 % 4 == 0 &&
+  return (vc_knob("VITCNN_TAP_PIPE", 7) >> mode & 1) && a.C % 4 == 0 && a.O % 4 == 0 && ld0 % 4 == 0 && ld1 % 4 == 0 &&
          ((uintptr_t)p0 % 16) == 0 && ((uintptr_t)p1 % 16) == 0 && in_b * std::max(ld0, ld1) < (1L << 31) &&
          out_b * std::max(ld0, ld1) < (1L << 31) && (long)a.O * 9 * a.Cw * 4 < (1L << 31);
 }
