@@ -77,16 +77,6 @@ VC_API int vc_gemm_tune(int bm, int bn, int nsplit, int pf, int combine);
  * (vc_bn_apply_partials finishes the BatchNorm).  A, W 16-B aligned, K, lda, ldw multiples of 4. */
 VC_API int vc_gemm_colstats(int M, int N, int K, const float* A, long lda, const float* W, long ldw, const float* bias,
                             float* C, long ldc, int flags, double* colstats, hipStream_t stream);
-/* Deferred split-K reduction: flags&128 (F_DEFER) -- the product's split-K slabs go to the caller's `ws` (a
- * buffer of its own, from its start, left intact) and are NOT reduced; a later call with the same arguments
- * and flags&256 (F_REDUCE_ONLY) launches only that reduction (inside a group: it joins the group's one
- * grouped reduce).  Lets a chain keep a weight gradient's reduce off its critical stream.  A product that
- * does not split, or whose kernel has no deferred form, ignores both bits (F_REDUCE_ONLY is then a no-op).
- * vc_gemm_defer_floats: the slab floats an F_DEFER call of the product needs, given the capacity ws_floats
- * it is planned with (0: nothing deferred). */
-VC_API int vc_gemm_defer_floats(int transA, int transB, int M, int N, int K, const float* A, long lda,
-                                const float* B, long ldb, int batch, int bias_grad, int flags, long ws_floats);
-
 /* Grouped launches: a horizontal fusion of independent products (a layer's weight and data
  * gradients, parallel branches).  `group` is caller-owned host memory of VC_GEMM_GROUP_BYTES bytes
  * (8-byte aligned) holding the group's state -- the library keeps none, so distinct groups (one per
@@ -383,13 +373,18 @@ VC_API int vc_rowchain_ln_part_floats(int rows, int E);
 
 /* ---------------------------------------------------------------- TokenLearner
  * TokenLearner(S) of SpatialAttention (Mutimodality_Mamba7.py:26-64) over x [B*HW, C] channels-last
- * (C % 4 == 0, ldx % 4 == 0, x / dZ 16-B aligned, S <= 128).  params: S x 5 floats [conv.0.weight(2),
+ * (C % 4 == 0, ldx % 4 == 0, x / dZ 16-B aligned; HW, S within the LDS plans: vc_tl_check).  params: S x 5
+ * floats [conv.0.weight(2),
  * conv.0.bias, conv.1.weight, conv.1.bias]; bn_buffers: S x 2 [running_mean, running_var]; stats: 2 S + 8
  * fp64 -- per token [mean, invstd] of its BN(1) input, then the shared moments of the pooled (max, mean)
  * pair [n, mbar, vbar, Cmm, Cmv, Cvv, Km, Kv] -- kept for the backward (statistics and gradient sums in
  * fp64, as torch's CPU BatchNorm accumulates); ws: vc_tl_ws_floats(B, HW, S) floats of per-call-site
  * scratch (8-B aligned).  vc_tl_pixel_stats leaves the moment partials in ws for vc_tl_fwd. */
 VC_API int vc_tl_ws_floats(int B, int HW, int S);
+/* 0 when vc_tl_pixel_stats / vc_tl_fwd / vc_tl_bwd support the shape (C <= 512; the tokens of the forward and the
+ * pixels of the backward are chunked so their LDS fits: up to 20 x 20 pixel grids with S = 18 x 18 tokens),
+ * 1 otherwise.  Host-only (no HIP call). */
+VC_API int vc_tl_check(int HW, int C, int S);
 /* per pixel row of x [M, C] (C <= 512): channel max, its first argmax, channel mean; + moment partials */
 VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg, double* ws,
                              hipStream_t stream);

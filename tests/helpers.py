@@ -57,9 +57,13 @@ def relu_masks_from_workspace(model, B):
     P = model.patch
     masks = {}
 
+    def nchw(name, H, C):
+        return ws.tensor(name)[: B * H * H * C].view(B, H, H, C).permute(0, 3, 1, 2).cpu()
+
     def grab(pfx, H, C):
-        t = ws.tensor(pfx + ".out")[: B * H * H * C].view(B, H, H, C).permute(0, 3, 1, 2).cpu()
+        t = nchw(pfx + ".out", H, C)
         masks[pfx] = t > 0
+        masks[pfx + "#out"] = t   # the HIP post-ReLU values (decision audit: the tensor's measured fp32 error)
 
     for blk, H, cout in (("hsi1", P, model.hsi1.cout), ("hsi2", P - 2, model.hsi2.cout)):
         S = H - 2
@@ -78,6 +82,8 @@ def relu_masks_from_workspace(model, B):
                                   params[pfx + ".tokenizers.0.conv.0.weight"], ws.tensor(pfx + ".st").data_ptr(),
                                   mask.data_ptr(), torch.cuda.current_stream().cuda_stream)
             masks[pfx] = mask.view(B, S, H, H).cpu().bool()
+            # the TokenLearner's HIP input (change_dim / channel_feature output) for the pooled-value audit
+            masks[pfx + "#x"] = nchw(blk + (".CD" if tl == ".global_feature" else ".CF"), H, cout)
     grab("lidar1", P - 2, 16)
     grab("lidar2", P - 4, 32)
     grab("fusion1.FusionLayer", P - 2, 128)
@@ -89,6 +95,8 @@ def relu_masks_from_workspace(model, B):
         Pk = (Hs // 2) ** 2
         pa = ws.tensor(blk + ".PA")[: B * Pk * 2 * Ci].view(B, Pk, 2 * Ci).cpu().long()
         masks[blk + ".FusionLayer.cross_attention.pool"] = pa
+        masks[blk + ".FusionLayer.cross_attention.pool#val"] = ws.tensor(blk + ".PP")[: B * Pk * 2 * Ci].view(
+            B, Pk, 2 * Ci).cpu()
     return masks
 
 
@@ -110,7 +118,101 @@ def tl_pooled_from_workspace(model, B):
     return out
 
 
-def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None):
+EPS32 = float(np.finfo(np.float32).eps)
+TIE_ULPS = 16   # a decision may differ from float64's only within this many fp32 ulps of the decision's scale
+
+
+def _audit_relu(audit, site, pre, mask, out=None, kind="relu"):
+    """One ReLU site: where the HIP decision `mask` differs from float64's (pre > 0), |pre| must be a near-tie --
+    within TIE_ULPS ulps of the tensor's largest |pre|, or within 2x the HIP values' own measured deviation from
+    float64 on that tensor (max |out - pre| over the elements both call positive)."""
+    p = pre.detach()
+    m = mask.to(torch.bool).expand_as(p)
+    d = (p > 0) != m
+    tie = TIE_ULPS * EPS32 * float(p.abs().max())
+    e_obs = 0.0
+    if out is not None:
+        both = (p > 0) & m
+        if bool(both.any()):
+            e_obs = float((out.double() - p)[both].abs().max())
+    tol = max(tie, 2.0 * e_obs)
+    dist = float(p[d].abs().max()) if bool(d.any()) else 0.0
+    audit.append(dict(site=site, kind=kind, n=p.numel(), disagree=int(d.sum()), dist=dist, tie=tie, e_obs=e_obs,
+                      worst=dist / tol if tol > 0 else (0.0 if dist == 0 else float("inf"))))
+
+
+def _audit_pool(audit, site, pre, taps, vals=None):
+    """One 2x2 max pool: where the HIP winning tap differs from float64's argmax (and is not an exact float64
+    tie), the window's top-2 gap must be within TIE_ULPS ulps of the window maximum (or 2x the HIP pooled
+    values' measured deviation from the float64 pooled values)."""
+    b, c, h, w = pre.shape
+    ph, pw = h // 2, w // 2
+    win = pre.detach()[:, :, :2 * ph, :2 * pw].reshape(b, c, ph, 2, pw, 2).permute(0, 1, 2, 4, 3, 5).reshape(
+        b, c, ph, pw, 4)
+    t = taps.transpose(1, 2).reshape(b, c, ph, pw, 1)
+    got = torch.gather(win, 4, t)[..., 0]
+    best = win.max(dim=4).values
+    gap = best - got
+    d = gap > 0
+    e_obs = 0.0
+    if vals is not None:
+        e_obs = float((vals.transpose(1, 2).reshape(b, c, ph, pw).double() - got).abs().max())
+    tol = torch.clamp(TIE_ULPS * EPS32 * best.abs(), min=2.0 * e_obs)
+    ratio = float((gap[d] / tol[d]).max()) if bool(d.any()) else 0.0
+    audit.append(dict(site=site, kind="maxpool", n=best.numel(), disagree=int(d.sum()),
+                      dist=float(gap[d].max()) if bool(d.any()) else 0.0, e_obs=e_obs, worst=ratio))
+
+
+def _audit_tl_pool(audit, site, x, pooled, x_hip=None):
+    """The TokenLearner pooled values the yardstick adopts from the HIP path: max / mean per pixel within the
+    HIP input's own deviation from float64 (max is 1-Lipschitz in the sup norm; the mean adds its fp32 sum's
+    rounding), and the HIP argmax channel a near-maximum of the float64 row."""
+    mx_h, amx_h, avg_h = pooled
+    x = x.detach()
+    ex = (x_hip.double() - x).abs().max(dim=1, keepdim=True).values if x_hip is not None else torch.zeros_like(mx_h)
+    xs = x.abs().max(dim=1, keepdim=True).values
+    mx64 = x.max(dim=1, keepdim=True).values
+    mean64 = x.mean(dim=1, keepdim=True)
+    tol_max = ex + 2 * EPS32 * xs
+    tol_mean = ex + TIE_ULPS * EPS32 * xs
+    r_max = float(((mx_h - mx64).abs() / tol_max).max())
+    r_mean = float(((avg_h - mean64).abs() / tol_mean).max())
+    at = torch.gather(x, 1, amx_h)
+    d = at < mx64
+    r_arg = float(((mx64 - at)[d] / (2 * tol_max[d])).max()) if bool(d.any()) else 0.0
+    rel = float(torch.cat([((mx_h - mx64).abs() / xs).flatten(), ((avg_h - mean64).abs() / xs).flatten()]).max())
+    audit.append(dict(site=site, kind="tl_pool", n=mx_h.numel(), disagree=int(d.sum()), rel=rel,
+                      worst=max(r_max, r_mean, r_arg)))
+
+
+def audit_summary(audit):
+    """{kind: [sites, decisions, disagreements, worst ratio to the tie bound]} + the failing records"""
+    out = {}
+    for r in audit:
+        k = out.setdefault(r["kind"], [0, 0, 0, 0.0])
+        k[0] += 1
+        k[1] += r["n"]
+        k[2] += r["disagree"]
+        k[3] = max(k[3], r["worst"])
+    return out, [r for r in audit if not r["worst"] <= 1.0]
+
+
+def check_audit(audit, name):
+    """assert every adopted HIP decision is a genuine fp32 near-tie; print the counts (and write them to
+    gpurun_out/decision_audit_<name>.json when that directory exists)"""
+    import json
+    summary, bad = audit_summary(audit)
+    print(f"decision audit {name}: " + ", ".join(f"{k}: {v[2]} of {v[1]} differ from float64 over {v[0]} sites "
+                                                 f"(worst {v[3]:.3g} of the tie bound)" for k, v in summary.items()))
+    if os.path.isdir("gpurun_out"):
+        with open(f"gpurun_out/decision_audit_{name}.json", "w") as f:
+            json.dump({"summary": summary, "records": audit}, f, indent=1)
+    assert summary, "no decision was audited"
+    assert not bad, bad[:5]
+    return summary
+
+
+def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None, audit=None):
     """oracle train step in which the conv/fusion ReLUs use the given masks (pre * mask) instead of
     their own sign test, and the NonLocal 2x2 max pools the given winning taps (`<prefix>.pool` entries).  A pre-activation within rounding distance of zero is an fp32 tie that the
     HIP path and the CPU reference may resolve differently; evaluating the float64 yardstick with the
@@ -120,7 +222,11 @@ def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None)
     normalises a 2->1 conv of the pooled channel max / mean whose spread is a tiny fraction of its
     mean, so the fp32 rounding of the pooled values is amplified by 1/std.  The yardstick then takes
     the HIP path's pooled VALUES (gradients still flow to the argmax channel and to every channel
-    through the mean, exactly as in the reference)."""
+    through the mean, exactly as in the reference).
+
+    `audit` (a list): every adopted decision is also compared with the float64 decision at the same site and
+    a record appended (helpers._audit_*: where the two differ, the float64 values must be a near-tie);
+    check_audit asserts them (the yardstick may not absorb a non-tie decision)."""
     orig = (O.bn_conv3_relu, O.conv_bn_relu_1x1, O.token_learner, O.non_local)
     F = torch.nn.functional
 
@@ -140,19 +246,28 @@ def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None)
         taps = masks[key]
         ci = taps.shape[2] // 2
         theta = O.conv2d(P, pfx + ".theta", x).flatten(2).transpose(1, 2)
-        phi = pool_taps(O.conv2d(P, pfx + ".phi.0", y), taps[:, :, :ci]).flatten(2)
+        phi_pre, g_pre = O.conv2d(P, pfx + ".phi.0", y), O.conv2d(P, pfx + ".g.0", z)
+        if audit is not None:
+            vals = masks.get(key + "#val")
+            _audit_pool(audit, key + ".phi", phi_pre, taps[:, :, :ci], None if vals is None else vals[:, :, :ci])
+            _audit_pool(audit, key + ".g", g_pre, taps[:, :, ci:], None if vals is None else vals[:, :, ci:])
+        phi = pool_taps(phi_pre, taps[:, :, :ci]).flatten(2)
         att = torch.softmax(theta @ phi, dim=-1)
-        g = pool_taps(O.conv2d(P, pfx + ".g.0", z), taps[:, :, ci:]).flatten(2).transpose(1, 2)
+        g = pool_taps(g_pre, taps[:, :, ci:]).flatten(2).transpose(1, 2)
         o = (att @ g).transpose(1, 2).reshape(b, -1, *x.shape[2:])
         wy = O.batchnorm(P, pfx + ".W.1", O.conv2d(P, pfx + ".W.0", o))
         return wy + z
 
     def bn_conv3(P, pfx, x):
         pre = O.conv2d(P, pfx + ".conv", O.batchnorm(P, pfx + ".bn", x))
+        if audit is not None and pfx in masks:
+            _audit_relu(audit, pfx, pre, masks[pfx], masks.get(pfx + "#out"))
         return pre * masks[pfx].to(pre.dtype) if pfx in masks else torch.relu(pre)
 
     def conv1x1(P, pfx, x):
         pre = O.batchnorm(P, pfx + ".1", O.conv2d(P, pfx + ".0", x))
+        if audit is not None and pfx in masks:
+            _audit_relu(audit, pfx, pre, masks[pfx], masks.get(pfx + "#out"))
         return pre * masks[pfx].to(pre.dtype) if pfx in masks else torch.relu(pre)
 
     def token_learner(P, pfx, x, S):   # oracle token_learner with the HIP path's decisions / pooling
@@ -161,6 +276,8 @@ def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None)
             return orig[2](P, pfx, x, S)
         if given:
             mx_h, amx_h, avg_h = (t.to(x.dtype) if t.is_floating_point() else t for t in pooled[pfx])
+            if audit is not None:
+                _audit_tl_pool(audit, pfx, x, (mx_h, amx_h, avg_h), masks.get(pfx + "#x"))
             g = torch.gather(x, 1, amx_h)
             m = x.mean(dim=1, keepdim=True)
             pool = torch.cat([mx_h + (g - g.detach()), avg_h + (m - m.detach())], dim=1)
@@ -171,6 +288,8 @@ def masked_oracle_step(O, state, hsi, lidar, target, weight, masks, pooled=None)
             t = f"{pfx}.tokenizers.{i}.conv"
             f = F.conv2d(pool, P[t + ".0.weight"], P[t + ".0.bias"])
             pre = O.batchnorm(P, t + ".1", f)
+            if audit is not None and pfx in masks:
+                _audit_relu(audit, f"{pfx}.tokenizers.{i}", pre, masks[pfx][:, i:i + 1], kind="tl_relu")
             a = torch.sigmoid(pre * masks[pfx][:, i:i + 1].to(pre.dtype) if pfx in masks else torch.relu(pre))
             toks.append((x * a).mean(dim=(-2, -1)))
         return torch.stack(toks, dim=1)

@@ -57,6 +57,23 @@ def test_c_abi_rejects_bad_shapes_without_a_gpu():
         L.vc_window_count(4, 4, 9, 1, ctypes.addressof(ctypes.c_long(0)))  # window larger than image
 
 
+def test_model_rejects_unsupported_patches_at_construction():
+    """a shape some kernel would refuse mid-step is refused by the constructor instead: patches beyond
+    the NonLocal's 16 pooled keys (P > 11), too many bands, and TokenLearner grids beyond its LDS plans."""
+    from vitcnn_amd import Multimodality_Mamba
+    from vitcnn_amd._lib import lib
+    for P in (7, 9, 11):
+        Multimodality_Mamba(P, 1, 1, 64, 2, 32, 12)
+    for P in (12, 13, 15):
+        with pytest.raises(ValueError, match="not supported"):
+            Multimodality_Mamba(P, 1, 1, 64, 2, 32, 12)
+    with pytest.raises(ValueError, match="bands"):
+        Multimodality_Mamba(9, 1, 1, 600, 1, 32, 16)
+    raw = lib().raw["vc_tl_check"]
+    assert all(raw(P * P, 256, (P - 2) ** 2) == 0 for P in range(3, 21))
+    assert raw(21 * 21, 256, 19 * 19) == 1 and raw(81, 513, 49) == 1
+
+
 def _ref_sliding_window_corners(W, H, P, step):
     """utils.py:357-399 restated (the order and clamping of the reference generator)."""
     offw, offh = (W - P) % step, (H - P) % step

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import (golden_batch, hash_state_dict, load_npz, masked_oracle_step, rel_err,
+from helpers import (check_audit, golden_batch, hash_state_dict, load_npz, masked_oracle_step, rel_err,
                      relu_masks_from_workspace, tl_pooled_from_workspace)
 from oracle import vitcnn_oracle as O
 
@@ -76,8 +76,9 @@ def b4():
     sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
     st64 = O.make_state(sd64)
     masks = relu_masks_from_workspace(m, 4)
+    audit = []
     masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(), masks,
-                       pooled=tl_pooled_from_workspace(m, 4))
+                       pooled=tl_pooled_from_workspace(m, 4), audit=audit)
     ref64 = {k: st64[k].grad for k in O.param_names(st64)}
     # fp32 reference's own error is measured against its own ReLU decisions
     st64r = O.make_state(sd64)
@@ -85,7 +86,7 @@ def b4():
     ref64_own = {k: st64r[k].grad for k in O.param_names(st64r)}
     return dict(m=m, ref_logits=ref_logits, ref_loss=ref_loss, ref_grads=ref_grads, ref64=ref64, ref64_own=ref64_own,
                 ref_state=state,
-                acts=acts,
+                acts=acts, audit=audit,
                 logits=logits.detach().cpu(), loss=float(loss.item()), hsi=hsi, lidar=lidar, target=target)
 
 
@@ -134,6 +135,14 @@ def test_gradients_b4(b4):
         if not (err <= 1e-3 * scale + floor or err <= 3.0 * err32 + floor):
             bad.append((n, err, err32, scale))
     assert not bad, bad[:5]
+
+
+def test_adopted_decisions_are_ties_b4(b4):
+    """the float64 yardstick of test_gradients_b4 takes the HIP path's ReLU masks, NonLocal
+    max-pool taps and TokenLearner pooled values; each is compared with the decision float64 takes at the same
+    site, and every disagreement must be a genuine fp32 near-tie (helpers._audit_*)."""
+    s = check_audit(b4["audit"], "b4")
+    assert s["relu"][1] > 100000 and s["maxpool"][1] > 10000 and s["tl_pool"][1] > 500 and s["tl_relu"][1] > 10000
 
 
 def test_running_stats_and_counters_b4(b4):
@@ -223,6 +232,68 @@ def test_b64_against_reference_golden():
             assert gn == 0.0, n
         else:
             assert abs(gn - ref_n) <= 2e-3 * ref_n + atol, (n, gn, float(ref_n))
+
+
+@pytest.mark.timeout(900)   # up to three B = 64 CPU oracle steps (two of them float64) on the box's 16 cores
+def test_b64_gradients_per_tensor_vs_oracle():
+    """the headline shape (Houston2013, B = 64) held per tensor, not by norm only.  The fp32
+    oracle (pinned to the reference's own B = 64 logits / loss / gradient norms, tests/test_oracle_golden.py)
+    runs the same step on the box; every parameter gradient must be within 1e-3 of its norm (+5e-5 of the
+    largest norm) of the oracle's, ||g - ref||.  A tensor outside that is then held to a float64 evaluation
+    that takes the HIP path's ReLU / max-pool / TokenLearner decisions -- each of which must be a genuine fp32
+    near-tie (the decision audit, always run here) -- and must be within the same bound of it, or no further
+    from it than 3x the fp32 oracle's own distance to the plain float64 evaluation."""
+    _need_gpu()
+    from vitcnn_amd import CrossEntropyLoss
+    sd = hash_state_dict()
+    hsi, lidar, target = golden_batch("golden.b64", 64)
+    w = O.ce_class_weights(16)
+    state = O.make_state(sd)
+    ref_logits, ref_loss = O.train_step(state, hsi, lidar, target, w)
+    print("b64: fp32 oracle step done", flush=True)
+    m = _product(sd).train()
+    logits = m(hsi.to(DEV), lidar.to(DEV))
+    loss = CrossEntropyLoss(weight=w.to(DEV))(logits, target.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel_err(logits.detach().cpu().numpy(), ref_logits.numpy()) < 1e-3
+    assert abs(float(loss) - float(ref_loss)) < 1e-3 * abs(float(ref_loss))
+    flat = m.flat_params.grad.detach().cpu()
+    named = dict(m.named_parameters())
+    names = O.param_names(state)
+    norms = {n: float(state[n].grad.norm()) for n in names if state[n].grad is not None}
+    gmax = max(norms.values())
+    atol = 5e-5 * gmax
+    got = {}
+    for n, off in m._poff.items():
+        g = flat[off:off + named[n].numel()].view(named[n].shape).double()
+        if n not in norms:
+            assert float(g.abs().max()) == 0.0, n
+            continue
+        got[n] = g
+    direct = [n for n, g in got.items() if float((g - state[n].grad.double()).norm()) <= 1e-3 * norms[n] + atol]
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    st64 = O.make_state(sd64)
+    audit = []
+    masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(), relu_masks_from_workspace(m, 64),
+                       pooled=tl_pooled_from_workspace(m, 64), audit=audit)
+    print("b64: decision-matched float64 step done", flush=True)
+    check_audit(audit, "b64")
+    cand = [n for n in got if n not in set(direct)]
+    far = [(n, float((got[n] - st64[n].grad).norm())) for n in cand]
+    far = [(n, e) for n, e in far if not e <= 1e-3 * float(st64[n].grad.norm()) + atol]
+    bad = []
+    if far:
+        st64r = O.make_state(sd64)
+        O.train_step(st64r, hsi.double(), lidar.double(), target, w.double())
+        for n, e in far:
+            own = float((state[n].grad.double() - st64r[n].grad).norm())
+            if not e <= 3.0 * own + atol:
+                bad.append((n, e, own, norms[n]))
+    print(f"b64 per-tensor: {len(direct)} of {len(got)} within 1e-3 of the fp32 oracle, {len(cand) - len(far)} "
+          f"within 1e-3 of the decision-matched float64 step, {len(far) - len(bad)} by the 3x-own-error argument")
+    assert len(direct) >= 0.9 * len(got), (len(direct), len(got))
+    assert not bad, bad[:5]
 
 
 def test_fused_step_and_graph_capture_match_autograd():

@@ -10,7 +10,7 @@ scale or 3x the fp32 oracle's own error, plus 1e-5 of the largest gradient."""
 import pytest
 import torch
 
-from helpers import masked_oracle_step, rel_err, relu_masks_from_workspace, tl_pooled_from_workspace
+from helpers import check_audit, masked_oracle_step, rel_err, relu_masks_from_workspace, tl_pooled_from_workspace
 from oracle import vitcnn_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -39,20 +39,26 @@ def muufl():
     torch.cuda.synchronize()
     sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
     st64 = O.make_state(sd64)
+    audit = []
     masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(), relu_masks_from_workspace(m, B),
-                       pooled=tl_pooled_from_workspace(m, B))
+                       pooled=tl_pooled_from_workspace(m, B), audit=audit)
     st64r = O.make_state(sd64)
     O.train_step(st64r, hsi.double(), lidar.double(), target, w.double())
     names = O.param_names(state)
     return dict(m=m, logits=logits.detach().cpu(), loss=float(loss.detach()), ref_logits=ref_logits, ref_loss=float(ref_loss),
                 ref=({k: state[k].grad for k in names}), ref64={k: st64[k].grad for k in names},
-                ref64_own={k: st64r[k].grad for k in names})
+                ref64_own={k: st64r[k].grad for k in names}, audit=audit)
 
 
 def test_muufl_logits_loss(muufl):
     assert muufl["logits"].shape == (B, NCLS)
     assert rel_err(muufl["logits"].numpy(), muufl["ref_logits"].numpy()) < 1e-3
     assert abs(muufl["loss"] - muufl["ref_loss"]) < 1e-3 * abs(muufl["ref_loss"])
+
+
+def test_muufl_adopted_decisions_are_ties(muufl):
+    """VERDICT r5 item 1a at the MUUFL shape: every HIP decision the float64 yardstick adopts is an fp32 near-tie"""
+    check_audit(muufl["audit"], "muufl_b4")
 
 
 def test_muufl_gradients(muufl):
@@ -129,8 +135,10 @@ def test_muufl_b64_parity():
         # moves a 3x3 conv's weight gradient by ~1e-3 of its norm in either fp32 execution
         sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
         st64 = O.make_state(sd64)
+        audit = []
         masked_oracle_step(O, st64, hsi.double(), lidar.double(), target, w.double(),
-                           relu_masks_from_workspace(m, Bb), pooled=tl_pooled_from_workspace(m, Bb))
+                           relu_masks_from_workspace(m, Bb), pooled=tl_pooled_from_workspace(m, Bb), audit=audit)
+        check_audit(audit, "muufl_b64")
         far = [(n, float((g - st64[n].grad).norm())) for n, g in cand]
         far = [(n, e64) for n, e64 in far if not e64 <= 1e-3 * norms[n] + 5e-5 * gmax]
         if far:   # the plain float64 step (the fp32 CPU reference's own error) only when it is needed

@@ -111,8 +111,11 @@ def _close(got, ref, rtol):
     return float((got - ref).abs().max()) <= rtol * max(float(ref.abs().max()), 1e-30)
 
 
+# the model's shapes (9x9 hsi1 / hsi2, MUUFL 11x11), a tiny one, and patches beyond the model's envelope (ADVICE
+# r5): 13x13 (HW > 128, one chunk each), 15x15 (the forward's tokens and the backward's pixels chunked to fit the
+# LDS) and 20x20 (the largest grid vc_tl_check accepts)
 @pytest.mark.parametrize("B,HW,C,S", [(64, 81, 256, 49), (64, 49, 144, 25), (4, 81, 256, 49), (5, 121, 64, 81),
-                                      (3, 9, 20, 4)])
+                                      (3, 9, 20, 4), (4, 169, 256, 121), (3, 225, 64, 169), (2, 400, 256, 324)])
 @pytest.mark.parametrize("regime", ["uniform", "illcond"])
 @pytest.mark.parametrize("train", [1, 0])
 def test_tokenlearner_vs_float64(L, B, HW, C, S, regime, train):

@@ -319,10 +319,24 @@ def test_check_loader_shard_lets_world1_loaders_through(monkeypatch):
     monkeypatch.setattr(parallel, "world", lambda: 2)
     monkeypatch.setattr(parallel, "rank", lambda: 1)
 
+    other_seed = [3]
+
+    def fake_all_reduce(t, op=None, group=None):   # MAX over this rank's tensor and the other rank's
+        o = torch.tensor([other_seed[0], -other_seed[0]], dtype=torch.int64)
+        t.copy_(torch.maximum(t, o))
+    monkeypatch.setattr(parallel.dist, "all_reduce", fake_all_reduce)
+    monkeypatch.setattr(parallel, "_scalar_device", lambda group=None: "cpu")
+
     class _PB1:
         rank, world, seed = 0, 1, 3
     parallel.check_loader_shard(_PB1())
     assert not parallel.is_sharded(_PB1())
+    # the world-1 loader's seed must still agree across ranks (train() cuts every rank's batches
+    # from its own shuffled order)
+    other_seed[0] = 4
+    with pytest.raises(RuntimeError, match="different seeds"):
+        parallel.check_loader_shard(_PB1())
+    other_seed[0] = 3
 
     class _PBbad:
         rank, world, seed = 0, 2, 3

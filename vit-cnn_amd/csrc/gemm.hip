@@ -18,8 +18,7 @@ namespace {
 constexpr int BM = 64, BN = 64;
 constexpr int LDS_STRIDE = 81;  // 64 + 17: conflict-free fragment reads, <=2-way stores
 
-enum { F_RELU = 1, F_BF16 = 2, F_LEGACY = 4, F_V2 = 8, F_PIPE = 16, F_NOPIPE = 32, F_MASK = 64, F_DEFER = 128,
-       F_REDUCE_ONLY = 256 };
+enum { F_RELU = 1, F_BF16 = 2, F_LEGACY = 4, F_V2 = 8, F_PIPE = 16, F_NOPIPE = 32, F_MASK = 64 };
 
 struct Epi {
   float alpha, beta;
@@ -1024,7 +1023,6 @@ struct LegacyPlan {
   GemmArgs g;
   int tn, tm, nz, variant;
   bool reduce;        // separate split-K reduce launch
-  bool deferred;      // F_DEFER: the slabs stay in the caller's buffer, reduced by a later F_REDUCE_ONLY call
   long ws_floats;     // split-K slab floats used
   int counters;       // arrival counters used (in-launch combine)
 };
@@ -1073,7 +1071,6 @@ static LegacyPlan plan_legacy(int transA, int transB, int M, int N, int K, float
   const bool vb = ((uintptr_t)B % 16 == 0) && (ldb % 4 == 0) && (batch == 1 || strideB % 4 == 0);
   pl.variant = (transA ? 8 : 0) | (transB ? 4 : 0) | (va ? 2 : 0) | (vb ? 1 : 0);
   pl.reduce = nsplit > 1 && !cnt;
-  pl.deferred = false;
   pl.ws_floats = nsplit > 1 ? (long)nsplit * batch * M * Ne : 0;
   pl.counters = cnt ? (int)tiles : 0;
   return pl;
@@ -1104,7 +1101,7 @@ static int launch_plan_pd(const LegacyPlan& pl, hipStream_t stream) {
   }
 #undef VC_L
   VC_CHECK_LAUNCH();
-  if (pl.reduce && !pl.deferred) {
+  if (pl.reduce) {
     const long nelem = (long)(pl.nz / g.nsplit) * g.M * g.Ne;
     const int G = g2::slab_groups(g.nsplit);
     VC_REQUIRE(nelem < (1L << 31));
@@ -1256,7 +1253,7 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
 #undef VC_GP_T
 #undef VC_GP
   VC_CHECK_LAUNCH();
-  if (p.nsplit > 1 && !cnt && !(flags & F_DEFER)) {
+  if (p.nsplit > 1 && !cnt) {
     const long nelem = (long)M * Ne;
     VC_REQUIRE(nelem < (1L << 31));
     hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, g, nelem, G);
@@ -1274,14 +1271,6 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
 struct PipeRec {
   GemmArgs g;
   int tn, tm, variant;   // variant = 2 transA + transB
-  bool deferred;         // F_DEFER: no reduce in this group (a later F_REDUCE_ONLY call reduces the slabs)
-};
-
-// F_REDUCE_ONLY: the split-K reduce of a problem whose GEMM ran earlier with F_DEFER (its slabs in the
-// caller's buffer), recorded for the group's one grouped reduce
-struct RedRec {
-  GemmArgs g;
-  int G, batch;
 };
 
 struct GroupState {
@@ -1290,8 +1279,6 @@ struct GroupState {
   int n, np;
   LegacyPlan plans[GROUP_MAX];
   PipeRec pipes[GROUP_MAX];
-  RedRec reds[GROUP_MAX];
-  int nr;
   long ws_used;
   int cnt_used;
   int err;
@@ -1313,19 +1300,18 @@ struct ReduceItems {
 };
 
 static int group_flush(GroupState& st) {
-  const int n = st.n, np = st.np, nr = st.nr;
-  st.n = st.np = st.nr = 0;
+  const int n = st.n, np = st.np;
+  st.n = st.np = 0;
   st.ws_used = 0;
   st.cnt_used = 0;
-  if (n + np + nr == 0) return VC_OK;
-  if (n == 1 && np == 0 && nr == 0) return launch_plan(st.plans[0], st.stream);
+  if (n + np == 0) return VC_OK;
+  if (n == 1 && np == 0) return launch_plan(st.plans[0], st.stream);
   ReduceItems red;
   red.R.n = 0;
-  for (int p = 0; p < nr; ++p) red.add(st.reds[p].g, st.reds[p].G, st.reds[p].batch);
   if (n == 1) {
     // one k-major problem: its own launch, its reduce (if any) joins the grouped one
     LegacyPlan pl = st.plans[0];
-    const bool reduce = pl.reduce && !pl.deferred;
+    const bool reduce = pl.reduce;
     pl.reduce = false;
     const int rc = launch_plan(pl, st.stream);
     if (rc) return rc;
@@ -1342,7 +1328,7 @@ static int group_flush(GroupState& st) {
       G.variant[p] = pl.variant;
       G.g[p] = pl.g;
       total += (long)pl.tn * pl.tm * pl.nz;
-      if (pl.reduce && !pl.deferred) red.add(pl.g, g2::slab_groups(pl.g.nsplit), pl.nz / pl.g.nsplit);
+      if (pl.reduce) red.add(pl.g, g2::slab_groups(pl.g.nsplit), pl.nz / pl.g.nsplit);
     }
     G.start[n] = (int)total;
     VC_REQUIRE(total < (1L << 31));
@@ -1362,7 +1348,7 @@ static int group_flush(GroupState& st) {
       P.variant[p] = pr.variant;
       P.g[p] = pr.g;
       total += (long)pr.tn * pr.tm * pr.g.nsplit;
-      if (pr.g.nsplit > 1 && !pr.deferred) red.add(pr.g, g2::slab_groups(pr.g.nsplit), 1);
+      if (pr.g.nsplit > 1) red.add(pr.g, g2::slab_groups(pr.g.nsplit), 1);
     }
     P.start[np] = (int)total;
     VC_REQUIRE(total < (1L << 31));
@@ -1399,7 +1385,7 @@ VC_EXPORT int vc_gemm_group_begin(void* group, hipStream_t stream) {
   VC_REQUIRE(st);
   st->magic = GROUP_MAGIC;
   st->stream = stream;
-  st->n = st->np = st->nr = 0;
+  st->n = st->np = 0;
   st->ws_used = 0;
   st->cnt_used = 0;
   st->err = 0;
@@ -1424,37 +1410,10 @@ static int launch_legacy(int transA, int transB, int M, int N, int K, float alph
   // the plan (split-K slices, combine path) depends on the problem and the caller's whole workspace /
   // counter arrays only -- never on what a group has used of them -- so a GEMM gives the same bits
   // grouped or alone, whatever its neighbours (tests/test_model_gpu.py::test_lane_schedules_*)
-  const bool defer = (flags & (F_DEFER | F_REDUCE_ONLY)) != 0;
   LegacyPlan pl = plan_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
-                              batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats,
-                              defer ? nullptr : tile_counters, defer ? 0 : n_counters);
-  if (flags & F_REDUCE_ONLY) {   // the reduce of an earlier F_DEFER launch (same arguments, so the same plan)
-    if (!pl.reduce) return VC_OK;
-    if (!st) {
-      const long nelem = (long)(pl.nz / pl.g.nsplit) * pl.g.M * pl.g.Ne;
-      const int G = g2::slab_groups(pl.g.nsplit);
-      VC_REQUIRE(nelem < (1L << 31));
-      hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, pl.g, nelem, G);
-      VC_CHECK_LAUNCH();
-      return VC_OK;
-    }
-    if (st->nr == GROUP_MAX || st->n + st->np + st->nr >= gp::RGROUP_MAX) {
-      const int rc = group_flush(*st);
-      if (rc) return rc;
-    }
-    st->reds[st->nr++] = RedRec{pl.g, g2::slab_groups(pl.g.nsplit), pl.nz / pl.g.nsplit};
-    return VC_OK;
-  }
-  pl.deferred = (flags & F_DEFER) && pl.reduce;
+                              batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,
+                              n_counters);
   if (!st) return launch_plan(pl, stream);
-  if (pl.deferred) {   // slabs in the caller's own buffer (from its start), no reduce in this group
-    if (st->n == GROUP_MAX) {
-      const int rc = group_flush(*st);
-      if (rc) return rc;
-    }
-    st->plans[st->n++] = pl;
-    return VC_OK;
-  }
   const long need = (pl.ws_floats + 63) / 64 * 64;
   if (st->n == GROUP_MAX || st->ws_used + need > ws_floats || st->cnt_used + pl.counters > n_counters) {
     const int rc = group_flush(*st);   // launch what is recorded; this problem starts a new group
@@ -1529,29 +1488,6 @@ VC_EXPORT int vc_gemm_colstats(int M, int N, int K, const float* A, long lda, co
   return VC_OK;
 }
 
-// floats of the caller-owned slab buffer an F_DEFER call of this problem writes (0: no split, nothing deferred),
-// given the workspace capacity it will be planned with (a buffer of that many floats passed as ws / ws_floats
-// gives the same plan as ws_floats >= it)
-VC_EXPORT int vc_gemm_defer_floats(int transA, int transB, int M, int N, int K, const float* A, long lda,
-                                   const float* B, long ldb, int batch, int bias_grad, int flags, long ws_floats) {
-  if (M <= 0 || N <= 0 || K < 0 || batch < 1) return 0;
-  const bool bf = (flags & F_BF16) != 0;
-  const int Ne = N + (bias_grad ? 1 : 0);
-  if (!(flags & (F_LEGACY | F_V2 | F_NOPIPE)) &&
-      pipe_fits(transA, transB, M, N, K, A, lda, B, ldb, batch, bias_grad ? reinterpret_cast<float*>(1) : nullptr) &&
-      ((flags & F_PIPE) || pipe_wanted(M, N, K))) {
-    const PipePlan p = plan_pipe(M, Ne, K, ws_floats, true, bf);
-    return p.nsplit > 1 ? (int)std::min<long>((long)p.nsplit * M * Ne, INT32_MAX) : 0;
-  }
-  const bool legacy = !bf && !(flags & F_V2) && ((flags & F_LEGACY) || K < 4096 || transA);
-  if (!legacy) return 0;
-  float dummy;
-  const LegacyPlan pl = plan_legacy(transA, transB, M, N, K, 1.f, A, lda, 0, B, ldb, 0, 0.f, &dummy, N, 0, batch,
-                                    nullptr, nullptr, 0, 0, flags, bias_grad ? &dummy : nullptr, &dummy, ws_floats,
-                                    nullptr, 0);
-  return pl.reduce ? (int)std::min<long>(pl.ws_floats, INT32_MAX) : 0;
-}
-
 VC_EXPORT int vc_gemm_ex(int transA, int transB, int M, int N, int K, float alpha,
                          const float* A, long lda, long strideA, const float* B, long ldb, long strideB,
                          float beta, float* C, long ldc, long strideC, int batch,
@@ -1579,37 +1515,15 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
   if (!(flags & (F_LEGACY | F_V2 | F_NOPIPE)) &&
       pipe_fits(transA, transB, M, N, K, A, lda, B, ldb, batch, bias_grad) &&
       ((flags & F_PIPE) || pipe_wanted(M, N, K))) {
-    const int fl = flags & ~(F_PIPE | F_NOPIPE | F_DEFER | F_REDUCE_ONLY);
+    const int fl = flags & ~(F_PIPE | F_NOPIPE);
     const int Ne = N + (bias_grad ? 1 : 0);
     const PipePlan p = plan_pipe(M, Ne, K, ws_floats, ws != nullptr, bf);
-    if (flags & F_REDUCE_ONLY) {   // the reduce of an earlier F_DEFER launch (same arguments, same plan)
-      if (p.nsplit == 1) return VC_OK;
-      Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, fl};
-      const GemmArgs g{M, N, K, Ne, p.k_chunk, p.nsplit, A, lda, 0, B, ldb, 0, C, ldc, 0, bias_grad, ws, nullptr, epi};
-      const int G = g2::slab_groups(p.nsplit);
-      if (!group) {
-        const long nelem = (long)M * Ne;
-        VC_REQUIRE(nelem < (1L << 31));
-        hipLaunchKernelGGL(g2::splitk_reduce4, dim3(vc_cdiv(nelem, 1024 / G)), dim3(256), 0, stream, g, nelem, G);
-        VC_CHECK_LAUNCH();
-        return VC_OK;
-      }
-      GroupState& st = *group;
-      if (st.nr == GROUP_MAX || st.n + st.np + st.nr >= gp::RGROUP_MAX) {
-        const int rc = group_flush(st);
-        if (rc) return rc;
-      }
-      st.reds[st.nr++] = RedRec{g, G, 1};
-      return VC_OK;
-    }
-    const bool defer = (flags & F_DEFER) && p.nsplit > 1;
     if (group) {
       // a problem whose own grid fills the chip launches alone (knob GEMM_GROUP_MAXB: the largest grid
       // that joins a group; probe library)
       const long own = (long)p.tn * p.tm * p.nsplit;
       if (p.bm == 64 && p.bn == 64 && p.ns == 2 && own <= vc_knob("VITCNN_GEMM_GROUP_MAXB", 1L << 30)) {
-        // a deferred problem's slabs go to the caller's own buffer from its start (not the group's scratch)
-        const long need = (p.nsplit > 1 && !defer) ? ((long)p.nsplit * M * Ne + 63) / 64 * 64 : 0;
+        const long need = p.nsplit > 1 ? ((long)p.nsplit * M * Ne + 63) / 64 * 64 : 0;
         GroupState& st = *group;
         if (st.np == GROUP_MAX || st.ws_used + need > ws_floats) {
           const int rc = group_flush(st);
@@ -1618,26 +1532,22 @@ static int gemm_impl(int transA, int transB, int M, int N, int K, float alpha,
         Epi epi{alpha, beta, bias, addend, add_ld, add_mod > 0 ? add_mod : M, fl};
         PipeRec& pr = st.pipes[st.np++];
         pr.g = GemmArgs{M, N, K, Ne, p.k_chunk, p.nsplit, A, lda, 0, B, ldb, 0, C, ldc, 0, bias_grad,
-                        (p.nsplit > 1 && !defer) ? ws + st.ws_used : ws, nullptr, epi};
+                        p.nsplit > 1 ? ws + st.ws_used : ws, nullptr, epi};
         pr.tn = p.tn;
         pr.tm = p.tm;
         pr.variant = (bf ? 4 : 0) | (transA ? 2 : 0) | (transB ? 1 : 0);
-        pr.deferred = defer;
         st.ws_used += need;
         return VC_OK;
       }
     }
     return launch_pipe(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, addend, add_ld, add_mod,
-                       fl | (defer ? F_DEFER : 0), bias_grad, ws, ws_floats, defer ? nullptr : tile_counters,
-                       defer ? 0 : n_counters, stream);
+                       fl, bias_grad, ws, ws_floats, tile_counters, n_counters, stream);
   }
   // fp32: the k-major kernel (faster on every shape of the ViT-CNN step, tools/gemm_census.py) except
   // long contractions (K >= 4096, e.g. FusAtNet's 3x3 convs over 1024-2193 channels), where the
   // K-contiguous kernel's two accumulator chains and <= 2048-long slices keep the fp32 rounding at
   // the CPU reference's level (tools/gemm_err.py).  F_LEGACY / F_V2 force either (tests, census).
   const bool legacy = !bf && !(flags & F_V2) && ((flags & F_LEGACY) || K < 4096 || transA);
-  // the K-contiguous kernel has no deferred form: its F_DEFER launch reduced at once, so F_REDUCE_ONLY is a no-op
-  if (!legacy && (flags & F_REDUCE_ONLY)) return VC_OK;
   if (legacy)
     return launch_legacy(transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C, ldc, strideC,
                          batch, bias, addend, add_ld, add_mod, flags, bias_grad, ws, ws_floats, tile_counters,

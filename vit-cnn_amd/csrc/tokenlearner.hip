@@ -273,24 +273,29 @@ __device__ __forceinline__ void tl_token_stats(int train, long n, int S, const f
 }
 
 // Forward: grid (B, ceil(C / 64)); block 256 (4 waves).  The block's sample b: its tokens' statistics, the
-// attention map a[s][q] = sigmoid(ReLU(BN_s(f_s[q]))) of all S tokens in LDS, and the pooled tokens of its 64
+// attention map a[s][q] = sigmoid(ReLU(BN_s(f_s[q]))) of the tokens in LDS, and the pooled tokens of its 64
 // channels Z[b, s, c] = (1/HW) sum_q a[s][q] x[b, q, c] on MFMA (A = a rows, B = x^T staged in LDS; the pixel
 // axis padded to 16 with zeros).  a is also written to `a_out` (optional, [B, S, HW]) by the y = 0 blocks.
-// LDS: al [Sp][Lp + 4] + xt [64][Lp + 4] floats (Sp = S rounded up to 16, Lp = HW rounded up to 16).
-__global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int C, int S, const float* __restrict__ x,
-                                                   long ldx, const float* __restrict__ mx,
+// The tokens go through the map in chunks of SC (a multiple of 16, chosen on the host so the LDS fits: all
+// Sp tokens at once for the model's patches, fewer for large patches); a tile's sum over the pixels is the
+// same whatever SC.
+// LDS (dynamic): tok_mean / tok_inv [S] doubles, xt [64][Lp + 4], al [SC][Lp + 4], the sample's pooled max /
+// mean [Lp] each and the tokens' parameters [S][TPAR] floats (Sp = S rounded up to 16, Lp = HW to 16).
+__global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int C, int S, int SC,
+                                                   const float* __restrict__ x, long ldx, const float* __restrict__ mx,
                                                    const float* __restrict__ avg, const float* __restrict__ par,
                                                    float* __restrict__ buf, float eps, float momentum,
                                                    const double* __restrict__ part, int P, double* __restrict__ stats,
                                                    float* __restrict__ a_out, float* __restrict__ Z) {
   extern __shared__ __attribute__((aligned(16))) float sm_f[];
   __shared__ double red[NMOM * 4];
-  __shared__ double tok_mean[128], tok_inv[128];
   const int b = blockIdx.x, c0 = blockIdx.y * TL_CT;
   const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15, LS = Lp + 4;
-  float* al = sm_f;              // [Sp][LS]
-  float* xt = sm_f + Sp * LS;    // [64][LS]  x^T of the block's channels
-  float* mxl = xt + TL_CT * LS;  // [Lp] the sample's pooled max / mean, [S][TPAR] the tokens' parameters
+  double* tok_mean = reinterpret_cast<double*>(sm_f);   // [S]
+  double* tok_inv = tok_mean + S;                       // [S]
+  float* xt = reinterpret_cast<float*>(tok_inv + S);    // [64][LS]  x^T of the block's channels (16-B aligned)
+  float* al = xt + TL_CT * LS;                          // [SC][LS]
+  float* mxl = al + SC * LS;                            // [Lp] the sample's pooled max / mean, [S][TPAR] params
   float* avl = mxl + Lp;
   float* parl = avl + Lp;
   const long n = (long)B * HW;
@@ -315,35 +320,40 @@ __global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int
   }
   for (int i = threadIdx.x; i < S * TPAR; i += 256) parl[i] = par[i];
   tl_token_stats(train, n, S, mx, avg, par, buf, eps, momentum, part, P, stats, red, tok_mean, tok_inv);
-  for (int i = threadIdx.x; i < Sp * Lp; i += 256) {
-    const int s = i / Lp, q = i - s * Lp;
-    float av = 0.f;
-    if (s < S && q < HW) {
-      const float* p = parl + s * TPAR;
-      double xh;
-      const float bn = tl_bnv(mxl[q], avl[q], p[0], p[1], p[2], tok_mean[s], tok_inv[s], p[3], p[4], xh);
-      av = sigmoid_f(fmaxf(bn, 0.f));
-      if (a_out && blockIdx.y == 0) a_out[((long)b * S + s) * HW + q] = av;
-    }
-    al[s * LS + q] = av;
-  }
-  __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
-  const int nst = Sp / 16, nct = TL_CT / 16, nkc = Lp / 16;
+  const int nct = TL_CT / 16, nkc = Lp / 16;
   const float inv_l = 1.f / (float)HW;
-  for (int t = w; t < nst * nct; t += 4) {
-    const int st = t / nct, ct = t - st * nct;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nkc; ++kc) {
-      const int k = 16 * kc + 4 * g;
-      mfma_k16(ld4_lds(al + (16 * st + r16) * LS + k), ld4_lds(xt + (16 * ct + r16) * LS + k), acc);
+  for (int sb = 0; sb < Sp; sb += SC) {
+    const int nsc = min(SC, Sp - sb);   // a multiple of 16
+    for (int i = threadIdx.x; i < nsc * Lp; i += 256) {
+      const int sl = i / Lp, q = i - sl * Lp, s = sb + sl;
+      float av = 0.f;
+      if (s < S && q < HW) {
+        const float* p = parl + s * TPAR;
+        double xh;
+        const float bn = tl_bnv(mxl[q], avl[q], p[0], p[1], p[2], tok_mean[s], tok_inv[s], p[3], p[4], xh);
+        av = sigmoid_f(fmaxf(bn, 0.f));
+        if (a_out && blockIdx.y == 0) a_out[((long)b * S + s) * HW + q] = av;
+      }
+      al[sl * LS + q] = av;
     }
-    const int c = c0 + 16 * ct + r16;
+    __syncthreads();
+    const int nst = nsc / 16;
+    for (int t = w; t < nst * nct; t += 4) {
+      const int st = t / nct, ct = t - st * nct;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < nkc; ++kc) {
+        const int k = 16 * kc + 4 * g;
+        mfma_k16(ld4_lds(al + (16 * st + r16) * LS + k), ld4_lds(xt + (16 * ct + r16) * LS + k), acc);
+      }
+      const int c = c0 + 16 * ct + r16;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int s = 16 * st + 4 * g + r;
-      if (s < S && c < C) Z[((long)b * S + s) * C + c] = acc[r] * inv_l;
+      for (int r = 0; r < 4; ++r) {
+        const int s = sb + 16 * st + 4 * g + r;
+        if (s < S && c < C) Z[((long)b * S + s) * C + c] = acc[r] * inv_l;
+      }
     }
+    __syncthreads();   // the next chunk overwrites al
   }
 }
 
@@ -455,26 +465,30 @@ __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, i
 // with df_s[q] = gamma_s invstd_s (g1 - s1/n - xh s2/n) (train; eval gamma invstd g1) in fp64 (dx overwritten):
 // the sums over the tokens in 8 chunks (8 adjacent lanes per pixel), then the chunks pairwise in a fixed order.
 // Block (0, 0) also writes the tokens' 5 parameter gradients (dparams).  The product runs as dx^T [c][q]: the
-// A operand (dZ rows, 16 channels x 4 tokens per MFMA) straight from L2, the B operand (a [s][q]) from LDS --
-// a small LDS footprint, so these blocks leave room for the selective-scan blocks running beside them.
-__global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C, int S, const float* __restrict__ mx,
-                                                 const float* __restrict__ avg, const int* __restrict__ amx,
-                                                 const float* __restrict__ par, const double* __restrict__ stats,
-                                                 const float* __restrict__ dZ, const float* __restrict__ da,
-                                                 const double* __restrict__ part, float* __restrict__ dx, long lddx,
-                                                 float* __restrict__ gpar) {
+// A operand (dZ rows, 16 channels x 4 tokens per MFMA) and the B operand (a [s][q]) from LDS -- a small LDS
+// footprint, so these blocks leave room for the selective-scan blocks running beside them.  The pixels go
+// through a and the MFMA tiles in chunks of QC (a multiple of 16 chosen on the host so the LDS fits: all Lp
+// pixels at once for the model's patches); every sum is over tokens, so the results do not depend on QC.
+// LDS (dynamic): q4 [4][S][2], tsum [2][S], tst [2][S] doubles; dzl [S4][68], al [S4][QC + 4],
+// tpar [S][TPAR] (rounded up to 4), gq [2][QC] floats.
+__global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C, int S, int QC,
+                                                 const float* __restrict__ mx, const float* __restrict__ avg,
+                                                 const int* __restrict__ amx, const float* __restrict__ par,
+                                                 const double* __restrict__ stats, const float* __restrict__ dZ,
+                                                 const float* __restrict__ da, const double* __restrict__ part,
+                                                 float* __restrict__ dx, long lddx, float* __restrict__ gpar) {
   extern __shared__ __attribute__((aligned(16))) float sm_f[];
-  __shared__ double q4[4][128][2];     // per token, 4 sample-quarter sums of two of the partial columns
-  __shared__ double tsum[2][128];      // s1 / n, s2 / n
-  __shared__ double tst[2][128];       // mean, invstd
-  __shared__ float tpar[128][TPAR];
-  __shared__ float gq[2][128];         // per pixel: sum_s w0 df, (sum_s w1 df) / C
   const int b = blockIdx.x, c0 = blockIdx.y * TL_CT;
   const bool b00 = blockIdx.x == 0 && blockIdx.y == 0;
-  const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15, LS = Lp + 4;
-  float* al = sm_f;                 // [S4][LS]  a[s][q] (zero padded)
-  float* dzl = sm_f + S4 * LS;      // [S4][64 + 4]  dZ[b, s, c0 + cl] (zero padded)
+  const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15, QS = QC + 4;
   constexpr int DZS = TL_CT + 4;
+  double* q4 = reinterpret_cast<double*>(sm_f);   // [4][S][2] per token, 4 sample-quarter sums of two columns
+  double* tsum = q4 + 8 * S;                      // [2][S]  s1 / n, s2 / n
+  double* tst = tsum + 2 * S;                     // [2][S]  mean, invstd
+  float* dzl = reinterpret_cast<float*>(tst + 2 * S);   // [S4][DZS]  dZ[b, s, c0 + cl] (zero padded; 16-B aligned)
+  float* al = dzl + S4 * DZS;                     // [S4][QS]  a[s][q0 + ql] (zero padded)
+  float* tpar = al + S4 * QS;                     // [S][TPAR]
+  float* gq = tpar + ((S * TPAR + 3) & ~3);       // [2][QC] per pixel: sum_s w0 df, (sum_s w1 df) / C
   const long n = (long)B * HW;
   const double nd = (double)n;
   for (int i = threadIdx.x; i < S4 * (TL_CT / 4); i += 256) {   // float4 runs of the block's 64 channels
@@ -489,10 +503,10 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
     }
     *reinterpret_cast<f32x4*>(dzl + s * DZS + c4) = v;
   }
-  for (int i = threadIdx.x; i < S * TPAR; i += 256) tpar[i / TPAR][i % TPAR] = par[i];
+  for (int i = threadIdx.x; i < S * TPAR; i += 256) tpar[i] = par[i];
   for (int s = threadIdx.x; s < S; s += 256) {
-    tst[0][s] = stats[2 * s];
-    tst[1][s] = stats[2 * s + 1];
+    tst[s] = stats[2 * s];
+    tst[S + s] = stats[2 * s + 1];
   }
   // the batch sums of partial columns j0, j0 + 1: 4 interleaved sample quarters, then the quarters in order
   auto batch_sums = [&](int j0) {
@@ -512,8 +526,8 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
           t0 += p0[k];
           t1 += p1[k];
         }
-        q4[u][s][0] = t0;
-        q4[u][s][1] = t1;
+        q4[(u * S + s) * 2] = t0;
+        q4[(u * S + s) * 2 + 1] = t1;
         continue;
       }
       for (int bb0 = u; bb0 < B; bb0 += 16) {
@@ -530,25 +544,29 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
           t1 += p1[k];
         }
       }
-      q4[u][s][0] = t0;
-      q4[u][s][1] = t1;
+      q4[(u * S + s) * 2] = t0;
+      q4[(u * S + s) * 2 + 1] = t1;
     }
     __syncthreads();
   };
+  auto qsum = [&](int s, int j) {
+    return ((q4[s * 2 + j] + q4[(S + s) * 2 + j]) + q4[(2 * S + s) * 2 + j]) + q4[(3 * S + s) * 2 + j];
+  };
   batch_sums(0);
   for (int s = threadIdx.x; s < S; s += 256) {
-    tsum[0][s] = (((q4[0][s][0] + q4[1][s][0]) + q4[2][s][0]) + q4[3][s][0]) / nd;
-    tsum[1][s] = (((q4[0][s][1] + q4[1][s][1]) + q4[2][s][1]) + q4[3][s][1]) / nd;
+    tsum[s] = qsum(s, 0) / nd;
+    tsum[S + s] = qsum(s, 1) / nd;
   }
   __syncthreads();
   if (b00) {   // parameter gradients: the other two partial columns too
     batch_sums(2);
     for (int s = threadIdx.x; s < S; s += 256) {
-      const double t0 = tsum[0][s] * nd, t1 = tsum[1][s] * nd;
-      const double t2 = ((q4[0][s][0] + q4[1][s][0]) + q4[2][s][0]) + q4[3][s][0];
-      const double t3 = ((q4[0][s][1] + q4[1][s][1]) + q4[2][s][1]) + q4[3][s][1];
-      const double w0 = tpar[s][0], w1 = tpar[s][1], gam = tpar[s][3];
-      const double invstd = tst[1][s];
+      const double t0 = tsum[s] * nd, t1 = tsum[S + s] * nd;
+      const double t2 = qsum(s, 0);
+      const double t3 = qsum(s, 1);
+      const float* ps = tpar + s * TPAR;
+      const double w0 = ps[0], w1 = ps[1], gam = ps[3];
+      const double invstd = tst[S + s];
       const double* mom = stats + 2 * S;   // n, mbar, vbar, Cmm, Cmv, Cvv
       double gw0, gw1, gb;
       if (train) {
@@ -569,80 +587,84 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
       gp[4] = (float)t0;
     }
   }
-  // a recomputed into LDS, and the pixel gradients: lane group of 8 per pixel, lane k of it sums the tokens
-  // k, k + 8, ... (fixed order), then the 8 lanes pairwise
-  const int lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < 8 * Lp; i += 256) {
-    const int q = i >> 3, k = i & 7;
-    const bool qok = q < HW;
-    const float m = qok ? mx[(long)b * HW + q] : 0.f, v = qok ? avg[(long)b * HW + q] : 0.f;
-    double gm = 0.0, ga = 0.0;
-    for (int s0 = k; s0 < S4; s0 += 32) {
-      float dav[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int s = s0 + 8 * u;
-        dav[u] = (qok && s < S) ? da[((long)b * S + s) * HW + q] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int s = s0 + 8 * u;
-        if (s >= S4) continue;
-        if (s >= S || !qok) {
-          if (s < S4) al[s * LS + q] = 0.f;
-          continue;
-        }
-        const float* p = tpar[s];
-        double xh;
-        const float bn = tl_bnv(m, v, p[0], p[1], p[2], tst[0][s], tst[1][s], p[3], p[4], xh);
-        al[s * LS + q] = sigmoid_f(fmaxf(bn, 0.f));
-        double g1 = 0.0;
-        if (bn > 0.f) {
-          const float sg = sigmoid_f(bn);
-          g1 = (double)(dav[u] * sg * (1.f - sg));
-        }
-        const double gi = (double)p[3] * tst[1][s];
-        const double d = train ? gi * (g1 - tsum[0][s] - xh * tsum[1][s]) : gi * g1;
-        gm += d * (double)p[0];
-        ga += d * (double)p[1];
-      }
-    }
-    // 8 lanes (k = 0..7) of pixel q: ((k0 + k1) + (k2 + k3)) + ((k4 + k5) + (k6 + k7))
-#pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
-      gm += __shfl_xor(gm, o, 64);
-      ga += __shfl_xor(ga, o, 64);
-    }
-    if ((lane & 7) == 0 && q < 128) {
-      gq[0][q] = (float)gm;
-      gq[1][q] = (float)(ga / (double)C);
-    }
-  }
-  __syncthreads();
-  // dx^T tiles: rows = channels (16 per tile), cols = pixels (16 per tile), k = tokens (4 per MFMA)
-  const int w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
-  const int nqt = Lp / 16, nct = TL_CT / 16, nk = S4 / 4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
+  const int nct = TL_CT / 16, nk = S4 / 4;
   const float inv_l = 1.f / (float)HW;
-  for (int t = w; t < nqt * nct; t += 4) {
-    const int ct = t / nqt, qt = t - ct * nqt;
-    const int cl = 16 * ct + r16;   // this lane's A row (channel, block-local)
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < nk; ++k) {
-      const int s = 4 * k + g;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dzl[s * DZS + cl], al[s * LS + 16 * qt + r16], acc, 0, 0, 0);
-    }
-    // acc[r] = dx^T (channel c0 + 16 ct + 4 g + r, pixel 16 qt + r16): 4 adjacent channels of one pixel row
-    const int q = 16 * qt + r16, cb = c0 + 16 * ct + 4 * g;
-    if (q < HW) {
-      const float gmf = gq[0][q], gaf = gq[1][q];
-      const int am = amx[(long)b * HW + q];
-      float* dr = dx + ((long)b * HW + q) * lddx;
+  for (int q0 = 0; q0 < Lp; q0 += QC) {
+    const int nq = min(QC, Lp - q0);   // a multiple of 16
+    // a recomputed into LDS, and the pixel gradients: lane group of 8 per pixel, lane k of it sums the tokens
+    // k, k + 8, ... (fixed order), then the 8 lanes pairwise
+    for (int i = threadIdx.x; i < 8 * nq; i += 256) {
+      const int ql = i >> 3, q = q0 + ql, k = i & 7;
+      const bool qok = q < HW;
+      const float m = qok ? mx[(long)b * HW + q] : 0.f, v = qok ? avg[(long)b * HW + q] : 0.f;
+      double gm = 0.0, ga = 0.0;
+      for (int s0 = k; s0 < S4; s0 += 32) {
+        float dav[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = cb + r;
-        if (c < C) dr[c] = acc[r] * inv_l + (gaf + (c == am ? gmf : 0.f));
+        for (int u = 0; u < 4; ++u) {
+          const int s = s0 + 8 * u;
+          dav[u] = (qok && s < S) ? da[((long)b * S + s) * HW + q] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int s = s0 + 8 * u;
+          if (s >= S4) continue;
+          if (s >= S || !qok) {
+            al[s * QS + ql] = 0.f;
+            continue;
+          }
+          const float* p = tpar + s * TPAR;
+          double xh;
+          const float bn = tl_bnv(m, v, p[0], p[1], p[2], tst[s], tst[S + s], p[3], p[4], xh);
+          al[s * QS + ql] = sigmoid_f(fmaxf(bn, 0.f));
+          double g1 = 0.0;
+          if (bn > 0.f) {
+            const float sg = sigmoid_f(bn);
+            g1 = (double)(dav[u] * sg * (1.f - sg));
+          }
+          const double gi = (double)p[3] * tst[S + s];
+          const double d = train ? gi * (g1 - tsum[s] - xh * tsum[S + s]) : gi * g1;
+          gm += d * (double)p[0];
+          ga += d * (double)p[1];
+        }
+      }
+      // 8 lanes (k = 0..7) of pixel q: ((k0 + k1) + (k2 + k3)) + ((k4 + k5) + (k6 + k7))
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        gm += __shfl_xor(gm, o, 64);
+        ga += __shfl_xor(ga, o, 64);
+      }
+      if ((lane & 7) == 0) {
+        gq[ql] = (float)gm;
+        gq[QC + ql] = (float)(ga / (double)C);
       }
     }
+    __syncthreads();
+    // dx^T tiles: rows = channels (16 per tile), cols = pixels (16 per tile), k = tokens (4 per MFMA)
+    const int nqt = nq / 16;
+    for (int t = w; t < nqt * nct; t += 4) {
+      const int ct = t / nqt, qt = t - ct * nqt;
+      const int cl = 16 * ct + r16;   // this lane's A row (channel, block-local)
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < nk; ++k) {
+        const int s = 4 * k + g;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dzl[s * DZS + cl], al[s * QS + 16 * qt + r16], acc, 0, 0, 0);
+      }
+      // acc[r] = dx^T (channel c0 + 16 ct + 4 g + r, pixel q0 + 16 qt + r16): 4 adjacent channels of one pixel
+      const int ql = 16 * qt + r16, q = q0 + ql, cb = c0 + 16 * ct + 4 * g;
+      if (q < HW) {
+        const float gmf = gq[ql], gaf = gq[QC + ql];
+        const int am = amx[(long)b * HW + q];
+        float* dr = dx + ((long)b * HW + q) * lddx;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb + r;
+          if (c < C) dr[c] = acc[r] * inv_l + (gaf + (c == am ? gmf : 0.f));
+        }
+      }
+    }
+    __syncthreads();   // the next chunk overwrites al / gq
   }
 }
 
@@ -681,24 +703,47 @@ VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx,
   return VC_OK;
 }
 
-static size_t tl_fwd_lds(int HW, int S) {
-  const int Sp = (S + 15) & ~15, Lp = (HW + 15) & ~15;
-  return (size_t)((Sp + TL_CT) * (Lp + 4) + 2 * Lp + S * TPAR) * sizeof(float);
+// LDS plans.  The dynamic allocation plus the kernel's static __shared__ arrays must fit the CU's 160 KB
+constexpr size_t TL_LDS_MAX = 160 * 1024;
+constexpr size_t TL_FWD_STATIC = NMOM * 4 * sizeof(double);   // tl_fwd_pool's `red`
+static size_t tl_fwd_lds(int HW, int S, int SC) {
+  const int Lp = (HW + 15) & ~15;
+  return 2 * (size_t)S * sizeof(double) + (size_t)((TL_CT + SC) * (Lp + 4) + 2 * Lp + S * TPAR) * sizeof(float);
 }
-static size_t tl_bwd_lds(int HW, int S) {
-  const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15;
-  return (size_t)S4 * (Lp + 4 + TL_CT + 4) * sizeof(float);
+static size_t tl_bwd_lds(int S, int QC) {
+  const int S4 = (S + 3) & ~3;
+  return 12 * (size_t)S * sizeof(double) +
+         (size_t)(S4 * (TL_CT + 4 + QC + 4) + ((S * TPAR + 3) & ~3) + 2 * QC) * sizeof(float);
+}
+// the token chunk of tl_fwd_pool: all tokens when they fit, else the largest multiple of 16 that does (0: none)
+static int tl_fwd_sc(int HW, int S) {
+  for (int sc = (S + 15) & ~15; sc >= 16; sc -= 16)
+    if (tl_fwd_lds(HW, S, sc) + TL_FWD_STATIC <= TL_LDS_MAX) return sc;
+  return 0;
+}
+// the pixel chunk of tl_bwd_dx, alike
+static int tl_bwd_qc(int HW, int S) {
+  for (int qc = (HW + 15) & ~15; qc >= 16; qc -= 16)
+    if (tl_bwd_lds(S, qc) <= TL_LDS_MAX) return qc;
+  return 0;
+}
+
+VC_API int vc_tl_check(int HW, int C, int S) {
+  VC_REQUIRE(HW > 0 && C > 0 && C <= 512 && S > 0);
+  VC_REQUIRE(tl_fwd_sc(HW, S) > 0 && tl_bwd_qc(HW, S) > 0);
+  return VC_OK;
 }
 
 VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
                      const float* avg, const float* params, float* bn_buffers, float eps, float momentum,
                      const double* ws, double* stats, float* a, float* Z, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && HW > 0 && C > 0 && S > 0 && S <= 128 && ws && stats && Z);
-  VC_REQUIRE(tl_fwd_lds(HW, S) <= 160 * 1024);
+  VC_REQUIRE(B > 0 && HW > 0 && C > 0 && S > 0 && ws && stats && Z);
+  const int SC = tl_fwd_sc(HW, S);
+  VC_REQUIRE(SC > 0);
   VC_REQUIRE_I32((long)B * HW * (S > C ? S : C));
   const int P = vc_cdiv((long)B * HW, PS_ROWS);
-  hipLaunchKernelGGL(tl_fwd_pool, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_fwd_lds(HW, S), stream, train, B, HW, C,
-                     S, x, ldx, mx, avg, params, bn_buffers, eps, momentum, ws, P, stats, a, Z);
+  hipLaunchKernelGGL(tl_fwd_pool, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_fwd_lds(HW, S, SC), stream, train, B, HW,
+                     C, S, SC, x, ldx, mx, avg, params, bn_buffers, eps, momentum, ws, P, stats, a, Z);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }
@@ -706,17 +751,17 @@ VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, lon
 VC_API int vc_tl_bwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
                      const float* avg, const int* amx, const float* params, const double* stats, const float* dZ,
                      float* da, double* ws, float* dx, long lddx, float* dparams, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && HW > 0 && HW <= 128 && C > 0 && C % 4 == 0 && ldx % 4 == 0 && S > 0 && S <= 128 && ws && da &&
-             dx);
+  VC_REQUIRE(B > 0 && HW > 0 && C > 0 && C % 4 == 0 && ldx % 4 == 0 && S > 0 && ws && da && dx);
   VC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)dZ & 15) == 0);
-  VC_REQUIRE(tl_bwd_lds(HW, S) <= 160 * 1024);
+  const int QC = tl_bwd_qc(HW, S);
+  VC_REQUIRE(QC > 0);
   VC_REQUIRE_I32((long)B * HW * (S > C ? S : C));
   double* part = ws + tl_pix_partials((long)B * HW);
   hipLaunchKernelGGL(tl_bwd_da, dim3(B, vc_cdiv(S, 16)), dim3(64 * TLDA_W), 0, stream, B, HW, C, S, x, ldx, mx, avg, params,
                      stats, dZ, da, part);
   VC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(tl_bwd_dx, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_bwd_lds(HW, S), stream, train, B, HW, C, S,
-                     mx, avg, amx, params, stats, dZ, da, part, dx, lddx, dparams);
+  hipLaunchKernelGGL(tl_bwd_dx, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_bwd_lds(S, QC), stream, train, B, HW, C, S,
+                     QC, mx, avg, amx, params, stats, dZ, da, part, dx, lddx, dparams);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

@@ -65,11 +65,6 @@ PARAM_ALIGN = 4            # floats: flat-buffer alignment (16 B) of every param
 ALIGN_MIN = 64
 GEMM_GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES (include/vitcnn.h)
 GEMM_MASK = 64             # vc_gemm flags: the addend is a ReLU mask (include/vitcnn.h)
-GEMM_DEFER = 128           # vc_gemm flags: split-K slabs left unreduced in the caller's buffer
-GEMM_REDUCE_ONLY = 256     # vc_gemm flags: only the reduction of an earlier GEMM_DEFER product
-# lane 1's weight-gradient split-K reductions queued for the weight-gradient lane (the products stay in the
-# chain's grouped launches): every grouped launch of the lane-1 backward chain loses its reduce launch
-_DEFER_REDUCE = False   # measured slower: 1.74-1.79 -> 2.00-2.09 ms (profiles/r05_ab_defer_reduce.log)
 # conv1x1 + BatchNorm (+ ReLU) forward: the statistics partials computed in the GEMM epilogue (vc_gemm_colstats)
 _GEMM_BNSTATS = True
 # GLfusion forward: the NonLocal phi | g projection on the channel lane (2) right after ln4, theta alone on lane 1
@@ -151,6 +146,26 @@ class _Workspace:
         return self.t[name]
 
 
+# the largest patch side the kernels take: hsi1's NonLocal attends over the 2x2-pooled (P - 2)^2 grid, at most 16
+# pooled keys per query (csrc/attention.hip MAXP), i.e. P <= 11 -- MUUFL's 11x11 (SURVEY.md row A-MUUFL)
+MAX_PATCH = 11
+
+
+def _check_supported(P, c1):
+    """Reject, at construction, a shape some kernel of the program would refuse mid-step: the patch
+    side (NonLocal pooled keys), the HSI band count (TokenLearner / NonLocal channel bounds) and each TokenLearner
+    call's LDS plan (vc_tl_check)."""
+    if P > MAX_PATCH:
+        raise ValueError(f"ViT-CNN patch {P}x{P} is not supported: at most {MAX_PATCH}x{MAX_PATCH} (the NonLocal "
+                         f"attention takes at most 16 pooled keys, ((P - 2) // 2)^2)")
+    if c1 > 512:
+        raise ValueError(f"ViT-CNN with {c1} HSI bands is not supported: at most 512")
+    L = lib()
+    for hw, c, s in ((P * P, 256, (P - 2) ** 2), ((P - 2) ** 2, c1, (P - 4) ** 2)):
+        if L.raw["vc_tl_check"](hw, c, s) != 0:
+            raise ValueError(f"ViT-CNN TokenLearner over {hw} pixels x {c} channels with {s} tokens is not supported")
+
+
 class Multimodality_Mamba(nn.Module):
     """ViT-CNN (ours).  Signature of Mutimodality_Mamba7.py:1142; like the reference, `patch_size`,
     `stride`, `dim_embedding` and `path_type` are accepted and ignored.  `img_size` is the patch
@@ -164,6 +179,7 @@ class Multimodality_Mamba(nn.Module):
         P = int(img_size)
         if P < 7:
             raise ValueError("ViT-CNN needs patches of at least 7x7 (two valid 3x3 stages + 2x2 pooling)")
+        _check_supported(P, int(in_channels1))
         self.patch, self.c1, self.c2, self.ncls = P, int(in_channels1), int(in_channels2), int(num_class)
         self.embedding_dim = dim_embedding
         plane_hsi = [self.c1, 256, self.c1]
@@ -583,19 +599,27 @@ class _Program:
         self._ev_i += 1
         return e
 
-    def gemm(self, *args, exact=False, ws=None):
-        """vc_gemm_ex on the current lane with its scratch and split-K tile counters; args are
-        vc_gemm's up to bias_grad (flags at index 21 get the model's precision bit unless `exact`);
-        ws = (pointer, floats): a caller-owned slab buffer instead of the lane's scratch (GEMM_DEFER)"""
+    def site_flags(self, ta, M, N, K, exact=False):
+        """one GEMM site of the program: its index (the _GEMM_SITES census, the _BF16_EXACT list) and the
+        precision flags the policy gives it (the model's bf16 bit unless exact / excluded / below _BF16_MIN_K).
+        Every GEMM entry point the program calls goes through here, so site indices stay stable"""
         i = self._gemm_i
         self._gemm_i += 1
         if _GEMM_SITES is not None:
-            f = sys._getframe(1)
+            f = sys._getframe(2)
             f = f.f_back if f.f_code.co_name.startswith("mm_") else f
-            _GEMM_SITES.append((i, f.f_code.co_name, f.f_lineno, args[2], args[3], args[4], exact))
-        if self.gemm_flags and not exact and i not in _BF16_EXACT and args[4] >= _BF16_MIN_K and not (
-                _BF16_MIN_K and args[0]):
-            args = args[:21] + (args[21] | self.gemm_flags,) + args[22:]
+            _GEMM_SITES.append((i, f.f_code.co_name, f.f_lineno, M, N, K, exact))
+        if self.gemm_flags and not exact and i not in _BF16_EXACT and K >= _BF16_MIN_K and not (_BF16_MIN_K and ta):
+            return self.gemm_flags
+        return 0
+
+    def gemm(self, *args, exact=False, ws=None):
+        """vc_gemm_ex on the current lane with its scratch and split-K tile counters; args are
+        vc_gemm's up to bias_grad (flags at index 21 get the model's precision bit unless `exact`);
+        ws = (pointer, floats): a caller-owned slab buffer instead of the lane's scratch"""
+        fl = self.site_flags(args[0], args[2], args[3], args[4], exact)
+        if fl:
+            args = args[:21] + (args[21] | fl,) + args[22:]
         wp, wn = ws if ws is not None else (self.scr_p, self.scr_n)
         if self._grouping is not None and self._group_lane == self.cur:
             self.L.vc_gemm_group_add(self._grouping, *args, wp, wn, self._cnt[self.cur], N_COUNTERS)
@@ -743,7 +767,8 @@ class _Program:
             # conv bias), then one statistics + apply + ReLU launch: 2 launches instead of 3
             P_ = -(-M // 64)
             cs = ws.get(seq + ".cs", 2 * P_ * Cout, torch.float64).data_ptr()
-            self.L.vc_gemm_colstats(M, Cout, Cin, X, Cin, W, Cin, bias, pre, Cout, self.gemm_flags, cs, self.s)
+            fl = self.site_flags(0, M, Cout, Cin)
+            self.L.vc_gemm_colstats(M, Cout, Cin, X, Cin, W, Cin, bias, pre, Cout, fl, cs, self.s)
             self.L.vc_bn_apply_partials(M, Cout, pre, Cout, P_, cs, bias, BN_EPS, BN_MOM, mean, inv,
                                         self.BUF[tag + ".running_mean"], self.BUF[tag + ".running_var"],
                                         self.P[tag + ".weight"], self.P[tag + ".bias"], 1, out, Cout, self.s)
@@ -1017,23 +1042,12 @@ class _Program:
 
     def defer_wgrad(self, defer, M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=0):
         """C[M,N] = A^T B (a weight gradient, mm_tn), now or -- defer on lane 0 with lanes on -- at the next
-        flush_wgrads().  On lane 1 (_DEFER_REDUCE) the product runs now, in the chain's grouped launch, but its
-        split-K reduction is queued for the weight-gradient lane (GEMM_DEFER: the slabs wait in a buffer of
-        the product's own), so the chain's next kernel does not wait for it."""
+        flush_wgrads().  (Round 5 also queued lane 1's split-K reductions for the weight-gradient lane: 1.74 ->
+        2.0-2.1 ms, profiles/r05_ab_defer_reduce.log; removed with its ABI in round 6.)"""
         if self._deferring(defer):
             (self.pending_wgrads if self.cur == 0 else self.pending_wgrads1).append(
                 lambda: self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad))
             return
-        if defer and _DEFER_REDUCE and self.lanes_on and self.cur == 1:
-            fl = self.gemm_flags if K >= _BF16_MIN_K else 0
-            need = self.L.vc_gemm_defer_floats(1, 0, M, N, K, A, lda, Bm, ldb, 1, 1 if bias_grad else 0, fl,
-                                               self.scr_n)
-            if need > 0:
-                buf = (self.ws.f("defer.%x" % C, need), need)
-                self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad, flags=GEMM_DEFER, ws=buf)
-                self.pending_wgrads1.append(lambda: self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad,
-                                                               flags=GEMM_REDUCE_ONLY, ws=buf))
-                return
         self.mm_tn(M, N, K, A, lda, Bm, ldb, C, ldc, bias_grad=bias_grad)
 
     def flush_wgrads(self):

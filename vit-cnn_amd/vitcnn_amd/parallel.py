@@ -418,9 +418,11 @@ def check_loader_shard(loader, group=None):
     group: its rank and world are this process's, and every rank built it from the same seed (the
     shuffled order the shards are cut from is then the same permutation on every rank).  Raises
     RuntimeError otherwise -- nothing else would notice overlapping or missing shards."""
-    if not is_distributed() or getattr(loader, "world", None) is None or int(loader.world) <= 1:
-        return   # a world-1 loader does not shard itself: train() wraps it in a ShardedLoader
-    if int(loader.world) != world() or int(loader.rank) != rank():
+    if not is_distributed() or getattr(loader, "world", None) is None:
+        return
+    # a world-1 loader does not shard itself (train() wraps it in a ShardedLoader, each rank taking batches
+    # b % world of ITS OWN shuffled order), so only its rank / world are exempt: the seeds must still agree
+    if int(loader.world) > 1 and (int(loader.world) != world() or int(loader.rank) != rank()):
         raise RuntimeError(f"loader shard (rank {loader.rank} of {loader.world}) does not match the process group "
                            f"(rank {rank()} of {world()})")
     seed = getattr(loader, "seed", None)
