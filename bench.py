@@ -383,6 +383,9 @@ def cpu_baseline(warmup, steps):
                       + ", ".join(f"{t:.2f}" for t in ts)}
 
 
+S2EFT_GFLOP_PER_STEP = 13.6  # S2EFT fwd + bwd GEMM work per B = 64 step
+
+
 def s2eft_leg(dev, steps, cpu_steps):
     """Config 5: S2EFT train step (forward, weighted CE, backward, Adam)
     at B = 64 on [64, 145, 147] synthetic tokens, eager launches; plus the CPU oracle on the same
@@ -433,9 +436,15 @@ def s2eft_leg(dev, steps, cpu_steps):
         step()
     torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t0) / steps * 1e3
+    tf = S2EFT_GFLOP_PER_STEP / ms   # GF / ms = TF/s
     out = {"workload": "S2EFT (CAF, depth 5, 4 heads x 16, dim 64) train step, x [64,145,147], 16 classes",
            "value": round(64 / ms * 1e3, 1), "unit": "patches/s", "ms_per_step": round(ms, 4), "dtype": "fp32",
-           "launch": launch}
+           "launch": launch,
+           # the step's algorithmic work (13.6 GF fwd + bwd per B = 64 step, FlopCounter)
+           # against the dense fp32 MFMA peak; the whole step's time, so launch gaps and the non-GEMM kernels count
+           "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                        "work": f"{S2EFT_GFLOP_PER_STEP} GFLOP per B=64 step / the step time"}}
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
 
     def cpu_leg():   # run after every GPU leg

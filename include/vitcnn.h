@@ -213,7 +213,8 @@ VC_API int vc_conv3x3_dgrad(int B, int H, int W, int C, int O, int pad, const fl
  *   mode 0: Wt [O][9][Cw] (fwd and dgrad), Cw = C rounded up to a multiple of 4, padding written 0
  *           (16-B aligned rows: float4 operand loads at any C)                mode 1: W2 [9][O][C]
  *   mode 2: w = beta w + dWt unpacked (wgrad's tap-major [O][9][C] gradient back to the torch layout)
- *   fwd:   y [B*OH*OW] (ld ldy) = conv(x) + bias (bias may be null)
+ *   fwd:   y [B*OH*OW] (ld ldy) = conv(x) + bias (bias may be null); with C % 4 != 0 and ldx % 4 == 0 the
+ *          row padding x[.][C .. C rounded to 4) is read (against zero weights) and must hold finite values
  *   wgrad: dWt [O][9][C] = sum over output pixels of dy x (overwritten; the bias gradient is colsum(dy))
  *   dgrad: dx (ld lddx) = beta dx + the conv's input gradient for dy
  * ws: split-K slabs when the tile grid is small (fixed-order sums; may be null: no split). */
@@ -463,6 +464,8 @@ VC_API int vc_index_add_i64(int n, const int* idx, long long* ptr, long long val
 /* dx = dy * (y > 0)  (nn.ReLU backward from the saved output) */
 VC_API int vc_relu_bwd(long n, const float* dy, const float* y, float* dx, hipStream_t stream);
 VC_API int vc_fill(long n, float* ptr, float value, hipStream_t stream);
+/* ptr[m * ld + c] = value over [M, C] strided rows (e.g. the padding columns of a channel concat) */
+VC_API int vc_fill_2d(long M, int C, float* ptr, long ld, float value, hipStream_t stream);
 /* ptr[idx[i]] = value  (the alignment gaps of the flat gradient: parameters start 16-B aligned) */
 VC_API int vc_fill_index(int n, const int* idx, float* ptr, float value, hipStream_t stream);
 

@@ -67,8 +67,11 @@ def test_conv_tap_fwd_wgrad_dgrad(B, H, C, O, pad, ldx, ws_log2):
     y_ref = y64.detach().permute(0, 2, 3, 1)
     dw_ref = w64.grad
     dx_ref = x64.grad.permute(0, 2, 3, 1) + dx0.double()
-    # device: x with row stride ldx (padding columns filled with garbage the kernel must not read)
-    xd = torch.full((B * H * H, ldx), float("nan"), device=DEV)
+    # device: x with row stride ldx (padding columns filled with garbage the kernel must not read).  With C % 4 != 0
+    # and ldx % 4 == 0 the pipelined forward reads the padding up to C rounded to 4 against zero weights: the
+    # contract (include/vitcnn.h) is finite values there, so finite garbage
+    pad_val = 3.0 if (C % 4 and ldx % 4 == 0) else float("nan")
+    xd = torch.full((B * H * H, ldx), pad_val, device=DEV)
     xd[:, :C] = x.reshape(-1, C).to(DEV)
     wd, bd, dyd = w.to(DEV).contiguous(), bias.to(DEV), dy.reshape(-1, O).to(DEV).contiguous()
     s = torch.cuda.current_stream().cuda_stream

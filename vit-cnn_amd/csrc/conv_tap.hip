@@ -622,13 +622,17 @@ int launch_conv_pipe(TapArgs& a, int grid_n, float* ws, long ws_floats, hipStrea
   return VC_OK;
 }
 
-// can the pipelined kernel take this conv: whole 16-B chunks everywhere (C, O and the leading dimensions
-// multiples of 4, 16-B aligned bases) and operands under 2 GB (32-bit buffer offsets).  Round 5, with the 8-wave
+// can the pipelined kernel take this conv: whole 16-B chunks everywhere (O and the leading dimensions multiples
+// of 4, 16-B aligned bases) and operands under 2 GB (32-bit buffer offsets).  Round 5, with the 8-wave
 // conv_pipe: every direction (FusAtNet step 18.21 -> 18.04-18.06 ms; wgrad only 18.14,
-// profiles/r05_fusat_conv_pipe_w8.log); knob TAP_PIPE = direction bit mask (probe library)
+// profiles/r05_fusat_conv_pipe_w8.log); knob TAP_PIPE = direction bit mask (probe library).
+// Round 6: C need not be a multiple of 4 (FusAtNet's 2193-channel concat, rows padded to 2196): with ldx % 4 == 0
+// the last 16-B chunk of an input row covers channels up to C rounded to 4, which meet the packed weights' zero
+// padding (forward; the caller keeps those columns finite, include/vitcnn.h) or land only in output columns >= C,
+// which are not stored (weight and data gradients)
 bool conv_pipe_ok(int mode, const TapArgs& a, const void* p0, long ld0, const void* p1, long ld1) {
   const long in_b = (long)a.nb * a.H * a.W * 4, out_b = (long)a.nb * a.OH * a.OW * 4;
-  return (vc_knob("VITCNN_TAP_PIPE", 7) >> mode & 1) && a.C % 4 == 0 && a.O % 4 == 0 && ld0 % 4 == 0 && ld1 % 4 == 0 &&
+  return (vc_knob("VITCNN_TAP_PIPE", 7) >> mode & 1) && a.O % 4 == 0 && ld0 % 4 == 0 && ld1 % 4 == 0 &&
          ((uintptr_t)p0 % 16) == 0 && ((uintptr_t)p1 % 16) == 0 && in_b * std::max(ld0, ld1) < (1L << 31) &&
          out_b * std::max(ld0, ld1) < (1L << 31) && (long)a.O * 9 * a.Cw * 4 < (1L << 31);
 }

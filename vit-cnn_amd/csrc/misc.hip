@@ -352,6 +352,11 @@ __global__ void fill_f32(long n, float* __restrict__ p, float v) {
   if (i < n) p[i] = v;
 }
 
+__global__ void fill2d_f32(long M, int C, float* __restrict__ p, long ld, float v) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M * C) p[(i / C) * ld + i % C] = v;
+}
+
 __global__ void fill_index_f32(int n, const int* __restrict__ idx, float* __restrict__ p, float v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[idx[i]] = v;
@@ -499,6 +504,14 @@ VC_API int vc_fill_index(int n, const int* idx, float* ptr, float value, hipStre
   VC_REQUIRE(n >= 0);
   if (n == 0) return VC_OK;
   hipLaunchKernelGGL(fill_index_f32, dim3(vc_cdiv(n, 256)), dim3(256), 0, stream, n, idx, ptr, value);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_fill_2d(long M, int C, float* ptr, long ld, float value, hipStream_t stream) {
+  VC_REQUIRE(M >= 0 && C >= 0 && ld >= C && ptr);
+  if (M == 0 || C == 0) return VC_OK;
+  hipLaunchKernelGGL(fill2d_f32, dim3(vc_cdiv(M * C, 256)), dim3(256), 0, stream, M, C, ptr, ld, value);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

@@ -15,6 +15,8 @@ import torch
 import torch.nn as nn
 
 F32 = 4
+PARAM_ALIGN = 4   # floats (16 B)
+ALIGN_MIN = 64
 
 
 def _last_active_name(model, names):
@@ -92,10 +94,16 @@ class FlatParams:
         named = list(nn.Module.named_parameters(self))
         self._poff, off = {}, 0
         for n, p in named:
+            # every parameter of >= ALIGN_MIN elements starts 16-B aligned, as in ViT-CNN's layout (model.py): the
+            # weights then qualify for the pipelined GEMM's 16-B LDS-DMA staging (gemm.hip pipe_fits); the gaps
+            # hold zeros in the parameters and in every gradient (the backward zero-fills the flat gradient)
+            if p.numel() >= ALIGN_MIN:
+                off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
             self._poff[n] = off
             off += p.numel()
+        off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
         self._n_params = self._n_active = off
-        flat = torch.empty(off, dtype=torch.float32, device=named[0][1].device)
+        flat = torch.zeros(off, dtype=torch.float32, device=named[0][1].device)
         for n, p in named:
             flat[self._poff[n]:self._poff[n] + p.numel()].copy_(p.detach().reshape(-1))
         self._pmods = {}
@@ -119,7 +127,7 @@ class FlatParams:
             p.data = base[o:o + p.numel()].view(p.shape)
 
     def _repack(self, device):
-        flat = torch.empty(self._n_params, dtype=torch.float32, device=device)
+        flat = torch.zeros(self._n_params, dtype=torch.float32, device=device)
         for n, (m, pn) in self._pmods.items():
             o = self._poff[n]
             flat[o:o + m._parameters[pn].numel()].copy_(m._parameters[pn].detach().reshape(-1))

@@ -493,6 +493,9 @@ class _Program:
         Cp = (Ct + 3) // 4 * 4    # row stride of the concat: 16-B aligned rows (float4 gathers in conv_tap)
         cat = self.new(B, P, P, Cp)                                           # cat([x1, x2, Ms, Mt], 1)
         self.cat = cat
+        # the row padding (Ct .. Cp) zeroed: the pipelined conv's last 16-B chunk of a row reads it against the packed
+        # weights' zero padding (conv_tap.hip conv_pipe_ok), so the 2193-channel convs run on conv_pipe
+        L.vc_fill_2d(M, Cp - Ct, cat.data_ptr() + F32 * Ct, Cp, 0.0, self.s)
         L.vc_add2_2d(M, c1, x1.data_ptr(), c1, None, 0, cat.data_ptr(), Cp, 0.0, self.s)
         L.vc_add2_2d(M, c2, x2.data_ptr(), c2, None, 0, cat.data_ptr() + F32 * c1, Cp, 0.0, self.s)
         offs = F32 * (c1 + c2)
