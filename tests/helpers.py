@@ -138,7 +138,8 @@ def _audit_relu(audit, site, pre, mask, out=None, kind="relu"):
     tol = max(tie, 2.0 * e_obs)
     dist = float(p[d].abs().max()) if bool(d.any()) else 0.0
     audit.append(dict(site=site, kind=kind, n=p.numel(), disagree=int(d.sum()), dist=dist, tie=tie, e_obs=e_obs,
-                      worst=dist / tol if tol > 0 else (0.0 if dist == 0 else float("inf"))))
+                      worst=dist / tol if tol > 0 else (0.0 if dist == 0 else float("inf")),
+                      worst_ulp=dist / tie if tie > 0 else 0.0))
 
 
 def _audit_pool(audit, site, pre, taps, vals=None):
@@ -157,10 +158,13 @@ def _audit_pool(audit, site, pre, taps, vals=None):
     e_obs = 0.0
     if vals is not None:
         e_obs = float((vals.transpose(1, 2).reshape(b, c, ph, pw).double() - got).abs().max())
-    tol = torch.clamp(TIE_ULPS * EPS32 * best.abs(), min=2.0 * e_obs)
+    tie = TIE_ULPS * EPS32 * best.abs()
+    tol = torch.clamp(tie, min=2.0 * e_obs)
     ratio = float((gap[d] / tol[d]).max()) if bool(d.any()) else 0.0
+    ratio_ulp = float((gap[d] / tie[d]).max()) if bool(d.any()) else 0.0
     audit.append(dict(site=site, kind="maxpool", n=best.numel(), disagree=int(d.sum()),
-                      dist=float(gap[d].max()) if bool(d.any()) else 0.0, e_obs=e_obs, worst=ratio))
+                      dist=float(gap[d].max()) if bool(d.any()) else 0.0, e_obs=e_obs, worst=ratio,
+                      worst_ulp=ratio_ulp))
 
 
 def _audit_tl_pool(audit, site, x, pooled, x_hip=None):
@@ -186,14 +190,16 @@ def _audit_tl_pool(audit, site, x, pooled, x_hip=None):
 
 
 def audit_summary(audit):
-    """{kind: [sites, decisions, disagreements, worst ratio to the tie bound]} + the failing records"""
+    """{kind: [sites, decisions, disagreements, worst ratio to the tie bound, worst ratio to TIE_ULPS ulps alone]}
+    + the failing records"""
     out = {}
     for r in audit:
-        k = out.setdefault(r["kind"], [0, 0, 0, 0.0])
+        k = out.setdefault(r["kind"], [0, 0, 0, 0.0, 0.0])
         k[0] += 1
         k[1] += r["n"]
         k[2] += r["disagree"]
         k[3] = max(k[3], r["worst"])
+        k[4] = max(k[4], r.get("worst_ulp", 0.0))
     return out, [r for r in audit if not r["worst"] <= 1.0]
 
 
@@ -203,7 +209,8 @@ def check_audit(audit, name):
     import json
     summary, bad = audit_summary(audit)
     print(f"decision audit {name}: " + ", ".join(f"{k}: {v[2]} of {v[1]} differ from float64 over {v[0]} sites "
-                                                 f"(worst {v[3]:.3g} of the tie bound)" for k, v in summary.items()))
+                                                 f"(worst {v[3]:.3g} of the tie bound, {v[4]:.3g} of {TIE_ULPS} ulps)"
+                                                 for k, v in summary.items()))
     if os.path.isdir("gpurun_out"):
         with open(f"gpurun_out/decision_audit_{name}.json", "w") as f:
             json.dump({"summary": summary, "records": audit}, f, indent=1)

@@ -94,6 +94,17 @@ def _gpu_case(sd, x, t, w):
     return logits.detach().cpu(), loss.detach().cpu(), out
 
 
+def _flat_ref(m, grads):
+    """per-parameter reference gradients laid out like the model's flat gradient (parameters start 16-B aligned,
+    vitcnn_amd.flat: the alignment gaps hold zeros); a None gradient is zeros"""
+    out = torch.zeros(m.flat_params.numel())
+    for n, o in m._poff.items():
+        g = grads.get(n)
+        if g is not None:
+            out[o:o + g.numel()] = g.reshape(-1)
+    return out
+
+
 def _check(sd, x, t, w):
     ol, oloss, og = O.train_step(sd, x, t, w)
     hl, hloss, hg = _gpu_case(sd, x, t, w)
@@ -189,7 +200,7 @@ def test_s2eft_gpu_pca30_vit_mode():
         CrossEntropyLoss(weight=w.cuda())(logits, t.cuda()).backward()
         assert _rel(logits.detach().cpu(), ol) < 1e-3
         flat = m.flat_params.grad.cpu()
-        gref = torch.cat([og[n].reshape(-1) for n in m._poff])
+        gref = _flat_ref(m, og)
         assert float((flat - gref).norm()) <= 1e-3 * float(gref.norm())
 
 
@@ -231,8 +242,7 @@ def test_s2eft_gpu_dropout_train():
     torch.nn.functional.cross_entropy(ref, t, weight=w).backward()
     assert _rel(logits.detach().cpu(), ref.detach()) < 1e-3
     flat = m.flat_params.grad.cpu()
-    gref = torch.cat([params[n].grad.reshape(-1) if params[n].grad is not None else torch.zeros(params[n].numel())
-                      for n in m._poff])
+    gref = _flat_ref(m, {n: params[n].grad for n in m._poff})
     assert float((flat - gref).norm()) <= 1e-3 * float(gref.norm())
     m.eval()
     with torch.no_grad():

@@ -1177,7 +1177,7 @@ static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws, bo
   const int kt = vc_cdiv(K, gp::KT);
   int nsplit = 1;
   const long target = vc_knob("VITCNN_PIPE_SPLIT_BLOCKS", 512);   // blocks a split aims at (knob: probe library)
-  if (have_ws && tiles < 128)
+  if (have_ws && tiles < vc_knob("VITCNN_PIPE_SPLIT_BELOW", 128))   // (knob: probe library)
     nsplit = (int)std::max<long>(1, std::min<long>(std::min<long>((target + tiles - 1) / tiles, kt / 4), 64));
   if (g_tune.nsplit) nsplit = std::min(g_tune.nsplit, std::max(1, kt));
   while (nsplit > 1 && (long)nsplit * M * Ne > ws_floats) --nsplit;

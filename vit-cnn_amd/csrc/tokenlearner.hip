@@ -361,8 +361,11 @@ __global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int
 // the block's 16 tokens (MFMA, both operands as float4 runs of their rows straight from L2), written to `da`;
 // then per token the fp64 sums over this sample's pixels of g1, g1 xh, g1 (m - mbar), g1 (v - vbar) ->
 // part[(b * S + s) * NBS + j] (summed over the pixel tiles in a fixed order).
-// TLDA_W waves per block: one 16-pixel tile per wave up to HW = 16 TLDA_W (a wave with two tiles doubled the
-// block's chain of dependent k-chunk loads)
+// Up to TLDA_W waves per block: one 16-pixel tile per wave up to HW = 16 TLDA_W (a wave with two tiles doubled
+// the block's chain of dependent k-chunk loads).  Round 6: the block has exactly min(tiles, TLDA_W) waves (hsi1:
+// 6, hsi2: 4) -- the round-5 blocks of 8 carried 2 / 4 idle waves whose registers and slots the concurrent
+// selective-scan backward could not use; the per-token sums over the missing waves were exact zeros, so the
+// results are unchanged bit for bit
 constexpr int TLDA_W = 8;
 __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, int S, const float* __restrict__ x,
                                                          long ldx, const float* __restrict__ mx,
@@ -374,6 +377,7 @@ __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, i
   const int b = blockIdx.x, s0 = blockIdx.y * 16;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
   const int Lp = (HW + 15) & ~15, nqt = Lp / 16, nkc = (C + 15) / 16;
+  const int nw = blockDim.x >> 6;
   const double mbar = stats[2 * S + 1], vbar = stats[2 * S + 2];
   const float inv_l = 1.f / (float)HW;
   // this lane's A row (token s0 + r16) and the tokens of its accumulator rows (s0 + 4 g + r)
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, i
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int j = 0; j < NBS; ++j) v[r][j] = 0.0;
-  for (int qt = w; qt < nqt; qt += TLDA_W) {
+  for (int qt = w; qt < nqt; qt += nw) {
     const int qb = 16 * qt + r16;   // this lane's B column (pixel)
     const float* brow = x + ((long)b * HW + min(qb, HW - 1)) * ldx;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, i
     const int tl = threadIdx.x / NBS, j = threadIdx.x - tl * NBS, s = s0 + tl;
     double t = tsum[0][tl][j];
 #pragma unroll
-    for (int ww = 1; ww < TLDA_W; ++ww) t += tsum[ww][tl][j];   // the waves in order
+    for (int ww = 1; ww < nw; ++ww) t += tsum[ww][tl][j];   // the waves in order
     if (s < S) part[((long)b * S + s) * NBS + j] = t;
   }
 }
@@ -757,7 +761,8 @@ VC_API int vc_tl_bwd(int train, int B, int HW, int C, int S, const float* x, lon
   VC_REQUIRE(QC > 0);
   VC_REQUIRE_I32((long)B * HW * (S > C ? S : C));
   double* part = ws + tl_pix_partials((long)B * HW);
-  hipLaunchKernelGGL(tl_bwd_da, dim3(B, vc_cdiv(S, 16)), dim3(64 * TLDA_W), 0, stream, B, HW, C, S, x, ldx, mx, avg, params,
+  const int da_waves = std::min(TLDA_W, (HW + 15) / 16);
+  hipLaunchKernelGGL(tl_bwd_da, dim3(B, vc_cdiv(S, 16)), dim3(64 * da_waves), 0, stream, B, HW, C, S, x, ldx, mx, avg, params,
                      stats, dZ, da, part);
   VC_CHECK_LAUNCH();
   hipLaunchKernelGGL(tl_bwd_dx, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_bwd_lds(S, QC), stream, train, B, HW, C, S,

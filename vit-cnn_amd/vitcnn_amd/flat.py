@@ -103,6 +103,7 @@ class FlatParams:
             off += p.numel()
         off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
         self._n_params = self._n_active = off
+        self._n_elems = sum(p.numel() for _, p in named)   # the parameters proper (without the alignment gaps)
         flat = torch.zeros(off, dtype=torch.float32, device=named[0][1].device)
         for n, p in named:
             flat[self._poff[n]:self._poff[n] + p.numel()].copy_(p.detach().reshape(-1))
