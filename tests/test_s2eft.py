@@ -248,3 +248,57 @@ def test_s2eft_gpu_dropout_train():
     with torch.no_grad():
         le = m(x.cuda()).cpu()
     assert _rel(le, O.forward(sd, x)) < 1e-3   # eval: no dropout
+
+
+def _s2eft_grad(side, captured):
+    """(loss, flat gradient) of one S2EFT train step at the config-5 shape, backward on two streams (side) or one,
+    eager or replayed from a hipGraph capture"""
+    import vitcnn_amd.s2eft as S
+    from vitcnn_amd import CrossEntropyLoss
+    saved = S._SIDE_STREAM
+    S._SIDE_STREAM = side
+    try:
+        torch.manual_seed(0)
+        m = S.ViT(image_size=7, near_band=3, num_patches=144, num_classes=16, dim=64, depth=5, heads=4, mlp_dim=8,
+                  dropout=0.0, emb_dropout=0.0, mode="CAF").cuda().train()
+        g = torch.Generator().manual_seed(7)
+        x = torch.rand(64, 145, 147, generator=g).cuda()
+        t = torch.randint(1, 16, (64,), generator=g).cuda()
+        w = torch.ones(16, device="cuda")
+        w[0] = 0.0
+        crit = CrossEntropyLoss(weight=w)
+        if not captured:
+            loss = crit(m(x), t)
+            loss.backward()
+            torch.cuda.synchronize()
+            return float(loss), m.flat_params.grad.detach().clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            crit(m(x), t).backward()
+        torch.cuda.current_stream().wait_stream(s)
+        m.zero_grad(set_to_none=True)
+        graph, holder = torch.cuda.CUDAGraph(), {}
+        with torch.cuda.graph(graph):
+            holder["l"] = crit(m(x), t)
+            holder["l"].backward()
+        graph.replay()
+        torch.cuda.synchronize()
+        return float(holder["l"]), m.flat_params.grad.detach().clone()
+    finally:
+        S._SIDE_STREAM = saved
+
+
+@pytest.mark.gpu
+def test_s2eft_side_stream_backward_is_bit_identical():
+    """Round 6: the backward's weight / bias gradients on a side stream beside the data-gradient chain (forked per
+    product, or once per layer) give the single-stream step's loss and flat gradient bit for bit, eager and replayed
+    from a hipGraph capture"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ref_loss, ref = _s2eft_grad(0, False)
+    for mode in (1, 2):
+        for captured in (False, True):
+            loss, g = _s2eft_grad(mode, captured)
+            assert loss == ref_loss, (mode, captured, loss, ref_loss)
+            assert torch.equal(g, ref), (mode, captured, float((g - ref).abs().max()))

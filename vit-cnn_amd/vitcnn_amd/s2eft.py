@@ -19,6 +19,8 @@ references an un-imported `F`, :58, and raises too).
 """
 from __future__ import annotations
 
+from functools import partial
+
 import torch
 import torch.nn as nn
 
@@ -133,6 +135,13 @@ class _S2EFTFunction(torch.autograd.Function):
         return None, None, grad, None
 
 
+# the backward's weight / bias gradients beside the data-gradient chain (round 6): 0 = one stream; 1 = each on a side
+# stream as soon as its inputs exist (one fork per product); 2 = a layer's parameter gradients queued and forked to
+# the side stream once, at the layer's end.  The same launches in the same order per stream: bit-identical results
+# (tests/test_s2eft.py).  Measured (tools/s2eft_step.py, 200 replays x 2): 0: 1.286 ms, 1: 1.497 ms
+_SIDE_STREAM = 0
+
+
 class _Program:
     """One forward (saving what the backward reads) and its hand-written backward."""
 
@@ -169,9 +178,12 @@ class _Program:
         return torch.empty(*shape, dtype=torch.float32, device=self.dev)
 
     def gemm(self, tA, tB, M, N, K, A, lda, sA, Bm, ldb, sB, beta, C, ldc, sC, batch=1, bias=None, add=None,
-             add_ld=0, add_mod=0, bias_grad=None, alpha=1.0):
+             add_ld=0, add_mod=0, bias_grad=None, alpha=1.0, side=None):
+        """vc_gemm on the program's stream with its scratch, or (side = (stream handle, scratch pointer)) on the
+        backward's weight-gradient stream"""
+        st, scr = side if side is not None else (self.s, self.scr.data_ptr())
         self.L.vc_gemm(tA, tB, M, N, K, alpha, A, lda, sA, Bm, ldb, sB, beta, C, ldc, sC, batch, bias, add, add_ld,
-                       add_mod, 0, bias_grad, self.scr.data_ptr(), self.SCRATCH, self.s)
+                       add_mod, 0, bias_grad, scr, self.SCRATCH, st)
 
     def ln(self, pfx, X, R, ldx):
         D = self.m.D
@@ -261,18 +273,60 @@ class _Program:
         return logits
 
     def backward(self, dlogits):
+        """The hand-written backward.  The data-gradient chain (dX through the layers) runs on the program's
+        stream; every weight / bias gradient (the weight-gradient GEMMs with their split-K reduces, the LayerNorm
+        parameter reductions, the skipcat and embedding column sums) goes through `side()`, which runs it on the chain
+        (_SIDE_STREAM 0, the default) or on a side stream forked from the chain and joined before the gradient is
+        returned (1, 2: measured slower, the cross-stream edges cost more than the overlap gains).  The chain never
+        writes a buffer the parameter gradients read (the LayerNorm backward writes the residual sum to a new
+        buffer: vc_layernorm_bwd_dx with res), and every buffer they read stays referenced until the join.
+        Per-launch arithmetic and per-stream order do not depend on the mode: the same bits."""
         m, L, B, T, N, C, D, Hh = self.m, self.L, self.B, self.T, self.m.N, self.m.C, self.m.D, self.m.heads
         R = B * T
         P = self.P
+        main = torch.cuda.current_stream(self.dev)
+        side_stream = self._side_stream() if _SIDE_STREAM else main
+        scr2 = self.new(self.SCRATCH) if _SIDE_STREAM else self.scr
+        sd = (side_stream.cuda_stream, scr2.data_ptr())
+        keep, pending = [scr2], []
+
+        def flush():   # the side stream continues after everything issued on the chain so far, runs the queue
+            if side_stream is not main:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side_stream.wait_event(ev)
+            for fn in pending:
+                fn()
+            pending.clear()
+
+        def side(bufs, *calls):
+            """parameter-gradient work (calls with their arguments bound), reading `bufs`: on the side stream now
+            (_SIDE_STREAM 1), queued for the layer's end (2), or on the chain (0)"""
+            keep.extend(bufs)
+            pending.extend(calls)
+            if _SIDE_STREAM != 2:
+                flush()
+
         grad = self.new(m._n_params)
         L.vc_fill(m._n_params, grad.data_ptr(), 0.0, self.s)
         gb = grad.data_ptr()
         G = {n: gb + F32 * o for n, o in m._poff.items()}
         scr, ns = self.scr.data_ptr(), self.SCRATCH
+        part_n = 1024 * 2 * D   # LayerNorm parameter partials (>= the kernel's partial rows: vc_layernorm_bwd's split)
+
+        def ln_bwd(pfx, dY, X, mu, rs, res, rows):
+            """dx = res + LN grad into a new buffer (chain); the weight / bias reduction on the side stream"""
+            out, part = self.new(rows, D), self.new(part_n)
+            L.vc_layernorm_bwd_dx(rows, D, dY.data_ptr(), D, X, D, P[pfx + ".weight"], mu.data_ptr(), rs.data_ptr(),
+                                  res, D, out.data_ptr(), D, 0.0, part.data_ptr(), part_n, self.s)
+            side((part,), partial(L.vc_layernorm_bwd_params, rows, D, part.data_ptr(), part_n, G[pfx + ".weight"],
+                                  G[pfx + ".bias"], 0.0, sd[0]))
+            return out
+
         # head
         Yc, muc, rsc = self.head
-        self.gemm(1, 0, m.ncls, D, B, dlogits.data_ptr(), m.ncls, 0, Yc.data_ptr(), D, 0, 0.0, G["mlp_head.1.weight"],
-                  D, 0, bias_grad=G["mlp_head.1.bias"])
+        side((dlogits,), partial(self.gemm, 1, 0, m.ncls, D, B, dlogits.data_ptr(), m.ncls, 0, Yc.data_ptr(), D, 0, 0.0,
+                                 G["mlp_head.1.weight"], D, 0, bias_grad=G["mlp_head.1.bias"], side=sd))
         dYc = self.new(B, D)
         self.gemm(0, 0, B, D, m.ncls, dlogits.data_ptr(), m.ncls, 0, P["mlp_head.1.weight"], D, 0, 0.0, dYc.data_ptr(),
                   D, 0)
@@ -285,15 +339,16 @@ class _Program:
         for li in reversed(range(m.depth)):
             pre = f"transformer.layers.{li}"
             st = self.saved[li]
-            # feed-forward: X3 = X2 + W2 gelu(W1 LN(X2) + b1) + b2 ; dX holds dX3, becomes dX2 in place
+            # feed-forward: X3 = X2 + W2 gelu(W1 LN(X2) + b1) + b2 ; dX holds dX3, then dX2 (a new buffer)
             dG = self.new(R, m.hidden)
             dF2 = dX
             if self.pd > 0:
                 dF2 = self.new(R, D)
                 L.vc_dropout_bwd(R * D, dX.data_ptr(), self.masks[f"{li}.ff2"].data_ptr(), self.pd, dF2.data_ptr(),
                                  self.s)
-            self.gemm(1, 0, D, m.hidden, R, dF2.data_ptr(), D, 0, st["G"].data_ptr(), m.hidden, 0, 0.0,
-                      G[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0, bias_grad=G[pre + ".1.fn.fn.net.3.bias"])
+            side((dF2,), partial(self.gemm, 1, 0, D, m.hidden, R, dF2.data_ptr(), D, 0, st["G"].data_ptr(), m.hidden, 0,
+                                 0.0, G[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0,
+                                 bias_grad=G[pre + ".1.fn.fn.net.3.bias"], side=sd))
             self.gemm(0, 0, R, m.hidden, D, dF2.data_ptr(), D, 0, P[pre + ".1.fn.fn.net.3.weight"], m.hidden, 0, 0.0,
                       dG.data_ptr(), m.hidden, 0)
             if self.pd > 0:
@@ -301,45 +356,45 @@ class _Program:
                                  dG.data_ptr(), self.s)
             dH = self.new(R, m.hidden)
             L.vc_gelu_bwd(R * m.hidden, dG.data_ptr(), st["Hd"].data_ptr(), dH.data_ptr(), self.s)
-            self.gemm(1, 0, m.hidden, D, R, dH.data_ptr(), m.hidden, 0, st["Y2"].data_ptr(), D, 0, 0.0,
-                      G[pre + ".1.fn.fn.net.0.weight"], D, 0, bias_grad=G[pre + ".1.fn.fn.net.0.bias"])
+            side((dH,), partial(self.gemm, 1, 0, m.hidden, D, R, dH.data_ptr(), m.hidden, 0, st["Y2"].data_ptr(), D, 0,
+                                0.0, G[pre + ".1.fn.fn.net.0.weight"], D, 0, bias_grad=G[pre + ".1.fn.fn.net.0.bias"],
+                                side=sd))
             dY2 = self.new(R, D)
             self.gemm(0, 0, R, D, m.hidden, dH.data_ptr(), m.hidden, 0, P[pre + ".1.fn.fn.net.0.weight"], D, 0, 0.0,
                       dY2.data_ptr(), D, 0)
-            L.vc_layernorm_bwd(R, D, dY2.data_ptr(), D, st["X2"].data_ptr(), D, P[pre + ".1.fn.norm.weight"],
-                               st["mu2"].data_ptr(), st["rs2"].data_ptr(), dX.data_ptr(), D, 1.0,
-                               G[pre + ".1.fn.norm.weight"], G[pre + ".1.fn.norm.bias"], 0.0, scr, ns, self.s)
-            # attention: X2 = Xs + Wo attn(Wqkv LN(Xs)) + bo ; dX becomes dXs in place
+            dX = ln_bwd(pre + ".1.fn.norm", dY2, st["X2"].data_ptr(), st["mu2"], st["rs2"], dX.data_ptr(), R)
+            # attention: X2 = Xs + Wo attn(Wqkv LN(Xs)) + bo ; dX holds dX2, then dXs (a new buffer)
             E = Hh * 16
             dA2 = dX
             if self.pd > 0:
                 dA2 = self.new(R, D)
                 L.vc_dropout_bwd(R * D, dX.data_ptr(), self.masks[f"{li}.attn"].data_ptr(), self.pd, dA2.data_ptr(),
                                  self.s)
-            self.gemm(1, 0, D, E, R, dA2.data_ptr(), D, 0, st["O"].data_ptr(), E, 0, 0.0,
-                      G[pre + ".0.fn.fn.to_out.0.weight"], E, 0, bias_grad=G[pre + ".0.fn.fn.to_out.0.bias"])
+            side((dA2,), partial(self.gemm, 1, 0, D, E, R, dA2.data_ptr(), D, 0, st["O"].data_ptr(), E, 0, 0.0,
+                                 G[pre + ".0.fn.fn.to_out.0.weight"], E, 0, bias_grad=G[pre + ".0.fn.fn.to_out.0.bias"],
+                                 side=sd))
             dO = self.new(R, E)
             self.gemm(0, 0, R, E, D, dA2.data_ptr(), D, 0, P[pre + ".0.fn.fn.to_out.0.weight"], E, 0, 0.0,
                       dO.data_ptr(), E, 0)
             dqkv = self.new(R, 3 * E)
             L.vc_s2eft_attn_bwd(B, T, Hh, st["qkv"].data_ptr(), st["O"].data_ptr(), dO.data_ptr(), st["lse"].data_ptr(),
                                 16 ** -0.5, dqkv.data_ptr(), self.s)
-            self.gemm(1, 0, 3 * E, D, R, dqkv.data_ptr(), 3 * E, 0, st["Y"].data_ptr(), D, 0, 0.0,
-                      G[pre + ".0.fn.fn.to_qkv.weight"], D, 0)
+            side((dqkv,), partial(self.gemm, 1, 0, 3 * E, D, R, dqkv.data_ptr(), 3 * E, 0, st["Y"].data_ptr(), D, 0, 0.0,
+                                  G[pre + ".0.fn.fn.to_qkv.weight"], D, 0, side=sd))
             dY = self.new(R, D)
             self.gemm(0, 0, R, D, 3 * E, dqkv.data_ptr(), 3 * E, 0, P[pre + ".0.fn.fn.to_qkv.weight"], D, 0, 0.0,
                       dY.data_ptr(), D, 0)
-            L.vc_layernorm_bwd(R, D, dY.data_ptr(), D, st["xs"].data_ptr(), D, P[pre + ".0.fn.norm.weight"],
-                               st["mu"].data_ptr(), st["rs"].data_ptr(), dX.data_ptr(), D, 1.0,
-                               G[pre + ".0.fn.norm.weight"], G[pre + ".0.fn.norm.bias"], 0.0, scr, ns, self.s)
-            # skipcat: Xs[b] = Wm Z[b] + bias  (Wm = weight viewed [T, 2T])
+            dX = ln_bwd(pre + ".0.fn.norm", dY, st["xs"].data_ptr(), st["mu"], st["rs"], dX.data_ptr(), R)
+            # skipcat: Xs[b] = Wm Z[b] + bias  (Wm = weight viewed [T, 2T]); its weight / bias gradients on the side
             if "Z" in st:
                 sk = f"transformer.skipcat.{li - 2}"
                 dWb = self.new(B, T * 2 * T)
-                self.gemm(0, 1, T, 2 * T, D, dX.data_ptr(), D, T * D, st["Z"].data_ptr(), D, 2 * T * D, 0.0,
-                          dWb.data_ptr(), 2 * T, T * 2 * T, batch=B)
-                L.vc_colsum(B, T * 2 * T, dWb.data_ptr(), T * 2 * T, G[sk + ".weight"], 0.0, scr, ns, self.s)
-                L.vc_s2eft_skip_bias_grad(B, T, D, dX.data_ptr(), G[sk + ".bias"], self.s)
+                side((dX, dWb),
+                     partial(self.gemm, 0, 1, T, 2 * T, D, dX.data_ptr(), D, T * D, st["Z"].data_ptr(), D, 2 * T * D, 0.0,
+                             dWb.data_ptr(), 2 * T, T * 2 * T, batch=B, side=sd),
+                     partial(L.vc_colsum, B, T * 2 * T, dWb.data_ptr(), T * 2 * T, G[sk + ".weight"], 0.0, sd[1], ns,
+                             sd[0]),
+                     partial(L.vc_s2eft_skip_bias_grad, B, T, D, dX.data_ptr(), G[sk + ".bias"], sd[0]))
                 dZ = self.new(B, 2 * T, D)
                 self.gemm(1, 0, 2 * T, D, T, P[sk + ".weight"], 2 * T, 0, dX.data_ptr(), D, T * D, 0.0, dZ.data_ptr(),
                           D, 2 * T * D, batch=B)
@@ -352,13 +407,30 @@ class _Program:
                 dX = dXin
             if li in dlast:  # this layer's input is also last_output[li] of layer li + 2
                 L.vc_add2_2d(R, D, dX.data_ptr(), D, dlast[li].data_ptr(), D, dX.data_ptr(), D, 0.0, self.s)
+            flush()   # _SIDE_STREAM 2: the layer's parameter gradients, one fork
         # embedding: X0 = dropout(cat(cls, xg W^T + b) + pos)
         if self.pe > 0:
             L.vc_dropout_bwd(R * D, dX.data_ptr(), self.masks["emb"].data_ptr(), self.pe, dX.data_ptr(), self.s)
-        L.vc_colsum(B, T * D, dX.data_ptr(), T * D, G["pos_embedding"], 0.0, scr, ns, self.s)
-        L.vc_colsum(B, D, dX.data_ptr(), T * D, G["cls_token"], 0.0, scr, ns, self.s)
         dE = self.new(B * N, D)
         L.vc_s2eft_strip_cls(B, N, D, dX.data_ptr(), dE.data_ptr(), self.s)
-        self.gemm(1, 0, D, C, B * N, dE.data_ptr(), D, 0, self.xg.data_ptr(), C, 0, 0.0,
-                  G["patch_to_embedding.weight"], C, 0, bias_grad=G["patch_to_embedding.bias"])
+        side((dX, dE),
+             partial(L.vc_colsum, B, T * D, dX.data_ptr(), T * D, G["pos_embedding"], 0.0, sd[1], ns, sd[0]),
+             partial(L.vc_colsum, B, D, dX.data_ptr(), T * D, G["cls_token"], 0.0, sd[1], ns, sd[0]),
+             partial(self.gemm, 1, 0, D, C, B * N, dE.data_ptr(), D, 0, self.xg.data_ptr(), C, 0, 0.0,
+                     G["patch_to_embedding.weight"], C, 0, bias_grad=G["patch_to_embedding.bias"], side=sd))
+        flush()
+        # join: the gradient is complete when the side stream is; its buffers may go back to the allocator after it
+        if side_stream is not main:
+            ev = torch.cuda.Event()
+            ev.record(side_stream)
+            main.wait_event(ev)
+        keep.clear()
         return grad
+
+    def _side_stream(self):
+        """the backward's weight-gradient stream: one per model and device"""
+        streams = self.m.__dict__.setdefault("_vc_side_streams", {})
+        key = str(self.dev)
+        if key not in streams:
+            streams[key] = torch.cuda.Stream(self.dev)
+        return streams[key]
