@@ -533,8 +533,10 @@ VC_API int vc_gelu_fwd(long n, const float* x, float* y, hipStream_t stream);
 VC_API int vc_gelu_bwd(long n, const float* dy, const float* x, float* dx, hipStream_t stream);
 VC_API int vc_s2eft_skip_pack(int B, int T, int D, const float* x, const float* last, const float* bias, float* Z,
                               float* biasmat, hipStream_t stream);
-VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx, int acc_x, float* dlast,
-                                hipStream_t stream);
+/* the skipcat backward's split of dZ [B, T, 2, D]: dx = (acc_x ? dx : 0) + dZ[:, :, 0] (+ addx, may be null: a
+ * residual gradient folded in), dlast = dZ[:, :, 1] (overwritten, round 6: each layer's is written once) */
+VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx, int acc_x, const float* addx,
+                                float* dlast, hipStream_t stream);
 VC_API int vc_s2eft_skip_bias_grad(int B, int T, int D, const float* dY, float* db, hipStream_t stream);
 /* nn.Dropout(p) in training (S2EFT emb_dropout :120, to_out :43, FeedForward :26, :28):
  * keep = hash(seed, i) >= p (counter-based), y = add + keep * x / (1 - p) (add may be null, y may

@@ -292,12 +292,12 @@ def _s2eft_grad(side, captured):
 @pytest.mark.gpu
 def test_s2eft_side_stream_backward_is_bit_identical():
     """Round 6: the backward's weight / bias gradients on a side stream beside the data-gradient chain (forked per
-    product, or once per layer) give the single-stream step's loss and flat gradient bit for bit, eager and replayed
-    from a hipGraph capture"""
+    product, or once per layer) or grouped per layer on the chain (vitcnn_amd.s2eft._SIDE_STREAM 1 / 2 / 3) give the
+    immediate single-stream step's loss and flat gradient bit for bit, eager and replayed from a hipGraph capture"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ref_loss, ref = _s2eft_grad(0, False)
-    for mode in (1, 2):
+    for mode in (1, 2, 3):
         for captured in (False, True):
             loss, g = _s2eft_grad(mode, captured)
             assert loss == ref_loss, (mode, captured, loss, ref_loss)

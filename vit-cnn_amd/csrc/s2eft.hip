@@ -361,15 +361,16 @@ __global__ void skip_pack(int B, int T, int D, const float* __restrict__ x, cons
   Z[(row * 2 + 1) * D + d] = last[i];
 }
 
-// dx (=/+=) dZ[:, :, 0, :]; dlast += dZ[:, :, 1, :]
+// dx (=/+=) dZ[:, :, 0, :] (+ addx); dlast = dZ[:, :, 1, :]
 __global__ void skip_unpack(int B, int T, int D, const float* __restrict__ dZ, float* __restrict__ dx, int acc_x,
-                            float* __restrict__ dlast) {
+                            const float* __restrict__ addx, float* __restrict__ dlast) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)B * T * D) return;
   const long row = i / D, d = i % D;
-  const float a = dZ[(row * 2) * D + d];
+  float a = dZ[(row * 2) * D + d];
+  if (addx) a = a + addx[i];
   dx[i] = acc_x ? dx[i] + a : a;
-  dlast[i] += dZ[(row * 2 + 1) * D + d];
+  dlast[i] = dZ[(row * 2 + 1) * D + d];
 }
 
 // dbias[o] = sum_{b, d} dY[b, o, d]  (one block per o)
@@ -510,11 +511,11 @@ VC_API int vc_s2eft_skip_pack(int B, int T, int D, const float* x, const float* 
   return VC_OK;
 }
 
-VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx, int acc_x, float* dlast,
-                                hipStream_t stream) {
+VC_API int vc_s2eft_skip_unpack(int B, int T, int D, const float* dZ, float* dx, int acc_x, const float* addx,
+                                float* dlast, hipStream_t stream) {
   VC_REQUIRE(B > 0 && T > 0 && D > 0);
   hipLaunchKernelGGL(skip_unpack, dim3(vc_cdiv((long)B * T * D, 256)), dim3(256), 0, stream, B, T, D, dZ, dx, acc_x,
-                     dlast);
+                     addx, dlast);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

@@ -19,6 +19,7 @@ references an un-imported `F`, :58, and raises too).
 """
 from __future__ import annotations
 
+import ctypes
 from functools import partial
 
 import torch
@@ -135,11 +136,15 @@ class _S2EFTFunction(torch.autograd.Function):
         return None, None, grad, None
 
 
-# the backward's weight / bias gradients beside the data-gradient chain (round 6): 0 = one stream; 1 = each on a side
+# the backward's parameter gradients (round 6): 0 = each on the chain where its inputs are made; 1 = each on a side
 # stream as soon as its inputs exist (one fork per product); 2 = a layer's parameter gradients queued and forked to
-# the side stream once, at the layer's end.  The same launches in the same order per stream: bit-identical results
-# (tests/test_s2eft.py).  Measured (tools/s2eft_step.py, 200 replays x 2): 0: 1.286 ms, 1: 1.497 ms
-_SIDE_STREAM = 0
+# the side stream once, at the layer's end; 3 = queued and issued on the chain at the layer's end, the layer's
+# weight-gradient GEMMs as ONE grouped launch + one grouped split-K reduce (vc_gemm_group_*).  Every GEMM's plan
+# depends on its shape and workspace only, and each stream runs its launches in one order: bit-identical results
+# in every mode (tests/test_s2eft.py).  Measured (tools/s2eft_step.py, 200 replays x 2, profiles/
+# r06_ab_s2eft_side_stream.log): 0: 1.28-1.32 ms, 1: 1.50 ms, 2: 1.35-1.36 ms, 3: 1.173-1.176 ms (default)
+_SIDE_STREAM = 3
+GEMM_GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES (include/vitcnn.h)
 
 
 class _Program:
@@ -166,6 +171,7 @@ class _Program:
             from .parallel import rank
             self.seed = (self.seed + 0x9E3779B97F4A7C15 * rank()) % (1 << 62)
         self.masks = {}
+        self._group = None
 
     def drop(self, site, x, add, y, n, p):
         """y = add + dropout_p(x) (add may be None); the keep mask is saved under `site`"""
@@ -182,6 +188,10 @@ class _Program:
         """vc_gemm on the program's stream with its scratch, or (side = (stream handle, scratch pointer)) on the
         backward's weight-gradient stream"""
         st, scr = side if side is not None else (self.s, self.scr.data_ptr())
+        if self._group is not None:   # recorded into the open group (launched at vc_gemm_group_end)
+            self.L.vc_gemm_group_add(self._group, tA, tB, M, N, K, alpha, A, lda, sA, Bm, ldb, sB, beta, C, ldc, sC,
+                                     batch, bias, add, add_ld, add_mod, 0, bias_grad, scr, self.SCRATCH, None, 0)
+            return
         self.L.vc_gemm(tA, tB, M, N, K, alpha, A, lda, sA, Bm, ldb, sB, beta, C, ldc, sC, batch, bias, add, add_ld,
                        add_mod, 0, bias_grad, scr, self.SCRATCH, st)
 
@@ -275,9 +285,11 @@ class _Program:
     def backward(self, dlogits):
         """The hand-written backward.  The data-gradient chain (dX through the layers) runs on the program's
         stream; every weight / bias gradient (the weight-gradient GEMMs with their split-K reduces, the LayerNorm
-        parameter reductions, the skipcat and embedding column sums) goes through `side()`, which runs it on the chain
-        (_SIDE_STREAM 0, the default) or on a side stream forked from the chain and joined before the gradient is
-        returned (1, 2: measured slower, the cross-stream edges cost more than the overlap gains).  The chain never
+        parameter reductions, the skipcat and embedding column sums) goes through `side()`, which by default
+        (_SIDE_STREAM 3) queues it to the layer's end, where the layer's weight-gradient GEMMs launch as ONE grouped
+        grid + one grouped split-K reduce (10 launches -> 2 per layer); it can also run each at once on the chain (0)
+        or on a side stream forked from the chain and joined before the gradient is returned (1, 2: measured slower,
+        the cross-stream edges cost more than the overlap gains).  The chain never
         writes a buffer the parameter gradients read (the LayerNorm backward writes the residual sum to a new
         buffer: vc_layernorm_bwd_dx with res), and every buffer they read stays referenced until the join.
         Per-launch arithmetic and per-stream order do not depend on the mode: the same bits."""
@@ -285,8 +297,8 @@ class _Program:
         R = B * T
         P = self.P
         main = torch.cuda.current_stream(self.dev)
-        side_stream = self._side_stream() if _SIDE_STREAM else main
-        scr2 = self.new(self.SCRATCH) if _SIDE_STREAM else self.scr
+        side_stream = self._side_stream() if _SIDE_STREAM in (1, 2) else main
+        scr2 = self.new(self.SCRATCH) if side_stream is not main else self.scr
         sd = (side_stream.cuda_stream, scr2.data_ptr())
         keep, pending = [scr2], []
 
@@ -295,16 +307,28 @@ class _Program:
                 ev = torch.cuda.Event()
                 ev.record(main)
                 side_stream.wait_event(ev)
+            if _SIDE_STREAM == 3:   # the queued GEMMs (independent products) as one grouped launch, then the rest
+                gemms = [fn for fn in pending if getattr(fn, "func", None) == self.gemm]
+                if gemms:
+                    self._group = self._group_buf()
+                    L.vc_gemm_group_begin(self._group, self.s)
+                    try:
+                        for fn in gemms:
+                            fn()
+                    finally:
+                        grp, self._group = self._group, None
+                        L.vc_gemm_group_end(grp)
+                pending[:] = [fn for fn in pending if getattr(fn, "func", None) != self.gemm]
             for fn in pending:
                 fn()
             pending.clear()
 
         def side(bufs, *calls):
-            """parameter-gradient work (calls with their arguments bound), reading `bufs`: on the side stream now
-            (_SIDE_STREAM 1), queued for the layer's end (2), or on the chain (0)"""
+            """parameter-gradient work (calls with their arguments bound), reading `bufs`: on the chain now
+            (_SIDE_STREAM 0), on the side stream now (1), queued for the layer's end (2, 3)"""
             keep.extend(bufs)
             pending.extend(calls)
-            if _SIDE_STREAM != 2:
+            if _SIDE_STREAM not in (2, 3):
                 flush()
 
         grad = self.new(m._n_params)
@@ -398,14 +422,13 @@ class _Program:
                 dZ = self.new(B, 2 * T, D)
                 self.gemm(1, 0, 2 * T, D, T, P[sk + ".weight"], 2 * T, 0, dX.data_ptr(), D, T * D, 0.0, dZ.data_ptr(),
                           D, 2 * T * D, batch=B)
-                if li - 2 not in dlast:
-                    dl = self.new(B, T, D)
-                    L.vc_fill(R * D, dl.data_ptr(), 0.0, self.s)
-                    dlast[li - 2] = dl
+                dlast[li - 2] = self.new(B, T, D)   # written once, by this unpack (layer li - 2's skip gradient)
                 dXin = self.new(B, T, D)
-                L.vc_s2eft_skip_unpack(B, T, D, dZ.data_ptr(), dXin.data_ptr(), 0, dlast[li - 2].data_ptr(), self.s)
+                # this layer's input is also last_output[li] of layer li + 2: its gradient folded in here
+                L.vc_s2eft_skip_unpack(B, T, D, dZ.data_ptr(), dXin.data_ptr(), 0,
+                                       dlast[li].data_ptr() if li in dlast else None, dlast[li - 2].data_ptr(), self.s)
                 dX = dXin
-            if li in dlast:  # this layer's input is also last_output[li] of layer li + 2
+            elif li in dlast:  # this layer's input is also last_output[li] of layer li + 2
                 L.vc_add2_2d(R, D, dX.data_ptr(), D, dlast[li].data_ptr(), D, dX.data_ptr(), D, 0.0, self.s)
             flush()   # _SIDE_STREAM 2: the layer's parameter gradients, one fork
         # embedding: X0 = dropout(cat(cls, xg W^T + b) + pos)
@@ -426,6 +449,14 @@ class _Program:
             main.wait_event(ev)
         keep.clear()
         return grad
+
+    def _group_buf(self):
+        """host memory of the backward's grouped-GEMM state (vc_gemm_group_*: the library keeps none)"""
+        buf = self.m.__dict__.get("_vc_group_buf")
+        if buf is None:
+            buf = ctypes.create_string_buffer(GEMM_GROUP_BYTES)
+            self.m.__dict__["_vc_group_buf"] = buf
+        return ctypes.addressof(buf)
 
     def _side_stream(self):
         """the backward's weight-gradient stream: one per model and device"""
