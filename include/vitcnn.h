@@ -182,6 +182,9 @@ VC_API int vc_bn_bwd_relu_ex(int train, long M, int C, const float* dy, long ldd
 /* ---------------------------------------------------------------- layout / spatial
  * NCHW input patches (the reference's batch layout, datasets.py:571-572) -> channels-last. */
 VC_API int vc_nchw_to_nhwc(int B, int C, int HW, const float* x, float* y, hipStream_t stream);
+/* the same into rows of ldy >= C floats with columns C .. ldy - 1 written 0 (FusAtNet's 1-band LiDAR input padded
+ * to 4 channels: 16-B rows for the pipelined conv) */
+VC_API int vc_nchw_to_nhwc_pad(int B, int C, int HW, const float* x, float* y, int ldy, hipStream_t stream);
 
 /* 3x3 valid im2col of a channels-last [B,H,W,C] map with the preceding BatchNorm's affine
  * (bn_* may be null) fused in: col[(b,oh,ow), c*9+kh*3+kw] — ms_conv_bn_relu

@@ -53,6 +53,7 @@ SWITCHES = {
     "VITCNN_CH_LANE": ("model", "_CH_LANE", int),
     "VITCNN_CH_ORDERED": ("model", "_CH_ORDERED", _FLAG),
     "VITCNN_FUSAT_IM2COL": ("fusatnet", "_TAP_CONV", lambda v: not _FLAG(v)),
+    "VITCNN_FUSAT_PAD_LIDAR": ("fusatnet", "_PAD_LIDAR", _FLAG),
     "VITCNN_GEMM_BNSTATS": ("model", "_GEMM_BNSTATS", _FLAG),
     "VITCNN_PG_LANE2": ("model", "_PG_LANE2", _FLAG),
 }

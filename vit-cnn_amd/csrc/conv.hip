@@ -9,9 +9,9 @@
 
 namespace {
 
-// y[b][p][c] = x[b][c][p] via 32x32 LDS tiles
+// y[b][p][c] = x[b][c][p] via 32x32 LDS tiles; rows of ldy floats, columns C .. ldy - 1 written 0
 __global__ __launch_bounds__(256) void nchw_to_nhwc(int B, int C, int HW, const float* __restrict__ x,
-                                                    float* __restrict__ y) {
+                                                    float* __restrict__ y, int ldy) {
   __shared__ float t[32][33];
   const int b = blockIdx.z;
   const int c0 = blockIdx.y * 32, p0 = blockIdx.x * 32;
@@ -22,10 +22,10 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc(int B, int C, int HW, const 
     t[i][tx] = (c < C && p < HW) ? xb[(long)c * HW + p] : 0.f;
   }
   __syncthreads();
-  float* yb = y + (long)b * C * HW;
+  float* yb = y + (long)b * ldy * HW;
   for (int i = ty; i < 32; i += 8) {
     int p = p0 + i, c = c0 + tx;
-    if (p < HW && c < C) yb[(long)p * C + c] = t[tx][i];
+    if (p < HW && c < ldy) yb[(long)p * ldy + c] = t[tx][i];
   }
 }
 
@@ -251,7 +251,16 @@ __global__ void maxpool2_bwd(int total, FastDiv fC, FastDiv fW, FastDiv fH, cons
 VC_API int vc_nchw_to_nhwc(int B, int C, int HW, const float* x, float* y, hipStream_t stream) {
   VC_REQUIRE(B >= 0 && C > 0 && HW > 0);
   if (B == 0) return VC_OK;
-  hipLaunchKernelGGL(nchw_to_nhwc, dim3(vc_cdiv(HW, 32), vc_cdiv(C, 32), B), dim3(256), 0, stream, B, C, HW, x, y);
+  hipLaunchKernelGGL(nchw_to_nhwc, dim3(vc_cdiv(HW, 32), vc_cdiv(C, 32), B), dim3(256), 0, stream, B, C, HW, x, y, C);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
+}
+
+VC_API int vc_nchw_to_nhwc_pad(int B, int C, int HW, const float* x, float* y, int ldy, hipStream_t stream) {
+  VC_REQUIRE(B >= 0 && C > 0 && HW > 0 && ldy >= C);
+  if (B == 0) return VC_OK;
+  hipLaunchKernelGGL(nchw_to_nhwc, dim3(vc_cdiv(HW, 32), vc_cdiv(ldy, 32), B), dim3(256), 0, stream, B, C, HW, x, y,
+                     ldy);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

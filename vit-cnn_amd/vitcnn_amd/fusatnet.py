@@ -36,6 +36,9 @@ from .model import _IMPLICIT_CONV, N_COUNTERS
 # 3x3 convs: the tap-major implicit GEMM (vc_conv3x3_tap_*, conv_tap.hip); False restores the im2col +
 # vc_gemm formulation of rounds 1-2 (a module constant: tools/knobs.py sets it from VITCNN_FUSAT_IM2COL=1)
 _TAP_CONV = True
+# the LiDAR input (C2 bands, 1 at config 5) laid out in rows padded to 4 floats with zero columns, so its 3x3 convs
+# take the pipelined conv (conv_tap.hip conv_pipe_ok: 16-B rows) instead of conv_tap
+_PAD_LIDAR = True
 
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
 _COUNTER_BUFS = {}
@@ -266,10 +269,15 @@ class _Program:
         g, beta = self.acc(t)
         self.add_into(g, src, M, C, beta=beta)
 
-    def nhwc(self, x):
+    def nhwc(self, x, ld=None):
+        """x [B, C, H, W] -> channels-last rows of ld >= C floats (columns C .. ld - 1 zero)"""
         B, C, H, W = x.shape
-        y = self.new(B, H, W, C)
-        self.L.vc_nchw_to_nhwc(B, C, H * W, x.data_ptr(), y.data_ptr(), self.s)
+        ld = ld or C
+        y = self.new(B, H, W, ld)
+        if ld == C:
+            self.L.vc_nchw_to_nhwc(B, C, H * W, x.data_ptr(), y.data_ptr(), self.s)
+        else:
+            self.L.vc_nchw_to_nhwc_pad(B, C, H * W, x.data_ptr(), y.data_ptr(), ld, self.s)
         self.no_grad_ids.add(id(y))
         return y
 
@@ -477,7 +485,8 @@ class _Program:
         m, L, B, P = self.m, self.L, self.B, self.P
         self.pack_all()
         c1, c2 = m.c1, m.c2
-        x1, x2 = self.nhwc(self.x1), self.nhwc(self.x2)
+        ld2 = (c2 + 3) // 4 * 4 if _PAD_LIDAR else c2
+        x1, x2 = self.nhwc(self.x1), self.nhwc(self.x2, ld2)
         HW = P * P
         M = B * HW
         Fhs = self.six(x1, c1, P, c1, m.hfe)                                  # [B,P,P,1024]
@@ -497,7 +506,7 @@ class _Program:
         # weights' zero padding (conv_tap.hip conv_pipe_ok), so the 2193-channel convs run on conv_pipe
         L.vc_fill_2d(M, Cp - Ct, cat.data_ptr() + F32 * Ct, Cp, 0.0, self.s)
         L.vc_add2_2d(M, c1, x1.data_ptr(), c1, None, 0, cat.data_ptr(), Cp, 0.0, self.s)
-        L.vc_add2_2d(M, c2, x2.data_ptr(), c2, None, 0, cat.data_ptr() + F32 * c1, Cp, 0.0, self.s)
+        L.vc_add2_2d(M, c2, x2.data_ptr(), ld2, None, 0, cat.data_ptr() + F32 * c1, Cp, 0.0, self.s)
         offs = F32 * (c1 + c2)
         L.vc_pool_scale(B, HW, Hp * Hp, 1024, t.data_ptr(), Fhs.data_ptr(), 1024, cat.data_ptr() + offs, Cp,
                         self.s)                                               # Ms
@@ -509,7 +518,7 @@ class _Program:
                                 dpooled.data_ptr(), self.s)
 
         self.record(ms_bwd, t, Fhs, cat)
-        Sp = self.res_attention(x2, c2, P, c2, m.spatial_am)
+        Sp = self.res_attention(x2, ld2, P, c2, m.spatial_am)
         offt = F32 * (c1 + c2 + 1024)
         self.mul(Sp, Fhs, M, 1024, cat.data_ptr() + offt, Cp,
                  lambda: (self.grad_of(cat).data_ptr() + offt, Cp))           # Mt
