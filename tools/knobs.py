@@ -47,6 +47,7 @@ SWITCHES = {
     "VITCNN_LANES_BWD": ("model", "_LANES_BWD", _FLAG),
     "VITCNN_GEMM_GROUP": ("model", "_GROUP", _FLAG),
     "VITCNN_BF16_MIN_K": ("model", "_BF16_MIN_K", int),
+    "VITCNN_GLOBAL_FIRST": ("model", "_GLOBAL_FIRST", _FLAG),
     "VITCNN_LANE_MAP": ("model", "_LANE_MAP", lambda v: [int(x) for x in v.split(",") if x]),
     "VITCNN_BN_TICKETS": ("model", "_BN_TICKETS", _FLAG),
     "VITCNN_BN_RELU_AFFINE": ("model", "_BN_RELU_AFFINE", _FLAG),

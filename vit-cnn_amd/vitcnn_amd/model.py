@@ -65,6 +65,10 @@ PARAM_ALIGN = 4            # floats: flat-buffer alignment (16 B) of every param
 ALIGN_MIN = 64
 GEMM_GROUP_BYTES = 16384   # VC_GEMM_GROUP_BYTES (include/vitcnn.h)
 GEMM_MASK = 64             # vc_gemm flags: the addend is a ReLU mask (include/vitcnn.h)
+# capture order of a GlobalLocal block's forward: lane 0's global view (the hsiMamba chain) captured before the local /
+# channel branches it runs beside (the same DAG, bit-identical).  Measured 1.695 vs 1.687 ms (3 rounds x 300 replays,
+# profiles/r06_ab_global_first.log): kept off
+_GLOBAL_FIRST = False
 # conv1x1 + BatchNorm (+ ReLU) forward: the statistics partials computed in the GEMM epilogue (vc_gemm_colstats)
 _GEMM_BNSTATS = True
 # GLfusion forward: the NonLocal phi | g projection on the channel lane (2) right after ln4, theta alone on lane 1
@@ -816,7 +820,31 @@ class _Program:
         gv, mx = pfx + ".global_view", pfx + ".global_view.layers.0"
         order, inv = self.tab[("order", H)].data_ptr(), self.tab[("inv", H)].data_ptr()
         M = B * S
+        if _GLOBAL_FIRST:
+            # lanes 1 / 2 fork here, but their launches are captured after lane 0's global view: the graph's
+            # executor hands the kernels to the hardware queues in capture order (section 14)
+            e0 = self.mark()
+            Fg = self.global_view(blk, pfx, X, H)
+            FM, e_fm = self.block_local_branch(blk, pfx, X, H, e0)
+            self.wait(e_fm)
+            return self.fusion(pfx + ".fusion", Fg, Cout, FM, Cout, M, Cout)
         FM, e_fm = self.block_local_branch(blk, pfx, X, H)
+        Fg = self.global_view(blk, pfx, X, H)
+        self.wait(e_fm)
+        # --- fusionBlock(global, fused) with ChannelExchange
+        return self.fusion(pfx + ".fusion", Fg, Cout, FM, Cout, M, Cout)
+
+    def global_view(self, blk, pfx, X, H):
+        """hsiMamba global view -> change_dim -> TokenLearner -> ln3 (lane 0); returns Fg"""
+        B, ws, P = self.B, self.ws, self.P
+        Cin, Cout, E = blk.cin, blk.cout, blk.embed
+        D, R = E // 2, math.ceil(E / 16)
+        XW = R + 32
+        L_, Hs = H * H, H - 2
+        S = Hs * Hs
+        rows = B * L_
+        gv, mx = pfx + ".global_view", pfx + ".global_view.layers.0"
+        order, inv = self.tab[("order", H)].data_ptr(), self.tab[("inv", H)].data_ptr()
         if self._tap_dgrad(blk):
             # the local conv's weight, tap-major, for its data gradient in the backward (lane 0 has slack here)
             self.L.vc_conv3x3_pack(Cout, Cin, 0, P[pfx + ".local_feature.conv.weight"],
@@ -872,20 +900,17 @@ class _Program:
             self.mm_nt(rows, Cout, E, G, E, P[pfx + ".change_dim.weight"], E, CD, Cout,
                        bias=P[pfx + ".change_dim.bias"])
         Zg = self.token_learner(pfx + ".global_feature", CD, L_, Cout, S)
-        Fg = self.layernorm(pfx + ".ln3", Zg, B * S, Cout, pfx + ".Fg")
-        self.wait(e_fm)
-        # --- fusionBlock(global, fused) with ChannelExchange
-        return self.fusion(pfx + ".fusion", Fg, Cout, FM, Cout, M, Cout)
+        return self.layernorm(pfx + ".ln3", Zg, B * S, Cout, pfx + ".Fg")
 
-    def block_local_branch(self, blk, pfx, X, H):
-        """local feature (lane 1) || channel feature (lane 2), then the GLfusionBlock on lane 1;
-        returns (FM, event on lane 1 after FM)."""
+    def block_local_branch(self, blk, pfx, X, H, e0=None):
+        """local feature (lane 1) || channel feature (lane 2), then the GLfusionBlock on lane 1, forked from lane 0 at
+        e0 (now if None); returns (FM, event on lane 1 after FM)."""
         B, ws, P = self.B, self.ws, self.P
         Cin, Cout = blk.cin, blk.cout
         L_, Hs = H * H, H - 2
         S, Ci, Pk = Hs * Hs, Cout // 2, (Hs // 2) * (Hs // 2)
         rows = B * L_
-        e0 = self.mark()
+        e0 = self.mark() if e0 is None else e0
         # --- local feature: BN -> conv3x3 -> ReLU
         with self.lane(1, e0):
             Fl = self.conv_bn_relu3(pfx + ".local_feature", X, H, Cin, Cout)
