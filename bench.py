@@ -82,7 +82,7 @@ def time_kernel(fn, reps, stream):
     return s.elapsed_time(e) / reps * 1e-3
 
 
-PMC_PROFILES = ("r05_pmc.json", "r03_pmc.json", "r02_pmc_s4.json", "r02_pmc.json", "r01_pmc.json")   # newest first
+PMC_PROFILES = ("r06_pmc.json", "r05_pmc.json", "r03_pmc.json", "r02_pmc_s4.json", "r02_pmc.json", "r01_pmc.json")   # newest first
 
 
 def _pmc_from_profile(kernel_key):

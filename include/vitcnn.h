@@ -393,17 +393,17 @@ VC_API int vc_tl_check(int HW, int C, int S);
 VC_API int vc_tl_pixel_stats(long M, int C, const float* x, long ldx, float* mx, int* amx, float* avg, double* ws,
                              hipStream_t stream);
 /* stats (train: batch statistics from the moments, running statistics updated; eval: the running ones),
- * the attention maps a [B, S, HW] (optional, may be null) and the pooled tokens Z [B, S, C] =
+ * the attention maps a [B, S, HW] (may be null when no backward follows) and the pooled tokens Z [B, S, C] =
  * (1/HW) a x, in one launch */
 VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
                      const float* avg, const float* params, float* bn_buffers, float eps, float momentum,
                      const double* ws, double* stats, float* a, float* Z, hipStream_t stream);
 /* backward from dZ [B, S, C]: dx [B*HW, C] (ld lddx, overwritten) = (1/HW) a^T dZ + the pooled-path gradient
- * (argmax channel and mean), dparams (S x 5, overwritten); da [B, S, HW] floats of scratch (the attention
- * maps' gradient).  Two launches. */
+ * (argmax channel and mean), dparams (S x 5, overwritten); a = the attention maps vc_tl_fwd wrote (round 6: the
+ * backward reads them instead of recomputing them; the round-5 `da` scratch argument is gone).  Two launches. */
 VC_API int vc_tl_bwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
-                     const float* avg, const int* amx, const float* params, const double* stats, const float* dZ,
-                     float* da, double* ws, float* dx, long lddx, float* dparams, hipStream_t stream);
+                     const float* avg, const int* amx, const float* params, const double* stats, const float* a,
+                     const float* dZ, double* ws, float* dx, long lddx, float* dparams, hipStream_t stream);
 /* mask [B, S, HW] uint8 = the ReLU decisions (BN(1) output > 0) vc_tl_fwd / vc_tl_bwd take, from the
  * same stats (test instrumentation: the float64 parity yardstick follows the HIP path's fp32 ties) */
 VC_API int vc_tl_relu_mask(int B, int HW, int S, const float* mx, const float* avg, const float* params,

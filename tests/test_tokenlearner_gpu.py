@@ -66,9 +66,8 @@ def _run_hip(L, train, x, B, HW, C, S, par, buf, dZ):
     mask = torch.empty(B * S * HW, dtype=torch.uint8, device=DEV)
     L.vc_tl_relu_mask(B, HW, S, P(mx), P(avg), P(pard), P(st), P(mask), _s())
     dx = torch.full((M, C), float("nan"), device=DEV)
-    da = torch.full((B * S * HW,), float("nan"), device=DEV)
     gp = torch.full((S * 5,), float("nan"), device=DEV)
-    L.vc_tl_bwd(train, B, HW, C, S, P(xd), C, P(mx), P(avg), P(amx), P(pard), P(st), P(dzd), P(da), P(ws), P(dx), C,
+    L.vc_tl_bwd(train, B, HW, C, S, P(xd), C, P(mx), P(avg), P(amx), P(pard), P(st), P(a), P(dzd), P(ws), P(dx), C,
                 P(gp), _s())
     torch.cuda.synchronize()
     return dict(mx=mx.cpu(), amx=amx.cpu().long(), avg=avg.cpu(), st=st.cpu(), a=a.cpu(), Z=Z.cpu(),

@@ -41,7 +41,7 @@ def main():
         stats = torch.empty(2 * S + 8, dtype=torch.float64, device=dev)
         Z = torch.empty(B * S * C, device=dev)
         dZ = torch.randn(B * S * C, device=dev, generator=g)
-        da = torch.empty(B * S * HW, device=dev)
+        amap = torch.empty(B * S * HW, device=dev)
         dx = torch.empty(M, C, device=dev)
         dpar = torch.empty(S * 5, device=dev)
 
@@ -50,11 +50,11 @@ def main():
 
         def fwd():
             L.vc_tl_fwd(1, B, HW, C, S, x.data_ptr(), C, mx.data_ptr(), avg.data_ptr(), par.data_ptr(), buf.data_ptr(),
-                        1e-5, 0.1, ws.data_ptr(), stats.data_ptr(), None, Z.data_ptr(), st)
+                        1e-5, 0.1, ws.data_ptr(), stats.data_ptr(), amap.data_ptr(), Z.data_ptr(), st)
 
         def bwd():
             L.vc_tl_bwd(1, B, HW, C, S, x.data_ptr(), C, mx.data_ptr(), avg.data_ptr(), amx.data_ptr(), par.data_ptr(),
-                        stats.data_ptr(), dZ.data_ptr(), da.data_ptr(), ws.data_ptr(), dx.data_ptr(), C,
+                        stats.data_ptr(), amap.data_ptr(), dZ.data_ptr(), ws.data_ptr(), dx.data_ptr(), C,
                         dpar.data_ptr(), st)
 
         pix()

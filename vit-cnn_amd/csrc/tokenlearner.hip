@@ -358,9 +358,12 @@ __global__ __launch_bounds__(256) void tl_fwd_pool(int train, int B, int HW, int
 }
 
 // Backward part 1: grid (B, ceil(S / 16)); block 256.  da[b, s, q] = (1/HW) sum_c dZ[b, s, c] x[b, q, c] for
-// the block's 16 tokens (MFMA, both operands as float4 runs of their rows straight from L2), written to `da`;
+// the block's 16 tokens (MFMA, both operands as float4 runs of their rows straight from L2), kept in registers;
 // then per token the fp64 sums over this sample's pixels of g1, g1 xh, g1 (m - mbar), g1 (v - vbar) ->
-// part[(b * S + s) * NBS + j] (summed over the pixel tiles in a fixed order).
+// part[(b * S + s) * NBS + j] (summed over the pixel tiles in a fixed order), and (round 6) per pixel the fp64
+// sums over the block's 16 tokens of w0_s gi_s g1 and w1_s gi_s g1 (gi = gamma invstd) -> apart[((b * nsb +
+// blockIdx.y) * HW + q) * 2 + j]: the token-sum part of the pixel gradients, so tl_bwd_dx needs neither da nor a
+// per-token loop (the batch-statistics part of df is affine in the pixel's (max, mean), section below).
 // Up to TLDA_W waves per block: one 16-pixel tile per wave up to HW = 16 TLDA_W (a wave with two tiles doubled
 // the block's chain of dependent k-chunk loads).  Round 6: the block has exactly min(tiles, TLDA_W) waves (hsi1:
 // 6, hsi2: 4) -- the round-5 blocks of 8 carried 2 / 4 idle waves whose registers and slots the concurrent
@@ -371,8 +374,8 @@ __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, i
                                                          long ldx, const float* __restrict__ mx,
                                                          const float* __restrict__ avg, const float* __restrict__ par,
                                                          const double* __restrict__ stats,
-                                                         const float* __restrict__ dZ, float* __restrict__ da,
-                                                         double* __restrict__ part) {
+                                                         const float* __restrict__ dZ, double* __restrict__ part,
+                                                         double* __restrict__ apart) {
   __shared__ double tsum[TLDA_W][16][NBS];   // [wave][token][sum]
   const int b = blockIdx.x, s0 = blockIdx.y * 16;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
@@ -421,19 +424,32 @@ __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, i
     // acc[r] = da(token s0 + 4 g + r, pixel qb') with qb' = 16 qt + r16 for the C/D layout: col = lane % 16
     const int q = 16 * qt + r16;
     const float m = q < HW ? mx[(long)b * HW + q] : 0.f, vq = q < HW ? avg[(long)b * HW + q] : 0.f;
+    double a0 = 0.0, a1 = 0.0;   // this lane's 4 tokens of sum_s w0 gi g1, sum_s w1 gi g1 (token order)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int s = s0 + 4 * g + r;
       const float dav = acc[r] * inv_l;
       if (s < S && q < HW) {
-        da[((long)b * S + s) * HW + q] = dav;
         double xh;
         const double g1 = tl_g1(m, vq, tp[r], tmean[r], tinv[r], dav, xh);
         v[r][0] += g1;
         v[r][1] += g1 * xh;
         v[r][2] += g1 * ((double)m - mbar);
         v[r][3] += g1 * ((double)vq - vbar);
+        const double gg = (double)tp[r][3] * tinv[r] * g1;
+        a0 += (double)tp[r][0] * gg;
+        a1 += (double)tp[r][1] * gg;
       }
+    }
+    // the 4 lane groups (tokens 4 g .. 4 g + 3) pairwise: (g0 + g1) + (g2 + g3)
+    a0 += __shfl_xor(a0, 16, 64);
+    a1 += __shfl_xor(a1, 16, 64);
+    a0 += __shfl_xor(a0, 32, 64);
+    a1 += __shfl_xor(a1, 32, 64);
+    if (g == 0 && q < HW) {
+      double* ap = apart + (((long)b * gridDim.y + blockIdx.y) * HW + q) * 2;
+      ap[0] = a0;
+      ap[1] = a1;
     }
   }
   // per token: the 16 pixel lanes of the row group, then the waves in order
@@ -464,27 +480,33 @@ __global__ __launch_bounds__(64 * TLDA_W) void tl_bwd_da(int B, int HW, int C, i
 // Backward part 2: grid (B, ceil(C / 64)); block 256.  The tokens' s1 / s2 over the batch (the per-sample
 // partials summed in 4 interleaved sample quarters, then the quarters in order), then for the block's sample
 // and 64 channels
-//   dx[b, q, c] = (1/HW) sum_s a[s][q] dZ[b, s, c]                      (MFMA; a recomputed into LDS)
+//   dx[b, q, c] = (1/HW) sum_s a[s][q] dZ[b, s, c]                      (MFMA; a as the forward wrote it)
 //               + (sum_s w1_s df_s[q]) / C + [c == argmax_q] sum_s w0_s df_s[q]
-// with df_s[q] = gamma_s invstd_s (g1 - s1/n - xh s2/n) (train; eval gamma invstd g1) in fp64 (dx overwritten):
-// the sums over the tokens in 8 chunks (8 adjacent lanes per pixel), then the chunks pairwise in a fixed order.
+// with df_s[q] = gi_s (g1 - s1/n - xh s2/n) (train; eval gi g1), gi = gamma invstd.  Round 6: the pixel sums
+// split as  sum_s wj_s df_s[q] = A_j[q] - K_j - (alpha_j m_q + beta_j v_q + gamma_j)  with A_j = sum_s wj_s gi_s g1
+// (tl_bwd_da's per-16-token partials, summed here in token-block order) and -- xh being affine in the pixel's
+// pooled (m, v) -- K_j, alpha_j, beta_j, gamma_j per-batch scalars from the tokens' statistics (fp64 block sums);
+// the round-5 form recomputed every token's g1 for every pixel in each of a sample's channel blocks.
 // Block (0, 0) also writes the tokens' 5 parameter gradients (dparams).  The product runs as dx^T [c][q]: the
-// A operand (dZ rows, 16 channels x 4 tokens per MFMA) and the B operand (a [s][q]) from LDS -- a small LDS
-// footprint, so these blocks leave room for the selective-scan blocks running beside them.  The pixels go
+// A operand (dZ rows, 16 channels x 4 tokens per MFMA) and the B operand (a [s][q]) from LDS.  The pixels go
 // through a and the MFMA tiles in chunks of QC (a multiple of 16 chosen on the host so the LDS fits: all Lp
 // pixels at once for the model's patches); every sum is over tokens, so the results do not depend on QC.
 // LDS (dynamic): q4 [4][S][2], tsum [2][S], tst [2][S] doubles; dzl [S4][68], al [S4][QC + 4],
 // tpar [S][TPAR] (rounded up to 4), gq [2][QC] floats.
+constexpr int TLDX_RED = 8 * 4;   // doubles of tl_bwd_dx's static reduction buffer
 __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C, int S, int QC,
                                                  const float* __restrict__ mx, const float* __restrict__ avg,
                                                  const int* __restrict__ amx, const float* __restrict__ par,
-                                                 const double* __restrict__ stats, const float* __restrict__ dZ,
-                                                 const float* __restrict__ da, const double* __restrict__ part,
-                                                 float* __restrict__ dx, long lddx, float* __restrict__ gpar) {
+                                                 const double* __restrict__ stats, const float* __restrict__ a,
+                                                 const float* __restrict__ dZ, const double* __restrict__ part,
+                                                 const double* __restrict__ apart, float* __restrict__ dx, long lddx,
+                                                 float* __restrict__ gpar) {
   extern __shared__ __attribute__((aligned(16))) float sm_f[];
+  __shared__ double red[TLDX_RED];
   const int b = blockIdx.x, c0 = blockIdx.y * TL_CT;
   const bool b00 = blockIdx.x == 0 && blockIdx.y == 0;
   const int S4 = (S + 3) & ~3, Lp = (HW + 15) & ~15, QS = QC + 4;
+  const int nsb = (S + 15) / 16;   // tl_bwd_da's token blocks
   constexpr int DZS = TL_CT + 4;
   double* q4 = reinterpret_cast<double*>(sm_f);   // [4][S][2] per token, 4 sample-quarter sums of two columns
   double* tsum = q4 + 8 * S;                      // [2][S]  s1 / n, s2 / n
@@ -562,6 +584,26 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
     tsum[S + s] = qsum(s, 1) / nd;
   }
   __syncthreads();
+  // the per-batch scalars of the pixel sums (train): per token, t_j = w_j gi, u = (s2 / n) invstd;
+  //   K_j = sum t_j s1/n, alpha_j = sum t_j u w0, beta_j = sum t_j u w1, gamma_j = sum t_j u (bc - mean)
+  double sc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (train) {
+    for (int s = threadIdx.x; s < S; s += 256) {   // a thread's tokens in order
+      const float* ps = tpar + s * TPAR;
+      const double gi = (double)ps[3] * tst[S + s];
+      const double t0 = (double)ps[0] * gi, t1 = (double)ps[1] * gi, u = tsum[S + s] * tst[S + s];
+      const double w0 = ps[0], w1 = ps[1], bm = (double)ps[2] - tst[s];
+      sc[0] += t0 * tsum[s];
+      sc[1] += t0 * u * w0;
+      sc[2] += t0 * u * w1;
+      sc[3] += t0 * u * bm;
+      sc[4] += t1 * tsum[s];
+      sc[5] += t1 * u * w0;
+      sc[6] += t1 * u * w1;
+      sc[7] += t1 * u * bm;
+    }
+  }
+  block256_sums_d<8>(sc, red);   // (uniform: every thread takes part)
   if (b00) {   // parameter gradients: the other two partial columns too
     batch_sums(2);
     for (int s = threadIdx.x; s < S; s += 256) {
@@ -596,53 +638,29 @@ __global__ __launch_bounds__(256) void tl_bwd_dx(int train, int B, int HW, int C
   const float inv_l = 1.f / (float)HW;
   for (int q0 = 0; q0 < Lp; q0 += QC) {
     const int nq = min(QC, Lp - q0);   // a multiple of 16
-    // a recomputed into LDS, and the pixel gradients: lane group of 8 per pixel, lane k of it sums the tokens
-    // k, k + 8, ... (fixed order), then the 8 lanes pairwise
-    for (int i = threadIdx.x; i < 8 * nq; i += 256) {
-      const int ql = i >> 3, q = q0 + ql, k = i & 7;
-      const bool qok = q < HW;
-      const float m = qok ? mx[(long)b * HW + q] : 0.f, v = qok ? avg[(long)b * HW + q] : 0.f;
+    // the attention maps of the chunk's pixels into LDS (rows of HW contiguous floats), zero padded
+    for (int i = threadIdx.x; i < S4 * nq; i += 256) {
+      const int sl = i / nq, ql = i - sl * nq, q = q0 + ql;
+      al[sl * QS + ql] = (sl < S && q < HW) ? a[((long)b * S + sl) * HW + q] : 0.f;
+    }
+    // the pixel gradients: the token-block partials in order, then the affine batch-statistics part
+    for (int ql = threadIdx.x; ql < nq; ql += 256) {
+      const int q = q0 + ql;
       double gm = 0.0, ga = 0.0;
-      for (int s0 = k; s0 < S4; s0 += 32) {
-        float dav[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int s = s0 + 8 * u;
-          dav[u] = (qok && s < S) ? da[((long)b * S + s) * HW + q] : 0.f;
+      if (q < HW) {
+        const double* ap = apart + ((long)b * nsb * HW + q) * 2;
+        for (int t = 0; t < nsb; ++t) {
+          gm += ap[(long)t * HW * 2];
+          ga += ap[(long)t * HW * 2 + 1];
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int s = s0 + 8 * u;
-          if (s >= S4) continue;
-          if (s >= S || !qok) {
-            al[s * QS + ql] = 0.f;
-            continue;
-          }
-          const float* p = tpar + s * TPAR;
-          double xh;
-          const float bn = tl_bnv(m, v, p[0], p[1], p[2], tst[s], tst[S + s], p[3], p[4], xh);
-          al[s * QS + ql] = sigmoid_f(fmaxf(bn, 0.f));
-          double g1 = 0.0;
-          if (bn > 0.f) {
-            const float sg = sigmoid_f(bn);
-            g1 = (double)(dav[u] * sg * (1.f - sg));
-          }
-          const double gi = (double)p[3] * tst[S + s];
-          const double d = train ? gi * (g1 - tsum[s] - xh * tsum[S + s]) : gi * g1;
-          gm += d * (double)p[0];
-          ga += d * (double)p[1];
+        if (train) {
+          const double m = mx[(long)b * HW + q], v = avg[(long)b * HW + q];
+          gm -= sc[0] + (sc[1] * m + sc[2] * v + sc[3]);
+          ga -= sc[4] + (sc[5] * m + sc[6] * v + sc[7]);
         }
       }
-      // 8 lanes (k = 0..7) of pixel q: ((k0 + k1) + (k2 + k3)) + ((k4 + k5) + (k6 + k7))
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        gm += __shfl_xor(gm, o, 64);
-        ga += __shfl_xor(ga, o, 64);
-      }
-      if ((lane & 7) == 0) {
-        gq[ql] = (float)gm;
-        gq[QC + ql] = (float)(ga / (double)C);
-      }
+      gq[ql] = (float)gm;
+      gq[QC + ql] = (float)(ga / (double)C);
     }
     __syncthreads();
     // dx^T tiles: rows = channels (16 per tile), cols = pixels (16 per tile), k = tokens (4 per MFMA)
@@ -690,9 +708,12 @@ __global__ __launch_bounds__(256) void attn_mask(int B, int HW, int S, const flo
 
 static long tl_pix_partials(long M) { return (long)vc_cdiv(M, PS_ROWS) * NMOM; }
 
+// fp64 scratch of one TokenLearner call site: the pixel_stats moment partials, the per-(sample, token) backward
+// partials, and the backward's per-(sample, 16-token block, pixel) pixel-gradient partials
+static long tl_apart(int B, int HW, int S) { return (long)B * ((S + 15) / 16) * HW * 2; }
 VC_API int vc_tl_ws_floats(int B, int HW, int S) {
   if (B <= 0 || HW <= 0 || S <= 0) return -1;
-  const long dbl = tl_pix_partials((long)B * HW) + (long)B * S * NBS;
+  const long dbl = tl_pix_partials((long)B * HW) + (long)B * S * NBS + tl_apart(B, HW, S);
   return (int)(2 * dbl + 2);
 }
 
@@ -714,6 +735,7 @@ static size_t tl_fwd_lds(int HW, int S, int SC) {
   const int Lp = (HW + 15) & ~15;
   return 2 * (size_t)S * sizeof(double) + (size_t)((TL_CT + SC) * (Lp + 4) + 2 * Lp + S * TPAR) * sizeof(float);
 }
+constexpr size_t TL_BWD_STATIC = TLDX_RED * sizeof(double);   // tl_bwd_dx's `red`
 static size_t tl_bwd_lds(int S, int QC) {
   const int S4 = (S + 3) & ~3;
   return 12 * (size_t)S * sizeof(double) +
@@ -728,7 +750,7 @@ static int tl_fwd_sc(int HW, int S) {
 // the pixel chunk of tl_bwd_dx, alike
 static int tl_bwd_qc(int HW, int S) {
   for (int qc = (HW + 15) & ~15; qc >= 16; qc -= 16)
-    if (tl_bwd_lds(S, qc) <= TL_LDS_MAX) return qc;
+    if (tl_bwd_lds(S, qc) + TL_BWD_STATIC <= TL_LDS_MAX) return qc;
   return 0;
 }
 
@@ -753,20 +775,21 @@ VC_API int vc_tl_fwd(int train, int B, int HW, int C, int S, const float* x, lon
 }
 
 VC_API int vc_tl_bwd(int train, int B, int HW, int C, int S, const float* x, long ldx, const float* mx,
-                     const float* avg, const int* amx, const float* params, const double* stats, const float* dZ,
-                     float* da, double* ws, float* dx, long lddx, float* dparams, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && HW > 0 && C > 0 && C % 4 == 0 && ldx % 4 == 0 && S > 0 && ws && da && dx);
+                     const float* avg, const int* amx, const float* params, const double* stats, const float* a,
+                     const float* dZ, double* ws, float* dx, long lddx, float* dparams, hipStream_t stream) {
+  VC_REQUIRE(B > 0 && HW > 0 && C > 0 && C % 4 == 0 && ldx % 4 == 0 && S > 0 && ws && a && dx);
   VC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)dZ & 15) == 0);
   const int QC = tl_bwd_qc(HW, S);
   VC_REQUIRE(QC > 0);
   VC_REQUIRE_I32((long)B * HW * (S > C ? S : C));
   double* part = ws + tl_pix_partials((long)B * HW);
+  double* apart = part + (long)B * S * NBS;
   const int da_waves = std::min(TLDA_W, (HW + 15) / 16);
   hipLaunchKernelGGL(tl_bwd_da, dim3(B, vc_cdiv(S, 16)), dim3(64 * da_waves), 0, stream, B, HW, C, S, x, ldx, mx, avg, params,
-                     stats, dZ, da, part);
+                     stats, dZ, part, apart);
   VC_CHECK_LAUNCH();
   hipLaunchKernelGGL(tl_bwd_dx, dim3(B, vc_cdiv(C, TL_CT)), dim3(256), tl_bwd_lds(S, QC), stream, train, B, HW, C, S,
-                     QC, mx, avg, amx, params, stats, dZ, da, part, dx, lddx, dparams);
+                     QC, mx, avg, amx, params, stats, a, dZ, part, apart, dx, lddx, dparams);
   VC_CHECK_LAUNCH();
   return VC_OK;
 }

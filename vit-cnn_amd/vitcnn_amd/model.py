@@ -805,8 +805,10 @@ class _Program:
         self.L.vc_tl_pixel_stats(rows, C, X, C, mx, amx, avg, tlw, self.s)
         st = ws.get(pfx + ".st", 2 * S + 8, torch.float64).data_ptr()
         Z = ws.f(pfx + ".Z", B * S * C)
+        # the attention maps, kept for the backward's pooling product (training with grad only)
+        amap = ws.f(pfx + ".a", B * S * L_) if self.ws_grad else None
         self.L.vc_tl_fwd(self.train, B, L_, C, S, X, C, mx, avg, self.P[pfx + ".tokenizers.0.conv.0.weight"],
-                         self.BUF[pfx + ".tokenizers.0.conv.1.running_mean"], BN_EPS, BN_MOM, tlw, st, None, Z, self.s)
+                         self.BUF[pfx + ".tokenizers.0.conv.1.running_mean"], BN_EPS, BN_MOM, tlw, st, amap, Z, self.s)
         return Z
 
     def block(self, blk, pfx, X, H):
@@ -1163,10 +1165,10 @@ class _Program:
         B, ws = self.B, self.ws
         rows = B * L_
         st = ws.get(pfx + ".st", 2 * S + 8, torch.float64).data_ptr()
-        da = ws.f(pfx + ".da", B * S * L_)
         self.L.vc_tl_bwd(self.train, B, L_, C, S, X, C, ws.f(pfx + ".mx", rows), ws.f(pfx + ".avg", rows),
                          ws.get(pfx + ".amx", rows, torch.int32).data_ptr(), self.P[pfx + ".tokenizers.0.conv.0.weight"],
-                         st, dZ, da, self.tl_ws(pfx, L_, S), dX, C, self.G[pfx + ".tokenizers.0.conv.0.weight"], self.s)
+                         st, ws.f(pfx + ".a", B * S * L_), dZ, self.tl_ws(pfx, L_, S), dX, C,
+                         self.G[pfx + ".tokenizers.0.conv.0.weight"], self.s)
 
     def block_bwd(self, blk, pfx, X, H, dOut, dX, dx_ready):
         """dX (accumulated, beta=1) = gradient w.r.t. the block input, or None to skip input grads;
