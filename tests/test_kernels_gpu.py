@@ -769,3 +769,44 @@ def test_bn_bwd_relu_affine_is_bit_identical(L, ws, train, M, C):
     for o in outs[1:]:
         for a_, b_ in zip(outs[0], o):
             assert torch.equal(a_, b_)
+
+
+@pytest.mark.parametrize("flags", [0, F_BF16])
+@pytest.mark.parametrize("grouped", [False, True])
+def test_gemm_pipe_two_ktiles_per_stage_is_bit_identical(probe, ws, flags, grouped, monkeypatch):
+    """The pipelined GEMM with two 32-wide k-tiles per ring stage (VITCNN_PIPE_KM=2, probe library: one DMA wait and
+    barrier per 64 of K) == one k-tile per stage, bit for bit: alone and grouped, fp32 and bf16 MFMAs, with the
+    bias-gradient ones column, split-K slices of an odd number of k-tiles and a ragged K (the shapes force the
+    pipelined kernel with F_PIPE)"""
+    probs = GROUP_PROBLEMS_PIPE + [(0, 1, 3136, 256, 1296, 1, False, 0.0), (1, 0, 256, 144, 3136, 1, True, 0.0),
+                                   (0, 0, 200, 96, 100, 1, False, 0.5)]
+    ins = []
+    for i, (ta, tb, M, N, K, batch, bg, beta) in enumerate(probs):
+        A = (rnd(K, M, seed=150 + i) if ta else rnd(M, K, seed=150 + i)).to(DEV)
+        B = (rnd(N, K, seed=170 + i) if tb else rnd(K, N, seed=170 + i)).to(DEV)
+        ins.append((A, B))
+    grp = ctypes.create_string_buffer(GROUP_BYTES)
+    outs = []
+    for km in ("1", "2"):
+        monkeypatch.setenv("VITCNN_PIPE_KM", km)
+        res = []
+        if grouped:
+            probe.vc_gemm_group_begin(ctypes.addressof(grp), S())
+        for i, (ta, tb, M, N, K, batch, bg, beta) in enumerate(probs):
+            A, B = ins[i]
+            C = rnd(M, N, seed=190 + i).to(DEV)
+            bgr = torch.full((M,), 0.25, device=DEV) if bg else None
+            args = (ta, tb, M, N, K, 1.0, P(A), M if ta else K, 0, P(B), K if tb else N, 0, beta, P(C), N, 0, 1, None,
+                    None, 0, 0, flags | F_PIPE, P(bgr), P(ws), ws.numel(), None, 0)
+            if grouped:
+                probe.vc_gemm_group_add(ctypes.addressof(grp), *args)
+            else:
+                probe.vc_gemm_ex(*args, S())
+            res.append((C, bgr))
+        if grouped:
+            probe.vc_gemm_group_end(ctypes.addressof(grp))
+        torch.cuda.synchronize()
+        outs.append([(c.cpu(), b.cpu() if b is not None else None) for c, b in res])
+    for (c0, b0), (c1, b1) in zip(outs[0], outs[1]):
+        assert torch.equal(c0, c1)
+        assert b0 is None or torch.equal(b0, b1)

@@ -706,16 +706,22 @@ __device__ __forceinline__ void mma_ktile_bf(const char* As, const char* Bs, int
 // issue overlap the other's MFMAs (one wave per SIMD left the 16x16x4 issue idle ~half the time on a
 // one-block-per-CU grid); the halves' accumulators are g2's NC = 2 partials, summed acc0 + acc1 through
 // the idle ring before the epilogue, which the kh = 0 waves run.
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false, int KS = 1>
+//
+// KM = 2 (round 6): each ring stage holds two consecutive 32-wide k-tiles (two A and two B images), so the block
+// runs one DMA wait + barrier per 64 of K instead of per 32 -- the per-k-tile overhead, not the MFMAs, sets the
+// time of the step's latency-bound shapes (more so with bf16 MFMAs, 1/8 of the fp32 count).  Same MFMAs in the
+// same order: bit-identical to KM = 1.
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false, int KS = 1, int KM = 1>
 __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int xn, int ym, int tn, int tm, int G,
                                           char* smem) {
   constexpr int NWT = WM * WN;                  // waves per k-split half
   constexpr int NW = NWT * KS, NTH = 64 * NW;   // all waves (they share the DMA of a stage)
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int MT = WTM / 16, NT = WTN / 16;
-  constexpr int SA_B = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int LOADS = (BM / 8 + BN / 8) / NW;   // DMA wave-instructions per wave and stage
+  constexpr int SA_B = BM * 128, SUB = (BM + BN) * 128, STAGE = KM * SUB;
+  constexpr int LOADS = KM * (BM / 8 + BN / 8) / NW;   // DMA wave-instructions per wave and stage
   static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static_assert(KM == 1 || (KM == 2 && KS == 1), "two k-tiles per stage: without k-split waves");
   static_assert(KS == 1 || (KS == 2 && !BF), "k-split waves: fp32 only");
   static_assert(KS == 1 || NWT * MT * NT * 4 * 64 * 4 <= ring_bytes<BM, BN, NS>(), "partials fit the ring");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -742,12 +748,15 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[0][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = kend > kbeg ? (kend - kbeg + KT - 1) / KT : 0;
+  const int nk = kend > kbeg ? (kend - kbeg + KM * KT - 1) / (KM * KT) : 0;   // stages
   auto issue = [&](int t) {
-    char* st = smem + (t % NS) * STAGE;
-    const int k0 = kbeg + t * KT;
-    fill<TA, BM, NW>(ra, st, m0, k0, kend, g.lda, wave, lane);
-    fill<!TB, BN, NW>(rb, st + SA_B, n0, k0, kend, g.ldb, wave, lane);
+#pragma unroll
+    for (int u = 0; u < KM; ++u) {
+      char* st = smem + (t % NS) * STAGE + u * SUB;
+      const int k0 = kbeg + (t * KM + u) * KT;
+      fill<TA, BM, NW>(ra, st, m0, k0, kend, g.lda, wave, lane);
+      fill<!TB, BN, NW>(rb, st + SA_B, n0, k0, kend, g.ldb, wave, lane);
+    }
   };
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
@@ -764,19 +773,25 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");                          // no LDS read moves above the barrier
     if (t + NS - 1 < nk) issue(t + NS - 1);
-    const char* cur = smem + (t % NS) * STAGE;
     if (ones_col >= 0) {
-      if (tid < KT) {
-        const int k = kbeg + t * KT + tid;
-        *reinterpret_cast<float*>(const_cast<char*>(cur) + SA_B + SB::rc_off(tid, ones_col)) = k < kend ? 1.f : 0.f;
+      if (tid < KM * KT) {
+        const int u = tid / KT, kk = tid - u * KT;
+        const int k = kbeg + (t * KM + u) * KT + kk;
+        char* img = smem + (t % NS) * STAGE + u * SUB + SA_B;
+        *reinterpret_cast<float*>(img + SB::rc_off(kk, ones_col)) = k < kend ? 1.f : 0.f;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    if constexpr (BF) mma_ktile_bf<MT, NT, SA, SB>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc[0]);
-    else if constexpr (KS == 2) g2::mma_substep<MT, NT, SA, SB>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, kh, acc[0]);
-    else g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
+#pragma unroll
+    for (int u = 0; u < KM; ++u) {
+      if (KM > 1 && kbeg + (t * KM + u) * KT >= kend) break;   // a ragged last stage (uniform)
+      const char* cur = smem + (t % NS) * STAGE + u * SUB;
+      if constexpr (BF) mma_ktile_bf<MT, NT, SA, SB>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc[0]);
+      else if constexpr (KS == 2) g2::mma_substep<MT, NT, SA, SB>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, kh, acc[0]);
+      else g2::mma_ktile<false, MT, NT, SA, SB, 1>(cur, cur + SA_B, wm * WTM, wn * WTN, lane, acc);
+    }
   }
   if constexpr (KS == 2) {   // acc = sub-step-0 partial + sub-step-1 partial (g2's NC = 2 order)
     float* xch = reinterpret_cast<float*>(smem);   // [NWT][MT][NT][4][64]
@@ -890,13 +905,13 @@ __device__ __forceinline__ void pipe_tile(const GemmArgs& g, int zb, int zs, int
   if (tid == 0) __hip_atomic_store(&g.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false, int KS = 1>
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int NS, bool BF = false, int KS = 1, int KM = 1>
 __global__ __launch_bounds__(64 * WM * WN * KS) void gemm_pipe(GemmArgs g, int tn, int tm, unsigned total, int G,
                                                                 int zfast) {
-  __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS>()];
+  __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS, KM>()];
   int zs, xn, ym, zb;
   tile_coords(xcd_linear(blockIdx.x, total), g.nsplit, tn, tm, zfast, zs, xn, ym, zb);
-  pipe_tile<BM, BN, WM, WN, TA, TB, NS, BF, KS>(g, zb, zs, xn, ym, tn, tm, G, smem);
+  pipe_tile<BM, BN, WM, WN, TA, TB, NS, BF, KS, KM>(g, zb, zs, xn, ym, tn, tm, G, smem);
 }
 
 // Grouped launch: up to GROUP_MAX independent problems (any of the four layouts, a runtime switch) in one
@@ -910,9 +925,9 @@ struct PipeGroup {
 };
 
 // KS = 2: fp32 problems only (the host launches a group holding a bf16 problem with KS = 1).
-template <int BM, int BN, int WM, int WN, int NS, int KS = 1>
+template <int BM, int BN, int WM, int WN, int NS, int KS = 1, int KM = 1>
 __global__ __launch_bounds__(64 * WM * WN * KS) void gemm_pipe_group(PipeGroup P, unsigned total) {
-  __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS>()];
+  __shared__ __attribute__((aligned(1024))) char smem[ring_bytes<BM, BN, NS, KM>()];
   const unsigned lin = xcd_linear(blockIdx.x, total);
   int p = 0;
 #pragma unroll
@@ -933,17 +948,17 @@ __global__ __launch_bounds__(64 * WM * WN * KS) void gemm_pipe_group(PipeGroup P
   int zs, xn, ym, zb;
   tile_coords(lin - (unsigned)start, g.nsplit, tn, tm, 1, zs, xn, ym, zb);
   switch (variant) {   // 4 BF + 2 TA + TB
-    case 0: pipe_tile<BM, BN, WM, WN, false, false, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 1: pipe_tile<BM, BN, WM, WN, false, true, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 2: pipe_tile<BM, BN, WM, WN, true, false, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-    case 3: pipe_tile<BM, BN, WM, WN, true, true, NS, false, KS>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 0: pipe_tile<BM, BN, WM, WN, false, false, NS, false, KS, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 1: pipe_tile<BM, BN, WM, WN, false, true, NS, false, KS, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 2: pipe_tile<BM, BN, WM, WN, true, false, NS, false, KS, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+    case 3: pipe_tile<BM, BN, WM, WN, true, true, NS, false, KS, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
     default:
       if constexpr (KS == 1) {
         switch (variant) {
-          case 4: pipe_tile<BM, BN, WM, WN, false, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-          case 5: pipe_tile<BM, BN, WM, WN, false, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-          case 6: pipe_tile<BM, BN, WM, WN, true, false, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
-          default: pipe_tile<BM, BN, WM, WN, true, true, NS, true>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+          case 4: pipe_tile<BM, BN, WM, WN, false, false, NS, true, 1, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+          case 5: pipe_tile<BM, BN, WM, WN, false, true, NS, true, 1, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+          case 6: pipe_tile<BM, BN, WM, WN, true, false, NS, true, 1, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
+          default: pipe_tile<BM, BN, WM, WN, true, true, NS, true, 1, KM>(g, zb, zs, xn, ym, tn, tm, 1, smem); break;
         }
       }
       break;
@@ -1147,6 +1162,8 @@ static int pipe_bf_w8() { return vc_knob("VITCNN_PIPE_BF_W8", 1) ? 1 : 0; }
 // the same for fp32 tiles: equal or 1-5 % faster on every shape of the step, step 1.714 -> 1.690 ms
 // (profiles/r05_gemm_f32_w8.log; knob: probe library)
 static int pipe_f32_w8() { return vc_knob("VITCNN_PIPE_F32_W8", 1) ? 1 : 0; }
+// k-tiles per ring stage of the 8-wave 64 x 64 kernels (pipe_tile KM; knob: probe library)
+static int pipe_km() { return vc_knob("VITCNN_PIPE_KM", 1) == 2 ? 2 : 1; }
 
 // k-split waves (gp::pipe_tile KS = 2) for fp32 64 x 64 tiles.  Rule 0: where the grid is at most one block per CU
 // and K is long (the local 3x3 convs, M = B 49, K = 9 C: 34.1 -> 31.8 us; elsewhere equal or slower,
@@ -1211,41 +1228,44 @@ static int launch_pipe(int transA, int transB, int M, int N, int K, float alpha,
   // faster for every split shape of the step, tools/gemm_lab.hip; the in-launch combine reads its slabs there)
   const int zfast = 1;
   dim3 grid((unsigned)total);
-#define VC_GP(BM_, BN_, WM_, WN_, NS_, KS_)                                                                     \
+#define VC_GP(BM_, BN_, WM_, WN_, NS_, KS_, KM_)                                                                \
   do {                                                                                                           \
     const dim3 blk(64 * WM_ * WN_ * KS_);                                                                        \
     if (transA && transB)                                                                                        \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, true, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);   \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, true, NS_, false, KS_, KM_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);   \
     else if (transA)                                                                                             \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, false, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, true, false, NS_, false, KS_, KM_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
     else if (transB)                                                                                             \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, true, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, true, NS_, false, KS_, KM_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast);  \
     else                                                                                                         \
-      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, false, NS_, false, KS_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast); \
+      hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, false, false, NS_, false, KS_, KM_>), grid, blk, 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast); \
   } while (0)
 #define VC_GP_T(NS_)                                                \
   do {                                                              \
-    if (p.bm == 128 && p.bn == 64) VC_GP(128, 64, 4, 2, NS_, 1);     \
-    else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_, 1); \
-    else if (pipe_ks(tiles, p.nsplit, K) == 2) VC_GP(64, 64, 2, 2, NS_, 2); \
-    else if (pipe_f32_w8()) VC_GP(64, 64, 2, 4, NS_, 1);            \
-    else VC_GP(64, 64, 2, 2, NS_, 1);                               \
+    if (p.bm == 128 && p.bn == 64) VC_GP(128, 64, 4, 2, NS_, 1, 1);     \
+    else if (p.bm == 64 && p.bn == 128) VC_GP(64, 128, 2, 4, NS_, 1, 1); \
+    else if (pipe_ks(tiles, p.nsplit, K) == 2) VC_GP(64, 64, 2, 2, NS_, 2, 1); \
+    else if (pipe_f32_w8() && km == 2) VC_GP(64, 64, 2, 4, NS_, 1, 2);  \
+    else if (pipe_f32_w8()) VC_GP(64, 64, 2, 4, NS_, 1, 1);            \
+    else VC_GP(64, 64, 2, 2, NS_, 1, 1);                               \
   } while (0)
-#define VC_GPB(BM_, BN_, WM_, WN_, TA_, TB_, NS_) \
-  hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, TA_, TB_, NS_, true>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
-#define VC_GPB_L(BM_, BN_, WM_, WN_, NS_)                          \
-  do {                                                             \
-    if (transA && transB) VC_GPB(BM_, BN_, WM_, WN_, true, true, NS_); \
-    else if (transA) VC_GPB(BM_, BN_, WM_, WN_, true, false, NS_);     \
-    else if (transB) VC_GPB(BM_, BN_, WM_, WN_, false, true, NS_);     \
-    else VC_GPB(BM_, BN_, WM_, WN_, false, false, NS_);                \
+#define VC_GPB(BM_, BN_, WM_, WN_, TA_, TB_, NS_, KM_) \
+  hipLaunchKernelGGL((gp::gemm_pipe<BM_, BN_, WM_, WN_, TA_, TB_, NS_, true, 1, KM_>), grid, dim3(64 * WM_ * WN_), 0, stream, g, p.tn, p.tm, (unsigned)total, G, zfast)
+#define VC_GPB_L(BM_, BN_, WM_, WN_, NS_, KM_)                          \
+  do {                                                                  \
+    if (transA && transB) VC_GPB(BM_, BN_, WM_, WN_, true, true, NS_, KM_); \
+    else if (transA) VC_GPB(BM_, BN_, WM_, WN_, true, false, NS_, KM_);     \
+    else if (transB) VC_GPB(BM_, BN_, WM_, WN_, false, true, NS_, KM_);     \
+    else VC_GPB(BM_, BN_, WM_, WN_, false, false, NS_, KM_);                \
   } while (0)
+  const int km = pipe_km();
   if (bf) {   // tiles other than 64 x 64 / 2 stages: measurement knobs (probe library)
-    if (p.bm == 128 && p.bn == 64) VC_GPB_L(128, 64, 4, 2, 2);
-    else if (p.bm == 64 && p.bn == 128) VC_GPB_L(64, 128, 2, 4, 2);
-    else if (p.ns == 4) VC_GPB_L(64, 64, 2, 2, 4);
-    else if (pipe_bf_w8()) VC_GPB_L(64, 64, 2, 4, 2);
-    else VC_GPB_L(64, 64, 2, 2, 2);
+    if (p.bm == 128 && p.bn == 64) VC_GPB_L(128, 64, 4, 2, 2, 1);
+    else if (p.bm == 64 && p.bn == 128) VC_GPB_L(64, 128, 2, 4, 2, 1);
+    else if (p.ns == 4) VC_GPB_L(64, 64, 2, 2, 4, 1);
+    else if (pipe_bf_w8() && km == 2) VC_GPB_L(64, 64, 2, 4, 2, 2);
+    else if (pipe_bf_w8()) VC_GPB_L(64, 64, 2, 4, 2, 1);
+    else VC_GPB_L(64, 64, 2, 2, 2, 1);
   } else if (p.ns == 4) VC_GP_T(4);
   else VC_GP_T(2);
 #undef VC_GPB_L
@@ -1357,6 +1377,9 @@ static int group_flush(GroupState& st) {
     if (!any_bf && vc_knob("VITCNN_PIPE_KS", 0) == 2)   // (grouped problems: measured no gain)
       hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 2, 2, 2>), dim3((unsigned)total), dim3(512), 0, st.stream, P,
                          (unsigned)total);
+    else if (((any_bf && pipe_bf_w8()) || (!any_bf && pipe_f32_w8())) && pipe_km() == 2)   // 8 waves, 2 k-tiles
+      hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 4, 2, 1, 2>), dim3((unsigned)total), dim3(512), 0, st.stream,
+                         P, (unsigned)total);
     else if ((any_bf && pipe_bf_w8()) || (!any_bf && pipe_f32_w8()))   // 8 waves of 32 x 16
       hipLaunchKernelGGL((gp::gemm_pipe_group<64, 64, 2, 4, 2>), dim3((unsigned)total), dim3(512), 0, st.stream, P,
                          (unsigned)total);

@@ -282,8 +282,8 @@ __device__ __forceinline__ void fill(__amdgpu_buffer_rsrc_t r, char* img, int ro
   }
 }
 
-template <int BM, int BN, int NS>
-constexpr int ring_bytes() { return NS * (BM + BN) * 128; }
+template <int BM, int BN, int NS, int KM = 1>
+constexpr int ring_bytes() { return NS * KM * (BM + BN) * 128; }
 
 // 1-D grid in XCD-aware order (g2::gemm_mfma): block i runs on XCD i % 8, each XCD gets a contiguous
 // run of logical blocks -- with zfast the K slices of a tile side by side
