@@ -128,9 +128,13 @@ def _s2eft_worker(rank, world, port, out):
     sl = slice(rank * 2, rank * 2 + 2)
     x, t, w = torch.from_numpy(z["x"])[sl], torch.from_numpy(z["target"])[sl], torch.from_numpy(z["weight"])
     _, _, g = O.train_step(sd, x, t, w)
-    m.flat_params.grad = torch.cat([g[n].reshape(-1) for n in m._poff])
+    fl = torch.zeros(m.flat_params.numel())   # the model's flat layout (16-B aligned parameters, zero gaps)
+    for n, o in m._poff.items():
+        fl[o:o + g[n].numel()] = g[n].reshape(-1)
+    m.flat_params.grad = fl
     parallel.allreduce_gradients(m, opt)
-    out[rank] = (m.flat_params.grad.clone() * opt.grad_scale, opt.grad_scale)
+    G = m.flat_params.grad * opt.grad_scale
+    out[rank] = (torch.cat([G[o:o + g[n].numel()] for n, o in m._poff.items()]), opt.grad_scale)
     dist.destroy_process_group()
 
 
