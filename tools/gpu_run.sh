@@ -22,7 +22,8 @@ for s in "$@"; do
     tests:*) step test 1100 python -u -m pytest ${s#tests:} -s -v -rf --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench:*) step bench 600 python bench.py ${s#bench:} ;;
-    prof:*) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python bench.py ${s#prof:} &&
-            python tools/rocprof_summary.py gpurun_out/prof_$TAG > gpurun_out/prof_summary_$TAG.md 2>&1 ;;
+    # the trace database stays on the box (/tmp): only its summary comes back under gpurun_out/ (<= 64 MiB)
+    prof:*) step prof 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG -o run -- python bench.py ${s#prof:} &&
+            python tools/rocprof_summary.py /tmp/prof_$TAG > gpurun_out/prof_summary_$TAG.md 2>&1 ;;
   esac
 done
