@@ -594,9 +594,11 @@ int launch_conv_pipe(TapArgs& a, int grid_n, float* ws, long ws_floats, hipStrea
   const int tm = vc_cdiv(a.M, CP_B);
   const long tiles = (long)grid_n * tm;
   int nsplit = 1;
-  // grids smaller than this split K (knobs; per direction)
+  // grids smaller than this split K (knobs; per direction).  Forward / data gradient 512, weight gradient 1024:
+  // FusAtNet's B=64 step 17.20 -> 17.07 ms against 1024 for all three (profiles/r06_ab_conv_pipe_tiles.log)
   static const char* const knob[3] = {"VITCNN_CONV_PIPE_TILES_F", "VITCNN_CONV_PIPE_TILES_W", "VITCNN_CONV_PIPE_TILES_D"};
-  const long below = vc_knob(knob[MODE], 1024);
+  static const long below_default[3] = {512, 1024, 512};
+  const long below = vc_knob(knob[MODE], below_default[MODE]);
   if (ws && tiles < below)
     nsplit = (int)std::max<long>(1, std::min<long>(std::min<long>((4 * below + tiles - 1) / tiles, a.nk / 4), 64));
   while (nsplit > 1 && (long)nsplit * a.M * a.N > ws_floats) --nsplit;
