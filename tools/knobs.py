@@ -18,7 +18,7 @@ PROBE_PATH = os.path.join(_REPO, "vit-cnn_amd", "vitcnn_amd", "libvitcnn_probe.s
 PROBE_KNOBS = ("VITCNN_NL_LEGACY", "VITCNN_C2I_LDS", "VITCNN_TAP_NOSPLIT", "VITCNN_BN_PCAP", "VITCNN_BN_APPLY_ROWS", "VITCNN_BN_IM2COL",
                "VITCNN_BN_GLF", "VITCNN_SCAN_RBS", "VITCNN_SCAN_SELECT_RS", "VITCNN_SCAN_TAIL",
                "VITCNN_SPLITK_COMBINE", "VITCNN_LEGACY_COMBINE", "VITCNN_GEMM_PD", "VITCNN_GEMM_PIPE", "VITCNN_GEMM_PIPE_SMALL",
-               "VITCNN_PIPE_NS", "VITCNN_PIPE_KS", "VITCNN_PIPE_BF_W8", "VITCNN_PIPE_F32_W8", "VITCNN_PIPE_SPLIT_BLOCKS", "VITCNN_PIPE_SPLIT_BELOW", "VITCNN_PIPE_KM", "VITCNN_GEMM_GROUP_MAXB",
+               "VITCNN_PIPE_NS", "VITCNN_PIPE_KS", "VITCNN_PIPE_BF_W8", "VITCNN_PIPE_F32_W8", "VITCNN_PIPE_SPLIT_BLOCKS", "VITCNN_PIPE_SPLIT_BELOW", "VITCNN_PIPE_SPLIT_FILL", "VITCNN_PIPE_KM", "VITCNN_GEMM_GROUP_MAXB",
                "VITCNN_TAP_TARGET", "VITCNN_TAP_PIPE", "VITCNN_CONV_PIPE_TILES_F", "VITCNN_CONV_PIPE_TILES_W",
                "VITCNN_CONV_PIPE_TILES_D", "VITCNN_CONV_PIPE_W8", "VITCNN_ATTN_BWD_WPB", "VITCNN_ATTN_FWD_WPB")
 

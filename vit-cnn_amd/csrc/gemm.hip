@@ -1194,8 +1194,28 @@ static PipePlan plan_pipe(int M, int Ne, int K, long ws_floats, bool have_ws, bo
   const int kt = vc_cdiv(K, gp::KT);
   int nsplit = 1;
   const long target = vc_knob("VITCNN_PIPE_SPLIT_BLOCKS", 512);   // blocks a split aims at (knob: probe library)
-  if (have_ws && tiles < vc_knob("VITCNN_PIPE_SPLIT_BELOW", 128))   // (knob: probe library)
-    nsplit = (int)std::max<long>(1, std::min<long>(std::min<long>((target + tiles - 1) / tiles, kt / 4), 64));
+  if (have_ws && tiles < vc_knob("VITCNN_PIPE_SPLIT_BELOW", 128)) {   // (knob: probe library)
+    const int cap = (int)std::max<long>(1, std::min<long>(kt / 4, 64));
+    const int n0 = (int)std::max<long>(1, std::min<long>((target + tiles - 1) / tiles, cap));
+    nsplit = n0;
+    // round 6: of the splits n0 .. 2 n0, the one whose grid fills whole rounds of the 256 CUs best (the slices
+    // after rounding to k-tiles; ties: fewer slabs), e.g. 84 tiles: 9 slices = 756 blocks, not 7 = 588 (ViT-CNN
+    // step -0.011 ms median of 6).  Only for modest splits (n0 <= 16, grids of >= 32 tiles): the deep splits of
+    // tiny grids (S2EFT's weight gradients, K = 9344) lost ~1 % with more slabs (profiles/r06_ab_split_fill.log)
+    if (vc_knob("VITCNN_PIPE_SPLIT_FILL", 1) && n0 <= 16) {
+      constexpr long NCU = 256;
+      double best = -1.0;
+      for (int n = n0; n <= std::min(2 * n0, cap); ++n) {
+        const int kc = vc_cdiv(vc_cdiv(K, n), gp::KT) * gp::KT;
+        const long blocks = tiles * vc_cdiv(K, kc);
+        const double fill = (double)blocks / (double)(vc_cdiv(blocks, NCU) * NCU);
+        if (fill > best + 1e-9) {
+          best = fill;
+          nsplit = n;
+        }
+      }
+    }
+  }
   if (g_tune.nsplit) nsplit = std::min(g_tune.nsplit, std::max(1, kt));
   while (nsplit > 1 && (long)nsplit * M * Ne > ws_floats) --nsplit;
   p.k_chunk = kt * gp::KT;
