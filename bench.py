@@ -237,7 +237,6 @@ def dominant_kernel_roofline(model, batch, reps):
     P = prog.P
     order = prog.tab[("order", H)].data_ptr()
     ckpt = L.vc_mamba_scan_ckpt_floats(batch, Lt, D, NDIR)
-    PP = D * R + D + XW * D   # the tail's dt_proj / x_proj weight-gradient partials per sequence (round 6)
     stream = torch.cuda.current_stream(dev)
 
     def fn():
@@ -247,12 +246,12 @@ def dominant_kernel_roofline(model, batch, reps):
                                   P[mx + ".A_log"], P[mx + ".D"], P[gv + ".weights"], f(pfx + ".Y", nr * D),
                                   f(pfx + ".dYP", rows * D), f(pfx + ".CKP", ckpt), f(pfx + ".dU", nr * D),
                                   f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW),
-                                  f(pfx + ".convpart", nseq * 5 * D), f(pfx + ".projpart", nseq * PP), None, None,
-                                  None, prog.scr_p, prog.scr_n, stream.cuda_stream)
+                                  f(pfx + ".convpart", nseq * 5 * D), None, None, None, prog.scr_p, prog.scr_n,
+                                  stream.cuda_stream)
 
     t = time_kernel(fn, reps, stream)
     reads = nr * D + nr * XW + nr * D + rows * D + rows * D + ckpt
-    writes = nr * D + nr * XW + nr * D + nseq * 5 * D + nseq * (D * 16 + D + 1) + nseq * PP
+    writes = nr * D + nr * XW + nr * D + nseq * 5 * D + nseq * (D * 16 + D + 1)
     algo = 4.0 * (reads + writes)
     achieved = algo / t / 1e9
     key = "scan_bwd<9, true, true>"

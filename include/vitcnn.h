@@ -324,26 +324,20 @@ VC_API int vc_mamba_scan_fwd_fused(int B, int L, int D, int R, int ndir, const f
 /* vc_mamba_scan_bwd followed, per sequence, by the dt_proj / x_proj data gradients and the conv1d + SiLU
  * backward (modeling_mamba.py:433-456 backward): dxdbl complete (all R+32 columns), dpre = d(conv
  * pre-activation) [ndir*B*L, D], ddt_lin and the scan parameter outputs as vc_mamba_scan_bwd, conv_part
- * [ndir*B][5D] the per-sequence conv weight / bias partials (reduce with vc_mamba_conv_params).  proj_part
- * (optional, round 6) [ndir*B][D*R + D + (R+32)*D]: the per-sequence dt_proj weight / bias and x_proj weight
- * gradient partials (reduce with vc_mamba_proj_params), which replace the two weight-gradient GEMMs over
- * ndir*B*L rows.  ckpt required.  The x half of dxz then comes from vc_mamba_dirconv_bwd_gather. */
+ * [ndir*B][5D] the per-sequence conv weight / bias partials (reduce with vc_mamba_conv_params).  ckpt
+ * required.  The x half of dxz then comes from vc_mamba_dirconv_bwd_gather. */
 VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const float* u, const float* xdbl,
                                    const int* order, const float* xz, const float* conv_w, const float* conv_b,
                                    const float* x_proj_w, const float* dt_w, const float* dt_b, const float* A_log,
                                    const float* Dskip, const float* gate_logits, const float* yp, const float* dyp,
                                    const float* ckpt, float* dpre, float* ddt_lin, float* dxdbl, float* conv_part,
-                                   float* proj_part, float* dA_log, float* dDskip, float* dgate_logits, float* ws,
-                                   long ws_floats, hipStream_t stream);
+                                   float* dA_log, float* dDskip, float* dgate_logits, float* ws, long ws_floats,
+                                   hipStream_t stream);
 VC_API int vc_mamba_dirconv_bwd_gather(int B, int L, int D, int ndir, const int* inv_order, const float* conv_w,
                                        const float* dpre, float* dxz, hipStream_t stream);
 /* conv1d weight [D,1,4] / bias [D] gradients (overwritten) from vc_mamba_scan_bwd_fused's partials */
 VC_API int vc_mamba_conv_params(int B, int D, int ndir, const float* conv_part, float* dconv_w, float* dconv_b,
                                 hipStream_t stream);
-/* dt_proj weight [D,R] / bias [D] and x_proj weight [R+32, D] gradients (overwritten) from
- * vc_mamba_scan_bwd_fused's proj_part (R <= 16) */
-VC_API int vc_mamba_proj_params(int B, int D, int R, int ndir, const float* proj_part, float* ddt_w, float* ddt_b,
-                                float* dx_proj_w, hipStream_t stream);
 
 /* ---------------------------------------------------------------- hsiMamba row chains
  * Two projections with a LayerNorm between them for 32-row blocks in one launch (rowchain.hip), fp32:

@@ -123,15 +123,14 @@ def test_mamba_fused_vs_float64(L, D, E):
     dU, dDTL = (torch.full((rows, D), float("nan"), device=DEV) for _ in range(2))
     dXD = torch.full((rows, XW), float("nan"), device=DEV)
     CP = torch.full((ndir * B * 5 * D,), float("nan"), device=DEV)
-    PPt = torch.full((ndir * B * (D * R + D + XW * D),), float("nan"), device=DEV)
     dXZ = torch.full((B * L, 2 * D), float("nan"), device=DEV)
     dYP = torch.empty(B * L, D, device=DEV)
     dA, dDs, dG = torch.empty(D, N, device=DEV), torch.empty(D, device=DEV), torch.empty(ndir, device=DEV)
     lib.vc_mamba_gate_bwd(B, L, D, P(c["xz"]), P(YP), P(c["dys"]), P(dYP), P(dXZ), s)
     assert lib.vc_mamba_scan_bwd_fused(B, L, D, R, ndir, P(U), P(XD), P(c["o32"]), P(c["xz"]), P(c["cw"]), P(c["cb"]),
                                        P(c["wx"]), P(c["wdt"]), P(c["bdt"]), P(c["alog"]), P(c["dsk"]), P(c["gate"]),
-                                       P(Y), P(dYP), P(CKP), P(dU), P(dDTL), P(dXD), P(CP), P(PPt), P(dA), P(dDs), P(dG),
-                                       P(ws), ws.numel(), s) == 0
+                                       P(Y), P(dYP), P(CKP), P(dU), P(dDTL), P(dXD), P(CP), P(dA), P(dDs), P(dG), P(ws),
+                                       ws.numel(), s) == 0
     lib.vc_mamba_dirconv_bwd_gather(B, L, D, ndir, P(c["inv32"]), P(c["cw"]), P(dU), P(dXZ), s)
     dCW, dCB = torch.empty(D, 4, device=DEV), torch.empty(D, device=DEV)
     lib.vc_mamba_conv_params(B, D, ndir, P(CP), P(dCW), P(dCB), s)
@@ -140,16 +139,9 @@ def test_mamba_fused_vs_float64(L, D, E):
                 P(dbdt), P(ws), ws.numel(), s)
     lib.vc_gemm(1, 0, XW, D, rows, 1.0, P(dXD), XW, 0, P(U), D, 0, 0.0, P(dWx), D, 0, 1, None, None, 0, 0, 0, None,
                 P(ws), ws.numel(), s)
-    # the tail's per-sequence dt_proj / x_proj weight-gradient partials (round 6), reduced
-    pWdt, pbdt, pWx = torch.empty(D, R, device=DEV), torch.empty(D, device=DEV), torch.empty(XW, D, device=DEV)
-    assert lib.vc_mamba_proj_params(B, D, R, ndir, P(PPt), P(pWdt), P(pbdt), P(pWx), s) == 0
     torch.cuda.synchronize()
     errs = _grad_errs([dXZ, dCW, dCB, dWx, dWdt, dbdt, dA, dDs, dG], c["leaves"])
     assert max(errs.values()) < 1e-4, errs
-    perrs = _grad_errs([dXZ, dCW, dCB, pWx, pWdt, pbdt, dA, dDs, dG], c["leaves"])
-    assert max(perrs.values()) < 1e-4, perrs
-    for a_, b_ in ((pWdt, dWdt), (pbdt, dbdt), (pWx, dWx)):   # the same sums in another order: fp32 rounding apart
-        assert float((a_ - b_).abs().max() / b_.abs().max()) < 1e-5
 
 
 @pytest.mark.parametrize("L,D,E,use_ckpt", [(81, 72, 144, True), (49, 128, 256, True), (81, 72, 144, False),

@@ -93,7 +93,7 @@ def main():
 
         def scan_bwd_fused():
             L.vc_mamba_scan_bwd_fused(B, Lt, D, R, NDIR, U, XD, order, XZ, cw, cb, wx, wdt, bdt, alog, dsk, gl, Y, dYP,
-                                      CKP, dU, dDTL, dXD, CP, None, None, None, None, wsp, wsn, s)
+                                      CKP, dU, dDTL, dXD, CP, None, None, None, wsp, wsn, s)
 
         def tail_mask(mask):   # measurement only: parts of the tail skipped (VITCNN_SCAN_TAIL bits)
             def fn():

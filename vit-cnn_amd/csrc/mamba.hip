@@ -524,11 +524,6 @@ __device__ __forceinline__ float reduce_scatter8_row_bm(const float (&v)[8]) {
 //   (c) dpre = du SiLU'(pre), pre recomputed from the 4 gathered taps (dirconv_fwd_run's fma order; xz is
 //       L2-resident), written to HBM; the sequence's conv weight / bias partials [nseq][5D]
 //       (c*4 + j | 4D + c), summed over its tokens in a fixed order.
-//   (d) (round 6, proj_part given) the sequence's dt_proj / x_proj weight-gradient partials, k = token on
-//       v_mfma_f32_16x16x4_f32: dW_dt[c, j] = sum_t ddtl[t, c] xr[t, j] (+ the bias sum_t ddtl[t, c]) and
-//       dW_x[j', c] = sum_t dxdbl[t, j'] u[t, c], with dxdbl = [dxr | dB | dC] read from the three LDS images
-//       (a, b, c left) -- the two long-K (10 B L rows) weight-gradient GEMMs become per-sequence partials
-//       [nseq][D R | D | XW D] and one row sum (vc_mamba_proj_params).
 // Global operands are issued ahead of their MFMAs (W_x fragments once per wave, the gathered taps for
 // two token tiles at a time).  In (b) / (c) wave w owns channels 16 w .. 16 w + 15, so a channel's conv
 // partials never leave its wave.  Needs R <= 16.
@@ -540,7 +535,6 @@ struct FusedBwd {
   float* conv_part;      // [nseq][5D] out
   int tail;              // 7 (all); measurement masks (VITCNN_SCAN_TAIL, results incomplete): bit 0 the
                          // tail at all, bit 1 phase (a), bit 2 phases (b) + (c)
-  float* proj_part;      // [nseq][D R + D + XW D] out (phase d), or null
 };
 
 struct ScanBwdOut {
@@ -709,55 +703,6 @@ __device__ __forceinline__ void fused_bwd_tail(const ScanArgs& a, const FusedBwd
     for (int e = 0; e < 4; ++e) cp[dl * 4 + e] = cacc[e];
     cp[4 * D + dl] = cacc[4];
   }
-  if (!fb.proj_part) return;
-  // (d) no barrier: (b) / (c) wrote only HBM and du (dts), and (d) reads the dxr / dB / dC / xr images.  Wave w owns
-  // channels c = 16 w + r: rows of dW_dt (A = ddtl rows, B = xr), columns of dW_x (A = the dxdbl images, B = u rows)
-  const float* drow = o.ddtl + base * D;
-  const float* urow = a.u + base * D;
-  f32x4 adt = {0.f, 0.f, 0.f, 0.f};
-  f32x4 ax[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  float bsum = 0.f;
-  const int nks = Lp / 4;
-  constexpr int KB = 7;   // k-steps whose global operands are loaded together
-  for (int k0 = 0; k0 < nks; k0 += KB) {
-    float av[KB], bv[KB];
-#pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      const int t = 4 * (k0 + u) + g;
-      const bool ok = dok && k0 + u < nks && t < L;
-      av[u] = ok ? drow[(long)t * D + dl] : 0.f;
-      bv[u] = ok ? urow[(long)t * D + dl] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      if (k0 + u >= nks) break;
-      const int t = 4 * (k0 + u) + g;
-      bsum += av[u];
-      adt = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], r < R ? m.xr[t * R + r] : 0.f, adt, 0, 0, 0);
-      ax[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(DX16[t * 16 + r], bv[u], ax[0], 0, 0, 0);
-      ax[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(m.Bs[t * NST + r], bv[u], ax[1], 0, 0, 0);
-      ax[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(m.Cs[t * NST + r], bv[u], ax[2], 0, 0, 0);
-    }
-  }
-  bsum = cross_row_sum(bsum);
-  float* pp = fb.proj_part + (long)s * (D * R + D + XW * D);
-  // dW_dt [D][R]: this lane's rows c = 16 w + 4 g + i, column j = r; the bias after it
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = 16 * wave + 4 * g + i;
-    if (c < D && r < R) pp[c * R + r] = adt[i];
-  }
-  if (g == 0 && dok) pp[D * R + dl] = bsum;
-  // dW_x [XW][D]: rows j' = 4 g + i of chunk kc (dt-rank columns < R, then B, then C), column c = dl
-  float* px = pp + D * R + D;
-#pragma unroll
-  for (int kc = 0; kc < 3; ++kc)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int jl = 4 * g + i;
-      const int j = kc == 0 ? jl : R + 16 * (kc - 1) + jl;
-      if (dok && (kc > 0 || jl < R)) px[j * D + dl] = ax[kc][i];
-    }
 }
 
 template <int RT, bool BM, bool FUSE>
@@ -1307,12 +1252,12 @@ VC_API int vc_mamba_scan_bwd_fused(int B, int L, int D, int R, int ndir, const f
                                    const float* x_proj_w, const float* dt_w, const float* dt_b, const float* A_log,
                                    const float* Dskip, const float* gate_logits, const float* y, const float* dyp,
                                    const float* ckpt, float* dpre, float* ddt_lin, float* dxdbl, float* conv_part,
-                                   float* proj_part, float* dA_log, float* dDskip, float* dgate_logits, float* ws,
-                                   long ws_floats, hipStream_t stream) {
+                                   float* dA_log, float* dDskip, float* dgate_logits, float* ws, long ws_floats,
+                                   hipStream_t stream) {
   VC_REQUIRE(xz && conv_w && conv_b && x_proj_w && conv_part);
   VC_REQUIRE_I32((long)B * L * 2 * D);
   // tail phase mask: 7 = every phase (the product); the probe library's knob SCAN_TAIL times phases alone
-  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part, (int)vc_knob("VITCNN_SCAN_TAIL", 7), proj_part};
+  const FusedBwd fb{xz, conv_w, conv_b, x_proj_w, conv_part, (int)vc_knob("VITCNN_SCAN_TAIL", 7)};
   return scan_bwd_impl(B, L, D, R, ndir, u, xdbl, order, dt_w, dt_b, A_log, Dskip, gate_logits, y, dyp, ckpt, dpre,
                        ddt_lin, dxdbl, dA_log, dDskip, dgate_logits, ws, ws_floats, &fb, stream);
 }
@@ -1363,45 +1308,6 @@ VC_API int vc_mamba_conv_params(int B, int D, int ndir, const float* conv_part, 
   const int rc = launch_sum_rows(nseq, 4 * D, conv_part, 5L * D, 0L, dconv_w, 0.f, stream);
   if (rc) return rc;
   return launch_sum_rows(nseq, D, conv_part, 5L * D, 4L * D, dconv_b, 0.f, stream);
-}
-
-// sum_rows_kernel's fixed-order column sums over P partial rows of C columns, the columns scattered to three
-// outputs: [0, n0) -> o0, [n0, n0 + n1) -> o1, the rest -> o2 (one launch for the three parameter tensors)
-static __global__ __launch_bounds__(256) void sum_rows3(int P, int C, const float* __restrict__ part, int n0, int n1,
-                                                        float* __restrict__ o0, float* __restrict__ o1,
-                                                        float* __restrict__ o2) {
-  __shared__ float sh[16][17];
-  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  float s = 0.f;
-  if (c < C) {
-#pragma unroll 4
-    for (int p = pl; p < P; p += 16) s += part[(long)p * C + c];
-  }
-  sh[pl][cl] = s;
-  __syncthreads();
-  if (pl == 0 && c < C) {
-    float v = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v += sh[i][cl];
-    if (c < n0) o0[c] = v;
-    else if (c < n0 + n1) o1[c - n0] = v;
-    else o2[c - n0 - n1] = v;
-  }
-}
-
-// dt_proj weight [D,R] / bias [D] and x_proj weight [R+32, D] gradients (overwritten) from vc_mamba_scan_bwd_fused's
-// per-sequence partials (proj_part [ndir*B][D R + D + (R+32) D]): one fixed-order row sum
-VC_API int vc_mamba_proj_params(int B, int D, int R, int ndir, const float* proj_part, float* ddt_w, float* ddt_b,
-                                float* dx_proj_w, hipStream_t stream) {
-  VC_REQUIRE(B > 0 && D > 0 && R > 0 && R <= 16 && ndir > 0 && proj_part && ddt_w && ddt_b && dx_proj_w);
-  const int nseq = ndir * B;
-  const long pp = (long)D * R + D + (long)(R + 2 * NST) * D;
-  VC_REQUIRE_I32(pp);
-  hipLaunchKernelGGL(sum_rows3, dim3((unsigned)vc_cdiv(pp, 16)), dim3(256), 0, stream, nseq, (int)pp, proj_part,
-                     D * R, D, ddt_w, ddt_b, dx_proj_w);
-  VC_CHECK_LAUNCH();
-  return VC_OK;
 }
 
 // The parameter-gradient reductions of vc_mamba_scan_bwd, run separately (later, or on another

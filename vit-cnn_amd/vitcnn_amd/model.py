@@ -39,7 +39,6 @@ BN_EPS = 1e-5
 BN_MOM = 0.1
 NDIR = 10
 N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
-_SCAN_PROJ_PARTIALS = True   # dt_proj / x_proj weight gradients from the scan backward's per-sequence partials
 WGRAD_LANE = 2             # backward: lane 0's deferred weight gradients (lane 2 is idle after the forward)
 WGRAD1_LANE = 3            # backward: lane 1's deferred weight gradients (lane 3: after the fusion1 / LiDAR chain)
 # Program switches.  Module constants -- the product reads no environment: each selects between two
@@ -1332,7 +1331,6 @@ class _Program:
         dU, dDTL, dXD, dXZ = f(pfx + ".dU", nr * D), f(pfx + ".dDTL", nr * D), f(pfx + ".dXD", nr * XW), f(
             pfx + ".dXZ", rows * 2 * D)
         CP = f(pfx + ".convpart", nseq * 5 * D)
-        PPt = f(pfx + ".projpart", nseq * (D * R + D + XW * D)) if _SCAN_PROJ_PARTIALS and R <= 16 else None
         defer = self._deferring(True)
         spn = nseq * D * 16 + nseq * D + nseq
         sp = f(pfx + ".scanpart", spn) if defer else self.scr_p
@@ -1341,29 +1339,22 @@ class _Program:
         self.L.vc_mamba_scan_bwd_fused(B, L_, D, R, NDIR, U, XD, order, XZ, P[mx + ".conv1d.weight"],
                                        P[mx + ".conv1d.bias"], P[mx + ".x_proj.weight"], P[mx + ".dt_proj.weight"],
                                        P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], gl, Y, dYP, CKPb, dU,
-                                       dDTL, dXD, CP, PPt, None if defer else ga, None if defer else gd,
+                                       dDTL, dXD, CP, None if defer else ga, None if defer else gd,
                                        None if defer else gg, sp, spn, self.s)
         if defer:
             self.pending_wgrads.append(
                 lambda: self.L.vc_mamba_scan_bwd_params(B, D, NDIR, gl, sp, ga, gd, gg, self.scr_p, self.scr_n,
                                                         self.s))
         self.L.vc_mamba_dirconv_bwd_gather(B, L_, D, NDIR, inv, P[mx + ".conv1d.weight"], dU, dXZ, self.s)
-        # parameter gradients: dt_proj (dDTL, XD's dt-rank columns), x_proj (dXD, U) -- the scan tail's
-        # per-sequence partials (round 6) or two GEMMs over the nr rows --, conv1d (partials)
+        # parameter gradients: dt_proj (dDTL, XD's dt-rank columns), x_proj (dXD, U), conv1d (partials)
+        self.defer_wgrad(True, D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, G[mx + ".dt_proj.bias"])
+        self.defer_wgrad(True, XW, D, nr, dXD, XW, U, D, G[mx + ".x_proj.weight"], D)
         cw, cb = G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"]
-        dtw, dtb, dxw = G[mx + ".dt_proj.weight"], G[mx + ".dt_proj.bias"], G[mx + ".x_proj.weight"]
-        if PPt is None:
-            self.defer_wgrad(True, D, R, nr, dDTL, D, XD, XW, dtw, R, dtb)
-            self.defer_wgrad(True, XW, D, nr, dXD, XW, U, D, dxw, D)
-
-        def params():
-            self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s)
-            if PPt is not None:
-                self.L.vc_mamba_proj_params(B, D, R, NDIR, PPt, dtw, dtb, dxw, self.s)
+        conv = lambda: self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s)  # noqa: E731
         if defer:
-            self.pending_wgrads.append(params)
+            self.pending_wgrads.append(conv)
         else:
-            params()
+            conv()
 
     def _chain_ok(self, blk):
         """the row-chain launches apply to this block's widths (rowchain.hip limits)"""
