@@ -338,6 +338,12 @@ VC_API int vc_mamba_dirconv_bwd_gather(int B, int L, int D, int ndir, const int*
 /* conv1d weight [D,1,4] / bias [D] gradients (overwritten) from vc_mamba_scan_bwd_fused's partials */
 VC_API int vc_mamba_conv_params(int B, int D, int ndir, const float* conv_part, float* dconv_w, float* dconv_b,
                                 hipStream_t stream);
+/* vc_mamba_scan_bwd_params and vc_mamba_conv_params in ONE launch (round 6): dA_log, D, the gate logits and the
+ * conv1d weight / bias gradients (all overwritten) from a deferred vc_mamba_scan_bwd_fused's partials (ws) and
+ * conv_part; ndir <= 64 */
+VC_API int vc_mamba_bwd_params(int B, int D, int ndir, const float* gate_logits, const float* ws, const float* conv_part,
+                               float* dA_log, float* dDskip, float* dgate_logits, float* dconv_w, float* dconv_b,
+                               hipStream_t stream);
 
 /* ---------------------------------------------------------------- hsiMamba row chains
  * Two projections with a LayerNorm between them for 32-row blocks in one launch (rowchain.hip), fp32:

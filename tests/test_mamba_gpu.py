@@ -142,6 +142,17 @@ def test_mamba_fused_vs_float64(L, D, E):
     torch.cuda.synchronize()
     errs = _grad_errs([dXZ, dCW, dCB, dWx, dWdt, dbdt, dA, dDs, dG], c["leaves"])
     assert max(errs.values()) < 1e-4, errs
+    # deferred: the partials left in ws, then every parameter reduction in one launch (vc_mamba_bwd_params)
+    assert lib.vc_mamba_scan_bwd_fused(B, L, D, R, ndir, P(U), P(XD), P(c["o32"]), P(c["xz"]), P(c["cw"]), P(c["cb"]),
+                                       P(c["wx"]), P(c["wdt"]), P(c["bdt"]), P(c["alog"]), P(c["dsk"]), P(c["gate"]),
+                                       P(Y), P(dYP), P(CKP), P(dU), P(dDTL), P(dXD), P(CP), None, None, None, P(ws),
+                                       ws.numel(), s) == 0
+    qA, qDs, qG = torch.full_like(dA, float("nan")), torch.full_like(dDs, float("nan")), torch.full_like(dG, float("nan"))
+    qCW, qCB = torch.full_like(dCW, float("nan")), torch.full_like(dCB, float("nan"))
+    assert lib.vc_mamba_bwd_params(B, D, ndir, P(c["gate"]), P(ws), P(CP), P(qA), P(qDs), P(qG), P(qCW), P(qCB), s) == 0
+    torch.cuda.synchronize()
+    for got, ref in ((qA, dA), (qDs, dDs), (qG, dG), (qCW, dCW), (qCB, dCB)):   # the same sums, another fixed order
+        assert float((got - ref).abs().max() / ref.abs().max()) < 1e-5
 
 
 @pytest.mark.parametrize("L,D,E,use_ckpt", [(81, 72, 144, True), (49, 128, 256, True), (81, 72, 144, False),

@@ -42,6 +42,7 @@ SWITCHES = {
     "VITCNN_SCAN_FUSED": ("model", "_SCAN_FUSED", _FLAG),
     "VITCNN_ROW_CHAIN": ("model", "_ROW_CHAIN", _FLAG),
     "VITCNN_GLF_FUSED": ("model", "_GLF_FUSED", _FLAG),
+    "VITCNN_ONE_PARAM_REDUCE": ("model", "_ONE_PARAM_REDUCE", _FLAG),
     "VITCNN_TAP_DGRAD": ("model", "_TAP_DGRAD", _FLAG),
     "VITCNN_LANES": ("model", "_LANES", _FLAG),
     "VITCNN_LANES_BWD": ("model", "_LANES_BWD", _FLAG),

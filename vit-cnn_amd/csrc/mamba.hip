@@ -946,10 +946,10 @@ __global__ void combine_fwd(int total, FastDiv fD, FastDiv fL, int B, int ndir, 
   out[idx] = acc * silu_f(xz[(long)bl * 2 * D + D + d]);
 }
 
-// dlogit_j = g_j (dg_j - sum_k g_k dg_k),  dg_k = sum over the k-th direction's partials
-__global__ __launch_bounds__(256) void gate_grad(int ndir, int per_dir, const float* __restrict__ logits,
-                                                 const float* __restrict__ part, float* __restrict__ dlogits) {
-  __shared__ float dg[64], gg[64];
+// dlogit_j = g_j (dg_j - sum_k g_k dg_k),  dg_k = sum over the k-th direction's partials (one 256-thread block)
+__device__ __forceinline__ void gate_grad_body(int ndir, int per_dir, const float* __restrict__ logits,
+                                               const float* __restrict__ part, float* __restrict__ dlogits,
+                                               float* dg, float* gg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int kk = wave; kk < ndir; kk += 4) {
     float s = 0.f;
@@ -965,6 +965,53 @@ __global__ __launch_bounds__(256) void gate_grad(int ndir, int per_dir, const fl
     float dot = 0.f;
     for (int i = 0; i < ndir; ++i) dot += gg[i] * dg[i];
     dlogits[threadIdx.x] = gg[threadIdx.x] * (dg[threadIdx.x] - dot);
+  }
+}
+
+__global__ __launch_bounds__(256) void gate_grad(int ndir, int per_dir, const float* __restrict__ logits,
+                                                 const float* __restrict__ part, float* __restrict__ dlogits) {
+  __shared__ float dg[64], gg[64];
+  gate_grad_body(ndir, per_dir, logits, part, dlogits, dg, gg);
+}
+
+// Every per-sequence partial of a hsiMamba block's scan backward reduced in ONE launch (round 6): column blocks of
+// 16 columns x 16 partial lanes over [dA_log 16D | D skip D | conv1d weight 4D | conv1d bias D] (sum_rows_kernel's
+// fixed order; the columns of one block may straddle two tensors), and one last block for the gate gradient --
+// instead of two two-phase column sums, the gate kernel and the conv row sum (6 launches at the end of the step)
+__global__ __launch_bounds__(256) void mamba_params(int nseq, int D, int ndir, int ncb, const float* __restrict__ logits,
+                                                    const float* __restrict__ pa, const float* __restrict__ pd,
+                                                    const float* __restrict__ pg, const float* __restrict__ cp,
+                                                    float* __restrict__ dA, float* __restrict__ dDs,
+                                                    float* __restrict__ dgl, float* __restrict__ dcw,
+                                                    float* __restrict__ dcb) {
+  __shared__ float sh[16][17];
+  __shared__ float dg[64], gg[64];
+  if ((int)blockIdx.x == ncb) {
+    gate_grad_body(ndir, nseq / ndir, logits, pg, dgl, dg, gg);
+    return;
+  }
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  const float* src = nullptr;
+  long stride = 0;
+  float* dst = nullptr;
+  int cc = 0;
+  if (c < NST * D) src = pa, stride = (long)NST * D, dst = dA, cc = c;
+  else if (c < (NST + 1) * D) src = pd, stride = D, dst = dDs, cc = c - NST * D;
+  else if (c < (NST + 5) * D) src = cp, stride = 5L * D, dst = dcw, cc = c - (NST + 1) * D;
+  else if (c < (NST + 6) * D) src = cp + 4L * D, stride = 5L * D, dst = dcb, cc = c - (NST + 5) * D;
+  float s = 0.f;
+  if (src) {
+#pragma unroll 4
+    for (int p = pl; p < nseq; p += 16) s += src[(long)p * stride + cc];
+  }
+  sh[pl][cl] = s;
+  __syncthreads();
+  if (pl == 0 && src) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v += sh[i][cl];
+    dst[cc] = v;
   }
 }
 
@@ -1308,6 +1355,24 @@ VC_API int vc_mamba_conv_params(int B, int D, int ndir, const float* conv_part, 
   const int rc = launch_sum_rows(nseq, 4 * D, conv_part, 5L * D, 0L, dconv_w, 0.f, stream);
   if (rc) return rc;
   return launch_sum_rows(nseq, D, conv_part, 5L * D, 4L * D, dconv_b, 0.f, stream);
+}
+
+// vc_mamba_scan_bwd_params + vc_mamba_conv_params in one launch (mamba_params): ws as vc_mamba_scan_bwd_params,
+// conv_part as vc_mamba_conv_params; every output overwritten
+VC_API int vc_mamba_bwd_params(int B, int D, int ndir, const float* gate_logits, const float* ws, const float* conv_part,
+                               float* dA_log, float* dDskip, float* dgate_logits, float* dconv_w, float* dconv_b,
+                               hipStream_t stream) {
+  VC_REQUIRE(B > 0 && D > 0 && ndir > 0 && ndir <= 64 && gate_logits && ws && conv_part && dA_log && dDskip &&
+             dgate_logits && dconv_w && dconv_b);
+  const int nseq = ndir * B;
+  const float* p_a = ws;
+  const float* p_d = p_a + (long)nseq * D * NST;
+  const float* p_g = p_d + (long)nseq * D;
+  const int ncb = vc_cdiv((NST + 6) * D, 16);
+  hipLaunchKernelGGL(mamba_params, dim3(ncb + 1), dim3(256), 0, stream, nseq, D, ndir, ncb, gate_logits, p_a, p_d,
+                     p_g, conv_part, dA_log, dDskip, dgate_logits, dconv_w, dconv_b);
+  VC_CHECK_LAUNCH();
+  return VC_OK;
 }
 
 // The parameter-gradient reductions of vc_mamba_scan_bwd, run separately (later, or on another

@@ -39,6 +39,7 @@ BN_EPS = 1e-5
 BN_MOM = 0.1
 NDIR = 10
 N_SIDE = 3                 # side streams: 1 = local/non-local branch, 2 = channel branch, 3 = LiDAR branch
+_ONE_PARAM_REDUCE = True   # a hsiMamba block's scan / conv1d parameter gradients in one reduction launch
 WGRAD_LANE = 2             # backward: lane 0's deferred weight gradients (lane 2 is idle after the forward)
 WGRAD1_LANE = 3            # backward: lane 1's deferred weight gradients (lane 3: after the fusion1 / LiDAR chain)
 # Program switches.  Module constants -- the product reads no environment: each selects between two
@@ -1333,28 +1334,29 @@ class _Program:
         CP = f(pfx + ".convpart", nseq * 5 * D)
         defer = self._deferring(True)
         spn = nseq * D * 16 + nseq * D + nseq
-        sp = f(pfx + ".scanpart", spn) if defer else self.scr_p
-        spn = spn if defer else self.scr_n
+        sp = f(pfx + ".scanpart", spn)
         gl, ga, gd, gg = P[gv + ".weights"], G[mx + ".A_log"], G[mx + ".D"], G[gv + ".weights"]
         self.L.vc_mamba_scan_bwd_fused(B, L_, D, R, NDIR, U, XD, order, XZ, P[mx + ".conv1d.weight"],
                                        P[mx + ".conv1d.bias"], P[mx + ".x_proj.weight"], P[mx + ".dt_proj.weight"],
                                        P[mx + ".dt_proj.bias"], P[mx + ".A_log"], P[mx + ".D"], gl, Y, dYP, CKPb, dU,
-                                       dDTL, dXD, CP, None if defer else ga, None if defer else gd,
-                                       None if defer else gg, sp, spn, self.s)
+                                       dDTL, dXD, CP, None, None, None, sp, spn, self.s)
+        cw, cb = G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"]
+        # A_log, D, gate and conv1d parameter gradients: one reduction launch (the same order deferred or not), on the
+        # weight-gradient lane when deferring (round 6; _ONE_PARAM_REDUCE = False: the round-5 launches)
+        if _ONE_PARAM_REDUCE:
+            params = lambda: self.L.vc_mamba_bwd_params(B, D, NDIR, gl, sp, CP, ga, gd, gg, cw, cb, self.s)  # noqa: E731
+        else:
+            def params():
+                self.L.vc_mamba_scan_bwd_params(B, D, NDIR, gl, sp, ga, gd, gg, self.scr_p, self.scr_n, self.s)
+                self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s)
         if defer:
-            self.pending_wgrads.append(
-                lambda: self.L.vc_mamba_scan_bwd_params(B, D, NDIR, gl, sp, ga, gd, gg, self.scr_p, self.scr_n,
-                                                        self.s))
+            self.pending_wgrads.append(params)
+        else:
+            params()
         self.L.vc_mamba_dirconv_bwd_gather(B, L_, D, NDIR, inv, P[mx + ".conv1d.weight"], dU, dXZ, self.s)
         # parameter gradients: dt_proj (dDTL, XD's dt-rank columns), x_proj (dXD, U), conv1d (partials)
         self.defer_wgrad(True, D, R, nr, dDTL, D, XD, XW, G[mx + ".dt_proj.weight"], R, G[mx + ".dt_proj.bias"])
         self.defer_wgrad(True, XW, D, nr, dXD, XW, U, D, G[mx + ".x_proj.weight"], D)
-        cw, cb = G[mx + ".conv1d.weight"], G[mx + ".conv1d.bias"]
-        conv = lambda: self.L.vc_mamba_conv_params(B, D, NDIR, CP, cw, cb, self.s)  # noqa: E731
-        if defer:
-            self.pending_wgrads.append(conv)
-        else:
-            conv()
 
     def _chain_ok(self, blk):
         """the row-chain launches apply to this block's widths (rowchain.hip limits)"""
